@@ -1,0 +1,145 @@
+#!/usr/bin/env python
+"""Headline benchmark: LLaMA3-8B-shape bf16 training tokens/s on 1..8 MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
+is launched under ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI).
+W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
+torch.cuda.synchronize() on both sides; the max elapsed over ranks is used and
+rank 0 prints one JSON line. ``value`` = whole-job tokens/s (all GPUs).
+
+A step is a full training step: forward, fused CE loss, backward (per-layer
+RCCL gradient buckets overlapped with backward when N>1), grad-norm clip,
+fused AdamW over the flat fp32 master/moment buffers. Synthetic token ids,
+random-init weights of the LLaMA3-8B architecture (D4096 L32 H32 KV8 FFN14336
+V128256), seq 8192, micro-batch 1 per GPU (weak scaling: global batch = N).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from solvingpapers_amd.models import llama3  # noqa: E402
+from solvingpapers_amd.parallel import dist as sdist  # noqa: E402
+from solvingpapers_amd.parallel.data_parallel import DataParallel  # noqa: E402
+from solvingpapers_amd.train.optim import FlatAdamW  # noqa: E402
+from solvingpapers_amd.utils.flat import FlatParams  # noqa: E402
+
+BASELINE_TOKS = None  # BASELINE.json "published": {} -> no reference number for this config
+PEAK_BF16 = 2.5e15
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama3_8b")
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--mb", type=int, default=1, help="micro-batch per GPU")
+    ap.add_argument("--accum", type=int, default=1, help="micro-batches per step")
+    ap.add_argument("--zero1", action="store_true")
+    ap.add_argument("--layers", type=int, default=None, help="override layer count (NOT for headline runs)")
+    a = ap.parse_args(argv)
+
+    info = sdist.init_distributed()
+    world = info.world_size
+    if world != a.gpus and info.is_main:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = info.device
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+    kw = {} if a.layers is None else {"n_layers": a.layers}
+    cfg = llama3.config(a.model, max_seq_len=a.seq, **kw)
+    model = llama3.Llama3(cfg, device=dev, dtype=torch.bfloat16, seed=1234)
+    flat = FlatParams(model, groups=model.param_groups(), grad_dtype=torch.bfloat16, align=64)
+    dp = DataParallel(model, flat, zero1=a.zero1) if world > 1 else None
+    if dp is not None:
+        dp.broadcast_params(0)
+    shard = (dp.shard_ranges(), None) if (dp is not None and a.zero1) else None
+    opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0, shard=shard)
+
+    gen = torch.Generator(device=dev).manual_seed(1000 + info.rank)
+    V, T, B = cfg.vocab_size, a.seq, a.mb
+
+    def batch():
+        t = torch.randint(0, V, (B, T + 1), device=dev, generator=gen)
+        return t[:, :-1], t[:, 1:]
+
+    last_loss = [None]
+
+    def step():
+        opt.zero_grad()
+        for i in range(a.accum):
+            x, y = batch()
+            sync = (i == a.accum - 1)
+            if dp is not None and not sync:
+                with dp.no_sync():
+                    loss = model(x, y) / a.accum
+                    loss.backward()
+            else:
+                loss = model(x, y) / a.accum
+                loss.backward()
+        if dp is not None:
+            dp.finish_grad_sync()
+        opt.step()
+        if dp is not None:
+            dp.gather_params()
+        last_loss[0] = loss
+
+    for _ in range(a.warmup):
+        step()
+    sdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    sdist.barrier()
+    t1 = time.perf_counter()
+    elapsed = sdist.all_reduce_max(t1 - t0)
+    loss_v = float(last_loss[0].item()) * a.accum
+
+    tokens = world * B * T * a.accum * a.steps
+    tok_s = tokens / elapsed
+    flops_tok = model.flops_per_token(T)
+    tflops_gpu = tok_s * flops_tok / world / 1e12
+    if info.is_main:
+        out = {
+            "metric": "training tokens/sec, LLaMA3-8B-shape bf16",
+            "value": round(tok_s, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (tok_s / BASELINE_TOKS) if BASELINE_TOKS else None,
+            "dtype": "bf16",
+            "data": "synthetic (random token ids, random-init weights)",
+            "config": {
+                "model": a.model if a.layers is None else f"{a.model}-L{a.layers}",
+                "global_batch": world * B * a.accum,
+                "seq_len": T,
+                "parallelism": f"dp{world}" + ("-zero1" if a.zero1 else ""),
+                "micro_batch": B,
+                "params": model.num_params(),
+            },
+            "tflops_per_gpu": round(tflops_gpu, 1),
+            "mfu_vs_2.5PF": round(tflops_gpu * 1e12 / PEAK_BF16, 4),
+            "loss": round(loss_v, 4),
+            "mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
+        }
+        print(json.dumps(out), flush=True)
+    sdist.cleanup()
+
+
+if __name__ == "__main__":
+    main()

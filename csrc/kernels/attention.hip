@@ -1,0 +1,632 @@
+// Flash attention (forward + backward) for gfx950 on MFMA v_mfma_f32_32x32x16_bf16.
+//
+// Covers the attention variants of the catalogue with one kernel family:
+//   causal MHA (gpt/gpt-jax.ipynb:344-353), GQA with RoPE'd q/k
+//   (llama3/LLaMA-jax.ipynb:809-829 — no materialised repeat_kv: q-head h reads
+//   kv-head h / (H/Hkv)), MQA (gemma/gemma.ipynb:238-256, Hkv = 1) and ViT
+//   non-causal self-attention (vision transformer/ViT.ipynb:208,221; T = 197 tails).
+//
+// Design (wave64, 32x32x16 MFMA):
+//  * Every product is arranged so the QUERY (fwd, dQ) or the KEY (dK/dV) sits on
+//    the MFMA lane:  S^T = K Q^T,  O^T = V^T P^T  (fwd);  S = Q K^T, dV^T = dO^T P,
+//    dK^T = Q^T dS  (dkdv);  dQ^T = K^T dS^T  (dq). The softmax state is then
+//    lane-local, and P / dS feed the next MFMA straight from the accumulator
+//    registers (their k order is permuted: element j of half h = row
+//    16s + 8(j>>2) + 4h + (j&3); the other operand is read with the same order).
+//  * The other operand of those "transposed" products (V^T, dO^T, Q^T, K^T) is read
+//    with ds_read_b64_tr_b16 from the SAME row-major LDS image that the row
+//    products read with ds_read_b128 — one image per tensor, written with 16-byte
+//    stores. Images use 16-byte-chunk XOR swizzles chosen so both read kinds are
+//    bank-conflict free (HD>=128: ch ^ ((r&3)<<2 | (r>>2)&3); HD=64: ch ^ ((r>>1&1)<<2 | (r>>2)&3)).
+//  * Double-buffered K/V (or Q/dO) LDS tiles with register prefetch two tiles
+//    ahead: one barrier per tile.
+//  * Forward: 8 waves x 32 query rows (2 waves / SIMD) for HD <= 128; the O
+//    rescale is skipped whenever no row max moved (wave-uniform test).
+//  * Causal: heavy blocks first; waves skip tiles entirely above their diagonal;
+//    masks only on straddling tiles.
+//  * Backward = two deterministic kernels (no float atomics): dq (query-parallel,
+//    also produces delta = rowsum(dO*O)) then dkdv (key-parallel, loops the GQA
+//    group's q-heads so dK/dV of a kv-head are summed in registers).
+// q/k/v/o and grads are addressed with (batch, seq, head) strides so the kernels
+// read/write a fused [B, T, H + 2*Hkv, hd] qkv buffer in place.
+#include "spa_common.h"
+
+namespace spa {
+
+struct AttnParams {
+  const bf16* q; const bf16* k; const bf16* v; const bf16* o; const bf16* dout;
+  bf16* out; bf16* dq; bf16* dk; bf16* dv;
+  float* lse; const float* lse_in; float* delta;
+  int B, H, Hkv, Tq, Tk;
+  long sqb, sqt, sqh, skb, skt, skh, svb, svt, svh, sob, sot, soh;
+  long sdob, sdot, sdoh;
+  long sdqb, sdqt, sdqh, sdkb, sdkt, sdkh, sdvb, sdvt, sdvh;
+  float scale;       // softmax scale (natural)
+  float scale_log2;  // scale * log2(e)
+  int causal_off;    // key j visible to query i iff j <= i + causal_off
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+  return z;
+}
+__device__ __forceinline__ void zero16(f32x16& a) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a[r] = 0.f;
+}
+// accumulator registers 8s..8s+7 -> bf16 operand fragment (permuted k order)
+__device__ __forceinline__ bf16x8 pack_acc(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+// ---- swizzled row-major [rows][HD] bf16 LDS images -------------------------
+template <int HD>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (HD >= 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+}
+template <int HD>
+__device__ __forceinline__ int img_off(int r, int ch) {  // element offset of 16B chunk ch of row r
+  return r * HD + 8 * (ch ^ swz<HD>(r));
+}
+// 16-byte row fragment: row r, elements [8ch, 8ch+8)
+template <int HD>
+__device__ __forceinline__ bf16x8 rd_row(const bf16* img, int r, int ch) {
+  return *reinterpret_cast<const bf16x8*>(img + img_off<HD>(r, ch));
+}
+// A/B operand "X^T" for one 16-deep k-step, where X is the row-major image with
+// rows = k index, columns = output index. Lane l gets X[r0 + 16s + perm(j)][c0 + (l&31)].
+template <int HD>
+__device__ __forceinline__ bf16x8 rd_tr(const bf16* img, int rbase, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3, hh = lane >> 5;
+  const int c = c0 + 16 * (g & 1) + 4 * pp;  // column (element) this lane addresses
+  const int ch = c >> 3, within = c & 7;
+  const int ra = rbase + 4 * hh + q, rb = ra + 8;
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4*)(img + ra * HD + 8 * (ch ^ swz<HD>(ra)) + within));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4*)(img + rb * HD + 8 * (ch ^ swz<HD>(rb)) + within));
+  // whole-vector bit casts: element-wise short->bf16 inserts miscompile (duplicated dwords)
+  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
+  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Register-staged tile loader: ROWS x HD bf16 tile of a strided tensor -> regs -> LDS image.
+template <int HD, int ROWS, int NT>
+struct TileLoader {
+  static constexpr int CH = ROWS * HD / 8 / NT;  // 16B chunks per thread
+  static_assert(CH >= 1 && ROWS * HD / 8 % NT == 0, "tile/threads mismatch");
+  bf16x8 r[CH];
+  __device__ __forceinline__ void load(const bf16* base, long stride, int row0, int nrows, int tid) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + c * NT;
+      const int rr = idx / (HD / 8), ch = idx % (HD / 8);
+      const int row = row0 + rr;
+      r[c] = row < nrows ? *reinterpret_cast<const bf16x8*>(base + (long)row * stride + ch * 8) : zero8();
+    }
+  }
+  __device__ __forceinline__ void store(bf16* img, int tid) const {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + c * NT;
+      const int rr = idx / (HD / 8), ch = idx % (HD / 8);
+      *reinterpret_cast<bf16x8*>(img + img_off<HD>(rr, ch)) = r[c];
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Forward: block = NW waves x 32 query rows; K/V tiles of 64 keys.
+// ---------------------------------------------------------------------------
+template <int HD, int NW, bool CAUSAL>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
+  constexpr int BN = 64, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
+  constexpr int TILE = BN * HD;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lq = lane & 31, hh = lane >> 5;
+  const int nqb = cdiv(p.Tq, BM);
+  const int nbh = p.H * p.B;
+  int qb = blockIdx.x / nbh;
+  const int bh = blockIdx.x % nbh;
+  if (CAUSAL) qb = nqb - 1 - qb;  // heaviest q-blocks first
+  const int h = bh % p.H, b = bh / p.H;
+  const int hk = h / (p.H / p.Hkv);
+  const int q0 = qb * BM + wave * 32;
+  const int q = q0 + lq;
+
+  bf16x8 qf[KS];
+  {
+    const bf16* qp = p.q + b * p.sqb + (long)q * p.sqt + h * p.sqh + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = q < p.Tq ? *reinterpret_cast<const bf16x8*>(qp + 16 * s) : zero8();
+  }
+  f32x16 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) zero16(o[i]);
+  float m = -1e30f, l = 0.f;
+
+  int kend = p.Tk;
+  if (CAUSAL) kend = min(p.Tk, qb * BM + BM + p.causal_off);
+  const int wave_kend = CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
+  const int ntiles = kend > 0 ? cdiv(kend, BN) : 0;
+
+  const bf16* kbase = p.k + b * p.skb + hk * p.skh;
+  const bf16* vbase = p.v + b * p.svb + hk * p.svh;
+  TileLoader<HD, BN, NT> lk, lv;
+  if (ntiles > 0) {
+    lk.load(kbase, p.skt, 0, p.Tk, tid);
+    lv.load(vbase, p.svt, 0, p.Tk, tid);
+    lk.store(smem, tid);
+    lv.store(smem + TILE, tid);
+    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk, tid); lv.load(vbase, p.svt, BN, p.Tk, tid); }
+  }
+  __syncthreads();
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * BN;
+    bf16* Ks = smem + (j & 1) * 2 * TILE;
+    bf16* Vs = Ks + TILE;
+    if (j + 1 < ntiles) {
+      bf16* Kn = smem + ((j + 1) & 1) * 2 * TILE;
+      lk.store(Kn, tid);
+      lv.store(Kn + TILE, tid);
+      if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk, tid); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk, tid); }
+    }
+    if (k0 < wave_kend) {
+      f32x16 s[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        zero16(s[t]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[t] = mfma32(rd_row<HD>(Ks, 32 * t + lq, 2 * ks + hh), qf[ks], s[t]);
+      }
+      const bool need_mask = (k0 + BN > p.Tk) || (CAUSAL && k0 + BN - 1 > q0 + p.causal_off);
+      float mx = -1e30f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = s[t][r] * p.scale_log2;
+          if (need_mask) {
+            const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= p.Tk || (CAUSAL && key > q + p.causal_off)) v = -INFINITY;
+          }
+          s[t][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      if (__any(mnew > m)) {  // wave-uniform: rescale only when some row max moved
+        const float alpha = exp2f(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < DT; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+        m = mnew;
+      }
+      float ls = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = exp2f(s[t][r] - m);
+          s[t][r] = e;
+          ls += e;
+        }
+      l += ls;
+      bf16x8 pf[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) pf[kk] = pack_acc(s[kk >> 1], kk & 1);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) o[dt] = mfma32(rd_tr<HD>(Vs, 16 * kk, 32 * dt, lane), pf[kk], o[dt]);
+    }
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (q < p.Tq) {
+    bf16* op = p.out + b * p.sob + (long)q * p.sot + h * p.soh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = (bf16)(o[dt][4 * g + i] * inv);
+        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * hh) = w;
+      }
+    if (hh == 0 && p.lse)
+      p.lse[((long)b * p.H + h) * p.Tq + q] = (l > 0.f) ? (m + log2f(l)) * 0.69314718055994531f : INFINITY;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward dQ (query-parallel; also writes delta = rowsum(dO*O)).
+//   S^T = K Q^T ; P^T = exp2(S^T*c - lse2) ; dP^T = V dO^T ; dS^T = P^T (dP^T - delta)
+//   dQ^T += K^T dS^T   (K^T via tr reads of the K image)
+// ---------------------------------------------------------------------------
+template <int HD, int NW, bool CAUSAL>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
+  constexpr int BN = 64, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
+  constexpr int TILE = BN * HD;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lq = lane & 31, hh = lane >> 5;
+  const int nqb = cdiv(p.Tq, BM);
+  const int nbh = p.H * p.B;
+  int qb = blockIdx.x / nbh;
+  const int bh = blockIdx.x % nbh;
+  if (CAUSAL) qb = nqb - 1 - qb;
+  const int h = bh % p.H, b = bh / p.H;
+  const int hk = h / (p.H / p.Hkv);
+  const int q0 = qb * BM + wave * 32;
+  const int q = q0 + lq;
+  const bool qvalid = q < p.Tq;
+
+  bf16x8 qf[KS], df[KS];
+  float dlt = 0.f;
+  {
+    const bf16* qp = p.q + b * p.sqb + (long)q * p.sqt + h * p.sqh + 8 * hh;
+    const bf16* dp = p.dout + b * p.sdob + (long)q * p.sdot + h * p.sdoh + 8 * hh;
+    const bf16* op = p.o + b * p.sob + (long)q * p.sot + h * p.soh + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf[s] = qvalid ? *reinterpret_cast<const bf16x8*>(qp + 16 * s) : zero8();
+      df[s] = qvalid ? *reinterpret_cast<const bf16x8*>(dp + 16 * s) : zero8();
+      const bf16x8 ov = qvalid ? *reinterpret_cast<const bf16x8*>(op + 16 * s) : zero8();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt += (float)ov[j] * (float)df[s][j];
+    }
+    dlt += __shfl_xor(dlt, 32, 64);
+  }
+  const long srow = ((long)b * p.H + h) * p.Tq + q;
+  if (qvalid && hh == 0) p.delta[srow] = dlt;
+  const float lse2 = qvalid ? p.lse_in[srow] * 1.4426950408889634f : INFINITY;
+  f32x16 acc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) zero16(acc[i]);
+
+  int kend = p.Tk;
+  if (CAUSAL) kend = min(p.Tk, qb * BM + BM + p.causal_off);
+  const int wave_kend = CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
+  const int ntiles = kend > 0 ? cdiv(kend, BN) : 0;
+  const bf16* kbase = p.k + b * p.skb + hk * p.skh;
+  const bf16* vbase = p.v + b * p.svb + hk * p.svh;
+  TileLoader<HD, BN, NT> lk, lv;
+  if (ntiles > 0) {
+    lk.load(kbase, p.skt, 0, p.Tk, tid);
+    lv.load(vbase, p.svt, 0, p.Tk, tid);
+    lk.store(smem, tid);
+    lv.store(smem + TILE, tid);
+    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk, tid); lv.load(vbase, p.svt, BN, p.Tk, tid); }
+  }
+  __syncthreads();
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * BN;
+    bf16* Ks = smem + (j & 1) * 2 * TILE;
+    bf16* Vs = Ks + TILE;
+    if (j + 1 < ntiles) {
+      bf16* Kn = smem + ((j + 1) & 1) * 2 * TILE;
+      lk.store(Kn, tid);
+      lv.store(Kn + TILE, tid);
+      if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk, tid); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk, tid); }
+    }
+    if (k0 < wave_kend) {
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        zero16(s[t]);
+        zero16(dp[t]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s[t] = mfma32(rd_row<HD>(Ks, 32 * t + lq, 2 * ks + hh), qf[ks], s[t]);
+          dp[t] = mfma32(rd_row<HD>(Vs, 32 * t + lq, 2 * ks + hh), df[ks], dp[t]);
+        }
+      }
+      const bool need_mask = (k0 + BN > p.Tk) || (CAUSAL && k0 + BN - 1 > q0 + p.causal_off);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float pr = exp2f(s[t][r] * p.scale_log2 - lse2);
+          if (need_mask) {
+            const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= p.Tk || (CAUSAL && key > q + p.causal_off)) pr = 0.f;
+          }
+          s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
+        }
+      bf16x8 sf[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) sf[kk] = pack_acc(s[kk >> 1], kk & 1);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) acc[dt] = mfma32(rd_tr<HD>(Ks, 16 * kk, 32 * dt, lane), sf[kk], acc[dt]);
+    }
+    __syncthreads();
+  }
+  if (qvalid) {
+    bf16* op = p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = (bf16)(acc[dt][4 * g + i] * p.scale);
+        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * hh) = w;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward dK/dV: key-block parallel (4 waves x 32 keys), key on the lane.
+//   S = Q K^T, dP = dO V^T     (A = Q / dO row reads, B = K / V fragments in regs)
+//   dV^T += dO^T P, dK^T += Q^T dS   (A = tr reads of the Q / dO images, B = accumulators)
+// Loops over the q-heads sharing this kv-head (GQA) so the group sum stays in regs.
+// ---------------------------------------------------------------------------
+template <int HD, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
+  constexpr int BMQ = 32, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 256;
+  constexpr int TILE = BMQ * HD;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][Q|dO]
+  __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];  // [buf][lse2 | delta]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lk = lane & 31, hh = lane >> 5;
+  const int nbh = p.Hkv * p.B;
+  const int kb = blockIdx.x / nbh;  // causal: low key blocks are heaviest, launched first
+  const int bh = blockIdx.x % nbh;
+  const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  const int G = p.H / p.Hkv;
+  const int kw0 = kb * BNK + wave * 32;
+  const int key = kw0 + lk;
+  const bool kvalid = key < p.Tk;
+
+  bf16x8 kf[KS], vf[KS];
+  {
+    const bf16* kp = p.k + b * p.skb + (long)key * p.skt + hk * p.skh + 8 * hh;
+    const bf16* vp = p.v + b * p.svb + (long)key * p.svt + hk * p.svh + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      kf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(kp + 16 * s) : zero8();
+      vf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(vp + 16 * s) : zero8();
+    }
+  }
+  f32x16 dkt[DT], dvt[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) { zero16(dkt[i]); zero16(dvt[i]); }
+
+  int qstart = 0, wave_qstart = 0;
+  if (CAUSAL) {
+    qstart = max(0, kb * BNK - p.causal_off);
+    wave_qstart = max(0, kw0 - p.causal_off);
+  }
+  const int t0 = qstart / BMQ;
+  const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
+  const int nper = ntq - t0 > 0 ? ntq - t0 : 0;  // q-tiles per head
+  const int total = nper * G;                      // (head, q-tile) iterations
+  TileLoader<HD, BMQ, NT> lq_, ld_;
+  float rl = 0.f, rd = 0.f;  // per-thread row constants for the prefetched tile (tid < 32)
+  auto fetch = [&](int it) {
+    const int hg = it / nper, tq = t0 + it % nper;
+    const int h = hk * G + hg;
+    const int qq0 = tq * BMQ;
+    lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq, tid);
+    ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq, tid);
+    if (tid < BMQ) {
+      const int qq = qq0 + tid;
+      const long rbase = ((long)b * p.H + h) * p.Tq;
+      rl = qq < p.Tq ? p.lse_in[rbase + qq] * 1.4426950408889634f : INFINITY;
+      rd = qq < p.Tq ? p.delta[rbase + qq] : 0.f;
+    }
+  };
+  auto commit_tile = [&](int buf) {
+    lq_.store(smem + buf * 2 * TILE, tid);
+    ld_.store(smem + buf * 2 * TILE + TILE, tid);
+    if (tid < BMQ) { rowc[buf][tid] = rl; rowc[buf][BMQ + tid] = rd; }
+  };
+  if (total > 0) {
+    fetch(0);
+    commit_tile(0);
+    if (total > 1) fetch(1);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int tq = t0 + it % nper;
+    const int qq0 = tq * BMQ;
+    const bf16* Qs = smem + (it & 1) * 2 * TILE;
+    const bf16* Ds = Qs + TILE;
+    const float* rc = rowc[it & 1];
+    if (it + 1 < total) {
+      commit_tile((it + 1) & 1);
+      if (it + 2 < total) fetch(it + 2);
+    }
+    const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
+    if (active) {
+      f32x16 s, dp;
+      zero16(s);
+      zero16(dp);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma32(rd_row<HD>(Qs, lk, 2 * ks + hh), kf[ks], s);
+        dp = mfma32(rd_row<HD>(Ds, lk, 2 * ks + hh), vf[ks], dp);
+      }
+      // rows of s/dp are queries qq0 + 8g + 4hh + i (r = 4g + i); column = key (lane)
+      const bool need_mask = CAUSAL && qq0 + p.causal_off < kw0 + 31;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 8 * g + 4 * hh);
+        const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 8 * g + 4 * hh);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i;
+          float pr = exp2f(s[r] * p.scale_log2 - lv[i]);  // rows >= Tq: lse=inf -> 0
+          if (need_mask) {
+            const int qq = qq0 + 8 * g + 4 * hh + i;
+            if (key > qq + p.causal_off) pr = 0.f;
+          }
+          s[r] = pr;
+          dp[r] = pr * (dp[r] - dv[i]);
+        }
+      }
+      bf16x8 pf[2], sf[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) { pf[kk] = pack_acc(s, kk); sf[kk] = pack_acc(dp, kk); }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          dvt[dt] = mfma32(rd_tr<HD>(Ds, 16 * kk, 32 * dt, lane), pf[kk], dvt[dt]);
+          dkt[dt] = mfma32(rd_tr<HD>(Qs, 16 * kk, 32 * dt, lane), sf[kk], dkt[dt]);
+        }
+    }
+    __syncthreads();
+  }
+  if (kvalid) {
+    bf16* kp = p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh;
+    bf16* vp = p.dv + b * p.sdvb + (long)key * p.sdvt + hk * p.sdvh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 wk, wv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          wk[i] = (bf16)(dkt[dt][4 * g + i] * p.scale);
+          wv[i] = (bf16)(dvt[dt][4 * g + i]);
+        }
+        *reinterpret_cast<bf16x4*>(kp + 32 * dt + 8 * g + 4 * hh) = wk;
+        *reinterpret_cast<bf16x4*>(vp + 32 * dt + 8 * g + 4 * hh) = wv;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static void check_qkv(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, n, " must be a bf16 HIP tensor");
+  TORCH_CHECK(t.dim() == 4, n, " must be [B, T, H, hd]");
+  TORCH_CHECK(t.stride(3) == 1, n, " must be contiguous in hd");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() % 16) == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+                  t.stride(0) % 8 == 0,
+              n, ": rows must be 16-byte aligned");
+}
+
+// forward / dq use 8 waves (2 per SIMD) for hd <= 128, 4 waves for hd = 256
+template <int HD> constexpr int fwd_waves() { return HD <= 128 ? 8 : 4; }
+
+#define HD_SWITCH(HDV, ...)                                                        \
+  if (HDV == 64) { constexpr int HD_ = 64; __VA_ARGS__; }                          \
+  else if (HDV == 128) { constexpr int HD_ = 128; __VA_ARGS__; }                   \
+  else if (HDV == 256) { constexpr int HD_ = 256; __VA_ARGS__; }                   \
+  else TORCH_CHECK(false, "flash attention: head dim must be 64, 128 or 256");
+
+static void fill_strides(AttnParams& p, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
+  p.sqb = q.stride(0); p.sqt = q.stride(1); p.sqh = q.stride(2);
+  p.skb = k.stride(0); p.skt = k.stride(1); p.skh = k.stride(2);
+  p.svb = v.stride(0); p.svt = v.stride(1); p.svh = v.stride(2);
+}
+
+// q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd] (strided views allowed). Returns (out [B,Tq,H,hd], lse [B,H,Tq]).
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
+                                 bool causal) {
+  check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v");
+  const int B = q.size(0), Tq = q.size(1), H = q.size(2), HD = q.size(3);
+  const int Tk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Tk && v.size(2) == Hkv && k.size(3) == HD &&
+              v.size(3) == HD, "attn: shape mismatch");
+  TORCH_CHECK(H % Hkv == 0, "attn: H must be a multiple of Hkv");
+  DeviceGuard g(q.device());
+  auto out = at::empty({B, Tq, H, HD}, q.options());
+  auto lse = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
+  AttnParams p{};
+  p.q = (const bf16*)q.data_ptr(); p.k = (const bf16*)k.data_ptr(); p.v = (const bf16*)v.data_ptr();
+  p.out = (bf16*)out.data_ptr(); p.lse = lse.data_ptr<float>();
+  p.B = B; p.H = H; p.Hkv = Hkv; p.Tq = Tq; p.Tk = Tk;
+  fill_strides(p, q, k, v);
+  p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
+  p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.causal_off = Tk - Tq;
+  if (B * Tq * H == 0) return {out, lse};
+  auto st = stream();
+  HD_SWITCH(HD, {
+    constexpr int NW = fwd_waves<HD_>();
+    const int grid = cdiv(Tq, 32 * NW) * H * B;
+    if (causal) attn_fwd_kernel<HD_, NW, true><<<grid, NW * 64, 0, st>>>(p);
+    else attn_fwd_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
+  });
+  SPA_LAUNCH_CHECK();
+  return {out, lse};
+}
+
+// Gradients written into dq/dk/dv (strided views allowed, e.g. slices of one dqkv buffer).
+void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+              const at::Tensor& out, const at::Tensor& lse, const at::Tensor& dq, const at::Tensor& dk,
+              const at::Tensor& dv, double scale, bool causal) {
+  check_qkv(dout, "dout"); check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(out, "out");
+  check_qkv(dq, "dq"); check_qkv(dk, "dk"); check_qkv(dv, "dv");
+  const int B = q.size(0), Tq = q.size(1), H = q.size(2), HD = q.size(3);
+  const int Tk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)B * H * Tq);
+  TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes());
+  TORCH_CHECK(dout.sizes() == q.sizes() && out.sizes() == q.sizes());
+  DeviceGuard g(q.device());
+  auto delta = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
+  AttnParams p{};
+  p.q = (const bf16*)q.data_ptr(); p.k = (const bf16*)k.data_ptr(); p.v = (const bf16*)v.data_ptr();
+  p.o = (const bf16*)out.data_ptr(); p.dout = (const bf16*)dout.data_ptr();
+  p.dq = (bf16*)dq.data_ptr(); p.dk = (bf16*)dk.data_ptr(); p.dv = (bf16*)dv.data_ptr();
+  p.lse_in = lse.data_ptr<float>(); p.delta = delta.data_ptr<float>();
+  p.B = B; p.H = H; p.Hkv = Hkv; p.Tq = Tq; p.Tk = Tk;
+  fill_strides(p, q, k, v);
+  p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
+  p.sdob = dout.stride(0); p.sdot = dout.stride(1); p.sdoh = dout.stride(2);
+  p.sdqb = dq.stride(0); p.sdqt = dq.stride(1); p.sdqh = dq.stride(2);
+  p.sdkb = dk.stride(0); p.sdkt = dk.stride(1); p.sdkh = dk.stride(2);
+  p.sdvb = dv.stride(0); p.sdvt = dv.stride(1); p.sdvh = dv.stride(2);
+  p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.causal_off = Tk - Tq;
+  if (B * H == 0) return;
+  auto st = stream();
+  if (Tq == 0) { dk.zero_(); dv.zero_(); return; }
+  HD_SWITCH(HD, {
+    constexpr int NW = fwd_waves<HD_>();
+    const int grid = cdiv(Tq, 32 * NW) * H * B;
+    if (causal) attn_bwd_dq_kernel<HD_, NW, true><<<grid, NW * 64, 0, st>>>(p);
+    else attn_bwd_dq_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
+    if (Tk > 0) {
+      const int g2 = cdiv(Tk, 128) * Hkv * B;
+      if (causal) attn_bwd_dkdv_kernel<HD_, true><<<g2, 256, 0, st>>>(p);
+      else attn_bwd_dkdv_kernel<HD_, false><<<g2, 256, 0, st>>>(p);
+    }
+  });
+  SPA_LAUNCH_CHECK();
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal) -> Tensor[]");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
+        "Tensor(c!) dv, float scale, bool causal) -> ()");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("attn_fwd", &spa::attn_fwd);
+  m.impl("attn_bwd", &spa::attn_bwd);
+}

@@ -1,0 +1,321 @@
+// RMSNorm / LayerNorm forward + backward for gfx950, with an optional fused
+// residual add (h = x + r; y = norm(h)) so the pre-norm transformer block reads
+// its residual stream exactly once per norm.
+//
+// Reference semantics: RMSNorm `x*w*rsqrt(mean(x^2)+eps)`
+//   llama3/LLaMA-jax.ipynb:536-538, gemma/gemma.ipynb:139-150 (fp32 compute),
+//   deepseekv3/deepseekv3.ipynb:911-917;
+// LayerNorm (weight+bias) gpt/gpt-jax.ipynb:414-416, vision transformer/ViT.ipynb:205-206.
+//
+// Mapping: one row per NT-thread group (NT = 256 for D >= 2048, else 64 = one wave
+// with 4 rows per 256-thread block). Each thread keeps its 8-element bf16 vectors
+// in registers (MAXV of them) so the row is read from HBM once. Stats in fp32.
+// Backward dw/db: each block accumulates a per-column partial over a strided set
+// of rows in registers, writes one fp32 partial row, a second tiny kernel sums the
+// partials (deterministic, no atomics).
+#include "spa_common.h"
+
+namespace spa {
+
+template <int NT, int MAXV, bool LN, bool RES, bool RESOUT>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ r, const bf16* __restrict__ w,
+    const bf16* __restrict__ b, bf16* __restrict__ y, bf16* __restrict__ hout,
+    float* __restrict__ rstd_out, float* __restrict__ mean_out, int M, int D, float eps) {
+  constexpr int RPB = 256 / NT;  // rows per block
+  __shared__ float red[RPB][NT / 64 > 0 ? NT / 64 : 1];
+  const int sub = threadIdx.x / NT, t = threadIdx.x % NT;
+  const int row = blockIdx.x * RPB + sub;
+  if (row >= M) return;  // whole group exits together (NT-aligned)
+  const int nv = D / 8;
+  float v[MAXV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = t + k * NT;
+    if (vi < nv) {
+      load8(x + (size_t)row * D + vi * 8, v[k]);
+      if constexpr (RES) {
+        float rr[8];
+        load8(r + (size_t)row * D + vi * 8, rr);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[k][i] += rr[i];
+        if constexpr (RESOUT) {
+          // round the residual stream to bf16 once, and normalise the rounded value
+          bf16x8 hv;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { hv[i] = (bf16)v[k][i]; v[k][i] = (float)hv[i]; }
+          *reinterpret_cast<bf16x8*>(hout + (size_t)row * D + vi * 8) = hv;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += LN ? v[k][i] : v[k][i] * v[k][i];
+    }
+  }
+  float mean = 0.f;
+  if constexpr (LN) {
+    float tot = NT == 64 ? wave_sum(s) : block_sum<NT>(s, red[sub]);
+    mean = tot / D;
+    s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+      if (t + k * NT < nv)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { float d = v[k][i] - mean; s += d * d; }
+    if (NT != 64) __syncthreads();
+  }
+  float tot = NT == 64 ? wave_sum(s) : block_sum<NT>(s, red[sub]);
+  const float rstd = rsqrtf(tot / D + eps);
+  if (t == 0) {
+    rstd_out[row] = rstd;
+    if constexpr (LN) mean_out[row] = mean;
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = t + k * NT;
+    if (vi < nv) {
+      float wv[8], o[8];
+      load8(w + vi * 8, wv);
+      if constexpr (LN) {
+        float bv[8];
+        load8(b + vi * 8, bv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mean) * rstd * wv[i] + bv[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = v[k][i] * rstd * wv[i];
+      }
+      store8(y + (size_t)row * D + vi * 8, o);
+    }
+  }
+}
+
+// Backward. grid.x = number of partial blocks; each block walks rows
+// blockIdx.x*RPB + sub, stepping by gridDim.x*RPB.
+template <int NT, int MAXV, bool LN, bool DRES>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(
+    const bf16* __restrict__ dy, const bf16* __restrict__ h, const bf16* __restrict__ w,
+    const float* __restrict__ rstd_in, const float* __restrict__ mean_in,
+    const bf16* __restrict__ dres, bf16* __restrict__ dx, float* __restrict__ dw_part,
+    float* __restrict__ db_part, int M, int D) {
+  constexpr int RPB = 256 / NT;
+  __shared__ float red[RPB][NT / 64 > 0 ? NT / 64 : 1];
+  const int sub = threadIdx.x / NT, t = threadIdx.x % NT;
+  const int nv = D / 8;
+  float dwacc[MAXV][8], dbacc[MAXV][8];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { dwacc[k][i] = 0.f; dbacc[k][i] = 0.f; }
+  float wv[MAXV][8];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (t + k * NT < nv) load8(w + (t + k * NT) * 8, wv[k]);
+
+  for (int row0 = blockIdx.x * RPB; row0 < M; row0 += gridDim.x * RPB) {
+    const int row = row0 + sub;
+    const bool valid = row < M;
+    float xh[MAXV][8], g[MAXV][8];
+    float s1 = 0.f, s2 = 0.f;
+    const float rstd = valid ? rstd_in[row] : 0.f;
+    const float mean = (LN && valid) ? mean_in[row] : 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = t + k * NT;
+      if (valid && vi < nv) {
+        float hv[8], dv[8];
+        load8(h + (size_t)row * D + vi * 8, hv);
+        load8(dy + (size_t)row * D + vi * 8, dv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xh[k][i] = (hv[i] - mean) * rstd;
+          g[k][i] = dv[i] * wv[k][i];
+          s1 += g[k][i] * xh[k][i];
+          if constexpr (LN) s2 += g[k][i];
+          dwacc[k][i] += dv[i] * xh[k][i];
+          if constexpr (LN) dbacc[k][i] += dv[i];
+        }
+      }
+    }
+    float a1, a2 = 0.f;
+    if (NT == 64) {
+      a1 = wave_sum(s1);
+      if constexpr (LN) a2 = wave_sum(s2);
+    } else {
+      a1 = block_sum<NT>(s1, red[sub]);
+      if constexpr (LN) { __syncthreads(); a2 = block_sum<NT>(s2, red[sub]); }
+      __syncthreads();
+    }
+    a1 /= D;
+    a2 /= D;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = t + k * NT;
+      if (valid && vi < nv) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = rstd * (g[k][i] - a2 - xh[k][i] * a1);
+        if constexpr (DRES) {
+          float rr[8];
+          load8(dres + (size_t)row * D + vi * 8, rr);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += rr[i];
+        }
+        store8(dx + (size_t)row * D + vi * 8, o);
+      }
+    }
+  }
+  if constexpr (RPB == 1) {
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = t + k * NT;
+      if (vi < nv) {
+        store8(dw_part + (size_t)blockIdx.x * D + vi * 8, dwacc[k]);
+        if constexpr (LN) store8(db_part + (size_t)blockIdx.x * D + vi * 8, dbacc[k]);
+      }
+    }
+  } else {
+    // small D (<= 2048): per-sub partial rows, reduced by the column kernel
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = t + k * NT;
+      if (vi < nv) {
+        const size_t prow = (size_t)blockIdx.x * RPB + sub;
+        store8(dw_part + prow * D + vi * 8, dwacc[k]);
+        if constexpr (LN) store8(db_part + prow * D + vi * 8, dbacc[k]);
+      }
+    }
+  }
+}
+
+// Column sums of a [P, D] fp32 partial matrix -> out[D] (dtype of param).
+template <typename OT>
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, OT* __restrict__ out,
+                                                     int P, int D) {
+  // 256 threads = 64 columns x 4 row-slices
+  __shared__ float s[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rs = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < D)
+    for (int p = rs; p < P; p += 4) acc += part[(size_t)p * D + c];
+  s[rs][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rs == 0 && c < D) out[c] = (OT)(s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
+}
+
+#define NORM_FWD_DISPATCH(NT, MAXV)                                                              \
+  do {                                                                                           \
+    dim3 grid(cdiv(M, 256 / NT));                                                                \
+    if (is_ln) {                                                                                 \
+      if (has_res) norm_fwd_kernel<NT, MAXV, true, true, true><<<grid, 256, 0, st>>>(ARGS);      \
+      else norm_fwd_kernel<NT, MAXV, true, false, false><<<grid, 256, 0, st>>>(ARGS);            \
+    } else {                                                                                     \
+      if (has_res) norm_fwd_kernel<NT, MAXV, false, true, true><<<grid, 256, 0, st>>>(ARGS);     \
+      else norm_fwd_kernel<NT, MAXV, false, false, false><<<grid, 256, 0, st>>>(ARGS);           \
+    }                                                                                            \
+  } while (0)
+
+// Returns (y, h_or_empty, rstd, mean_or_empty)
+std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
+                                 const at::Tensor& w, const c10::optional<at::Tensor>& b, double eps) {
+  SPA_CHECK_CUDA(x); SPA_CHECK_BF16(x); SPA_CHECK_CONTIG(x); SPA_CHECK_BF16(w);
+  const bool is_ln = b.has_value();
+  const bool has_res = residual.has_value();
+  const int D = x.size(-1);
+  const int M = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 16384, "norm: D must be a multiple of 8 and <= 16384");
+  TORCH_CHECK(w.numel() == D && w.is_contiguous());
+  DeviceGuard g(x.device());
+  auto y = at::empty_like(x);
+  at::Tensor h = has_res ? at::empty_like(x) : at::Tensor();
+  if (has_res) { SPA_CHECK_BF16(*residual); SPA_CHECK_CONTIG(*residual); TORCH_CHECK(residual->sizes() == x.sizes()); }
+  if (is_ln) { SPA_CHECK_BF16(*b); TORCH_CHECK(b->numel() == D && b->is_contiguous()); }
+  auto opts = x.options().dtype(at::kFloat);
+  auto rstd = at::empty({M}, opts);
+  auto mean = is_ln ? at::empty({M}, opts) : at::Tensor();
+  auto st = stream();
+  if (M == 0) return {y, h, rstd, mean};
+#define ARGS                                                                                       \
+  (const bf16*)x.data_ptr(), has_res ? (const bf16*)residual->data_ptr() : nullptr,                \
+      (const bf16*)w.data_ptr(), is_ln ? (const bf16*)b->data_ptr() : nullptr, (bf16*)y.data_ptr(), \
+      has_res ? (bf16*)h.data_ptr() : nullptr, rstd.data_ptr<float>(),                             \
+      is_ln ? mean.data_ptr<float>() : nullptr, M, D, (float)eps
+  const int nv = D / 8;
+  if (nv <= 64) NORM_FWD_DISPATCH(64, 1);
+  else if (nv <= 128) NORM_FWD_DISPATCH(64, 2);
+  else if (nv <= 256) NORM_FWD_DISPATCH(256, 1);
+  else if (nv <= 512) NORM_FWD_DISPATCH(256, 2);
+  else if (nv <= 1024) NORM_FWD_DISPATCH(256, 4);
+  else NORM_FWD_DISPATCH(256, 8);
+#undef ARGS
+  SPA_LAUNCH_CHECK();
+  return {y, h, rstd, mean};
+}
+
+#define NORM_BWD_DISPATCH(NT, MAXV)                                                        \
+  do {                                                                                     \
+    constexpr int RPB = 256 / NT;                                                          \
+    nblk = std::min(cdiv(M, RPB), 1024);                                                   \
+    nparts = nblk * RPB;                                                                   \
+    dw_part = at::empty({nparts, D}, opts);                                                \
+    if (is_ln) db_part = at::empty({nparts, D}, opts);                                     \
+    if (is_ln) {                                                                           \
+      if (has_dres) norm_bwd_kernel<NT, MAXV, true, true><<<nblk, 256, 0, st>>>(ARGS);     \
+      else norm_bwd_kernel<NT, MAXV, true, false><<<nblk, 256, 0, st>>>(ARGS);             \
+    } else {                                                                               \
+      if (has_dres) norm_bwd_kernel<NT, MAXV, false, true><<<nblk, 256, 0, st>>>(ARGS);    \
+      else norm_bwd_kernel<NT, MAXV, false, false><<<nblk, 256, 0, st>>>(ARGS);            \
+    }                                                                                      \
+  } while (0)
+
+// Returns (dx, dw, db_or_empty). dres (optional) is added into dx (gradient flowing
+// along the residual stream past the fused add).
+std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w,
+                                 const at::Tensor& rstd, const c10::optional<at::Tensor>& mean,
+                                 const c10::optional<at::Tensor>& dres) {
+  SPA_CHECK_BF16(dy); SPA_CHECK_BF16(h); SPA_CHECK_CONTIG(dy); SPA_CHECK_CONTIG(h);
+  const bool is_ln = mean.has_value();
+  const bool has_dres = dres.has_value();
+  const int D = h.size(-1);
+  const int M = h.numel() / D;
+  DeviceGuard g(h.device());
+  auto dx = at::empty_like(h);
+  auto opts = h.options().dtype(at::kFloat);
+  auto st = stream();
+  at::Tensor dw_part, db_part;
+  int nblk = 0, nparts = 0;
+  if (has_dres) { SPA_CHECK_BF16(*dres); SPA_CHECK_CONTIG(*dres); }
+  auto dw = at::empty({D}, w.options());
+  auto db = is_ln ? at::empty({D}, w.options()) : at::Tensor();
+  if (M == 0) { dw.zero_(); if (is_ln) db.zero_(); return {dx, dw, db}; }
+#define ARGS                                                                                \
+  (const bf16*)dy.data_ptr(), (const bf16*)h.data_ptr(), (const bf16*)w.data_ptr(),         \
+      rstd.data_ptr<float>(), is_ln ? mean->data_ptr<float>() : nullptr,                    \
+      has_dres ? (const bf16*)dres->data_ptr() : nullptr, (bf16*)dx.data_ptr(),             \
+      dw_part.data_ptr<float>(), is_ln ? db_part.data_ptr<float>() : nullptr, M, D
+  const int nv = D / 8;
+  if (nv <= 64) NORM_BWD_DISPATCH(64, 1);
+  else if (nv <= 128) NORM_BWD_DISPATCH(64, 2);
+  else if (nv <= 256) NORM_BWD_DISPATCH(256, 1);
+  else if (nv <= 512) NORM_BWD_DISPATCH(256, 2);
+  else if (nv <= 1024) NORM_BWD_DISPATCH(256, 4);
+  else NORM_BWD_DISPATCH(256, 8);
+#undef ARGS
+  SPA_LAUNCH_CHECK();
+  colsum_kernel<bf16><<<cdiv(D, 64), 256, 0, st>>>(dw_part.data_ptr<float>(), (bf16*)dw.data_ptr(), nparts, D);
+  if (is_ln) colsum_kernel<bf16><<<cdiv(D, 64), 256, 0, st>>>(db_part.data_ptr<float>(), (bf16*)db.data_ptr(), nparts, D);
+  SPA_LAUNCH_CHECK();
+  return {dx, dw, db};
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("norm_fwd(Tensor x, Tensor? residual, Tensor w, Tensor? b, float eps) -> Tensor[]");
+  m.def("norm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? mean, Tensor? dres) -> Tensor[]");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("norm_fwd", &spa::norm_fwd);
+  m.impl("norm_bwd", &spa::norm_bwd);
+}

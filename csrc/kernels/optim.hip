@@ -1,0 +1,210 @@
+// Fused optimizer kernels over FLAT parameter buffers.
+//
+// Every trainable tensor of a model is a view into one contiguous buffer per
+// param group (see solvingpapers_amd/utils/flat.py), so one launch updates all
+// 8B parameters of LLaMA3-8B with no multi-tensor pointer lists; DP gradient
+// buckets and ZeRO-1 shards are plain contiguous slices of the same buffers.
+//
+// Reference optimizers: AdamW (gpt/gpt-jax.ipynb:600 optax.adamw; gemma/gemma.ipynb:517;
+// deepseekv3/deepseekv3.ipynb:2350-2356 betas (0.9,0.95), wd 0.1, eps 1e-8), Adam
+// (vision transformer/ViT.ipynb:287, autoencoder, knowledge distillation/kd.py:92,109),
+// plain SGD (llama3/LLaMA-jax.ipynb:996-1000). Grad-norm clipping
+// (deepseekv3/deepseekv3.ipynb:2434-2439) is applied via a device-resident
+// coefficient so clipping never syncs the host.
+//
+// Math matches torch.optim.AdamW: p *= 1 - lr*wd; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).
+#include "spa_common.h"
+
+namespace spa {
+
+template <typename PT, typename GT, bool MASTER>
+__global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* __restrict__ master,
+                                                    const GT* __restrict__ g, float* __restrict__ m,
+                                                    float* __restrict__ v, long n, float lr, float b1, float b2,
+                                                    float eps, float wd, float inv_bc1, float inv_sqrt_bc2,
+                                                    const float* __restrict__ coef_ptr, int adam_l2) {
+  const float coef = coef_ptr ? *coef_ptr : 1.f;
+  const long nv = n / 8;
+  const long stride = (long)gridDim.x * 256;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nv + (n % 8 ? 1 : 0); i += stride) {
+    const long base = i * 8;
+    float pv[8], gv[8], mv[8], vv[8];
+    const bool full = base + 8 <= n;
+    if (full) {
+      if constexpr (MASTER) load8(master + base, pv); else load8(p + base, pv);
+      load8(g + base, gv);
+      load8(m + base, mv);
+      load8(v + base, vv);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const long j = base + k;
+        pv[k] = j < n ? (MASTER ? master[j] : (float)p[j]) : 0.f;
+        gv[k] = j < n ? (float)g[j] : 0.f;
+        mv[k] = j < n ? m[j] : 0.f;
+        vv[k] = j < n ? v[j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float gr = gv[k] * coef;
+      if (adam_l2) gr += wd * pv[k];  // classic Adam weight decay (L2 in the gradient)
+      mv[k] = b1 * mv[k] + (1.f - b1) * gr;
+      vv[k] = b2 * vv[k] + (1.f - b2) * gr * gr;
+      const float denom = sqrtf(vv[k]) * inv_sqrt_bc2 + eps;
+      float pp = pv[k];
+      if (!adam_l2) pp *= (1.f - lr * wd);
+      pv[k] = pp - lr * inv_bc1 * mv[k] / denom;
+    }
+    if (full) {
+      if constexpr (MASTER) { store8(master + base, pv); store8(p + base, pv); }
+      else store8(p + base, pv);
+      store8(m + base, mv);
+      store8(v + base, vv);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const long j = base + k;
+        if (j < n) {
+          if constexpr (MASTER) master[j] = pv[k];
+          p[j] = (PT)pv[k];
+          m[j] = mv[k];
+          v[j] = vv[k];
+        }
+      }
+    }
+  }
+}
+
+template <typename PT, typename GT, bool MASTER>
+__global__ __launch_bounds__(256) void sgd_kernel(PT* __restrict__ p, float* __restrict__ master,
+                                                  const GT* __restrict__ g, float* __restrict__ buf, long n, float lr,
+                                                  float momentum, float wd, const float* __restrict__ coef_ptr) {
+  const float coef = coef_ptr ? *coef_ptr : 1.f;
+  for (long j = blockIdx.x * 256L + threadIdx.x; j < n; j += (long)gridDim.x * 256) {
+    float pv = MASTER ? master[j] : (float)p[j];
+    float gr = (float)g[j] * coef + wd * pv;
+    if (buf) { gr = momentum * buf[j] + gr; buf[j] = gr; }
+    pv -= lr * gr;
+    if constexpr (MASTER) master[j] = pv;
+    p[j] = (PT)pv;
+  }
+}
+
+// partial sums of squares; one partial per block
+template <typename GT>
+__global__ __launch_bounds__(256) void sqsum_kernel(const GT* __restrict__ g, long n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const long nv = n / 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
+    float v[8];
+    load8(g + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k] * v[k];
+  }
+  for (long j = nv * 8 + blockIdx.x * 256L + threadIdx.x; j < n; j += (long)gridDim.x * 256) {
+    const float x = (float)g[j];
+    acc += x * x;
+  }
+  acc = block_sum<256>(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ part, int np,
+                                                           float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+  acc = block_sum<256>(acc, red);
+  if (threadIdx.x == 0) out[0] = acc;
+}
+
+static int opt_grid(long n) { return (int)std::max<long>(1, std::min<long>((n / 8 + 255) / 256 + 1, 4096)); }
+
+void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g, const at::Tensor& m,
+            const at::Tensor& v, double lr, double b1, double b2, double eps, double wd, int64_t step,
+            const c10::optional<at::Tensor>& coef, bool adam_l2) {
+  SPA_CHECK_CUDA(p);
+  for (auto* t : {&p, &g, &m, &v}) TORCH_CHECK(t->is_contiguous(), "adamw: flat contiguous buffers required");
+  const long n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n);
+  TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat);
+  if (master) TORCH_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous());
+  if (coef) TORCH_CHECK(coef->scalar_type() == at::kFloat && coef->numel() == 1);
+  if (n == 0) return;
+  DeviceGuard gd(p.device());
+  auto st = stream();
+  const float inv_bc1 = 1.f / (1.f - std::pow((float)b1, (float)step));
+  const float inv_sqrt_bc2 = 1.f / std::sqrt(1.f - std::pow((float)b2, (float)step));
+  const float* cp = coef ? coef->data_ptr<float>() : nullptr;
+#define AL(PT, GT, MS)                                                                                           \
+  adamw_kernel<PT, GT, MS><<<opt_grid(n), 256, 0, st>>>(                                                         \
+      (PT*)p.data_ptr(), MS ? master->data_ptr<float>() : nullptr, (const GT*)g.data_ptr(), m.data_ptr<float>(), \
+      v.data_ptr<float>(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cp,  \
+      adam_l2 ? 1 : 0)
+  const bool pb = p.scalar_type() == at::kBFloat16, gb = g.scalar_type() == at::kBFloat16;
+  if (pb && gb) { TORCH_CHECK(master.has_value(), "bf16 params need an fp32 master"); AL(bf16, bf16, true); }
+  else if (pb && !gb) { TORCH_CHECK(master.has_value(), "bf16 params need an fp32 master"); AL(bf16, float, true); }
+  else if (!pb && gb) { if (master) AL(float, bf16, true); else AL(float, bf16, false); }
+  else { if (master) AL(float, float, true); else AL(float, float, false); }
+#undef AL
+  SPA_LAUNCH_CHECK();
+}
+
+void sgd_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g,
+          const c10::optional<at::Tensor>& buf, double lr, double momentum, double wd,
+          const c10::optional<at::Tensor>& coef) {
+  const long n = p.numel();
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && g.numel() == n);
+  if (n == 0) return;
+  DeviceGuard gd(p.device());
+  auto st = stream();
+  const float* cp = coef ? coef->data_ptr<float>() : nullptr;
+  float* bp = buf ? buf->data_ptr<float>() : nullptr;
+  const int grid = (int)std::min<long>((n + 255) / 256, 8192);
+#define SL(PT, GT, MS)                                                                                          \
+  sgd_kernel<PT, GT, MS><<<grid, 256, 0, st>>>((PT*)p.data_ptr(), MS ? master->data_ptr<float>() : nullptr,     \
+                                               (const GT*)g.data_ptr(), bp, n, (float)lr, (float)momentum,       \
+                                               (float)wd, cp)
+  const bool pb = p.scalar_type() == at::kBFloat16, gb = g.scalar_type() == at::kBFloat16;
+  if (pb) { TORCH_CHECK(master.has_value()); if (gb) SL(bf16, bf16, true); else SL(bf16, float, true); }
+  else { if (gb) { if (master) SL(float, bf16, true); else SL(float, bf16, false); }
+         else { if (master) SL(float, float, true); else SL(float, float, false); } }
+#undef SL
+  SPA_LAUNCH_CHECK();
+}
+
+// Sum of squares of a flat buffer -> fp32 [1] tensor (deterministic two-stage reduction).
+at::Tensor sqsum(const at::Tensor& g) {
+  SPA_CHECK_CUDA(g); TORCH_CHECK(g.is_contiguous());
+  const long n = g.numel();
+  DeviceGuard gd(g.device());
+  auto out = at::zeros({1}, g.options().dtype(at::kFloat));
+  if (n == 0) return out;
+  const int nb = (int)std::max<long>(1, std::min<long>((n / 8 + 255) / 256, 2048));
+  auto part = at::empty({nb}, g.options().dtype(at::kFloat));
+  auto st = stream();
+  if (g.scalar_type() == at::kBFloat16)
+    sqsum_kernel<bf16><<<nb, 256, 0, st>>>((const bf16*)g.data_ptr(), n, part.data_ptr<float>());
+  else if (g.scalar_type() == at::kFloat)
+    sqsum_kernel<float><<<nb, 256, 0, st>>>(g.data_ptr<float>(), n, part.data_ptr<float>());
+  else TORCH_CHECK(false, "sqsum: bf16/fp32 only");
+  sum_partials_kernel<<<1, 256, 0, st>>>(part.data_ptr<float>(), nb, out.data_ptr<float>());
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("adamw_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!) m, Tensor(d!) v, float lr, float b1, "
+        "float b2, float eps, float wd, int step, Tensor? coef, bool adam_l2) -> ()");
+  m.def("sgd_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!)? buf, float lr, float momentum, float wd, "
+        "Tensor? coef) -> ()");
+  m.def("sqsum(Tensor g) -> Tensor");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("adamw_", &spa::adamw_);
+  m.impl("sgd_", &spa::sgd_);
+  m.impl("sqsum", &spa::sqsum);
+}

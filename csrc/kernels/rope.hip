@@ -1,0 +1,103 @@
+// Rotary position embedding, applied in place on the q/k heads of a fused
+// [B, T, NH, hd] projection buffer (NH = H + 2*Hkv for a packed qkv), so no
+// split/transpose copy is ever made. Backward = the same kernel with the
+// inverse rotation (sin negated) on the incoming gradient.
+//
+// Reference: llama3/LLaMA-jax.ipynb:563-601 (precompute_freqs_cis / apply_rotary_emb:
+// interleaved pairs (x[2i], x[2i+1]) rotated by t*theta^(-2i/hd)). A non-interleaved
+// "rotate_half" layout is also provided (pairs (x[i], x[i+hd/2])).
+//
+// Layout: each thread owns 8 contiguous bf16 of one head row (16-byte load/store);
+// cos/sin come from an fp32 table [Tmax, hd/2] (L2/LLC resident).
+#include "spa_common.h"
+
+namespace spa {
+
+template <bool INTERLEAVED>
+__global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ x, const float* __restrict__ cosT,
+                                                   const float* __restrict__ sinT, const int* __restrict__ pos,
+                                                   long sb, long st, long sh, int B, int T, int nrot, int hd,
+                                                   int pos_off, float sign) {
+  const int vpr = hd / 8;                 // vectors per head row
+  const long total = (long)B * T * nrot * vpr;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int v = i % vpr;
+    long r = i / vpr;
+    const int hh = r % nrot;
+    r /= nrot;
+    const int t = r % T;
+    const int b = r / T;
+    const int ps = pos ? pos[b * T + t] : t + pos_off;
+    bf16* p = x + b * sb + t * st + hh * sh;
+    const float* c = cosT + (long)ps * (hd / 2);
+    const float* s = sinT + (long)ps * (hd / 2);
+    if constexpr (INTERLEAVED) {
+      float a[8];
+      load8(p + v * 8, a);
+      const f32x4 cv = *reinterpret_cast<const f32x4*>(c + v * 4);
+      const f32x4 sv = *reinterpret_cast<const f32x4*>(s + v * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x0 = a[2 * k], x1 = a[2 * k + 1];
+        const float cs = cv[k], sn = sign * sv[k];
+        a[2 * k] = x0 * cs - x1 * sn;
+        a[2 * k + 1] = x0 * sn + x1 * cs;
+      }
+      store8(p + v * 8, a);
+    } else {
+      // rotate_half: thread v < vpr/2 handles elements [8v, 8v+8) and their partners at +hd/2
+      if (v >= vpr / 2) continue;
+      float a[8], bq[8];
+      load8(p + v * 8, a);
+      load8(p + hd / 2 + v * 8, bq);
+      float cv[8], sv[8];
+      load8(c + v * 8, cv);
+      load8(s + v * 8, sv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float x0 = a[k], x1 = bq[k], sn = sign * sv[k];
+        a[k] = x0 * cv[k] - x1 * sn;
+        bq[k] = x0 * sn + x1 * cv[k];
+      }
+      store8(p + v * 8, a);
+      store8(p + hd / 2 + v * 8, bq);
+    }
+  }
+}
+
+// x: [B, T, NH, hd] view (hd contiguous), rotates heads [0, nrot). In place.
+void rope_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const c10::optional<at::Tensor>& pos,
+           int64_t nrot, int64_t pos_off, bool interleaved, bool inverse) {
+  SPA_CHECK_CUDA(x); SPA_CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "rope: x must be [B,T,NH,hd] with contiguous hd");
+  const int B = x.size(0), T = x.size(1), hd = x.size(3);
+  TORCH_CHECK(hd % 16 == 0, "rope: hd must be a multiple of 16");
+  TORCH_CHECK(nrot <= x.size(2));
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous() && cos.size(1) == hd / 2);
+  TORCH_CHECK(x.stride(1) % 8 == 0 && x.stride(2) % 8 == 0 && x.stride(0) % 8 == 0);
+  if (pos) { TORCH_CHECK(pos->scalar_type() == at::kInt && pos->is_contiguous() && pos->numel() == (int64_t)B * T); }
+  else { TORCH_CHECK(pos_off + T <= cos.size(0), "rope: table too short"); }
+  DeviceGuard g(x.device());
+  const long total = (long)B * T * nrot * (hd / 8);
+  if (total == 0) return;
+  const int grid = (int)std::min<long>((total + 255) / 256, 4096);
+  auto st = stream();
+  const float sign = inverse ? -1.f : 1.f;
+  if (interleaved)
+    rope_kernel<true><<<grid, 256, 0, st>>>((bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                                            pos ? pos->data_ptr<int>() : nullptr, x.stride(0), x.stride(1),
+                                            x.stride(2), B, T, (int)nrot, hd, (int)pos_off, sign);
+  else
+    rope_kernel<false><<<grid, 256, 0, st>>>((bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                                             pos ? pos->data_ptr<int>() : nullptr, x.stride(0), x.stride(1),
+                                             x.stride(2), B, T, (int)nrot, hd, (int)pos_off, sign);
+  SPA_LAUNCH_CHECK();
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int nrot, int pos_off, bool interleaved, "
+        "bool inverse) -> ()");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("rope_", &spa::rope_); }

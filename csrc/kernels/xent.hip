@@ -1,0 +1,138 @@
+// Softmax cross-entropy over a vocabulary row, with the gradient written IN PLACE
+// over the logits during the forward pass (the logits are dead after the loss),
+// so a [T, V] = 8192 x 128256 LM head never holds a second V-wide buffer.
+//
+// Reference sites: gpt/gpt-jax.ipynb:503 (optax integer-label CE),
+// llama3/LLaMA-jax.ipynb:961-967 (-mean(log_softmax gathered)),
+// gemma/gemma.ipynb:534,564 and deepseekv3/deepseekv3.ipynb:2417-2421 (F.cross_entropy).
+//
+// One 256-thread block per row: pass 1 online (max, sum-exp) with 16-byte loads,
+// block-combine, loss = lse - x[target]; pass 2 (optional) re-reads the row and
+// writes (softmax - onehot) * scale, where scale lives on the device (1/num_valid)
+// so there is no host sync. ignore_index rows get loss 0 and zero gradient.
+#include "spa_common.h"
+
+namespace spa {
+
+template <typename T, bool VEC, bool GRAD>
+__global__ __launch_bounds__(256) void xent_kernel(T* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                   float* __restrict__ loss, float* __restrict__ lse_out,
+                                                   const float* __restrict__ scale_ptr, int V, long ld,
+                                                   int64_t ignore_index, float smoothing) {
+  __shared__ float red_m[4], red_s[4], red_x[4];
+  const int row = blockIdx.x;
+  T* x = logits + (long)row * ld;
+  const int64_t y = tgt[row];
+  float m = -INFINITY, s = 0.f, sx = 0.f;  // sx = sum of logits (label smoothing)
+  auto upd = [&](float v) {
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+    else s += __expf(v - m);
+    sx += v;
+  };
+  if constexpr (VEC) {
+    const int nv = V / 8;
+    for (int i = threadIdx.x; i < nv; i += 256) {
+      float v[8];
+      load8(x + i * 8, v);
+      float lm = v[0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) lm = fmaxf(lm, v[k]);
+      const float nm = fmaxf(m, lm);
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { acc += __expf(v[k] - nm); sx += v[k]; }
+      s = s * __expf(m - nm) + acc;
+      m = nm;
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += 256) upd((float)x[i]);
+  }
+  // combine (m, s) across the block
+  float wm = wave_max(m);
+  float ws = (m == -INFINITY) ? 0.f : s * __expf(m - wm);  // idle threads (V < 8*256) hold m=-inf
+  ws = wave_sum(ws);
+  float wx = wave_sum(sx);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) { red_m[w] = wm; red_s[w] = ws; red_x[w] = wx; }
+  __syncthreads();
+  float M = fmaxf(fmaxf(red_m[0], red_m[1]), fmaxf(red_m[2], red_m[3]));
+  float S = 0.f, SX = red_x[0] + red_x[1] + red_x[2] + red_x[3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) S += (red_m[i] == -INFINITY) ? 0.f : red_s[i] * __expf(red_m[i] - M);
+  const float lse = M + __logf(S);
+  const bool valid = y != ignore_index;
+  if (threadIdx.x == 0) {
+    float li = 0.f;
+    if (valid) {
+      const float xt = (float)x[y];
+      li = (1.f - smoothing) * (lse - xt) + smoothing * (lse - SX / V);
+    }
+    loss[row] = li;
+    if (lse_out) lse_out[row] = lse;
+  }
+  if constexpr (GRAD) {
+    __syncthreads();  // thread 0 has read x[y] before anyone overwrites it
+    const float sc = valid ? (scale_ptr ? *scale_ptr : 1.f) : 0.f;
+    const float onv = 1.f - smoothing, off = smoothing / V;
+    if constexpr (VEC) {
+      const int nv = V / 8;
+      for (int i = threadIdx.x; i < nv; i += 256) {
+        float v[8];
+        load8(x + i * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int c = i * 8 + k;
+          v[k] = sc * (__expf(v[k] - lse) - off - (c == y ? onv : 0.f));
+        }
+        store8(x + i * 8, v);
+      }
+    } else {
+      for (int i = threadIdx.x; i < V; i += 256) {
+        const float v = (float)x[i];
+        x[i] = (T)(sc * (__expf(v - lse) - off - (i == y ? onv : 0.f)));
+      }
+    }
+  }
+}
+
+// logits [N, V] (row stride ld, last dim contiguous). Returns (loss[N], lse[N]).
+// If write_grad, logits is overwritten with d(sum_i scale*loss_i)/dlogits.
+std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index,
+                                 double smoothing, bool write_grad, const c10::optional<at::Tensor>& scale) {
+  SPA_CHECK_CUDA(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: logits must be [N, V] with contiguous V");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous() && target.numel() == logits.size(0));
+  const int N = logits.size(0), V = logits.size(1);
+  const long ld = logits.stride(0);
+  DeviceGuard g(logits.device());
+  auto opts = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({N}, opts);
+  auto lse = at::empty({N}, opts);
+  if (N == 0) return {loss, lse};
+  if (scale) TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1);
+  const bool vec = (V % 8 == 0) && (ld % 8 == 0) && ((uintptr_t)logits.data_ptr() % 16 == 0);
+  auto st = stream();
+  const float* sp = scale ? scale->data_ptr<float>() : nullptr;
+#define XL(T, VEC, GR)                                                                                     \
+  xent_kernel<T, VEC, GR><<<N, 256, 0, st>>>((T*)logits.data_ptr(), target.data_ptr<int64_t>(),            \
+                                             loss.data_ptr<float>(), lse.data_ptr<float>(), sp, V, ld,      \
+                                             ignore_index, (float)smoothing)
+#define XL2(T)                                 \
+  if (vec) { if (write_grad) XL(T, true, true); else XL(T, true, false); } \
+  else { if (write_grad) XL(T, false, true); else XL(T, false, false); }
+  if (logits.scalar_type() == at::kBFloat16) { XL2(bf16) }
+  else if (logits.scalar_type() == at::kFloat) { XL2(float) }
+  else TORCH_CHECK(false, "xent: bf16/fp32 only");
+#undef XL2
+#undef XL
+  SPA_LAUNCH_CHECK();
+  return {loss, lse};
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("xent_fwd(Tensor(a!) logits, Tensor target, int ignore_index, float smoothing, bool write_grad, "
+        "Tensor? scale) -> Tensor[]");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("xent_fwd", &spa::xent_fwd); }

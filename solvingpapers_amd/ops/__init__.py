@@ -1,0 +1,16 @@
+"""Hot-path ops: each is a hand-written gfx950 HIP kernel (csrc/kernels/*.hip)
+registered as ``torch.ops.spa.*``, with a pure-PyTorch oracle for CPU tensors."""
+from . import _ext, reference
+from .activation import act, elu, geglu, gelu, glu, leaky_relu, prelu, relu, sigmoid, silu, swiglu
+from .attention import attention_packed, flash_attention
+from .embedding import embedding
+from .linear import Linear, linear
+from .norm import layer_norm, rms_norm
+from .rope import apply_rope, rope_packed_
+from .xent import cross_entropy, linear_cross_entropy, per_row_loss
+
+__all__ = [
+    "act", "elu", "geglu", "gelu", "glu", "leaky_relu", "prelu", "relu", "sigmoid", "silu", "swiglu",
+    "attention_packed", "flash_attention", "embedding", "Linear", "linear", "layer_norm", "rms_norm",
+    "apply_rope", "rope_packed_", "cross_entropy", "linear_cross_entropy", "per_row_loss", "reference",
+]

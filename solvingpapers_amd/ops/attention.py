@@ -1,0 +1,110 @@
+"""Flash attention (HIP: csrc/kernels/attention.hip) with GQA/MQA head mapping.
+
+Tensors are [B, T, H, hd] views (hd contiguous); the kernels take (b, t, h)
+strides, so q/k/v may be slices of one packed qkv projection output and the
+gradients can be written into slices of one dqkv buffer (``attention_packed``).
+Head dims 64/128/256 run the MFMA flash kernel; other head dims fall back to a
+materialised GEMM + softmax path (used only by reference-parity presets such
+as Gemma-ref's 768-wide heads).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _ext, reference
+
+FLASH_HD = (64, 128, 256)
+
+
+def _flash_ok(q):
+    return q.is_cuda and q.dtype == torch.bfloat16 and (q.dim() == 3 or q.shape[-1] in FLASH_HD)
+
+
+class _FlashFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        dq = torch.empty_like(q, memory_format=torch.contiguous_format)
+        dk = torch.empty_like(k, memory_format=torch.contiguous_format)
+        dv = torch.empty_like(v, memory_format=torch.contiguous_format)
+        _ext.ops().attn_bwd(dout.contiguous(), q, k, v, out, lse, dq, dk, dv, ctx.scale, ctx.causal)
+        return dq, dk, dv, None, None
+
+
+class _PackedFn(torch.autograd.Function):
+    """Attention reading q/k/v from one [B, T, (H+2Hkv)*hd] buffer and writing the
+    three gradients into one dqkv buffer of the same layout (no cat/split).
+    Output is [B, T, H*hd] (a fresh tensor, ready for the output projection)."""
+
+    @staticmethod
+    def forward(ctx, qkv, H, Hkv, hd, causal, scale):
+        B, T = qkv.shape[0], qkv.shape[1]
+        x4 = qkv.view(B, T, H + 2 * Hkv, hd)
+        q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
+        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.H, ctx.Hkv, ctx.hd, ctx.causal, ctx.scale = H, Hkv, hd, causal, scale
+        return torch.ops.aten._unsafe_view(out, (B, T, H * hd))
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        H, Hkv, hd = ctx.H, ctx.Hkv, ctx.hd
+        B, T = qkv.shape[0], qkv.shape[1]
+        dqkv = torch.empty_like(qkv)
+        x4 = qkv.view(B, T, H + 2 * Hkv, hd)
+        d4 = dqkv.view(B, T, H + 2 * Hkv, hd)
+        _ext.ops().attn_bwd(dout.contiguous().view(B, T, H, hd), x4[:, :, :H], x4[:, :, H:H + Hkv],
+                            x4[:, :, H + Hkv:], out, lse, d4[:, :, :H], d4[:, :, H:H + Hkv], d4[:, :, H + Hkv:],
+                            ctx.scale, ctx.causal)
+        return dqkv, None, None, None, None, None
+
+
+def _materialised(q, k, v, causal, scale):
+    """GEMM + softmax path for unsupported head dims (autograd through torch ops)."""
+    B, Tq, H, hd = q.shape
+    Tk, Hkv = k.shape[1], k.shape[2]
+    rep = H // Hkv
+    qh = q.transpose(1, 2)
+    kh = k.transpose(1, 2).repeat_interleave(rep, dim=1)
+    vh = v.transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = torch.matmul(qh, kh.transpose(-1, -2)).float() * scale
+    if causal:
+        i = torch.arange(Tq, device=q.device)[:, None]
+        j = torch.arange(Tk, device=q.device)[None, :]
+        s = s.masked_fill(j > i + (Tk - Tq), float("-inf"))
+    p = torch.softmax(s, dim=-1).to(q.dtype)
+    return torch.matmul(p, vh).transpose(1, 2)
+
+
+def flash_attention(q, k, v, causal=True, scale=None):
+    """softmax(q k^T * scale [+causal]) v.  q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd]."""
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if _flash_ok(q):
+        return _FlashFn.apply(q, k, v, causal, scale)
+    if q.is_cuda:
+        return _materialised(q, k, v, causal, scale)
+    if torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad):
+        return _materialised(q, k, v, causal, scale)
+    return reference.attention(q, k, v, causal, scale)[0]
+
+
+def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None):
+    """qkv [B, T, H+2Hkv, hd] (or [B, T, (H+2Hkv)*hd] with head_dim) -> out [B, T, H*hd]."""
+    hd = head_dim if head_dim is not None else qkv.shape[-1]
+    B, T = qkv.shape[0], qkv.shape[1]
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
+    if _flash_ok(qkv) and hd in FLASH_HD:
+        return _PackedFn.apply(qkv, H, Hkv, hd, causal, scale)
+    x4 = qkv.view(B, T, H + 2 * Hkv, hd)
+    q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
+    return flash_attention(q, k, v, causal, scale).reshape(B, T, H * hd)

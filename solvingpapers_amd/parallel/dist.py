@@ -1,0 +1,93 @@
+"""Process-group bootstrap: one process per GPU, torch.distributed over RCCL.
+
+On ROCm the ``"nccl"`` backend IS RCCL (xGMI point-to-point links between the
+8 MI355X of a node). CPU tests use ``"gloo"`` with the same code paths.
+Launch: ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...``.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+
+_INFO = DistInfo()
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> DistInfo:
+    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    global _INFO
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cuda = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if cuda else "gloo"
+    if cuda:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl" and cuda:
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    _INFO = DistInfo(rank, world, local, backend if world > 1 else "none", device)
+    return _INFO
+
+
+def info() -> DistInfo:
+    return _INFO
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def barrier(group=None):
+    if is_dist():
+        if _INFO.backend == "nccl":
+            dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier(group=group)
+
+
+def all_reduce_max(x: float) -> float:
+    if not is_dist():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=_INFO.device if _INFO.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_mean(t: torch.Tensor, group=None) -> torch.Tensor:
+    if not is_dist():
+        return t
+    t = t.clone()
+    dist.all_reduce(t, group=group)
+    return t / dist.get_world_size(group)
+
+
+def cleanup():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,155 @@
+"""Optimizers over :class:`~solvingpapers_amd.utils.flat.FlatParams`.
+
+AdamW/Adam/SGD with bf16 params + fp32 master copy + fp32 moments, grad-norm
+clipping via a device-resident coefficient (no host sync), optional ZeRO-1
+(each rank updates only its shard of every bucket; see parallel/data_parallel.py).
+Reference optimizers: gpt/gpt-jax.ipynb:600 (optax.adamw 3e-4, wd 0.01),
+deepseekv3/deepseekv3.ipynb:2350-2356 (AdamW betas .9/.95 wd .1 eps 1e-8, clip 1.0),
+llama3/LLaMA-jax.ipynb:993-1001 (plain SGD 3e-4).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import torch
+
+from ..ops import optim_kernels as K
+from ..utils.flat import FlatParams
+
+
+class FlatOptimizer:
+    def __init__(self, flat: FlatParams, lr: float, weight_decay: float = 0.0, max_grad_norm: Optional[float] = None,
+                 shard: Optional[Tuple[List[Tuple[int, int]], object]] = None):
+        self.flat = flat
+        self.lr = lr
+        self.weight_decay = weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.step_count = 0
+        # ranges of the flat buffer this optimizer owns (all, or this rank's ZeRO shard)
+        self.ranges = shard[0] if shard else [(0, flat.numel)]
+        self.norm_group = shard[1] if shard else None
+        self.use_master = flat.param_dtype != torch.float32
+        self.last_grad_norm: Optional[torch.Tensor] = None
+        # owned element count and per-range state offsets
+        self.state_off = []
+        o = 0
+        for a, b in self.ranges:
+            self.state_off.append(o)
+            o += b - a
+        self.state_numel = o
+        self.master = None
+        if self.use_master:
+            self.master = torch.empty(o, dtype=torch.float32, device=flat.device)
+            for (a, b), so in zip(self.ranges, self.state_off):
+                self.master[so:so + b - a].copy_(flat.param[a:b].float())
+
+    def _segments(self):
+        """(flat_a, flat_b, state_a, decay) pieces = owned ranges x decay segments."""
+        out = []
+        for (a, b), so in zip(self.ranges, self.state_off):
+            for sa, sb, dec in self.flat.decay_segments:
+                lo, hi = max(a, sa), min(b, sb)
+                if lo < hi:
+                    out.append((lo, hi, so + lo - a, dec))
+        return out
+
+    def grad_norm(self) -> torch.Tensor:
+        """Global L2 norm of the (already reduced) gradient, on the device."""
+        tot = None
+        for a, b in self.ranges:
+            s = K.sqsum(self.flat.grad[a:b])
+            tot = s if tot is None else tot + s
+        if self.norm_group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(tot, group=self.norm_group)
+        return tot.sqrt()
+
+    def clip_coef(self):
+        if self.max_grad_norm is None:
+            self.last_grad_norm = None
+            return None
+        n = self.grad_norm()
+        self.last_grad_norm = n
+        return torch.clamp(self.max_grad_norm / (n + 1e-6), max=1.0).float().reshape(1)
+
+    def zero_grad(self):
+        from ..utils.grad import next_generation
+        next_generation()
+
+
+class FlatAdamW(FlatOptimizer):
+    def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=None,
+                 adam_l2=False, shard=None):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, shard)
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.adam_l2 = adam_l2
+        self.m = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device)
+        self.v = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device)
+
+    @torch.no_grad()
+    def step(self, lr: Optional[float] = None):
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        coef = self.clip_coef()
+        f = self.flat
+        for a, b, so, dec in self._segments():
+            n = b - a
+            K.adamw_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
+                     self.m[so:so + n], self.v[so:so + n], lr, self.b1, self.b2, self.eps,
+                     self.weight_decay if dec else 0.0, self.step_count, coef, self.adam_l2)
+
+    def state_dict(self):
+        return {"step": self.step_count, "m": self.m, "v": self.v, "master": self.master, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        if self.master is not None and sd.get("master") is not None:
+            self.master.copy_(sd["master"])
+
+
+def FlatAdam(flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_grad_norm=None, shard=None):
+    """torch.optim.Adam semantics (L2 weight decay folded into the gradient)."""
+    return FlatAdamW(flat, lr, betas, eps, weight_decay, max_grad_norm, adam_l2=True, shard=shard)
+
+
+class FlatSGD(FlatOptimizer):
+    def __init__(self, flat, lr=1e-3, momentum=0.0, weight_decay=0.0, max_grad_norm=None, shard=None):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, shard)
+        self.momentum = momentum
+        self.buf = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device) if momentum else None
+
+    @torch.no_grad()
+    def step(self, lr: Optional[float] = None):
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        coef = self.clip_coef()
+        f = self.flat
+        for a, b, so, dec in self._segments():
+            n = b - a
+            K.sgd_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
+                   self.buf[so:so + n] if self.buf is not None else None, lr, self.momentum,
+                   self.weight_decay if dec else 0.0, coef)
+
+    def state_dict(self):
+        return {"step": self.step_count, "buf": self.buf, "master": self.master, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        if self.buf is not None and sd.get("buf") is not None:
+            self.buf.copy_(sd["buf"])
+        if self.master is not None and sd.get("master") is not None:
+            self.master.copy_(sd["master"])
+
+
+def cosine_lr(step, max_lr, warmup, total, min_lr):
+    """deepseekv3/deepseekv3.ipynb:1976-1986: linear warmup max_lr*(s+1)/(warmup+1) -> cosine -> min_lr."""
+    if step < warmup:
+        return max_lr * (step + 1) / (warmup + 1)
+    if step > total:
+        return min_lr
+    r = (step - warmup) / max(1, total - warmup)
+    return min_lr + 0.5 * (1.0 + math.cos(math.pi * r)) * (max_lr - min_lr)

@@ -1,0 +1,224 @@
+"""HIP kernel numerics vs plain-PyTorch fp32 oracles (SURVEY.md §4.2 tier T1).
+
+Every test asserts the extension is loaded (no silent eager fallback) and runs
+the torch.ops.spa kernel against the oracle in ops/reference.py on edge shapes
+(T not a multiple of the tile, T=197 for ViT, hd 64/128/256, Hkv=1 MQA).
+"""
+import math
+
+import pytest
+import torch
+
+from solvingpapers_amd.ops import _ext, reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _need_ext():
+    assert _ext.load(), "HIP extension must load on the GPU box"
+    torch.manual_seed(0)
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("D", [64, 256, 768, 1000, 4096])
+@pytest.mark.parametrize("ln", [False, True])
+@pytest.mark.parametrize("res", [False, True])
+def test_norm_fwd_bwd(D, ln, res):
+    if D % 8:
+        pytest.skip("D%8 required")
+    from solvingpapers_amd.ops import layer_norm, rms_norm
+    M = 300
+    x = torch.randn(M, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(M, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) if res else None
+    w = (torch.rand(D, device=DEV) + 0.5).bfloat16().requires_grad_()
+    b = torch.randn(D, device=DEV).bfloat16().requires_grad_() if ln else None
+    dy = torch.randn(M, D, device=DEV, dtype=torch.bfloat16)
+    dh = torch.randn(M, D, device=DEV, dtype=torch.bfloat16) if res else None
+    out = layer_norm(x, w, b, 1e-5, residual=r) if ln else rms_norm(x, w, 1e-5, residual=r)
+    y, h = (out if res else (out, None))
+    loss = (y.float() * dy.float()).sum() + ((h.float() * dh.float()).sum() if res else 0)
+    loss.backward()
+    xs = [t.detach().float().requires_grad_() for t in (x, w)]
+    rf = r.detach().float().requires_grad_() if res else None
+    bf = b.detach().float().requires_grad_() if ln else None
+    hf = xs[0] + rf if res else xs[0]
+    if ln:
+        yf = torch.nn.functional.layer_norm(hf, (D,), xs[1], bf, 1e-5)
+    else:
+        yf = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * xs[1]
+    lf = (yf * dy.float()).sum() + ((hf * dh.float()).sum() if res else 0)
+    lf.backward()
+    assert rel(y, yf) < 1e-2
+    assert rel(x.grad, xs[0].grad) < 2e-2
+    assert rel(w.grad, xs[1].grad) < 2e-2
+    if ln:
+        assert rel(b.grad, bf.grad) < 2e-2
+    if res:
+        assert rel(r.grad, rf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("kind", ["relu", "leaky_relu", "prelu", "elu", "gelu_tanh", "gelu", "silu", "sigmoid", "tanh"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_activation(kind, dtype):
+    from solvingpapers_amd.ops import act
+    x = (torch.randn(1003, device=DEV) * 3).to(dtype).requires_grad_()
+    alpha = {"prelu": 0.3, "elu": 0.4, "leaky_relu": 0.01}.get(kind)
+    y = act(x, kind, alpha)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xf = x.detach().float().requires_grad_()
+    yf = R.act(xf, kind, alpha or 0.0)
+    (yf * g.float()).sum().backward()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(y, yf) < tol
+    assert rel(x.grad, xf.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("kind", ["silu", "gelu", "gelu_tanh"])
+def test_glu(kind):
+    from solvingpapers_amd.ops import glu
+    gu = torch.randn(64, 2 * 1536, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = glu(gu, kind)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    gf = gu.detach().float().requires_grad_()
+    yf = R.glu(gf, kind)
+    (yf * g.float()).sum().backward()
+    assert rel(y, yf) < 1e-2 and rel(gu.grad, gf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("interleaved", [True, False])
+def test_rope(interleaved):
+    from solvingpapers_amd.ops.rope import RopeCache
+    B, T, NH, hd, nrot = 2, 77, 6, 128, 4
+    x = torch.randn(B, T, NH, hd, device=DEV, dtype=torch.bfloat16)
+    cos, sin = RopeCache.get(T + 5, hd, 500000.0, x.device)
+    y = x.clone()
+    _ext.ops().rope_(y, cos, sin, None, nrot, 3, interleaved, False)
+    ref = R.rope(x[:, :, :nrot], cos, sin, 3, interleaved)
+    assert rel(y[:, :, :nrot], ref) < 1e-2
+    assert torch.equal(y[:, :, nrot:], x[:, :, nrot:])
+    _ext.ops().rope_(y, cos, sin, None, nrot, 3, interleaved, True)  # inverse
+    assert rel(y, x) < 1e-2
+
+
+@pytest.mark.parametrize("V", [65, 50257, 128256])
+def test_xent(V):
+    from solvingpapers_amd.ops import cross_entropy
+    N = 37
+    logits = (torch.randn(N, V, device=DEV) * 2).bfloat16()
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[3] = -100
+    lf = logits.float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(lf, tgt, ignore_index=-100)
+    ref.backward()
+    lg = logits.clone().requires_grad_()
+    work = lg * 1  # non-leaf so it may be overwritten in place
+    loss = cross_entropy(work, tgt)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) < 2e-2 * max(1.0, abs(ref.item()))
+    assert rel(lg.grad, lf.grad) < 2e-2
+
+
+def test_embedding():
+    from solvingpapers_amd.ops import embedding
+    V, D = 1000, 256
+    W = torch.randn(V, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    idx = torch.randint(0, V, (4, 33), device=DEV)
+    idx[0, :5] = 7  # repeated rows -> atomics on one row
+    y = embedding(W, idx)
+    assert torch.equal(y, W.detach()[idx])
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    ref = torch.zeros(V, D, device=DEV).index_add_(0, idx.reshape(-1), g.reshape(-1, D).float())
+    assert rel(W.grad, ref) < 1e-2
+
+
+def test_adamw_matches_torch():
+    from solvingpapers_amd.ops import optim_kernels as K
+    n = 10007
+    p0 = torch.randn(n, device=DEV)
+    grads = [torch.randn(n, device=DEV) for _ in range(3)]
+    tp = p0.clone().requires_grad_()
+    topt = torch.optim.AdamW([tp], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    p = p0.clone()
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    for s, g in enumerate(grads, 1):
+        tp.grad = g.clone()
+        topt.step()
+        K.adamw_(p, None, g, m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, s)
+    assert rel(p, tp.detach()) < 1e-6
+    # bf16 params + fp32 master
+    pb = p0.bfloat16()
+    master = p0.clone()
+    m.zero_(); v.zero_()
+    for s, g in enumerate(grads, 1):
+        K.adamw_(pb, master, g.bfloat16(), m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, s)
+    assert rel(master, tp.detach()) < 1e-2
+    assert abs(K.sqsum(grads[0]).item() - grads[0].pow(2).sum().item()) < 1e-2 * grads[0].pow(2).sum().item()
+
+
+ATTN_CASES = [
+    # B, Tq, Tk, H, Hkv, hd, causal
+    (2, 128, 128, 4, 4, 64, True),
+    (1, 200, 200, 8, 2, 128, True),    # GQA, ragged tail
+    (2, 197, 197, 3, 3, 64, False),    # ViT-B/16 length
+    (1, 256, 256, 4, 1, 256, True),    # MQA, Gemma head dim
+    (1, 64, 320, 4, 2, 128, True),     # Tq < Tk (chunked prefill / decode alignment)
+    (1, 1, 77, 4, 2, 128, True),       # single-token decode
+    (1, 1024, 1024, 8, 8, 128, True),
+]
+
+
+@pytest.mark.parametrize("B,Tq,Tk,H,Hkv,hd,causal", ATTN_CASES)
+def test_flash_attention(B, Tq, Tk, H, Hkv, hd, causal):
+    from solvingpapers_amd.ops import flash_attention
+    torch.manual_seed(1)
+    q = torch.randn(B, Tq, H, hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Tk, Hkv, hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Tk, Hkv, hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attention(q, k, v, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qf, kf, vf = (t.detach().float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention(qf, kf, vf, causal)
+    of.backward(do.float())
+    assert rel(o, of) < 2e-2, rel(o, of)
+    assert rel(q.grad, qf.grad) < 3e-2, rel(q.grad, qf.grad)
+    assert rel(k.grad, kf.grad) < 3e-2, rel(k.grad, kf.grad)
+    assert rel(v.grad, vf.grad) < 3e-2, rel(v.grad, vf.grad)
+
+
+def test_flash_lse_and_spike():
+    """Force the online-softmax rescale: one key spiked against one query (rule 26)."""
+    B, T, H, hd = 1, 300, 2, 128
+    q = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16) * 0.1
+    k = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16) * 0.1
+    v = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16)
+    q[0, 250, 0] = 3.0
+    k[0, 200, 0] = 3.0  # late tile with a huge score for query 250
+    out, lse = _ext.ops().attn_fwd(q, k, v, 1 / math.sqrt(hd), True)
+    of, lf = R.attention(q.float(), k.float(), v.float(), True)
+    assert rel(out, of) < 2e-2
+    assert (lse - lf).abs().max().item() < 5e-2
+
+
+def test_packed_attention_matches_split():
+    from solvingpapers_amd.ops import attention_packed, flash_attention
+    B, T, H, Hkv, hd = 2, 150, 8, 2, 128
+    qkv = torch.randn(B, T, (H + 2 * Hkv) * hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = attention_packed(qkv, H, Hkv, head_dim=hd)
+    g = torch.randn_like(o)
+    o.backward(g)
+    q2 = qkv.detach().clone().view(B, T, H + 2 * Hkv, hd).requires_grad_()
+    o2 = flash_attention(q2[:, :, :H], q2[:, :, H:H + Hkv], q2[:, :, H + Hkv:]).reshape(B, T, H * hd)
+    o2.backward(g)
+    assert torch.equal(o, o2)
+    assert rel(qkv.grad, q2.grad.reshape(B, T, -1)) < 1e-3

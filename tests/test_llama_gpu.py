@@ -1,0 +1,61 @@
+"""LLaMA3 on the GPU (HIP path) vs the same weights on the CPU fp32 oracle path."""
+import pytest
+import torch
+
+from solvingpapers_amd.models import llama3
+from solvingpapers_amd.ops import _ext
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(preset="llama3_tiny", **kw):
+    c = llama3.config(preset, **kw)
+    cpu = llama3.Llama3(c, device="cpu", dtype=torch.float32, seed=3)
+    gpu = llama3.Llama3(c, device="cuda", dtype=torch.bfloat16, seed=3)
+    with torch.no_grad():
+        for a, b in zip(cpu.parameters(), gpu.parameters()):
+            b.copy_(a)
+    return c, cpu, gpu
+
+
+def test_llama_forward_backward_matches_cpu():
+    assert _ext.load()
+    c, cpu, gpu = _pair()
+    ids = torch.randint(0, c.vocab_size, (2, 200))
+    tgt = torch.randint(0, c.vocab_size, (2, 200))
+    lc = cpu(ids, tgt)
+    lc.backward()
+    lg = gpu(ids.cuda(), tgt.cuda())
+    lg.backward()
+    assert abs(lg.item() - lc.item()) < 2e-2 * abs(lc.item())
+    for (n, a), b in zip(cpu.named_parameters(), gpu.parameters()):
+        ga, gb = a.grad.float(), b.grad.float().cpu()
+        r = ((ga - gb).norm() / ga.norm().clamp_min(1e-12)).item()
+        assert r < 6e-2, (n, r)
+
+
+def test_llama_train_step_flat_adamw_loss_drops():
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = llama3.config("llama3_tiny")
+    m = llama3.Llama3(c, device="cuda", dtype=torch.bfloat16)
+    flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
+    opt = FlatAdamW(flat, lr=2e-3, betas=(0.9, 0.95), weight_decay=0.0, max_grad_norm=1.0)
+    ids = torch.randint(0, 64, (4, 129), device="cuda")  # small alphabet -> learnable
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = m(ids[:, :-1], ids[:, 1:])
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0] - 1.0, losses
+
+
+def test_llama_generate_kv_cache_matches_full_forward():
+    c, cpu, gpu = _pair()
+    ids = torch.randint(0, c.vocab_size, (1, 9), device="cuda")
+    out = gpu.generate(ids, 6, greedy=True)
+    # greedy re-forward without cache must agree on the first generated token
+    lg = gpu(ids)[:, -1].float()
+    assert out[0, 9].item() == lg.argmax(-1).item()
