@@ -30,6 +30,7 @@
 // q/k/v/o and grads are addressed with (batch, seq, head) strides so the kernels
 // read/write a fused [B, T, H + 2*Hkv, hd] qkv buffer in place.
 #include "spa_common.h"
+#include <type_traits>
 
 namespace spa {
 
@@ -101,6 +102,40 @@ __device__ __forceinline__ bf16x8 rd_tr(const bf16* img, int rbase, int c0, int 
   const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
   return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+
+// Per-lane LDS element offsets, computed once per kernel (the swizzle term is
+// invariant under the +32-row / +16-row steps of the loops, which become
+// immediate offsets): row reads (row = lane&31, chunk = 2ks + half) and the
+// two halves of each transposed read (k-step rows 0..15, d-tile dt).
+template <int HD>
+struct LdsOff {
+  int row[HD / 16];
+  int tra[HD / 32], trb[HD / 32];
+  __device__ __forceinline__ void init(int lane) {
+    const int l32 = lane & 31, hh = lane >> 5, g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int ks = 0; ks < HD / 16; ++ks) row[ks] = l32 * HD + 8 * ((2 * ks + hh) ^ swz<HD>(l32));
+    const int ra = 4 * hh + q, rb = ra + 8;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt) {
+      const int c = 32 * dt + 16 * (g & 1) + 4 * pp;
+      const int ch = c >> 3, within = c & 7;
+      tra[dt] = ra * HD + 8 * (ch ^ swz<HD>(ra)) + within;
+      trb[dt] = rb * HD + 8 * (ch ^ swz<HD>(rb)) + within;
+    }
+  }
+};
+__device__ __forceinline__ bf16x8 ld_row(const bf16* img, int off) {
+  return *reinterpret_cast<const bf16x8*>(img + off);
+}
+__device__ __forceinline__ bf16x8 ld_tr(const bf16* img, int offa, int offb) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + offa));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + offb));
+  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
+  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <int V> using IC = std::integral_constant<int, V>;
 
 // Register-staged tile loader: ROWS x HD bf16 tile of a strided tensor -> regs -> LDS image.
 template <int HD, int ROWS, int NT>
@@ -174,12 +209,17 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk, tid); lv.load(vbase, p.svt, BN, p.Tk, tid); }
   }
   __syncthreads();
-  for (int j = 0; j < ntiles; ++j) {
+  LdsOff<HD> off;
+  off.init(lane);
+  // body(j, buffer) with the buffer a compile-time constant (loop unrolled x2) so
+  // every LDS address is a precomputed lane offset + an immediate
+  auto body = [&](const int j, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
     const int k0 = j * BN;
-    bf16* Ks = smem + (j & 1) * 2 * TILE;
-    bf16* Vs = Ks + TILE;
+    const bf16* Ks = smem + BUF * 2 * TILE;
+    const bf16* Vs = Ks + TILE;
     if (j + 1 < ntiles) {
-      bf16* Kn = smem + ((j + 1) & 1) * 2 * TILE;
+      bf16* Kn = smem + (1 - BUF) * 2 * TILE;
       lk.store(Kn, tid);
       lv.store(Kn + TILE, tid);
       if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk, tid); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk, tid); }
@@ -190,7 +230,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
       for (int t = 0; t < 2; ++t) {
         zero16(s[t]);
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[t] = mfma32(rd_row<HD>(Ks, 32 * t + lq, 2 * ks + hh), qf[ks], s[t]);
+        for (int ks = 0; ks < KS; ++ks) s[t] = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s[t]);
       }
       const bool need_mask = (k0 + BN > p.Tk) || (CAUSAL && k0 + BN - 1 > q0 + p.causal_off);
       float mx = -1e30f;
@@ -233,9 +273,13 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) o[dt] = mfma32(rd_tr<HD>(Vs, 16 * kk, 32 * dt, lane), pf[kk], o[dt]);
+        for (int kk = 0; kk < 4; ++kk) o[dt] = mfma32(ld_tr(Vs + 16 * kk * HD, off.tra[dt], off.trb[dt]), pf[kk], o[dt]);
     }
     __syncthreads();
+  };
+  for (int j = 0; j < ntiles; j += 2) {
+    body(j, IC<0>{});
+    if (j + 1 < ntiles) body(j + 1, IC<1>{});
   }
   l += __shfl_xor(l, 32, 64);
   const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -316,12 +360,15 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk, tid); lv.load(vbase, p.svt, BN, p.Tk, tid); }
   }
   __syncthreads();
-  for (int j = 0; j < ntiles; ++j) {
+  LdsOff<HD> off;
+  off.init(lane);
+  auto body = [&](const int j, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
     const int k0 = j * BN;
-    bf16* Ks = smem + (j & 1) * 2 * TILE;
-    bf16* Vs = Ks + TILE;
+    const bf16* Ks = smem + BUF * 2 * TILE;
+    const bf16* Vs = Ks + TILE;
     if (j + 1 < ntiles) {
-      bf16* Kn = smem + ((j + 1) & 1) * 2 * TILE;
+      bf16* Kn = smem + (1 - BUF) * 2 * TILE;
       lk.store(Kn, tid);
       lv.store(Kn + TILE, tid);
       if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk, tid); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk, tid); }
@@ -334,8 +381,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
         zero16(dp[t]);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          s[t] = mfma32(rd_row<HD>(Ks, 32 * t + lq, 2 * ks + hh), qf[ks], s[t]);
-          dp[t] = mfma32(rd_row<HD>(Vs, 32 * t + lq, 2 * ks + hh), df[ks], dp[t]);
+          s[t] = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s[t]);
+          dp[t] = mfma32(ld_row(Vs + 32 * t * HD, off.row[ks]), df[ks], dp[t]);
         }
       }
       const bool need_mask = (k0 + BN > p.Tk) || (CAUSAL && k0 + BN - 1 > q0 + p.causal_off);
@@ -356,9 +403,13 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) acc[dt] = mfma32(rd_tr<HD>(Ks, 16 * kk, 32 * dt, lane), sf[kk], acc[dt]);
+        for (int kk = 0; kk < 4; ++kk) acc[dt] = mfma32(ld_tr(Ks + 16 * kk * HD, off.tra[dt], off.trb[dt]), sf[kk], acc[dt]);
     }
     __syncthreads();
+  };
+  for (int j = 0; j < ntiles; j += 2) {
+    body(j, IC<0>{});
+    if (j + 1 < ntiles) body(j + 1, IC<1>{});
   }
   if (qvalid) {
     bf16* op = p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh;
@@ -380,9 +431,10 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 //   dV^T += dO^T P, dK^T += Q^T dS   (A = tr reads of the Q / dO images, B = accumulators)
 // Loops over the q-heads sharing this kv-head (GQA) so the group sum stays in regs.
 // ---------------------------------------------------------------------------
-template <int HD, bool CAUSAL>
+template <int HD, bool CAUSAL, int MT>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
-  constexpr int BMQ = 32, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 256;
+  // MT 32-row q sub-tiles per iteration (more MFMA work per barrier / LDS fill)
+  constexpr int BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 256;
   constexpr int TILE = BMQ * HD;
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][Q|dO]
   __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];  // [buf][lse2 | delta]
@@ -421,7 +473,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int nper = ntq - t0 > 0 ? ntq - t0 : 0;  // q-tiles per head
   const int total = nper * G;                      // (head, q-tile) iterations
   TileLoader<HD, BMQ, NT> lq_, ld_;
-  float rl = 0.f, rd = 0.f;  // per-thread row constants for the prefetched tile (tid < 32)
+  float rl = 0.f, rd = 0.f;  // per-thread row constants for the prefetched tile (tid < BMQ)
   auto fetch = [&](int it) {
     const int hg = it / nper, tq = t0 + it % nper;
     const int h = hk * G + hg;
@@ -446,56 +498,68 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     if (total > 1) fetch(1);
   }
   __syncthreads();
-  for (int it = 0; it < total; ++it) {
+  LdsOff<HD> off;
+  off.init(lane);
+  auto body = [&](const int it, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
     const int tq = t0 + it % nper;
     const int qq0 = tq * BMQ;
-    const bf16* Qs = smem + (it & 1) * 2 * TILE;
+    const bf16* Qs = smem + BUF * 2 * TILE;
     const bf16* Ds = Qs + TILE;
-    const float* rc = rowc[it & 1];
+    const float* rc = rowc[BUF];
     if (it + 1 < total) {
-      commit_tile((it + 1) & 1);
+      commit_tile(1 - BUF);
       if (it + 2 < total) fetch(it + 2);
     }
     const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
     if (active) {
-      f32x16 s, dp;
-      zero16(s);
-      zero16(dp);
+      f32x16 s[MT], dp[MT];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        s = mfma32(rd_row<HD>(Qs, lk, 2 * ks + hh), kf[ks], s);
-        dp = mfma32(rd_row<HD>(Ds, lk, 2 * ks + hh), vf[ks], dp);
-      }
-      // rows of s/dp are queries qq0 + 8g + 4hh + i (r = 4g + i); column = key (lane)
-      const bool need_mask = CAUSAL && qq0 + p.causal_off < kw0 + 31;
+      for (int t = 0; t < MT; ++t) {
+        zero16(s[t]);
+        zero16(dp[t]);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 8 * g + 4 * hh);
-        const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 8 * g + 4 * hh);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * g + i;
-          float pr = exp2f(s[r] * p.scale_log2 - lv[i]);  // rows >= Tq: lse=inf -> 0
-          if (need_mask) {
-            const int qq = qq0 + 8 * g + 4 * hh + i;
-            if (key > qq + p.causal_off) pr = 0.f;
-          }
-          s[r] = pr;
-          dp[r] = pr * (dp[r] - dv[i]);
+        for (int ks = 0; ks < KS; ++ks) {
+          s[t] = mfma32(ld_row(Qs + 32 * t * HD, off.row[ks]), kf[ks], s[t]);
+          dp[t] = mfma32(ld_row(Ds + 32 * t * HD, off.row[ks]), vf[ks], dp[t]);
         }
       }
-      bf16x8 pf[2], sf[2];
+      // rows of s/dp[t] are queries qq0 + 32t + 8g + 4hh + i (r = 4g + i); column = key (lane)
+      const bool need_mask = CAUSAL && qq0 + p.causal_off < kw0 + 31;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) { pf[kk] = pack_acc(s, kk); sf[kk] = pack_acc(dp, kk); }
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 32 * t + 8 * g + 4 * hh);
+          const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i;
+            float pr = exp2f(s[t][r] * p.scale_log2 - lv[i]);  // rows >= Tq: lse=inf -> 0
+            if (need_mask) {
+              const int qq = qq0 + 32 * t + 8 * g + 4 * hh + i;
+              if (key > qq + p.causal_off) pr = 0.f;
+            }
+            s[t][r] = pr;
+            dp[t][r] = pr * (dp[t][r] - dv[i]);
+          }
+        }
+      bf16x8 pf[2 * MT], sf[2 * MT];
+#pragma unroll
+      for (int kk = 0; kk < 2 * MT; ++kk) { pf[kk] = pack_acc(s[kk >> 1], kk & 1); sf[kk] = pack_acc(dp[kk >> 1], kk & 1); }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          dvt[dt] = mfma32(rd_tr<HD>(Ds, 16 * kk, 32 * dt, lane), pf[kk], dvt[dt]);
-          dkt[dt] = mfma32(rd_tr<HD>(Qs, 16 * kk, 32 * dt, lane), sf[kk], dkt[dt]);
+        for (int kk = 0; kk < 2 * MT; ++kk) {
+          dvt[dt] = mfma32(ld_tr(Ds + 16 * kk * HD, off.tra[dt], off.trb[dt]), pf[kk], dvt[dt]);
+          dkt[dt] = mfma32(ld_tr(Qs + 16 * kk * HD, off.tra[dt], off.trb[dt]), sf[kk], dkt[dt]);
         }
     }
     __syncthreads();
+  };
+  for (int it = 0; it < total; it += 2) {
+    body(it, IC<0>{});
+    if (it + 1 < total) body(it + 1, IC<1>{});
   }
   if (kvalid) {
     bf16* kp = p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh;
@@ -612,8 +676,9 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
     else attn_bwd_dq_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
     if (Tk > 0) {
       const int g2 = cdiv(Tk, 128) * Hkv * B;
-      if (causal) attn_bwd_dkdv_kernel<HD_, true><<<g2, 256, 0, st>>>(p);
-      else attn_bwd_dkdv_kernel<HD_, false><<<g2, 256, 0, st>>>(p);
+      constexpr int MT = HD_ == 128 ? 2 : 1;
+      if (causal) attn_bwd_dkdv_kernel<HD_, true, MT><<<g2, 256, 0, st>>>(p);
+      else attn_bwd_dkdv_kernel<HD_, false, MT><<<g2, 256, 0, st>>>(p);
     }
   });
   SPA_LAUNCH_CHECK();

@@ -43,6 +43,7 @@ class LlamaConfig:
     norm_eps: float = 1e-6
     rope_theta: float = 10000.0
     gate: str = "w3"            # reference quirk (Q10): SwiGLU gate on w3; Meta uses w1
+    ref_freqs: bool = True      # reference quirk: RoPE freq theta^(-i/hd) (LLaMA-jax.ipynb:563-567)
     init: str = "ref"           # "ref": N(0,1)/sqrt(fan_in) & N(0,1) norms; "std": N(0,0.02) & ones
     tie_embeddings: bool = False
     batch_size: int = 16
@@ -59,11 +60,11 @@ PRESETS = {
     # BASELINE.json north-star shape (public LLaMA3-8B card)
     "llama3_8b": LlamaConfig(vocab_size=128256, dim=4096, n_layers=32, n_heads=32, n_kv_heads=8, ffn_hidden=14336,
                              max_seq_len=8192, norm_eps=1e-5, rope_theta=500000.0, gate="w1", init="std",
-                             batch_size=1, lr=3e-4),
+                             ref_freqs=False, batch_size=1, lr=3e-4),
     # small GPU smoke shape with the 8B's head geometry
     "llama3_tiny": LlamaConfig(vocab_size=1024, dim=512, n_layers=2, n_heads=4, n_kv_heads=2, ffn_hidden=1536,
                                max_seq_len=256, norm_eps=1e-5, rope_theta=500000.0, gate="w1", init="std",
-                               batch_size=2),
+                               ref_freqs=False, batch_size=2),
 }
 
 
@@ -103,12 +104,12 @@ class LlamaBlock(nn.Module):
         hd = c.head_dim
         qkv = linear(n1, self.wqkv)  # [B, T, (H+2Hkv)*hd]
         if kv_cache is None:
-            qkv = rope_packed_(qkv, c.n_heads + c.n_kv_heads, c.rope_theta, 0, head_dim=hd)
+            qkv = rope_packed_(qkv, c.n_heads + c.n_kv_heads, c.rope_theta, 0, head_dim=hd, ref_freqs=c.ref_freqs)
             o = attention_packed(qkv, c.n_heads, c.n_kv_heads, causal=True, head_dim=hd)
         else:
             qkv = qkv.view(B, T, c.n_heads + 2 * c.n_kv_heads, hd)
-            q = apply_rope(qkv[:, :, :c.n_heads], c.rope_theta, pos)
-            k = apply_rope(qkv[:, :, c.n_heads:c.n_heads + c.n_kv_heads], c.rope_theta, pos)
+            q = apply_rope(qkv[:, :, :c.n_heads], c.rope_theta, pos, ref_freqs=c.ref_freqs)
+            k = apply_rope(qkv[:, :, c.n_heads:c.n_heads + c.n_kv_heads], c.rope_theta, pos, ref_freqs=c.ref_freqs)
             v = qkv[:, :, c.n_heads + c.n_kv_heads:]
             kc, vc = kv_cache
             kc[:, pos:pos + T] = k

@@ -64,9 +64,13 @@ def glu(gu, kind: str):
     return (act(g, kind).float() * u).to(gu.dtype)
 
 
-def rope_tables(T, hd, theta=10000.0, device=None):
-    """llama3/LLaMA-jax.ipynb:563-567: freqs = theta^(-2i/hd), angles t*freq."""
-    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
+def rope_tables(T, hd, theta=10000.0, device=None, ref_freqs=False):
+    """Angles t*freq_i, i < hd/2. Standard (Meta) freq_i = theta^(-2i/hd);
+    ``ref_freqs=True`` reproduces llama3/LLaMA-jax.ipynb:563-567 exactly, whose
+    precompute_freqs_cis uses arange(0, dim//2)/dim, i.e. theta^(-i/hd)."""
+    expo = torch.arange(0, hd // 2, dtype=torch.float64) / hd if ref_freqs else \
+        torch.arange(0, hd, 2, dtype=torch.float64) / hd
+    inv = 1.0 / (theta ** expo)
     t = torch.arange(T, dtype=torch.float64)
     ang = torch.outer(t, inv)
     return ang.cos().float().to(device), ang.sin().float().to(device)

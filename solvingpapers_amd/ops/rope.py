@@ -18,12 +18,12 @@ class RopeCache:
     _tables: dict = {}
 
     @classmethod
-    def get(cls, T, hd, theta, device):
-        key = (str(device), hd, float(theta))
+    def get(cls, T, hd, theta, device, ref_freqs=False):
+        key = (str(device), hd, float(theta), bool(ref_freqs))
         tab = cls._tables.get(key)
         if tab is None or tab[0].shape[0] < T:
             n = max(T, 1 << max(0, (T - 1).bit_length()))
-            cos, sin = reference.rope_tables(n, hd, theta, device=device)
+            cos, sin = reference.rope_tables(n, hd, theta, device=device, ref_freqs=ref_freqs)
             tab = (cos.contiguous(), sin.contiguous())
             cls._tables[key] = tab
         return tab
@@ -51,7 +51,7 @@ class _RopeFn(torch.autograd.Function):
         return g, None, None, None, None, None, None, None
 
 
-def rope_packed_(x, nrot, theta=10000.0, pos_off=0, interleaved=True, head_dim=None):
+def rope_packed_(x, nrot, theta=10000.0, pos_off=0, interleaved=True, head_dim=None, ref_freqs=False):
     """In-place rotation of heads [0, nrot) of x ([B, T, NH, hd], or [B, T, NH*hd]
     with ``head_dim``); returns x.
 
@@ -59,7 +59,7 @@ def rope_packed_(x, nrot, theta=10000.0, pos_off=0, interleaved=True, head_dim=N
     rotated back in place)."""
     hd = head_dim if head_dim is not None else x.shape[-1]
     B, T = x.shape[0], x.shape[1]
-    cos, sin = RopeCache.get(pos_off + T, hd, theta, x.device)
+    cos, sin = RopeCache.get(pos_off + T, hd, theta, x.device, ref_freqs)
     if x.is_cuda:
         return _RopeFn.apply(x, nrot, cos, sin, pos_off, interleaved, True, hd)
     x4 = x.view(B, T, -1, hd)
@@ -67,11 +67,11 @@ def rope_packed_(x, nrot, theta=10000.0, pos_off=0, interleaved=True, head_dim=N
     return torch.cat([rot, x4[:, :, nrot:]], dim=2).view(x.shape)
 
 
-def apply_rope(x, theta=10000.0, pos_off=0, interleaved=True, positions=None):
+def apply_rope(x, theta=10000.0, pos_off=0, interleaved=True, positions=None, ref_freqs=False):
     """Out-of-place rotation of every head of x [B, T, H, hd]."""
     B, T, H, hd = x.shape
     n = (int(positions.max()) + 1) if positions is not None else pos_off + T
-    cos, sin = RopeCache.get(n, hd, theta, x.device)
+    cos, sin = RopeCache.get(n, hd, theta, x.device, ref_freqs)
     if x.is_cuda and positions is None:
         return _RopeFn.apply(x.clone(), H, cos, sin, pos_off, interleaved, False, hd)
     if x.is_cuda:

@@ -44,7 +44,8 @@ class FlatParams:
 
     def __init__(self, module: torch.nn.Module, groups: Optional[Sequence[Sequence[torch.nn.Parameter]]] = None,
                  param_dtype: Optional[torch.dtype] = None, grad_dtype: Optional[torch.dtype] = None,
-                 device=None, align: int = 64, no_decay: Optional[Callable[[str, torch.nn.Parameter], bool]] = None):
+                 device=None, align: int = 64, no_decay: Optional[Callable[[str, torch.nn.Parameter], bool]] = None,
+                 hook_autograd: bool = True):
         params = [p for p in module.parameters() if p.requires_grad]
         names = {id(p): n for n, p in module.named_parameters()}
         seen = set()
@@ -101,6 +102,8 @@ class FlatParams:
             else:
                 segs.append([o, o + p.numel(), flag])
         self.decay_segments = [(a, b, f) for a, b, f in segs]
+        if hook_autograd:
+            attach_autograd_grads(self)
 
     def bucket_of(self, p) -> Bucket:
         o = self.offsets[id(p)]
@@ -120,3 +123,20 @@ class FlatParams:
         return {"param": self.param, "names": self.names,
                 "offsets": [self.offsets[id(p)] for p in self.params],
                 "shapes": [tuple(p.shape) for p in self.params]}
+
+
+def attach_autograd_grads(flat: "FlatParams"):
+    """Route gradients that arrive through plain autograd (parameters used by
+    non-fused torch ops) into ``main_grad`` as soon as they are accumulated, then
+    drop ``.grad`` so no second copy stays alive. Idempotent."""
+    from .grad import commit_tensor
+
+    def _hook(p):
+        if p.grad is not None:
+            commit_tensor(p, p.grad)
+            p.grad = None
+
+    for p in flat.params:
+        if not getattr(p, "_spa_hooked", False):
+            p.register_post_accumulate_grad_hook(_hook)
+            p._spa_hooked = True
