@@ -46,6 +46,7 @@ def main(argv=None):
     ap.add_argument("--accum", type=int, default=1, help="micro-batches per step")
     ap.add_argument("--zero1", action="store_true")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (NOT for headline runs)")
+    ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
     a = ap.parse_args(argv)
 
     info = sdist.init_distributed()
@@ -64,6 +65,9 @@ def main(argv=None):
         dp.broadcast_params(0)
     shard = (dp.shard_ranges(), None) if (dp is not None and a.zero1) else None
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0, shard=shard)
+    overlap = not a.no_opt_overlap and not a.zero1
+    if overlap:
+        model.param_wait_cb = flat.wait_bucket
 
     gen = torch.Generator(device=dev).manual_seed(1000 + info.rank)
     V, T, B = cfg.vocab_size, a.seq, a.mb
@@ -88,7 +92,7 @@ def main(argv=None):
                 loss.backward()
         if dp is not None:
             dp.finish_grad_sync()
-        opt.step()
+        opt.step(overlap=overlap)
         if dp is not None:
             dp.gather_params()
         last_loss[0] = loss

@@ -17,10 +17,10 @@
 
 namespace spa {
 
-template <int NT, int MAXV, bool LN, bool RES, bool RESOUT>
+template <typename T, int NT, int MAXV, bool LN, bool RES, bool RESOUT>
 __global__ __launch_bounds__(256) void norm_fwd_kernel(
-    const bf16* __restrict__ x, const bf16* __restrict__ r, const bf16* __restrict__ w,
-    const bf16* __restrict__ b, bf16* __restrict__ y, bf16* __restrict__ hout,
+    const T* __restrict__ x, const T* __restrict__ r, const T* __restrict__ w,
+    const T* __restrict__ b, T* __restrict__ y, T* __restrict__ hout,
     float* __restrict__ rstd_out, float* __restrict__ mean_out, int M, int D, float eps) {
   constexpr int RPB = 256 / NT;  // rows per block
   __shared__ float red[RPB][NT / 64 > 0 ? NT / 64 : 1];
@@ -41,11 +41,10 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[k][i] += rr[i];
         if constexpr (RESOUT) {
-          // round the residual stream to bf16 once, and normalise the rounded value
-          bf16x8 hv;
+          // round the residual stream to the I/O dtype once, and normalise the rounded value
 #pragma unroll
-          for (int i = 0; i < 8; ++i) { hv[i] = (bf16)v[k][i]; v[k][i] = (float)hv[i]; }
-          *reinterpret_cast<bf16x8*>(hout + (size_t)row * D + vi * 8) = hv;
+          for (int i = 0; i < 8; ++i) v[k][i] = (float)(T)v[k][i];
+          store8(hout + (size_t)row * D + vi * 8, v[k]);
         }
       }
 #pragma unroll
@@ -92,11 +91,11 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
 
 // Backward. grid.x = number of partial blocks; each block walks rows
 // blockIdx.x*RPB + sub, stepping by gridDim.x*RPB.
-template <int NT, int MAXV, bool LN, bool DRES>
+template <typename T, int NT, int MAXV, bool LN, bool DRES>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(
-    const bf16* __restrict__ dy, const bf16* __restrict__ h, const bf16* __restrict__ w,
+    const T* __restrict__ dy, const T* __restrict__ h, const T* __restrict__ w,
     const float* __restrict__ rstd_in, const float* __restrict__ mean_in,
-    const bf16* __restrict__ dres, bf16* __restrict__ dx, float* __restrict__ dw_part,
+    const T* __restrict__ dres, T* __restrict__ dx, float* __restrict__ dw_part,
     float* __restrict__ db_part, int M, int D) {
   constexpr int RPB = 256 / NT;
   __shared__ float red[RPB][NT / 64 > 0 ? NT / 64 : 1];
@@ -208,18 +207,21 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   do {                                                                                           \
     dim3 grid(cdiv(M, 256 / NT));                                                                \
     if (is_ln) {                                                                                 \
-      if (has_res) norm_fwd_kernel<NT, MAXV, true, true, true><<<grid, 256, 0, st>>>(ARGS);      \
-      else norm_fwd_kernel<NT, MAXV, true, false, false><<<grid, 256, 0, st>>>(ARGS);            \
+      if (has_res) norm_fwd_kernel<T, NT, MAXV, true, true, true><<<grid, 256, 0, st>>>(ARGS);   \
+      else norm_fwd_kernel<T, NT, MAXV, true, false, false><<<grid, 256, 0, st>>>(ARGS);         \
     } else {                                                                                     \
-      if (has_res) norm_fwd_kernel<NT, MAXV, false, true, true><<<grid, 256, 0, st>>>(ARGS);     \
-      else norm_fwd_kernel<NT, MAXV, false, false, false><<<grid, 256, 0, st>>>(ARGS);           \
+      if (has_res) norm_fwd_kernel<T, NT, MAXV, false, true, true><<<grid, 256, 0, st>>>(ARGS);  \
+      else norm_fwd_kernel<T, NT, MAXV, false, false, false><<<grid, 256, 0, st>>>(ARGS);        \
     }                                                                                            \
   } while (0)
 
-// Returns (y, h_or_empty, rstd, mean_or_empty)
+// Returns (y, h_or_empty, rstd, mean_or_empty). bf16 or fp32 I/O (weights same dtype).
 std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
                                  const at::Tensor& w, const c10::optional<at::Tensor>& b, double eps) {
-  SPA_CHECK_CUDA(x); SPA_CHECK_BF16(x); SPA_CHECK_CONTIG(x); SPA_CHECK_BF16(w);
+  SPA_CHECK_CUDA(x); SPA_CHECK_CONTIG(x);
+  const auto dt = x.scalar_type();
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kFloat, "norm: bf16/fp32 only");
+  TORCH_CHECK(w.scalar_type() == dt, "norm: weight dtype must match x");
   const bool is_ln = b.has_value();
   const bool has_res = residual.has_value();
   const int D = x.size(-1);
@@ -229,26 +231,30 @@ std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const c10::optional<at::Te
   DeviceGuard g(x.device());
   auto y = at::empty_like(x);
   at::Tensor h = has_res ? at::empty_like(x) : at::Tensor();
-  if (has_res) { SPA_CHECK_BF16(*residual); SPA_CHECK_CONTIG(*residual); TORCH_CHECK(residual->sizes() == x.sizes()); }
-  if (is_ln) { SPA_CHECK_BF16(*b); TORCH_CHECK(b->numel() == D && b->is_contiguous()); }
+  if (has_res) { TORCH_CHECK(residual->scalar_type() == dt); SPA_CHECK_CONTIG(*residual); TORCH_CHECK(residual->sizes() == x.sizes()); }
+  if (is_ln) { TORCH_CHECK(b->scalar_type() == dt); TORCH_CHECK(b->numel() == D && b->is_contiguous()); }
   auto opts = x.options().dtype(at::kFloat);
   auto rstd = at::empty({M}, opts);
   auto mean = is_ln ? at::empty({M}, opts) : at::Tensor();
   auto st = stream();
   if (M == 0) return {y, h, rstd, mean};
-#define ARGS                                                                                       \
-  (const bf16*)x.data_ptr(), has_res ? (const bf16*)residual->data_ptr() : nullptr,                \
-      (const bf16*)w.data_ptr(), is_ln ? (const bf16*)b->data_ptr() : nullptr, (bf16*)y.data_ptr(), \
-      has_res ? (bf16*)h.data_ptr() : nullptr, rstd.data_ptr<float>(),                             \
-      is_ln ? mean.data_ptr<float>() : nullptr, M, D, (float)eps
   const int nv = D / 8;
-  if (nv <= 64) NORM_FWD_DISPATCH(64, 1);
-  else if (nv <= 128) NORM_FWD_DISPATCH(64, 2);
-  else if (nv <= 256) NORM_FWD_DISPATCH(256, 1);
-  else if (nv <= 512) NORM_FWD_DISPATCH(256, 2);
-  else if (nv <= 1024) NORM_FWD_DISPATCH(256, 4);
-  else NORM_FWD_DISPATCH(256, 8);
+  auto run = [&](auto tag) {
+    using T = decltype(tag);
+#define ARGS                                                                                   \
+  (const T*)x.data_ptr(), has_res ? (const T*)residual->data_ptr() : nullptr,                  \
+      (const T*)w.data_ptr(), is_ln ? (const T*)b->data_ptr() : nullptr, (T*)y.data_ptr(),     \
+      has_res ? (T*)h.data_ptr() : nullptr, rstd.data_ptr<float>(),                            \
+      is_ln ? mean.data_ptr<float>() : nullptr, M, D, (float)eps
+    if (nv <= 64) NORM_FWD_DISPATCH(64, 1);
+    else if (nv <= 128) NORM_FWD_DISPATCH(64, 2);
+    else if (nv <= 256) NORM_FWD_DISPATCH(256, 1);
+    else if (nv <= 512) NORM_FWD_DISPATCH(256, 2);
+    else if (nv <= 1024) NORM_FWD_DISPATCH(256, 4);
+    else NORM_FWD_DISPATCH(256, 8);
 #undef ARGS
+  };
+  if (dt == at::kBFloat16) run(bf16{}); else run(float{});
   SPA_LAUNCH_CHECK();
   return {y, h, rstd, mean};
 }
@@ -261,20 +267,24 @@ std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const c10::optional<at::Te
     dw_part = at::empty({nparts, D}, opts);                                                \
     if (is_ln) db_part = at::empty({nparts, D}, opts);                                     \
     if (is_ln) {                                                                           \
-      if (has_dres) norm_bwd_kernel<NT, MAXV, true, true><<<nblk, 256, 0, st>>>(ARGS);     \
-      else norm_bwd_kernel<NT, MAXV, true, false><<<nblk, 256, 0, st>>>(ARGS);             \
+      if (has_dres) norm_bwd_kernel<T, NT, MAXV, true, true><<<nblk, 256, 0, st>>>(ARGS);  \
+      else norm_bwd_kernel<T, NT, MAXV, true, false><<<nblk, 256, 0, st>>>(ARGS);          \
     } else {                                                                               \
-      if (has_dres) norm_bwd_kernel<NT, MAXV, false, true><<<nblk, 256, 0, st>>>(ARGS);    \
-      else norm_bwd_kernel<NT, MAXV, false, false><<<nblk, 256, 0, st>>>(ARGS);            \
+      if (has_dres) norm_bwd_kernel<T, NT, MAXV, false, true><<<nblk, 256, 0, st>>>(ARGS); \
+      else norm_bwd_kernel<T, NT, MAXV, false, false><<<nblk, 256, 0, st>>>(ARGS);         \
     }                                                                                      \
   } while (0)
 
 // Returns (dx, dw, db_or_empty). dres (optional) is added into dx (gradient flowing
-// along the residual stream past the fused add).
+// along the residual stream past the fused add). dw_out / db_out (optional): write the
+// weight gradients straight into these (e.g. main_grad views) instead of new tensors.
 std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w,
                                  const at::Tensor& rstd, const c10::optional<at::Tensor>& mean,
-                                 const c10::optional<at::Tensor>& dres) {
-  SPA_CHECK_BF16(dy); SPA_CHECK_BF16(h); SPA_CHECK_CONTIG(dy); SPA_CHECK_CONTIG(h);
+                                 const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& dw_out,
+                                 const c10::optional<at::Tensor>& db_out) {
+  SPA_CHECK_CONTIG(dy); SPA_CHECK_CONTIG(h);
+  const auto dt = h.scalar_type();
+  TORCH_CHECK(dy.scalar_type() == dt && w.scalar_type() == dt, "norm_bwd: dtype mismatch");
   const bool is_ln = mean.has_value();
   const bool has_dres = dres.has_value();
   const int D = h.size(-1);
@@ -285,26 +295,37 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& h, cons
   auto st = stream();
   at::Tensor dw_part, db_part;
   int nblk = 0, nparts = 0;
-  if (has_dres) { SPA_CHECK_BF16(*dres); SPA_CHECK_CONTIG(*dres); }
-  auto dw = at::empty({D}, w.options());
-  auto db = is_ln ? at::empty({D}, w.options()) : at::Tensor();
+  if (has_dres) { TORCH_CHECK(dres->scalar_type() == dt); SPA_CHECK_CONTIG(*dres); }
+  auto dw = dw_out ? *dw_out : at::empty({D}, w.options());
+  auto db = is_ln ? (db_out ? *db_out : at::empty({D}, w.options())) : at::Tensor();
+  TORCH_CHECK(dw.is_contiguous() && dw.numel() == D);
   if (M == 0) { dw.zero_(); if (is_ln) db.zero_(); return {dx, dw, db}; }
-#define ARGS                                                                                \
-  (const bf16*)dy.data_ptr(), (const bf16*)h.data_ptr(), (const bf16*)w.data_ptr(),         \
-      rstd.data_ptr<float>(), is_ln ? mean->data_ptr<float>() : nullptr,                    \
-      has_dres ? (const bf16*)dres->data_ptr() : nullptr, (bf16*)dx.data_ptr(),             \
-      dw_part.data_ptr<float>(), is_ln ? db_part.data_ptr<float>() : nullptr, M, D
   const int nv = D / 8;
-  if (nv <= 64) NORM_BWD_DISPATCH(64, 1);
-  else if (nv <= 128) NORM_BWD_DISPATCH(64, 2);
-  else if (nv <= 256) NORM_BWD_DISPATCH(256, 1);
-  else if (nv <= 512) NORM_BWD_DISPATCH(256, 2);
-  else if (nv <= 1024) NORM_BWD_DISPATCH(256, 4);
-  else NORM_BWD_DISPATCH(256, 8);
+  auto run = [&](auto tag) {
+    using T = decltype(tag);
+#define ARGS                                                                            \
+  (const T*)dy.data_ptr(), (const T*)h.data_ptr(), (const T*)w.data_ptr(),              \
+      rstd.data_ptr<float>(), is_ln ? mean->data_ptr<float>() : nullptr,                \
+      has_dres ? (const T*)dres->data_ptr() : nullptr, (T*)dx.data_ptr(),               \
+      dw_part.data_ptr<float>(), is_ln ? db_part.data_ptr<float>() : nullptr, M, D
+    if (nv <= 64) NORM_BWD_DISPATCH(64, 1);
+    else if (nv <= 128) NORM_BWD_DISPATCH(64, 2);
+    else if (nv <= 256) NORM_BWD_DISPATCH(256, 1);
+    else if (nv <= 512) NORM_BWD_DISPATCH(256, 2);
+    else if (nv <= 1024) NORM_BWD_DISPATCH(256, 4);
+    else NORM_BWD_DISPATCH(256, 8);
 #undef ARGS
-  SPA_LAUNCH_CHECK();
-  colsum_kernel<bf16><<<cdiv(D, 64), 256, 0, st>>>(dw_part.data_ptr<float>(), (bf16*)dw.data_ptr(), nparts, D);
-  if (is_ln) colsum_kernel<bf16><<<cdiv(D, 64), 256, 0, st>>>(db_part.data_ptr<float>(), (bf16*)db.data_ptr(), nparts, D);
+    SPA_LAUNCH_CHECK();
+    auto colsum = [&](const at::Tensor& part, const at::Tensor& out) {
+      if (out.scalar_type() == at::kFloat)
+        colsum_kernel<float><<<cdiv(D, 64), 256, 0, st>>>(part.data_ptr<float>(), out.data_ptr<float>(), nparts, D);
+      else
+        colsum_kernel<bf16><<<cdiv(D, 64), 256, 0, st>>>(part.data_ptr<float>(), (bf16*)out.data_ptr(), nparts, D);
+    };
+    colsum(dw_part, dw);
+    if (is_ln) colsum(db_part, db);
+  };
+  if (dt == at::kBFloat16) run(bf16{}); else run(float{});
   SPA_LAUNCH_CHECK();
   return {dx, dw, db};
 }
@@ -313,7 +334,8 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& h, cons
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("norm_fwd(Tensor x, Tensor? residual, Tensor w, Tensor? b, float eps) -> Tensor[]");
-  m.def("norm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? mean, Tensor? dres) -> Tensor[]");
+  m.def("norm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? mean, Tensor? dres, Tensor(a!)? dw_out, "
+        "Tensor(b!)? db_out) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("norm_fwd", &spa::norm_fwd);

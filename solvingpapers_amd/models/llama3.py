@@ -140,7 +140,8 @@ class Llama3(nn.Module):
         self.layers = nn.ModuleList([LlamaBlock(c, **fk) for _ in range(c.n_layers)])
         self.norm_f = nn.Parameter(torch.ones(c.dim, **fk))
         self.output = None if c.tie_embeddings else nn.Parameter(torch.empty(c.vocab_size, c.dim, **fk))
-        self.grad_ready_cb = None
+        self.grad_ready_cb = None   # DP: launch gradient bucket i when its layer's backward is done
+        self.param_wait_cb = None   # optimizer overlap: wait for bucket i's update before using it
         self.reset_parameters(seed)
 
     @torch.no_grad()
@@ -168,12 +169,16 @@ class Llama3(nn.Module):
 
     def hidden(self, ids, kv_caches=None, pos=0):
         c = self.c
+        wait = self.param_wait_cb or (lambda i: None)
+        wait(0)
         x = embedding(self.tok_embeddings, ids)
         res, delta = None, x
         cb = self.grad_ready_cb
         for i, layer in enumerate(self.layers):
+            wait(i + 1)
             delta = mark_ready(delta, cb, i + 1)
             res, delta = layer(res, delta, None if kv_caches is None else kv_caches[i], pos)
+        wait(len(self.layers) + 1)
         delta = mark_ready(delta, cb, len(self.layers) + 1)
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
         return n

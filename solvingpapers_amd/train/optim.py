@@ -45,14 +45,52 @@ class FlatOptimizer:
                 self.master[so:so + b - a].copy_(flat.param[a:b].float())
 
     def _segments(self):
-        """(flat_a, flat_b, state_a, decay) pieces = owned ranges x decay segments."""
+        """(flat_a, flat_b, state_a, decay, bucket) pieces = owned ranges x decay segments,
+        in bucket (= forward) order."""
         out = []
         for (a, b), so in zip(self.ranges, self.state_off):
             for sa, sb, dec in self.flat.decay_segments:
                 lo, hi = max(a, sa), min(b, sb)
                 if lo < hi:
-                    out.append((lo, hi, so + lo - a, dec))
+                    bi = next(i for i, bk in enumerate(self.flat.buckets) if bk.start <= lo < bk.end)
+                    out.append((lo, hi, so + lo - a, dec, bi))
+        out.sort(key=lambda x: x[0])
         return out
+
+    def _run(self, lr, overlap: bool):
+        """Apply self._update to every owned segment. With ``overlap`` (GPU), the
+        updates run on a low-priority side stream, one event per bucket, so the
+        memory-bound optimizer overlaps the compute-bound forward of the next
+        step (see FlatParams.wait_bucket)."""
+        self.step_count += 1
+        coef = self.clip_coef()
+        segs = self._segments()
+        if overlap and self.flat.device.type == "cuda":
+            main = torch.cuda.current_stream(self.flat.device)
+            if not hasattr(self, "_side"):
+                self._side = torch.cuda.Stream(self.flat.device, priority=0)
+            side = self._side
+            side.wait_stream(main)
+            if coef is not None:
+                coef.record_stream(side)
+            with torch.cuda.stream(side):
+                last = None
+                for a, b, so, dec, bi in segs:
+                    if last is not None and bi != last:
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                        self.flat.set_ready_event(last, ev)
+                    self._update(a, b, so, dec, lr, coef)
+                    last = bi
+                if last is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    self.flat.set_ready_event(last, ev)
+                # anything the model does not wait on explicitly (e.g. checkpoint
+                # reads) is ordered by wait_all()
+        else:
+            for a, b, so, dec, bi in segs:
+                self._update(a, b, so, dec, lr, coef)
 
     def grad_norm(self) -> torch.Tensor:
         """Global L2 norm of the (already reduced) gradient, on the device."""
@@ -89,16 +127,15 @@ class FlatAdamW(FlatOptimizer):
         self.v = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device)
 
     @torch.no_grad()
-    def step(self, lr: Optional[float] = None):
-        lr = self.lr if lr is None else lr
-        self.step_count += 1
-        coef = self.clip_coef()
+    def step(self, lr: Optional[float] = None, overlap: bool = False):
+        self._run(self.lr if lr is None else lr, overlap)
+
+    def _update(self, a, b, so, dec, lr, coef):
         f = self.flat
-        for a, b, so, dec in self._segments():
-            n = b - a
-            K.adamw_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
-                     self.m[so:so + n], self.v[so:so + n], lr, self.b1, self.b2, self.eps,
-                     self.weight_decay if dec else 0.0, self.step_count, coef, self.adam_l2)
+        n = b - a
+        K.adamw_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
+                 self.m[so:so + n], self.v[so:so + n], lr, self.b1, self.b2, self.eps,
+                 self.weight_decay if dec else 0.0, self.step_count, coef, self.adam_l2)
 
     def state_dict(self):
         return {"step": self.step_count, "m": self.m, "v": self.v, "master": self.master, "lr": self.lr}
@@ -123,16 +160,15 @@ class FlatSGD(FlatOptimizer):
         self.buf = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device) if momentum else None
 
     @torch.no_grad()
-    def step(self, lr: Optional[float] = None):
-        lr = self.lr if lr is None else lr
-        self.step_count += 1
-        coef = self.clip_coef()
+    def step(self, lr: Optional[float] = None, overlap: bool = False):
+        self._run(self.lr if lr is None else lr, overlap)
+
+    def _update(self, a, b, so, dec, lr, coef):
         f = self.flat
-        for a, b, so, dec in self._segments():
-            n = b - a
-            K.sgd_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
-                   self.buf[so:so + n] if self.buf is not None else None, lr, self.momentum,
-                   self.weight_decay if dec else 0.0, coef)
+        n = b - a
+        K.sgd_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
+               self.buf[so:so + n] if self.buf is not None else None, lr, self.momentum,
+               self.weight_decay if dec else 0.0, coef)
 
     def state_dict(self):
         return {"step": self.step_count, "buf": self.buf, "master": self.master, "lr": self.lr}

@@ -105,6 +105,28 @@ class FlatParams:
         if hook_autograd:
             attach_autograd_grads(self)
 
+    # ---- overlap of the optimizer step with the next forward -----------------
+    # The optimizer may update buckets on a side stream, recording one event per
+    # bucket; the model calls wait_bucket(i) right before it first reads bucket
+    # i's parameters, so the update of layer i overlaps the forward of layers < i.
+    def set_ready_event(self, idx: int, ev):
+        if not hasattr(self, "_ready"):
+            self._ready = {}
+        self._ready[idx] = ev
+
+    def wait_bucket(self, idx: int):
+        r = getattr(self, "_ready", None)
+        if r:
+            ev = r.pop(idx, None)
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def wait_all(self):
+        r = getattr(self, "_ready", None)
+        if r:
+            for idx in list(r):
+                self.wait_bucket(idx)
+
     def bucket_of(self, p) -> Bucket:
         o = self.offsets[id(p)]
         for b in self.buckets:

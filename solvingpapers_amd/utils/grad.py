@@ -41,6 +41,17 @@ def commit(p: torch.Tensor, compute: Callable[[Optional[torch.Tensor], bool], Op
     return None
 
 
+def direct_out(p: torch.Tensor):
+    """If ``p``'s next commit is an overwrite and the main_grad view is contiguous
+    with p's dtype, claim it and return it so a kernel can write the gradient
+    straight into it (no temporary + copy). Returns None otherwise."""
+    mg = getattr(p, "main_grad", None)
+    if mg is None or getattr(p, "_spa_gen", -1) == _Gen.value or mg.dtype != p.dtype or not mg.is_contiguous():
+        return None
+    p._spa_gen = _Gen.value
+    return mg
+
+
 def commit_tensor(p: torch.Tensor, g: torch.Tensor):
     """Commit an already-computed gradient tensor."""
     def _c(out, acc):

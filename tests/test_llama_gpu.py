@@ -59,3 +59,26 @@ def test_llama_generate_kv_cache_matches_full_forward():
     # greedy re-forward without cache must agree on the first generated token
     lg = gpu(ids)[:, -1].float()
     assert out[0, 9].item() == lg.argmax(-1).item()
+
+
+def test_optimizer_overlap_bitwise_equal():
+    """AdamW on a side stream overlapped with the next forward == serial AdamW."""
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = llama3.config("llama3_tiny")
+    res = []
+    for overlap in (False, True):
+        m = llama3.Llama3(c, device="cuda", dtype=torch.bfloat16, seed=11)
+        flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
+        opt = FlatAdamW(flat, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
+        if overlap:
+            m.param_wait_cb = flat.wait_bucket
+        g = torch.Generator(device="cuda").manual_seed(5)
+        for _ in range(4):
+            ids = torch.randint(0, c.vocab_size, (2, 129), device="cuda", generator=g)
+            opt.zero_grad()
+            m(ids[:, :-1], ids[:, 1:]).backward()
+            opt.step(overlap=overlap)
+        torch.cuda.synchronize()
+        res.append(flat.param.clone())
+    assert torch.equal(res[0], res[1])
