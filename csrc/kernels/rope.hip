@@ -10,11 +10,18 @@
 // Layout: each thread owns 8 contiguous bf16 of one head row (16-byte load/store);
 // cos/sin come from an fp32 table [Tmax, hd/2] (L2/LLC resident).
 #include "spa_common.h"
+#include <type_traits>
 
 namespace spa {
 
-template <bool INTERLEAVED>
-__global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ x, const float* __restrict__ cosT,
+// MODE 0: interleaved pairs (x[2i], x[2i+1]) rotated (LLaMA-jax);
+// MODE 1: rotate_half pairs (x[i], x[i+hd/2]);
+// MODE 2: Gemma-ref quirk (gemma/gemma.ipynb:182-200: per-position dense matrix with
+//         2x2 blocks [[cos, cos], [-sin, sin]], NOT a rotation) applied elementwise:
+//         y_e = c (x_e + x_o), y_o = s (x_o - x_e); "inverse" applies the transpose
+//         (the exact backward of the forward map).
+template <typename DT, int MODE>
+__global__ __launch_bounds__(256) void rope_kernel(DT* __restrict__ x, const float* __restrict__ cosT,
                                                    const float* __restrict__ sinT, const int* __restrict__ pos,
                                                    long sb, long st, long sh, int B, int T, int nrot, int hd,
                                                    int pos_off, float sign) {
@@ -28,10 +35,10 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ x, const f
     const int t = r % T;
     const int b = r / T;
     const int ps = pos ? pos[b * T + t] : t + pos_off;
-    bf16* p = x + b * sb + t * st + hh * sh;
+    DT* p = x + b * sb + t * st + hh * sh;
     const float* c = cosT + (long)ps * (hd / 2);
     const float* s = sinT + (long)ps * (hd / 2);
-    if constexpr (INTERLEAVED) {
+    if constexpr (MODE == 0 || MODE == 2) {
       float a[8];
       load8(p + v * 8, a);
       const f32x4 cv = *reinterpret_cast<const f32x4*>(c + v * 4);
@@ -39,9 +46,18 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ x, const f
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float x0 = a[2 * k], x1 = a[2 * k + 1];
-        const float cs = cv[k], sn = sign * sv[k];
-        a[2 * k] = x0 * cs - x1 * sn;
-        a[2 * k + 1] = x0 * sn + x1 * cs;
+        const float cs = cv[k];
+        if constexpr (MODE == 0) {
+          const float sn = sign * sv[k];
+          a[2 * k] = x0 * cs - x1 * sn;
+          a[2 * k + 1] = x0 * sn + x1 * cs;
+        } else if (sign > 0.f) {   // forward: [[c, c], [-s, s]] x
+          a[2 * k] = cs * (x0 + x1);
+          a[2 * k + 1] = sv[k] * (x1 - x0);
+        } else {                   // transpose: [[c, -s], [c, s]] dy
+          a[2 * k] = cs * x0 - sv[k] * x1;
+          a[2 * k + 1] = cs * x0 + sv[k] * x1;
+        }
       }
       store8(p + v * 8, a);
     } else {
@@ -67,14 +83,15 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ x, const f
 
 // x: [B, T, NH, hd] view (hd contiguous), rotates heads [0, nrot). In place.
 void rope_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const c10::optional<at::Tensor>& pos,
-           int64_t nrot, int64_t pos_off, bool interleaved, bool inverse) {
-  SPA_CHECK_CUDA(x); SPA_CHECK_BF16(x);
+           int64_t nrot, int64_t pos_off, int64_t mode, bool inverse) {
+  SPA_CHECK_CUDA(x);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "rope: bf16/fp32");
   TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "rope: x must be [B,T,NH,hd] with contiguous hd");
   const int B = x.size(0), T = x.size(1), hd = x.size(3);
   TORCH_CHECK(hd % 16 == 0, "rope: hd must be a multiple of 16");
   TORCH_CHECK(nrot <= x.size(2));
   TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous() && cos.size(1) == hd / 2);
-  TORCH_CHECK(x.stride(1) % 8 == 0 && x.stride(2) % 8 == 0 && x.stride(0) % 8 == 0);
+  TORCH_CHECK(x.stride(1) % 8 == 0 && x.stride(2) % 8 == 0 && x.stride(0) % 8 == 0 && (uintptr_t)x.data_ptr() % 16 == 0);
   if (pos) { TORCH_CHECK(pos->scalar_type() == at::kInt && pos->is_contiguous() && pos->numel() == (int64_t)B * T); }
   else { TORCH_CHECK(pos_off + T <= cos.size(0), "rope: table too short"); }
   DeviceGuard g(x.device());
@@ -83,21 +100,28 @@ void rope_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, co
   const int grid = (int)std::min<long>((total + 255) / 256, 4096);
   auto st = stream();
   const float sign = inverse ? -1.f : 1.f;
-  if (interleaved)
-    rope_kernel<true><<<grid, 256, 0, st>>>((bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(),
-                                            pos ? pos->data_ptr<int>() : nullptr, x.stride(0), x.stride(1),
-                                            x.stride(2), B, T, (int)nrot, hd, (int)pos_off, sign);
-  else
-    rope_kernel<false><<<grid, 256, 0, st>>>((bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(),
-                                             pos ? pos->data_ptr<int>() : nullptr, x.stride(0), x.stride(1),
-                                             x.stride(2), B, T, (int)nrot, hd, (int)pos_off, sign);
+  auto launch = [&](auto modec) {
+    constexpr int M = decltype(modec)::value;
+    if (x.scalar_type() == at::kBFloat16)
+      rope_kernel<bf16, M><<<grid, 256, 0, st>>>((bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                                                 pos ? pos->data_ptr<int>() : nullptr, x.stride(0), x.stride(1),
+                                                 x.stride(2), B, T, (int)nrot, hd, (int)pos_off, sign);
+    else
+      rope_kernel<float, M><<<grid, 256, 0, st>>>(x.data_ptr<float>(), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                                                  pos ? pos->data_ptr<int>() : nullptr, x.stride(0), x.stride(1),
+                                                  x.stride(2), B, T, (int)nrot, hd, (int)pos_off, sign);
+  };
+  if (mode == 0) launch(std::integral_constant<int, 0>{});
+  else if (mode == 1) launch(std::integral_constant<int, 1>{});
+  else if (mode == 2) launch(std::integral_constant<int, 2>{});
+  else TORCH_CHECK(false, "rope: mode must be 0, 1 or 2");
   SPA_LAUNCH_CHECK();
 }
 
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
-  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int nrot, int pos_off, bool interleaved, "
+  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int nrot, int pos_off, int mode, "
         "bool inverse) -> ()");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("rope_", &spa::rope_); }

@@ -44,9 +44,11 @@ def _templates(C: int, H: int, W: int, classes: int, seed: int) -> np.ndarray:
 
 
 def synthetic_images(n: int, C: int = 1, H: int = 28, W: int = 28, classes: int = 10, seed: int = 0,
-                     noise: float = 0.15) -> Tuple[torch.Tensor, torch.Tensor]:
+                     noise: float = 0.15, template_seed: int = 1234) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``template_seed`` fixes the class templates (shared by train and test splits);
+    ``seed`` draws labels, shifts and noise."""
     rng = np.random.default_rng(seed + 1)
-    temp = _templates(C, H, W, classes, seed)
+    temp = _templates(C, H, W, classes, template_seed)
     y = rng.integers(0, classes, n)
     x = temp[y].copy()
     sh = rng.integers(-2, 3, (n, 2))

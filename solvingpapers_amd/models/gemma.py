@@ -1,0 +1,259 @@
+"""Gemma: reference-parity model (gemma/gemma.ipynb) and a paper-style Gemma-7B-shape
+MQA model with tensor parallelism (BASELINE.json config #4).
+
+GemmaRef reproduces the notebook exactly:
+  RMSNorm fp32 eps 1e-6 :139-159; the "rotary" per-position dense matrix :169-208 (here
+  the fused gemma_ref mode of the HIP rope kernel — no (T, D, D) materialisation);
+  MQA :218-259 with heads//kv_heads = 2 full-width (D) query projections, one shared
+  K and V, -inf mask then /sqrt(D), dropout on the attention output, concat -> Linear
+  (2D->D); GeGLU :269-286 (exact-erf GELU, hidden 4D) + dropout; pre-norm decoder
+  :320-337; Embedding (no sqrt(D) scale) -> dropout -> 12 layers -> norm -> Linear
+  with bias (untied) :347-368. State-dict keys are identical to the reference.
+
+Gemma (paper-style): fused QKV GEMM, true RoPE, H query heads x hd 256 with ONE KV head
+(MQA), GeGLU fused [gate|up] GEMM + HIP glu kernel, sqrt(D)-scaled tied embedding,
+RMSNorm; ``tp`` > 1 shards query heads, GeGLU hidden and the vocabulary over a TP
+process group (K/V replicated because Hkv = 1 < tp; see parallel/tensor_parallel.py).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, replace
+from typing import Optional
+
+import torch
+import torch.nn as tnn
+
+from .. import nn as snn
+from ..ops import attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
+from ..ops.attention import flash_attention
+from ..ops.misc import dropout
+from ..ops.rope import gemma_ref_rotate
+from ..utils.grad import mark_ready
+
+
+# =============================================================================== reference
+@dataclass
+class GemmaRefConfig:
+    block_size: int = 128
+    batch_size: int = 64
+    embeddings_dims: int = 768
+    attn_dropout: float = 0.1
+    no_of_heads: int = 4
+    dropout: float = 0.1
+    max_lr: float = 2.5e-4
+    no_of_decoder_layers: int = 12
+    no_kv_heads: int = 2
+    vocab_size: int = 65
+    total_steps: int = 5000
+    eval_iters: int = 100
+
+
+class _RMS(tnn.Module):
+    def __init__(self, D):
+        super().__init__()
+        self.rmsnorm_layer = snn.RMSNorm(D, 1e-6)
+
+    def forward(self, x):
+        return self.rmsnorm_layer(x)
+
+
+class MQARef(tnn.Module):
+    def __init__(self, c: GemmaRefConfig):
+        super().__init__()
+        D = c.embeddings_dims
+        self.c = c
+        self.no_of_q_heads = c.no_of_heads // c.no_kv_heads if c.no_kv_heads > 0 else 1
+        self.multi_query = tnn.ModuleList([snn.Linear(D, D, bias=False) for _ in range(self.no_of_q_heads)])
+        self.key = snn.Linear(D, D, bias=False)
+        self.value = snn.Linear(D, D, bias=False)
+        self.linear_layer = snn.Linear(D * self.no_of_q_heads, D, bias=False)
+
+    def forward(self, x):
+        B, T, D = x.shape
+        p = self.c.attn_dropout if self.training else 0.0
+        q = torch.stack([qp(x) for qp in self.multi_query], dim=2)      # [B, T, Hq, D]
+        k = self.key(x).unsqueeze(2)                                      # [B, T, 1, D]
+        v = self.value(x).unsqueeze(2)
+        o = flash_attention(gemma_ref_rotate(q), gemma_ref_rotate(k), v, causal=True, scale=1.0 / math.sqrt(D))
+        o = dropout(o, p, self.training)                                  # dropout on each head's output
+        return dropout(self.linear_layer(o.reshape(B, T, -1)), p, self.training)
+
+
+class GeGLURef(tnn.Module):
+    def __init__(self, D):
+        super().__init__()
+        self.linear_layer1 = snn.Linear(D, 4 * D, bias=False)
+        self.linear_layer2 = snn.Linear(D, 4 * D, bias=False)
+        self.linear_layer3 = snn.Linear(4 * D, D, bias=False)
+
+    def forward(self, x):
+        # act(l1 x) * (l2 x) through the fused HIP glu kernel on the concatenated outputs
+        gu = torch.cat([self.linear_layer1(x), self.linear_layer2(x)], dim=-1)
+        return self.linear_layer3(glu(gu, "gelu"))
+
+
+class FFNRef(tnn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.gglu = GeGLURef(c.embeddings_dims)
+        self.p = c.dropout
+
+    def forward(self, x):
+        return dropout(self.gglu(x), self.p, self.training)
+
+
+class DecoderLayerRef(tnn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.feedforward_network = FFNRef(c)
+        self.mqa = MQARef(c)
+        self.norm1 = _RMS(c.embeddings_dims)
+        self.norm2 = _RMS(c.embeddings_dims)
+
+    def forward(self, x):
+        x = x + self.mqa(self.norm1(x))
+        return x + self.feedforward_network(self.norm2(x))
+
+
+class GemmaRef(tnn.Module):
+    def __init__(self, c: GemmaRefConfig = GemmaRefConfig()):
+        super().__init__()
+        self.c = c
+        self.embeddings = snn.Embedding(c.vocab_size, c.embeddings_dims)
+        self.decoder = tnn.Sequential(*[DecoderLayerRef(c) for _ in range(c.no_of_decoder_layers)])
+        self.linear_layer = snn.Linear(c.embeddings_dims, c.vocab_size)
+        self.norm = _RMS(c.embeddings_dims)
+
+    def forward(self, x, targets=None):
+        x = dropout(self.embeddings(x), self.c.dropout, self.training)
+        x = self.norm(self.decoder(x))
+        if targets is None:
+            return self.linear_layer(x)
+        return linear_cross_entropy(x.reshape(-1, x.shape[-1]), self.linear_layer.weight, targets.reshape(-1),
+                                    bias=self.linear_layer.bias)
+
+    @torch.no_grad()
+    def generate(self, idx, max_new_tokens, generator=None):
+        """gemma.ipynb:608-630: crop to block_size, softmax + multinomial."""
+        was = self.training
+        self.eval()
+        for _ in range(max_new_tokens):
+            lg = self(idx[:, -self.c.block_size:])[:, -1].float()
+            idx = torch.cat([idx, torch.multinomial(torch.softmax(lg, -1), 1, generator=generator)], 1)
+        self.train(was)
+        return idx
+
+
+# =============================================================================== paper-style
+@dataclass
+class GemmaConfig:
+    vocab_size: int = 256000
+    dim: int = 3072
+    n_layers: int = 28
+    n_heads: int = 16
+    n_kv_heads: int = 1           # MQA (BASELINE.json config #4)
+    head_dim: int = 256
+    ffn_hidden: int = 24576
+    max_seq_len: int = 8192
+    norm_eps: float = 1e-6
+    rope_theta: float = 10000.0
+    batch_size: int = 1
+
+
+PRESETS = {
+    "gemma_ref": GemmaRefConfig(),
+    "gemma_7b_mqa": GemmaConfig(),
+    "gemma_tiny": GemmaConfig(vocab_size=1024, dim=512, n_layers=2, n_heads=8, n_kv_heads=1, head_dim=64,
+                              ffn_hidden=1024, max_seq_len=256),
+}
+
+
+def config(name, **kw):
+    return replace(PRESETS[name], **kw)
+
+
+class GemmaBlock(tnn.Module):
+    def __init__(self, c: GemmaConfig, tp_size: int = 1, **fk):
+        super().__init__()
+        self.c, self.tp = c, tp_size
+        assert c.n_heads % tp_size == 0 and c.ffn_hidden % tp_size == 0
+        self.hl = c.n_heads // tp_size                                   # local query heads
+        self.attn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
+        self.wq = tnn.Parameter(torch.empty(self.hl * c.head_dim, c.dim, **fk))      # column-parallel
+        self.wkv = tnn.Parameter(torch.empty(2 * c.n_kv_heads * c.head_dim, c.dim, **fk))  # replicated
+        self.wo = tnn.Parameter(torch.empty(c.dim, self.hl * c.head_dim, **fk))      # row-parallel
+        self.ffn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
+        self.w13 = tnn.Parameter(torch.empty(2 * c.ffn_hidden // tp_size, c.dim, **fk))  # column-parallel [gate|up]
+        self.w2 = tnn.Parameter(torch.empty(c.dim, c.ffn_hidden // tp_size, **fk))       # row-parallel
+        self.wkv.tp_replicated = True
+
+    @torch.no_grad()
+    def reset_parameters(self, g):
+        for w in (self.wq, self.wkv, self.wo, self.w13, self.w2):
+            w.normal_(0.0, 0.02, generator=g)
+
+    def forward(self, res, delta, tp_group=None):
+        from ..parallel.tensor_parallel import copy_to_tp, reduce_from_tp, reduce_grad_tp
+        c = self.c
+        if res is None:
+            n1, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
+        else:
+            n1, h = rms_norm(delta, self.attn_norm, c.norm_eps, residual=res)
+        B, T, _ = n1.shape
+        hd, KV = c.head_dim, c.n_kv_heads
+        n1p = copy_to_tp(n1, tp_group)
+        q = linear(n1p, self.wq)                                         # [B, T, hl*hd]
+        kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)              # replicated K/V, grads summed over TP
+        qkv = torch.cat([q, kv], dim=-1)
+        qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, 0, interleaved=False, head_dim=hd)
+        o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
+        a = reduce_from_tp(linear(o, self.wo), tp_group)
+        n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
+        f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
+        return h2, reduce_from_tp(linear(f, self.w2), tp_group)
+
+
+class Gemma(tnn.Module):
+    def __init__(self, c: GemmaConfig, device=None, dtype=torch.float32, tp_group=None, seed=0):
+        super().__init__()
+        from ..parallel.tensor_parallel import tp_rank_size
+        self.c = c
+        self.tp_group = tp_group
+        self.tp_rank, self.tp = tp_rank_size(tp_group)
+        assert c.vocab_size % self.tp == 0
+        fk = dict(device=device, dtype=dtype)
+        self.embed = tnn.Parameter(torch.empty(c.vocab_size // self.tp, c.dim, **fk))   # vocab-parallel, tied head
+        self.layers = tnn.ModuleList([GemmaBlock(c, self.tp, **fk) for _ in range(c.n_layers)])
+        self.norm_f = tnn.Parameter(torch.ones(c.dim, **fk))
+        self.grad_ready_cb = None
+        with torch.no_grad():
+            g = torch.Generator(device=self.embed.device).manual_seed(seed + 1000 * self.tp_rank)
+            self.embed.normal_(0.0, 0.02, generator=g)
+            gl = torch.Generator(device=self.embed.device).manual_seed(seed)  # replicated params identical
+            for l in self.layers:
+                l.reset_parameters(gl)
+
+    def param_groups(self):
+        return [[self.embed]] + [list(l.parameters()) for l in self.layers] + [[self.norm_f]]
+
+    def forward(self, ids, targets=None):
+        from ..parallel.tensor_parallel import vocab_parallel_cross_entropy, vocab_parallel_embedding
+        c = self.c
+        x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim))
+        res, delta = None, x
+        for i, l in enumerate(self.layers):
+            delta = mark_ready(delta, self.grad_ready_cb, i + 1)
+            res, delta = l(res, delta, self.tp_group)
+        delta = mark_ready(delta, self.grad_ready_cb, len(self.layers) + 1)
+        n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
+        if targets is None:
+            from ..parallel.tensor_parallel import gather_vocab_logits
+            return gather_vocab_logits(linear(n, self.embed), self.tp_group)
+        return vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, targets.reshape(-1), self.tp_group)
+
+    def flops_per_token(self, T):
+        c = self.c
+        per = c.dim * (c.n_heads + 2 * c.n_kv_heads) * c.head_dim + c.dim * c.n_heads * c.head_dim + \
+            3 * c.dim * c.ffn_hidden
+        return 6 * (c.n_layers * per + c.vocab_size * c.dim) + 6 * c.n_layers * c.n_heads * c.head_dim * T

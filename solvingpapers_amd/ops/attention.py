@@ -108,3 +108,27 @@ def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None):
     x4 = qkv.view(B, T, H + 2 * Hkv, hd)
     q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
     return flash_attention(q, k, v, causal, scale).reshape(B, T, H * hd)
+
+
+def attention_dropout(q, k, v, causal=True, scale=None, p=0.0, training=True, neg=float("-inf")):
+    """Materialised attention with dropout on the probability matrix (GPT-ref
+    gpt/gpt-jax.ipynb:351 / DeepSeek-ref attention dropout). Used only when a
+    reference preset trains with attention-weight dropout; inference and p=0 take
+    the flash kernels. q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd]."""
+    from .misc import dropout
+    if not training or p == 0.0:
+        return flash_attention(q, k, v, causal, scale)
+    B, Tq, H, hd = q.shape
+    Tk, Hkv = k.shape[1], k.shape[2]
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
+    rep = H // Hkv
+    qh = q.transpose(1, 2)
+    kh = k.transpose(1, 2).repeat_interleave(rep, dim=1)
+    vh = v.transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = torch.matmul(qh, kh.transpose(-1, -2)).float() * scale
+    if causal:
+        i = torch.arange(Tq, device=q.device)[:, None]
+        j = torch.arange(Tk, device=q.device)[None, :]
+        s = s.masked_fill(j > i + (Tk - Tq), neg)
+    pr = dropout(torch.softmax(s, dim=-1).to(q.dtype), p, training)
+    return torch.matmul(pr, vh).transpose(1, 2)

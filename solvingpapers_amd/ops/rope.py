@@ -12,6 +12,13 @@ import torch
 from . import _ext, reference
 
 
+def _mode(interleaved):
+    """interleaved=True -> 0, False (rotate_half) -> 1, "gemma_ref" -> 2."""
+    if interleaved == "gemma_ref":
+        return 2
+    return 0 if interleaved else 1
+
+
 class RopeCache:
     """Per-(device, hd, theta) cos/sin tables [Tmax, hd/2] fp32, grown on demand."""
 
@@ -34,7 +41,7 @@ class _RopeFn(torch.autograd.Function):
     def forward(ctx, x, nrot, cos, sin, pos_off, interleaved, grad_inplace, hd):
         # x may be [B, T, NH*hd] (packed projection output) or [B, T, NH, hd]
         x4 = x.view(x.shape[0], x.shape[1], -1, hd)
-        _ext.ops().rope_(x4, cos, sin, None, nrot, pos_off, interleaved, False)
+        _ext.ops().rope_(x4, cos, sin, None, nrot, pos_off, _mode(interleaved), False)
         ctx.mark_dirty(x)
         ctx.args = (nrot, cos, sin, pos_off, interleaved, grad_inplace, hd)
         return x
@@ -47,7 +54,7 @@ class _RopeFn(torch.autograd.Function):
         # fresh dqkv), so the inverse rotation runs in place; otherwise copy first.
         if not (grad_inplace and g.is_contiguous()):
             g = g.contiguous().clone()
-        _ext.ops().rope_(g.view(g.shape[0], g.shape[1], -1, hd), cos, sin, None, nrot, pos_off, interleaved, True)
+        _ext.ops().rope_(g.view(g.shape[0], g.shape[1], -1, hd), cos, sin, None, nrot, pos_off, _mode(interleaved), True)
         return g, None, None, None, None, None, None, None
 
 
@@ -76,6 +83,34 @@ def apply_rope(x, theta=10000.0, pos_off=0, interleaved=True, positions=None, re
         return _RopeFn.apply(x.clone(), H, cos, sin, pos_off, interleaved, False, hd)
     if x.is_cuda:
         y = x.clone()
-        _ext.ops().rope_(y, cos, sin, positions.int().contiguous(), H, 0, interleaved, False)
+        _ext.ops().rope_(y, cos, sin, positions.int().contiguous(), H, 0, _mode(interleaved), False)
         return y
     return reference.rope(x, cos, sin, pos_off, interleaved, positions=positions)
+
+
+def gemma_ref_tables(T, D, device):
+    """gemma/gemma.ipynb:182-200 quirk: angle depends on position only,
+    theta_p = 10000^(-2(p-1)/D), angle = p*theta_p; broadcast to [T, D/2]."""
+    key = ("gemma_ref", str(device), T, D)
+    tab = RopeCache._tables.get(key)
+    if tab is None:
+        p = torch.arange(T, dtype=torch.float64)
+        ang = p * (10000.0 ** (-2.0 * (p - 1) / D))
+        cos = ang.cos().float()[:, None].expand(T, D // 2).contiguous().to(device)
+        sin = ang.sin().float()[:, None].expand(T, D // 2).contiguous().to(device)
+        tab = (cos, sin)
+        RopeCache._tables[key] = tab
+    return tab
+
+
+def gemma_ref_rotate(x):
+    """Apply the reference's per-position (D x D) 'rotary' matrix (2x2 blocks
+    [[cos, cos], [-sin, sin]]) to every head of x [B, T, H, D] without
+    materialising the (T, D, D) matrix: y_e = c(x_e + x_o), y_o = s(x_o - x_e)."""
+    B, T, H, D = x.shape
+    cos, sin = gemma_ref_tables(T, D, x.device)
+    if x.is_cuda:
+        return _RopeFn.apply(x.contiguous().clone(), H, cos, sin, 0, "gemma_ref", False, D)
+    xe, xo = x[..., 0::2].float(), x[..., 1::2].float()
+    c, s = cos[None, :, None, :], sin[None, :, None, :]
+    return torch.stack([c * (xe + xo), s * (xo - xe)], -1).flatten(-2).to(x.dtype)

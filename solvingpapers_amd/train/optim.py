@@ -28,6 +28,7 @@ class FlatOptimizer:
         self.step_count = 0
         # ranges of the flat buffer this optimizer owns (all, or this rank's ZeRO shard)
         self.ranges = shard[0] if shard else [(0, flat.numel)]
+        self.sharded = shard is not None          # ZeRO-1: grad-norm partials summed over the DP group
         self.norm_group = shard[1] if shard else None
         self.use_master = flat.param_dtype != torch.float32
         self.last_grad_norm: Optional[torch.Tensor] = None
@@ -98,9 +99,10 @@ class FlatOptimizer:
         for a, b in self.ranges:
             s = K.sqsum(self.flat.grad[a:b])
             tot = s if tot is None else tot + s
-        if self.norm_group is not None:
+        if self.sharded:
             import torch.distributed as dist
-            dist.all_reduce(tot, group=self.norm_group)
+            if dist.is_initialized():
+                dist.all_reduce(tot, group=self.norm_group)
         return tot.sqrt()
 
     def clip_coef(self):

