@@ -1,0 +1,555 @@
+// Mixture-of-Experts kernels for gfx950: router top-k, deterministic token permute,
+// row gather / weighted combine, and an MFMA grouped GEMM (fwd, dX, dW) whose
+// per-expert row counts live on the device (no host sync, no per-expert launches).
+//
+// Reference: deepseekv3/deepseekv3.ipynb:1014-1088 (MoeLayer): gate GEMM -> +routing_bias
+// -> topk(2) -> softmax over the masked (top-k only) logits -> shared expert + Python
+// loop over 8 experts with boolean gathers, a host sync per expert (`mask.any()`) and
+// masked_scatter_; aux-free bias update sign(mean - load). Here the loop becomes:
+//   moe_route      one wave per token: top-k (register insertion sort) + renormalised
+//                  softmax over the selected logits (+ optional bias in the weights);
+//   moe_permute    per-expert stable counting sort -> perm / inverse / offsets [E+1];
+//   gather_rows    x_perm[i] = x[perm[i] / k]  (16-byte vectors);
+//   grouped_gemm   Y_e = X_e W_e^T  and its two backward products, one launch each;
+//   combine        y[n] = sum_j w[n,j] * y_perm[inv[n,j]]  (gather form: deterministic).
+#include "spa_common.h"
+
+namespace spa {
+
+// --------------------------------------------------------------------------- router
+// logits [N, E] fp32; bias [E] (may be null). Outputs idx [N, k] int32 (descending score),
+// w [N, k] fp32 = softmax over the k selected values of (logits + bias if bias_in_w else logits).
+template <int MAXK>
+__global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict__ logits, const float* __restrict__ bias,
+                                                        int* __restrict__ idx, float* __restrict__ w, int N, int E,
+                                                        int k, int bias_in_w) {
+  const int tok = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (tok >= N) return;
+  const float* lg = logits + (long)tok * E;
+  // each lane keeps its best candidates; merge k times with wave argmax
+  float sel_v[MAXK];
+  int sel_i[MAXK];
+  float prev = INFINITY;
+  int prev_i = -1;
+  for (int j = 0; j < k; ++j) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int e = lane; e < E; e += 64) {
+      const float v = lg[e] + (bias ? bias[e] : 0.f);
+      // strictly below the previous pick (ties broken by lower index first)
+      const bool ok = (v < prev) || (v == prev && e > prev_i);
+      if (ok && (v > best || (v == best && e < bi))) { best = v; bi = e; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    sel_v[j] = best;
+    sel_i[j] = bi;
+    prev = best;
+    prev_i = bi;
+  }
+  if (lane == 0) {
+    float m = -INFINITY;
+    for (int j = 0; j < k; ++j) {
+      const float v = bias_in_w ? sel_v[j] : lg[sel_i[j]];
+      sel_v[j] = v;
+      m = fmaxf(m, v);
+    }
+    float z = 0.f;
+    for (int j = 0; j < k; ++j) z += __expf(sel_v[j] - m);
+    for (int j = 0; j < k; ++j) {
+      idx[(long)tok * k + j] = sel_i[j];
+      w[(long)tok * k + j] = __expf(sel_v[j] - m) / z;
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- permute
+// Block per expert: stable order of assignments a = n*k + j with idx[a] == e.
+// perm[off_e + r] = a ; inv[a] = off_e + r. counts computed by a first pass kernel.
+__global__ __launch_bounds__(256) void moe_count_kernel(const int* __restrict__ idx, int A, int E,
+                                                        int* __restrict__ counts) {
+  const int e = blockIdx.x;
+  __shared__ int red[4];
+  int c = 0;
+  for (int a = threadIdx.x; a < A; a += 256) c += idx[a] == e;
+  c = (int)block_sum<256>((float)c, (float*)red);
+  if (threadIdx.x == 0) counts[e] = c;
+}
+__global__ void moe_offsets_kernel(const int* __restrict__ counts, int E, int* __restrict__ offsets) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    int s = 0;
+    for (int e = 0; e < E; ++e) { offsets[e] = s; s += counts[e]; }
+    offsets[E] = s;
+  }
+}
+__global__ __launch_bounds__(256) void moe_scatter_kernel(const int* __restrict__ idx, int A,
+                                                          const int* __restrict__ offsets, int* __restrict__ perm,
+                                                          int* __restrict__ inv) {
+  const int e = blockIdx.x;
+  __shared__ int wcount[4];
+  int base = offsets[e];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int a0 = 0; a0 < A; a0 += 256) {
+    const int a = a0 + threadIdx.x;
+    const bool hit = a < A && idx[a] == e;
+    const unsigned long long bal = __ballot(hit);
+    const int before = __popcll(bal & ((1ULL << lane) - 1ULL));
+    if (lane == 0) wcount[wv] = __popcll(bal);
+    __syncthreads();
+    int woff = 0;
+    for (int i = 0; i < wv; ++i) woff += wcount[i];
+    const int tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    if (hit) {
+      const int pos = base + woff + before;
+      perm[pos] = a;
+      inv[a] = pos;
+    }
+    base += tot;
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------------------------------- gather / combine
+// rows are moved as 16-byte units (bf16 or fp32 rows alike): nv = row_bytes / 16
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint4* __restrict__ x, const int* __restrict__ perm,
+                                                          uint4* __restrict__ out, int rows, int nv, int div) {
+  const long total = (long)rows * nv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / nv;
+    const int c = i % nv;
+    out[r * nv + c] = x[(long)(perm[r] / div) * nv + c];
+  }
+}
+// y[n] = sum_j w[n, j] * yp[inv[n*k + j]]; also usable for the dX of the gather (w = 1)
+template <typename T>
+__global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ yp, const int* __restrict__ inv,
+                                                      const float* __restrict__ w, T* __restrict__ y, int N, int D,
+                                                      int k) {
+  const int dv = D / 8;
+  const long total = (long)N * dv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long n = i / dv;
+    const int c = (i % dv) * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const float wj = w ? w[n * k + j] : 1.f;
+      float v[8];
+      load8(yp + (long)inv[n * k + j] * D + c, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * v[q];
+    }
+    store8(y + n * D + c, acc);
+  }
+}
+// dw[n, j] = <dy[n], yp[inv[n*k+j]]>  (gradient of the combine weights), one wave per (n, j)
+template <typename T>
+__global__ __launch_bounds__(256) void combine_dw_kernel(const T* __restrict__ dy, const T* __restrict__ yp,
+                                                         const int* __restrict__ inv, float* __restrict__ dw, int N,
+                                                         int D, int k) {
+  const int a = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (a >= N * k) return;
+  const long n = a / k;
+  const T* yr = yp + (long)inv[a] * D;
+  const T* dr = dy + n * D;
+  float acc = 0.f;
+  for (int c = lane * 8; c < D; c += 512) {
+    float u[8], v[8];
+    load8(dr + c, u);
+    load8(yr + c, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc += u[q] * v[q];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) dw[a] = acc;
+}
+// rows of yp scaled by per-assignment weight: out[i] = w[perm[i]] * g[perm[i]/k] (dY_perm of the combine)
+template <typename T>
+__global__ __launch_bounds__(256) void scatter_grad_kernel(const T* __restrict__ g, const int* __restrict__ perm,
+                                                           const float* __restrict__ w, T* __restrict__ out, int rows,
+                                                           int D, int k) {
+  const int dv = D / 8;
+  const long total = (long)rows * dv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / dv;
+    const int c = (i % dv) * 8;
+    const int a = perm[r];
+    const float wa = w[a];
+    float v[8];
+    load8(g + (long)(a / k) * D + c, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] *= wa;
+    store8(out + r * D + c, v);
+  }
+}
+
+// --------------------------------------------------------------------------- grouped GEMM
+// C (M x N, row-major, ldc) = A (M x K) * B (K x N), grouped by expert. Operand storage:
+//   A_KC: A stored [M][K] (lda) else [K][M];  B_KC: B stored [N][K] (ldb) else [K][N].
+// GROUP_K = false: groups split M (rows of A and C): expert e owns rows [off_e, off_e+1),
+//                  B_e = B + e * strideB.   (fwd:  X_e W_e^T ; dX: dY_e W_e)
+// GROUP_K = true : groups split K (the token dim): C_e = C + e * strideC, reduction over
+//                  rows [off_e, off_e+1) of the token-major A and B. (dW_e = dY_e^T X_e)
+// Tile 128x128x32, 4 waves as 2x2 of 64x64; MFMA 32x32x16 bf16, computing C^T per wave
+// so the epilogue stores 4 consecutive columns (8 bytes) per lane.
+// LDS: K-contiguous tiles [128][32] with an 8-byte-unit XOR swizzle (u ^ (r>>2)&7);
+// K-strided tiles [32][128] read with ds_read_b64_tr_b16 and the attention image swizzle.
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+template <bool KC>
+struct OpTile {
+  // element offset of (row r, 8-byte unit u) in a [128][32] K-contiguous tile
+  static __device__ __forceinline__ int kc_off(int r, int u) { return r * 32 + 4 * (u ^ ((r >> 2) & 7)); }
+  // element offset of (k row r, 16B chunk ch) in a [32][128] K-strided tile
+  static __device__ __forceinline__ int ks_off(int r, int ch) {
+    return r * 128 + 8 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+  }
+};
+
+__device__ __forceinline__ bf16x8 ld_kc(const bf16* t, int row, int s, int hh) {
+  // MFMA operand with permuted k order: k = 16s + 4hh + {0..3}, 16s + 8 + 4hh + {0..3}
+  typedef OpTile<true> O;
+  const bf16x4 a = *reinterpret_cast<const bf16x4*>(t + O::kc_off(row, 4 * s + hh));
+  const bf16x4 b = *reinterpret_cast<const bf16x4*>(t + O::kc_off(row, 4 * s + 2 + hh));
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 ld_ks(const bf16* t, int col0, int s, int lane) {
+  typedef OpTile<false> O;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3, hh = lane >> 5;
+  const int c = col0 + 16 * (g & 1) + 4 * pp;
+  const int ra = 16 * s + 4 * hh + q, rb = ra + 8;
+  typedef __attribute__((address_space(3))) s16x4_t L;
+  const s16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((L*)(t + O::ks_off(ra, c >> 3) + (c & 7)));
+  const s16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((L*)(t + O::ks_off(rb, c >> 3) + (c & 7)));
+  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
+  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <bool A_KC, bool B_KC, bool GROUP_K>
+__global__ __launch_bounds__(256) void grouped_gemm_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           bf16* __restrict__ C, const int* __restrict__ offsets,
+                                                           int E, int M, int N, int K, long lda, long ldb, long ldc,
+                                                           long strideB, long strideC, int accumulate) {
+  constexpr int BM = 128, BN = 128, BK = 32;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM * BK + BN * BK)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;   // 2x2 waves, 64x64 each
+  const int nnt = (N + BN - 1) / BN;
+  const int nt = blockIdx.x % nnt;
+  int mt = blockIdx.x / nnt;
+  // ---- decode (expert, tile) ----
+  int e = 0, m0 = 0, mend = M, k0 = 0, kend = K;
+  const bf16* Bp = B;
+  bf16* Cp = C;
+  if (!GROUP_K) {
+    for (e = 0; e < E; ++e) {
+      const int cnt = offsets[e + 1] - offsets[e];
+      const int tiles = (cnt + BM - 1) / BM;
+      if (mt < tiles) break;
+      mt -= tiles;
+    }
+    if (e >= E) return;
+    m0 = offsets[e] + mt * BM;
+    mend = offsets[e + 1];
+    Bp = B + e * strideB;
+  } else {
+    // grid.x = E * (M/BM) * nnt : blocks of one expert cover its whole output C_e
+    const int nmt = (M + BM - 1) / BM;
+    e = mt / nmt;
+    mt = mt % nmt;
+    if (e >= E) return;
+    m0 = mt * BM;
+    k0 = offsets[e];
+    kend = offsets[e + 1];
+    Cp = C + e * strideC;
+  }
+  const int n0 = nt * BN;
+  // ---- staging: 256 threads, A tile 128x32 = 512 chunks of 8, B tile 512 chunks ----
+  bf16x8 ra[2], rb[2];
+  auto load_tiles = [&](int kk) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int idx = tid + c * 256;
+      if (A_KC) {  // [128 rows][32 k]: row = idx/4, kchunk = idx%4
+        const int r = idx >> 2, kc = (idx & 3) * 8;
+        const int gm = m0 + r, gk = kk + kc;
+        ra[c] = (gm < mend && gk < kend) ? *reinterpret_cast<const bf16x8*>(A + (long)gm * lda + gk) : bf16x8{};
+      } else {     // [32 k][128 m]: k = idx/16, mchunk = idx%16
+        const int r = idx >> 4, mc = (idx & 15) * 8;
+        const int gk = kk + r, gm = m0 + mc;
+        ra[c] = (gk < kend && gm < mend) ? *reinterpret_cast<const bf16x8*>(A + (long)gk * lda + gm) : bf16x8{};
+      }
+      if (B_KC) {  // [128 n][32 k]
+        const int r = idx >> 2, kc = (idx & 3) * 8;
+        const int gn = n0 + r, gk = kk + kc;
+        rb[c] = (gn < N && gk < kend) ? *reinterpret_cast<const bf16x8*>(Bp + (long)gn * ldb + gk) : bf16x8{};
+      } else {     // [32 k][128 n]
+        const int r = idx >> 4, nc = (idx & 15) * 8;
+        const int gk = kk + r, gn = n0 + nc;
+        rb[c] = (gk < kend && gn < N) ? *reinterpret_cast<const bf16x8*>(Bp + (long)gk * ldb + gn) : bf16x8{};
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    bf16* At = smem + buf * (BM * BK + BN * BK);
+    bf16* Bt = At + BM * BK;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int idx = tid + c * 256;
+      if (A_KC) {
+        const int r = idx >> 2, u = (idx & 3) * 2;
+        *reinterpret_cast<bf16x4*>(At + OpTile<true>::kc_off(r, u)) = __builtin_shufflevector(ra[c], ra[c], 0, 1, 2, 3);
+        *reinterpret_cast<bf16x4*>(At + OpTile<true>::kc_off(r, u + 1)) = __builtin_shufflevector(ra[c], ra[c], 4, 5, 6, 7);
+      } else {
+        const int r = idx >> 4, ch = idx & 15;
+        *reinterpret_cast<bf16x8*>(At + OpTile<false>::ks_off(r, ch)) = ra[c];
+      }
+      if (B_KC) {
+        const int r = idx >> 2, u = (idx & 3) * 2;
+        *reinterpret_cast<bf16x4*>(Bt + OpTile<true>::kc_off(r, u)) = __builtin_shufflevector(rb[c], rb[c], 0, 1, 2, 3);
+        *reinterpret_cast<bf16x4*>(Bt + OpTile<true>::kc_off(r, u + 1)) = __builtin_shufflevector(rb[c], rb[c], 4, 5, 6, 7);
+      } else {
+        const int r = idx >> 4, ch = idx & 15;
+        *reinterpret_cast<bf16x8*>(Bt + OpTile<false>::ks_off(r, ch)) = rb[c];
+      }
+    }
+  };
+  f32x16 acc[2][2];  // [n sub-tile][m sub-tile]: C^T tiles (rows = n, cols = m)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int kt = (kend - k0 + BK - 1) / BK;
+  const int l32 = lane & 31, hh = lane >> 5;
+  if (kt > 0) {
+    load_tiles(k0);
+    store_tiles(0);
+    if (kt > 1) load_tiles(k0 + BK);
+  }
+  __syncthreads();
+  for (int t = 0; t < kt; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < kt) {
+      store_tiles(buf ^ 1);
+      if (t + 2 < kt) load_tiles(k0 + (t + 2) * BK);
+    }
+    const bf16* At = smem + buf * (BM * BK + BN * BK);
+    const bf16* Bt = At + BM * BK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int mrow = wm * 64 + j * 32;
+        af[j] = A_KC ? ld_kc(At, mrow + l32, s, hh) : ld_ks(At, mrow, s, lane);
+        const int ncol = wn * 64 + j * 32;
+        bfr[j] = B_KC ? ld_kc(Bt, ncol + l32, s, hh) : ld_ks(Bt, ncol, s, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)  // C^T[n][m] += B^T-frag (rows n) x A-frag^T (cols m)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // ---- epilogue: lane holds column m = l32 of each C^T tile, rows n = 8g + 4hh + {0..3}
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gm = m0 + wm * 64 + j * 32 + l32;
+      if (GROUP_K ? gm >= M : gm >= mend) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int gn = n0 + wn * 64 + i * 32 + 8 * g + 4 * hh;
+        if (gn >= N) continue;
+        bf16* cp = Cp + (long)gm * ldc + gn;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
+        if (accumulate) {
+          const bf16x4 o = *reinterpret_cast<const bf16x4*>(cp);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += (float)o[q];
+        }
+        bf16x4 w4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+        *reinterpret_cast<bf16x4*>(cp) = w4;
+      }
+    }
+}
+
+// --------------------------------------------------------------------------- host
+std::vector<at::Tensor> moe_route(const at::Tensor& logits_, const c10::optional<at::Tensor>& bias, int64_t k,
+                                  bool bias_in_w) {
+  auto logits = logits_.contiguous().to(at::kFloat);
+  const int N = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(k >= 1 && k <= 8 && k <= E, "moe_route: 1 <= k <= 8");
+  DeviceGuard g(logits.device());
+  auto idx = at::empty({N, k}, logits.options().dtype(at::kInt));
+  auto w = at::empty({N, k}, logits.options());
+  if (N == 0) return {idx, w};
+  at::Tensor b = bias ? bias->contiguous().to(at::kFloat) : at::Tensor();
+  moe_route_kernel<8><<<cdiv(N, 4), 256, 0, stream()>>>(logits.data_ptr<float>(), bias ? b.data_ptr<float>() : nullptr,
+                                                       idx.data_ptr<int>(), w.data_ptr<float>(), N, E, k,
+                                                       bias_in_w ? 1 : 0);
+  SPA_LAUNCH_CHECK();
+  return {idx, w};
+}
+
+// returns (perm [A], inv [A], offsets [E+1], counts [E]) for assignments idx [N, k]
+std::vector<at::Tensor> moe_permute(const at::Tensor& idx_, int64_t E) {
+  auto idx = idx_.contiguous();
+  TORCH_CHECK(idx.scalar_type() == at::kInt);
+  const int A = idx.numel();
+  DeviceGuard g(idx.device());
+  auto opts = idx.options();
+  auto perm = at::empty({A}, opts), inv = at::empty({A}, opts);
+  auto counts = at::empty({E}, opts), offsets = at::empty({E + 1}, opts);
+  auto st = stream();
+  moe_count_kernel<<<E, 256, 0, st>>>(idx.data_ptr<int>(), A, E, counts.data_ptr<int>());
+  moe_offsets_kernel<<<1, 64, 0, st>>>(counts.data_ptr<int>(), E, offsets.data_ptr<int>());
+  moe_scatter_kernel<<<E, 256, 0, st>>>(idx.data_ptr<int>(), A, offsets.data_ptr<int>(), perm.data_ptr<int>(),
+                                        inv.data_ptr<int>());
+  SPA_LAUNCH_CHECK();
+  return {perm, inv, offsets, counts};
+}
+
+at::Tensor moe_gather(const at::Tensor& x_, const at::Tensor& perm, int64_t div) {
+  auto x = x_.contiguous();
+  const int D = x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat));
+  const int rows = perm.numel();
+  DeviceGuard g(x.device());
+  auto out = at::empty({rows, D}, x.options());
+  if (rows == 0) return out;
+  const int nv = D * (int)x.element_size() / 16;
+  const int grid = (int)std::min<long>(((long)rows * nv + 255) / 256, 16384);
+  gather_rows_kernel<<<grid, 256, 0, stream()>>>((const uint4*)x.data_ptr(), perm.data_ptr<int>(),
+                                                 (uint4*)out.data_ptr(), rows, nv, div);
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor moe_combine(const at::Tensor& yp_, const at::Tensor& inv, const c10::optional<at::Tensor>& w,
+                       int64_t N, int64_t k) {
+  auto yp = yp_.contiguous();
+  const int D = yp.size(-1);
+  DeviceGuard g(yp.device());
+  auto y = at::empty({N, D}, yp.options());
+  if (N == 0) return y;
+  const int grid = (int)std::min<long>((N * D / 8 + 255) / 256, 16384);
+  const float* wp = w ? w->data_ptr<float>() : nullptr;
+  if (yp.scalar_type() == at::kBFloat16)
+    combine_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)yp.data_ptr(), inv.data_ptr<int>(), wp,
+                                                     (bf16*)y.data_ptr(), N, D, k);
+  else
+    combine_kernel<float><<<grid, 256, 0, stream()>>>(yp.data_ptr<float>(), inv.data_ptr<int>(), wp,
+                                                      y.data_ptr<float>(), N, D, k);
+  SPA_LAUNCH_CHECK();
+  return y;
+}
+
+// backward of combine: (dyp [A, D] = w * dy rows in permuted order, dw [N, k])
+std::vector<at::Tensor> moe_combine_bwd(const at::Tensor& dy_, const at::Tensor& yp_, const at::Tensor& perm,
+                                        const at::Tensor& inv, const at::Tensor& w, int64_t k) {
+  auto dy = dy_.contiguous(), yp = yp_.contiguous();
+  const int N = dy.size(0), D = dy.size(1);
+  const int A = perm.numel();
+  DeviceGuard g(dy.device());
+  auto dyp = at::empty({A, D}, dy.options());
+  auto dw = at::empty({N, k}, dy.options().dtype(at::kFloat));
+  if (A == 0) return {dyp, dw};
+  auto st = stream();
+  const int grid = (int)std::min<long>(((long)A * D / 8 + 255) / 256, 16384);
+  if (dy.scalar_type() == at::kBFloat16) {
+    scatter_grad_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dy.data_ptr(), perm.data_ptr<int>(),
+                                                    w.data_ptr<float>(), (bf16*)dyp.data_ptr(), A, D, k);
+    combine_dw_kernel<bf16><<<cdiv(A, 4), 256, 0, st>>>((const bf16*)dy.data_ptr(), (const bf16*)yp.data_ptr(),
+                                                        inv.data_ptr<int>(), dw.data_ptr<float>(), N, D, k);
+  } else {
+    scatter_grad_kernel<float><<<grid, 256, 0, st>>>(dy.data_ptr<float>(), perm.data_ptr<int>(), w.data_ptr<float>(),
+                                                     dyp.data_ptr<float>(), A, D, k);
+    combine_dw_kernel<float><<<cdiv(A, 4), 256, 0, st>>>(dy.data_ptr<float>(), yp.data_ptr<float>(),
+                                                         inv.data_ptr<int>(), dw.data_ptr<float>(), N, D, k);
+  }
+  SPA_LAUNCH_CHECK();
+  return {dyp, dw};
+}
+
+// mode 0: Y[M,N] = X[M,K] W_e[N,K]^T   (rows grouped by offsets; W [E, N, K])
+// mode 1: dX[M,K] = dY[M,N] W_e[N,K]   (rows grouped; W [E, N, K])
+// mode 2: dW_e[N,K] = dY_e[.,N]^T X_e[.,K]  (token dim grouped; out [E, N, K]); accumulate -> +=
+at::Tensor grouped_gemm(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t mode,
+                        const c10::optional<at::Tensor>& out_, bool accumulate) {
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "grouped_gemm: bf16");
+  TORCH_CHECK(a.is_contiguous() && w.is_contiguous() && offsets.scalar_type() == at::kInt);
+  const int E = offsets.numel() - 1;
+  DeviceGuard g(a.device());
+  auto st = stream();
+  if (mode == 0 || mode == 1) {
+    TORCH_CHECK(w.dim() == 3 && w.size(0) == E);
+    const int M = a.size(0);
+    const int Nw = w.size(1), Kw = w.size(2);
+    const int N = mode == 0 ? Nw : Kw;   // output cols
+    const int K = mode == 0 ? Kw : Nw;   // reduction
+    TORCH_CHECK(a.size(1) == K, "grouped_gemm: A/W shape mismatch");
+    TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "grouped_gemm: dims must be multiples of 8");
+    auto out = out_ ? *out_ : at::empty({M, N}, a.options());
+    if (M == 0) return out;
+    const int nnt = cdiv(N, 128);
+    const int mtiles = cdiv(M, 128) + E;  // upper bound on per-expert m-tiles
+    if (mode == 0)
+      grouped_gemm_kernel<true, true, false><<<mtiles * nnt, 256, 0, st>>>(
+          (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,
+          N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0);
+    else
+      grouped_gemm_kernel<true, false, false><<<mtiles * nnt, 256, 0, st>>>(
+          (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,
+          N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0);
+    SPA_LAUNCH_CHECK();
+    return out;
+  }
+  TORCH_CHECK(mode == 2, "grouped_gemm: mode 0/1/2");
+  // a = dY [T, N], w = X [T, K]  -> out [E, N, K]
+  const int N = a.size(1), K = w.size(1);
+  TORCH_CHECK(a.size(0) == w.size(0) && N % 8 == 0 && K % 8 == 0);
+  auto out = out_ ? *out_ : at::empty({E, N, K}, a.options());
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * N * K);
+  if (E == 0) return out;
+  // C_e (M=N rows, N=K cols) = A (dY^T, stored [k=token][m]) * B (X, stored [k=token][n])
+  const int nnt = cdiv(K, 128), nmt = cdiv(N, 128);
+  grouped_gemm_kernel<false, false, true><<<E * nmt * nnt, 256, 0, st>>>(
+      (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K,
+      0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0);
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("moe_route(Tensor logits, Tensor? bias, int k, bool bias_in_w) -> Tensor[]");
+  m.def("moe_permute(Tensor idx, int E) -> Tensor[]");
+  m.def("moe_gather(Tensor x, Tensor perm, int div) -> Tensor");
+  m.def("moe_combine(Tensor yp, Tensor inv, Tensor? w, int N, int k) -> Tensor");
+  m.def("moe_combine_bwd(Tensor dy, Tensor yp, Tensor perm, Tensor inv, Tensor w, int k) -> Tensor[]");
+  m.def("grouped_gemm(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("moe_route", &spa::moe_route);
+  m.impl("moe_permute", &spa::moe_permute);
+  m.impl("moe_gather", &spa::moe_gather);
+  m.impl("moe_combine", &spa::moe_combine);
+  m.impl("moe_combine_bwd", &spa::moe_combine_bwd);
+  m.impl("grouped_gemm", &spa::grouped_gemm);
+}

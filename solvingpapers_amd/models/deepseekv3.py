@@ -1,0 +1,665 @@
+"""DeepSeek-V3: multi-head latent attention + DeepSeekMoE (shared + routed experts with
+aux-loss-free balancing) + multi-token prediction — deepseekv3/deepseekv3.ipynb.
+
+One model class, two attention families selected by the config:
+
+``attention="ref"`` (preset ``dsv3_ref``) reproduces the notebook exactly (SURVEY
+Appendix A Q1-Q5): per-head latents ``W_dkv`` (:1143-1148), absorbed query
+``x @ (query.W^T W_k.W)`` scored against the latent, values ``W_v(latent)``; the
+``kv_cache`` threaded through every head and layer (:1256-1261,1406-1408) plus the
+``tril(T, Tc)`` mask means every head of every layer attends ONLY to layer-0/head-0's
+latent — so here that latent ``L0`` is computed once and all layers attend to it with
+a single H-head / 1-KV-head flash attention (``k = v = L0``, hd = latent) followed by
+the per-head ``W_v`` up-projection (the absorbed-V form, identical math). Sinusoidal
+PE (:836-842), tied embedding/LM head (:1393,1501), ``x * 2 * L^-0.5`` before the final
+RMSNorm (:1411), torch RMSNorm with eps = finfo(fp32).eps (:914), MoE with
+softmax-over-(logits+bias)-top-k gating and the SOFT-mass bias update (:1041-1086).
+
+``attention="mla"`` (presets ``dsv3_style`` / ``dsv3_tiny``) is the paper's MLA: one
+shared compressed KV latent per layer (kv_lora) + a decoupled RoPE key shared across
+heads, optional low-rank query, per-head nope/rope/v dims; training runs the flash
+kernel on the up-projected heads, cached decoding runs in latent space with the
+up-projections absorbed (cache = kv_lora + rope floats per token per layer). Routing
+bias steers selection only and is updated from token COUNTS all-reduced over the
+data/expert-parallel group; MTP depth-k modules predict token i+k+1.
+
+Routed experts run through ops/moe.py (HIP router, counting-sort permute, MFMA grouped
+GEMMs, weighted combine) or parallel/expert_parallel.py under EP. Expert hidden sizes
+are padded to a multiple of 8 internally (zero rows/cols: exact, gradients stay zero)
+so the reference's 1365 runs on the vectorised kernels; the reference state-dict
+exporter slices the padding off.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, replace
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as tnn
+
+from ..ops import apply_rope, embedding, glu, layer_norm, linear, linear_cross_entropy, rms_norm
+from ..ops.attention import FLASH_HD, attention_dropout, flash_attention
+from ..ops.misc import dropout
+from ..ops.moe import route
+from ..utils.grad import mark_ready
+from .llama3 import sample
+
+FP32_EPS = float(torch.finfo(torch.float32).eps)
+
+
+@dataclass
+class DSV3Config:
+    vocab_size: int = 50257
+    block_size: int = 256
+    dim: int = 512
+    n_layers: int = 6
+    n_heads: int = 8
+    attention: str = "ref"          # "ref" (notebook latent heads) | "mla" (paper MLA)
+    latent_dim: int = 64            # ref: per-head latent width
+    q_lora_rank: int = 0            # mla
+    kv_lora_rank: int = 512
+    qk_nope_dim: int = 64
+    qk_rope_dim: int = 64
+    v_head_dim: int = 128
+    rope_theta: float = 10000.0
+    pos_emb: str = "sinusoidal"     # "sinusoidal" (ref) | "none"
+    n_experts: int = 8
+    top_k: int = 2
+    n_shared: int = 1
+    expert_hidden: int = 0          # 0 -> (2*D*4)//3 (reference SWiGLUExpert)
+    n_dense_layers: int = 0         # leading layers with a dense SwiGLU FFN
+    dense_hidden: int = 0
+    aux_free: bool = True
+    bias_update_rate: float = 1e-3
+    bias_in_weights: bool = True    # ref: softmax over (logits + bias); paper: bias steers selection only
+    balance_stat: str = "soft"      # "soft" (ref Q4: probability mass) | "counts" (tokens, all-reduced)
+    dropout: float = 0.1
+    attn_dropout: float = 0.1
+    final_scale: bool = True        # x * 2 * L^-0.5 before the final norm
+    norm_eps: float = FP32_EPS
+    mtp_heads: int = 0
+    mtp_lambda: float = 0.3
+    init_std: float = 0.02
+    # reference training hyper-parameters (deepseekv3.ipynb:369-396,1923-1934)
+    batch_size: int = 16
+    max_lr: float = 6e-4
+    min_lr: float = 6e-5
+    warmup_iters: int = 400
+    total_iters: int = 10000
+    weight_decay: float = 0.1
+    beta1: float = 0.9
+    beta2: float = 0.95
+    eps: float = 1e-8
+    clip: float = 1.0
+
+    @property
+    def head_size(self):
+        return self.dim // self.n_heads
+
+    @property
+    def ffn_hidden(self):
+        return self.expert_hidden or (self.dim * 2 * 4) // 3
+
+    @property
+    def qk_head_dim(self):
+        return self.qk_nope_dim + self.qk_rope_dim
+
+
+PRESETS = {
+    "dsv3_ref": DSV3Config(),
+    "dsv3_tiny": DSV3Config(vocab_size=512, block_size=128, dim=256, n_layers=2, n_heads=4, attention="mla",
+                            kv_lora_rank=64, qk_nope_dim=32, qk_rope_dim=32, v_head_dim=64, n_experts=8, top_k=2,
+                            n_shared=1, expert_hidden=128, n_dense_layers=1, dense_hidden=512, pos_emb="none",
+                            bias_in_weights=False, balance_stat="counts", final_scale=False, norm_eps=1e-6,
+                            dropout=0.0, attn_dropout=0.0, mtp_heads=1),
+    # DeepSeek-V2-Lite-like widths (D2048, 16 heads, kv_lora 512, 64 routed experts top-6 +
+    # 2 shared, hidden 1408, 1 dense layer), qk = 64 nope + 64 rope = 128 = v so attention
+    # stays on the hd-128 flash kernel. Depth is a bench knob.
+    "dsv3_style": DSV3Config(vocab_size=102400, block_size=4096, dim=2048, n_layers=12, n_heads=16,
+                             attention="mla", q_lora_rank=0, kv_lora_rank=512, qk_nope_dim=64, qk_rope_dim=64,
+                             v_head_dim=128, n_experts=64, top_k=6, n_shared=2, expert_hidden=1408,
+                             n_dense_layers=1, dense_hidden=10944, pos_emb="none", bias_in_weights=False,
+                             balance_stat="counts", final_scale=False, norm_eps=1e-6, dropout=0.0,
+                             attn_dropout=0.0, mtp_heads=1, batch_size=1),
+}
+
+
+def config(name, **kw):
+    return replace(PRESETS[name], **kw)
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+def sinusoidal_pe(block_size, dim, device=None):
+    """deepseekv3.ipynb:836-842 (fp32, [1, T, D])."""
+    pe = torch.zeros(block_size, dim, device=device)
+    pos = torch.arange(0, block_size, dtype=torch.float, device=device).unsqueeze(1)
+    div = torch.exp(torch.arange(0, dim, 2, dtype=torch.float, device=device) * (-math.log(10000.0) / dim))
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe.unsqueeze(0)
+
+
+# =============================================================================== attention
+class RefLatentAttention(tnn.Module):
+    """MHLA of the notebook (:1135-1265) with its per-head parameters stacked."""
+
+    def __init__(self, c: DSV3Config, **fk):
+        super().__init__()
+        H, D, L, hs = c.n_heads, c.dim, c.latent_dim, c.head_size
+        self.c = c
+        self.wdkv = tnn.Parameter(torch.empty(H, L, D, **fk))   # heads.h.W_dkv
+        self.wk = tnn.Parameter(torch.empty(H, hs, L, **fk))    # heads.h.W_k
+        self.wv = tnn.Parameter(torch.empty(H, hs, L, **fk))    # heads.h.W_v
+        self.wq = tnn.Parameter(torch.empty(H, hs, D, **fk))    # heads.h.query
+        self.wo = tnn.Parameter(torch.empty(D, D, **fk))        # linear
+
+    def params(self):
+        return [self.wdkv, self.wk, self.wv, self.wq, self.wo]
+
+    def latent0(self, xn):
+        return linear(xn, self.wdkv[0])                          # [B, T, latent]
+
+    def forward(self, xn, L0, cache=None, pos=0):
+        c = self.c
+        B, T, D = xn.shape
+        H, L, hs = c.n_heads, c.latent_dim, c.head_size
+        # absorbed query weights A_h = query_h^T W_k_h  -> one [D, H*L] GEMM
+        A = torch.einsum("hsd,hsl->hld", self.wq, self.wk).reshape(H * L, D)
+        q = linear(xn, A).view(B, T, H, L)
+        kv = L0.unsqueeze(2)                                     # one shared "head": k = v = L0
+        if cache is not None:
+            kv = cache[:, :pos + T].unsqueeze(2)
+        p = c.attn_dropout if self.training else 0.0
+        o = attention_dropout(q, kv, kv, causal=True, scale=hs ** -0.5, p=p, training=self.training)
+        o = torch.einsum("bthl,hsl->bths", o, self.wv).reshape(B, T, H * hs)
+        return dropout(linear(o, self.wo), p, self.training)
+
+
+class MLA(tnn.Module):
+    """Paper MLA: c_kv = norm(W_dkv x)[:kv_lora], k_rope = RoPE(W_dkv x)[kv_lora:] shared by all
+    heads; [k_nope | v] = W_ukv c_kv; q = W_uq norm(W_dq x) (or W_q x)."""
+
+    def __init__(self, c: DSV3Config, **fk):
+        super().__init__()
+        H, D = c.n_heads, c.dim
+        self.c = c
+        qd = H * c.qk_head_dim
+        if c.q_lora_rank:
+            self.wdq = tnn.Parameter(torch.empty(c.q_lora_rank, D, **fk))
+            self.q_norm = tnn.Parameter(torch.ones(c.q_lora_rank, **fk))
+            self.wuq = tnn.Parameter(torch.empty(qd, c.q_lora_rank, **fk))
+        else:
+            self.wq = tnn.Parameter(torch.empty(qd, D, **fk))
+        self.wdkv = tnn.Parameter(torch.empty(c.kv_lora_rank + c.qk_rope_dim, D, **fk))
+        self.kv_norm = tnn.Parameter(torch.ones(c.kv_lora_rank, **fk))
+        self.wukv = tnn.Parameter(torch.empty(H * (c.qk_nope_dim + c.v_head_dim), c.kv_lora_rank, **fk))
+        self.wo = tnn.Parameter(torch.empty(D, H * c.v_head_dim, **fk))
+
+    def params(self):
+        return list(self.parameters())
+
+    def _q(self, xn):
+        c = self.c
+        if c.q_lora_rank:
+            return linear(rms_norm(linear(xn, self.wdq), self.q_norm, c.norm_eps), self.wuq)
+        return linear(xn, self.wq)
+
+    def _latent(self, xn, pos):
+        c = self.c
+        B, T, _ = xn.shape
+        ckr = linear(xn, self.wdkv)
+        ckv = rms_norm(ckr[..., :c.kv_lora_rank].contiguous(), self.kv_norm, c.norm_eps)
+        kr = apply_rope(ckr[..., c.kv_lora_rank:].reshape(B, T, 1, c.qk_rope_dim), c.rope_theta, pos)
+        return ckv, kr
+
+    def forward(self, xn, L0=None, cache=None, pos=0):
+        c = self.c
+        B, T, _ = xn.shape
+        H, dn, dr, dv = c.n_heads, c.qk_nope_dim, c.qk_rope_dim, c.v_head_dim
+        scale = 1.0 / math.sqrt(dn + dr)
+        q = self._q(xn).view(B, T, H, dn + dr)
+        qr = apply_rope(q[..., dn:], c.rope_theta, pos)
+        ckv, kr = self._latent(xn, pos)
+        if cache is not None:
+            return self._decode(q[..., :dn], qr, ckv, kr, cache, pos, scale)
+        kv = linear(ckv, self.wukv).view(B, T, H, dn + dv)
+        qf = torch.cat([q[..., :dn], qr], dim=-1)
+        k = torch.cat([kv[..., :dn], kr.expand(B, T, H, dr)], dim=-1)
+        v = kv[..., dn:]
+        if dv == dn + dr and dv in FLASH_HD:
+            o = flash_attention(qf, k, v.contiguous(), causal=True, scale=scale)
+        else:
+            o = attention_dropout(qf, k, v, causal=True, scale=scale, p=0.0)
+        return linear(o.reshape(B, T, H * dv), self.wo)
+
+    def _decode(self, qn, qr, ckv, kr, cache, pos, scale):
+        """Latent-space attention over the compressed cache (W_uk absorbed into q, W_uv applied
+        after): per token the cache holds kv_lora + rope values instead of 2*H*hd."""
+        c = self.c
+        B, T, H, dn = qn.shape
+        cc, cr = cache
+        cc[:, pos:pos + T] = ckv.to(cc.dtype)
+        cr[:, pos:pos + T] = kr.reshape(B, T, -1).to(cr.dtype)
+        S = pos + T
+        w = self.wukv.view(H, dn + c.v_head_dim, c.kv_lora_rank)
+        q_abs = torch.einsum("bthn,hnc->bthc", qn.float(), w[:, :dn].float())
+        s = (torch.einsum("bthc,bsc->bhts", q_abs, cc[:, :S].float())
+             + torch.einsum("bthr,bsr->bhts", qr.float(), cr[:, :S].float())) * scale
+        i = torch.arange(T, device=s.device)[:, None] + pos
+        j = torch.arange(S, device=s.device)[None, :]
+        s = s.masked_fill(j > i, float("-inf"))
+        o_lat = torch.einsum("bhts,bsc->bthc", torch.softmax(s, -1), cc[:, :S].float())
+        o = torch.einsum("bthc,hvc->bthv", o_lat, w[:, dn:].float()).to(qn.dtype)
+        return linear(o.reshape(B, T, H * c.v_head_dim), self.wo)
+
+
+# =============================================================================== FFN / MoE
+class DenseFFN(tnn.Module):
+    def __init__(self, D, F, **fk):
+        super().__init__()
+        self.F, self.Fp = F, _pad8(F)
+        self.w13 = tnn.Parameter(torch.zeros(2 * self.Fp, D, **fk))    # [gate ; up], padded rows zero
+        self.w2 = tnn.Parameter(torch.zeros(D, self.Fp, **fk))
+
+    @torch.no_grad()
+    def reset_parameters(self, std, g):
+        F, Fp = self.F, self.Fp
+        self.w13.zero_()
+        self.w2.zero_()
+        self.w13[:F].normal_(0, std, generator=g)
+        self.w13[Fp:Fp + F].normal_(0, std, generator=g)
+        self.w2[:, :F].normal_(0, std, generator=g)
+
+    def forward(self, x):
+        return linear(glu(linear(x, self.w13), "silu"), self.w2)
+
+
+class MoE(tnn.Module):
+    """DeepSeekMoE: shared experts + top-k routed experts with aux-free load balancing.
+    Under EP (``ep_group`` of size P) this rank holds experts [r*E/P, (r+1)*E/P)."""
+
+    def __init__(self, c: DSV3Config, ep_group=None, **fk):
+        super().__init__()
+        from ..parallel.expert_parallel import ep_rank_size
+        self.c = c
+        self.ep_group = ep_group
+        self.ep_rank, self.ep = ep_rank_size(ep_group)
+        assert c.n_experts % self.ep == 0
+        El = c.n_experts // self.ep
+        D, F = c.dim, c.ffn_hidden
+        self.F, self.Fp = F, _pad8(F)
+        self.gate = tnn.Parameter(torch.empty(c.n_experts, D, **fk))
+        self.w13 = tnn.Parameter(torch.zeros(El, 2 * self.Fp, D, **fk))
+        self.w2 = tnn.Parameter(torch.zeros(El, D, self.Fp, **fk))
+        self.w13.expert_parallel = self.ep > 1
+        self.w2.expert_parallel = self.ep > 1
+        self.shared = DenseFFN(D, F * c.n_shared, **fk) if c.n_shared else None
+        self.register_buffer("routing_bias", torch.zeros(c.n_experts, device=fk.get("device")))
+        self.balance_group = None      # DP group for the counts all-reduce (set by the trainer)
+        self.last_counts = None
+
+    @torch.no_grad()
+    def reset_parameters(self, std, g):
+        F, Fp = self.F, self.Fp
+        self.gate.normal_(0, std, generator=g)
+        self.w13.zero_()
+        self.w2.zero_()
+        self.w13[:, :F].normal_(0, std, generator=g)
+        self.w13[:, Fp:Fp + F].normal_(0, std, generator=g)
+        self.w2[:, :, :F].normal_(0, std, generator=g)
+        if self.shared is not None:
+            self.shared.reset_parameters(std, g)
+
+    def expert_params(self):
+        return [self.w13, self.w2]
+
+    def forward(self, x):
+        from ..parallel.expert_parallel import ep_moe_ffn
+        c = self.c
+        B, T, D = x.shape
+        x2 = x.reshape(-1, D)
+        logits = torch.mm(x2.float(), self.gate.float().t())
+        idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
+        y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group)
+        if self.shared is not None:
+            y = y + self.shared(x2)
+        self.last_counts = plan.counts
+        if c.aux_free and self.training:
+            self._update_bias(idx, w, plan)
+        return y.view(B, T, D)
+
+    @torch.no_grad()
+    def _update_bias(self, idx, w, plan):
+        c = self.c
+        if c.balance_stat == "soft":            # deepseekv3.ipynb:1082-1086
+            load = torch.zeros(idx.shape[0], c.n_experts, device=w.device).scatter_(1, idx.long(), w).sum(0)
+        else:
+            load = plan.counts.float()
+            grp = self.balance_group
+            if grp is not None or (dist.is_initialized() and dist.get_world_size() > 1):
+                dist.all_reduce(load, group=grp)
+        err = load.mean() - load
+        self.routing_bias.add_(c.bias_update_rate * torch.sign(err))
+
+
+# =============================================================================== layers
+class DSV3Layer(tnn.Module):
+    def __init__(self, c: DSV3Config, dense: bool, ep_group=None, **fk):
+        super().__init__()
+        self.c = c
+        self.attn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
+        self.ffn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
+        self.attn = RefLatentAttention(c, **fk) if c.attention == "ref" else MLA(c, **fk)
+        if dense:
+            self.ffn = DenseFFN(c.dim, c.dense_hidden or c.ffn_hidden, **fk)
+        else:
+            self.ffn = MoE(c, ep_group, **fk)
+
+    @torch.no_grad()
+    def reset_parameters(self, g):
+        std = self.c.init_std
+        for n, p in self.attn.named_parameters():
+            if n.endswith("norm"):
+                p.fill_(1.0)
+            else:
+                p.normal_(0, std, generator=g)
+        self.ffn.reset_parameters(std, g)
+        self.attn_norm.fill_(1.0)
+        self.ffn_norm.fill_(1.0)
+
+    def dense_params(self):
+        ex = {id(p) for p in self.expert_params()}
+        return [p for p in self.parameters() if id(p) not in ex]
+
+    def expert_params(self):
+        return self.ffn.expert_params() if isinstance(self.ffn, MoE) else []
+
+    def forward(self, x, L0=None, cache=None, pos=0):
+        c = self.c
+        xn = rms_norm(x, self.attn_norm, c.norm_eps)
+        if c.attention == "ref" and L0 is None:
+            L0 = self.attn.latent0(xn)                 # the only latent anybody attends to (Q1)
+            if cache is not None:
+                cache[:, pos:pos + x.shape[1]] = L0.to(cache.dtype)
+        a = self.attn(xn, L0, cache, pos)
+        x = x + a
+        x = x + self.ffn(rms_norm(x, self.ffn_norm, c.norm_eps))
+        return x, L0
+
+
+class DeepSeekV3(tnn.Module):
+    def __init__(self, c: DSV3Config, device=None, dtype=torch.float32, seed: int = 0, ep_group=None):
+        super().__init__()
+        self.c = c
+        fk = dict(device=device, dtype=dtype)
+        self.embed = tnn.Parameter(torch.empty(c.vocab_size, c.dim, **fk))     # tied LM head
+        self.layers = tnn.ModuleList([DSV3Layer(c, i < c.n_dense_layers, ep_group, **fk)
+                                      for i in range(c.n_layers)])
+        self.norm_f = tnn.Parameter(torch.ones(c.dim, **fk))
+        # MTP (deepseekv3.ipynb:1466-1485): norm1 on the shifted-token embedding, norm2 on the
+        # previous depth's hidden state, linear_layer [2D -> D], one decoder layer per depth.
+        D = c.dim
+        self.mtp_norm1_w = tnn.Parameter(torch.ones(D, **fk))
+        self.mtp_norm1_b = tnn.Parameter(torch.zeros(D, **fk))
+        self.mtp_norm2_w = tnn.Parameter(torch.ones(D, **fk))
+        self.mtp_norm2_b = tnn.Parameter(torch.zeros(D, **fk))
+        self.mtp_proj = tnn.Parameter(torch.empty(D, 2 * D, **fk))
+        self.mtp_heads = tnn.ParameterList([tnn.Parameter(torch.empty(D, D, **fk)) for _ in range(c.mtp_heads)])
+        self.mtp_layers = tnn.ModuleList([DSV3Layer(c, False, ep_group, **fk) for _ in range(c.mtp_heads)])
+        if c.pos_emb == "sinusoidal":
+            self.register_buffer("pe", sinusoidal_pe(c.block_size, c.dim, device=device).to(dtype))
+        else:
+            self.pe = None
+        self.grad_ready_cb = None
+        self.param_wait_cb = None
+        self.reset_parameters(seed)
+
+    @torch.no_grad()
+    def reset_parameters(self, seed=0):
+        g = torch.Generator(device=self.embed.device).manual_seed(seed)
+        std = self.c.init_std
+        self.embed.normal_(0, std, generator=g)
+        self.norm_f.fill_(1.0)
+        for l in list(self.layers) + list(self.mtp_layers):
+            l.reset_parameters(g)
+        self.mtp_proj.normal_(0, std, generator=g)
+        for h in self.mtp_heads:
+            h.normal_(0, std, generator=g)
+
+    def moe_layers(self) -> List[MoE]:
+        return [l.ffn for l in list(self.layers) + list(self.mtp_layers) if isinstance(l.ffn, MoE)]
+
+    def param_groups(self):
+        """Buckets: [embed], per-layer dense params, [head + MTP dense], then the expert
+        buckets (kept apart so DP skips them under EP)."""
+        head = [self.norm_f, self.mtp_norm1_w, self.mtp_norm1_b, self.mtp_norm2_w, self.mtp_norm2_b,
+                self.mtp_proj] + list(self.mtp_heads)
+        for l in self.mtp_layers:
+            head += l.dense_params()
+        groups = [[self.embed]] + [l.dense_params() for l in self.layers] + [head]
+        return groups + [l.expert_params() for l in list(self.layers) + list(self.mtp_layers) if l.expert_params()]
+
+    # ------------------------------------------------------------------ forward
+    def _embed(self, ids, pos=0):
+        T = ids.shape[1]
+        pe = None if self.pe is None else self.pe[0, pos:pos + T]
+        return embedding(self.embed, ids, pe)
+
+    def hidden(self, ids, caches=None, pos=0):
+        c = self.c
+        wait = self.param_wait_cb or (lambda i: None)
+        wait(0)
+        x = self._embed(ids, pos)
+        x0 = x
+        L0 = None
+        cb = self.grad_ready_cb
+        for i, layer in enumerate(self.layers):
+            wait(i + 1)
+            x = mark_ready(x, cb, i + 1)
+            if c.attention == "ref":
+                x, L0 = layer(x, L0, None if caches is None else caches[0], pos)
+            else:
+                x, _ = layer(x, None, None if caches is None else caches[i], pos)
+        wait(len(self.layers) + 1)
+        x = mark_ready(x, cb, len(self.layers) + 1)
+        x = dropout(x, c.dropout, self.training)
+        if c.final_scale:
+            x = x * (2.0 * c.n_layers ** -0.5)
+        return rms_norm(x, self.norm_f, c.norm_eps), x0
+
+    def logits(self, n):
+        return linear(n, self.embed)
+
+    def forward(self, ids, targets=None):
+        n, x0 = self.hidden(ids)
+        if targets is None:
+            return self.logits(n)
+        D = self.c.dim
+        loss = linear_cross_entropy(n.reshape(-1, D), self.embed, targets.reshape(-1))
+        if self.c.mtp_heads and self.training:
+            loss = loss + self.mtp_loss(n, x0, targets)
+        return loss
+
+    def mtp_loss(self, h, emb, targets):
+        """DeepSeek-V3 MTP: depth k combines h^{k-1}_i with Emb(t_{i+k}) and predicts t_{i+k+1}
+        through the shared head; loss = lambda * mean_k CE_k (targets[:, i] = t_{i+1})."""
+        c = self.c
+        B, T, D = h.shape
+        tot = 0.0
+        for k, layer in enumerate(self.mtp_layers, start=1):
+            if T - k <= 0:
+                break
+            e = layer_norm(emb[:, k:], self.mtp_norm1_w, self.mtp_norm1_b, 1e-6)
+            hp = layer_norm(h[:, :T - k], self.mtp_norm2_w, self.mtp_norm2_b, 1e-6)
+            hk = linear(torch.cat([e, hp], dim=-1), self.mtp_proj)
+            hk, _ = layer(hk)
+            hk = rms_norm(hk, self.norm_f, c.norm_eps)
+            tgt = targets[:, k:]
+            tot = tot + linear_cross_entropy(hk.reshape(-1, D), self.embed, tgt.reshape(-1))
+            h = hk
+        return c.mtp_lambda * tot / max(1, len(self.mtp_layers))
+
+    # ---------------------------------------------------------------- inference
+    def new_cache(self, B, Tmax):
+        c = self.c
+        dev, dt = self.embed.device, self.embed.dtype
+        if c.attention == "ref":
+            return [torch.zeros(B, Tmax, c.latent_dim, device=dev, dtype=dt)]
+        return [(torch.zeros(B, Tmax, c.kv_lora_rank, device=dev, dtype=dt),
+                 torch.zeros(B, Tmax, c.qk_rope_dim, device=dev, dtype=dt)) for _ in self.layers]
+
+    @torch.no_grad()
+    def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None):
+        """Cached decoding (ref: one latent cache, Q1; mla: per-layer compressed cache).
+        Reference sampling (deepseekv3.ipynb:1850-1873) recomputes the whole prefix per token
+        with top-k + temperature; results are identical, the cache removes the recompute."""
+        c = self.c
+        was = self.training
+        self.eval()
+        B, T0 = ids.shape
+        Tmax = min(c.block_size, T0 + max_new_tokens) if c.pos_emb == "sinusoidal" else T0 + max_new_tokens
+        caches = self.new_cache(B, Tmax)
+        out, cur, pos = ids, ids[:, -Tmax:], 0
+        for _ in range(max_new_tokens):
+            if pos + cur.shape[1] > Tmax:
+                break
+            n, _ = self.hidden(cur, caches, pos)
+            lg = self.logits(n[:, -1:]).float()[:, -1]
+            pos += cur.shape[1]
+            nxt = sample(lg, temperature, top_k, greedy, generator)
+            out = torch.cat([out, nxt], 1)
+            cur = nxt
+        self.train(was)
+        return out
+
+    # ------------------------------------------------------------------- metrics
+    def num_params(self, active=False):
+        n = sum(p.numel() for p in self.parameters())
+        if active:
+            for m in self.moe_layers():
+                per = (m.w13.numel() + m.w2.numel()) // m.w13.shape[0]
+                n -= (m.w13.shape[0] - self.c.top_k) * per
+        return n
+
+    def flops_per_token(self, T):
+        """6 x active matmul params (routed: top-k experts) + causal attention."""
+        c = self.c
+        n_mm = self.num_params(active=True) - sum(p.numel() for n, p in self.named_parameters() if p.dim() == 1)
+        if c.attention == "ref":
+            attn = 6 * c.n_layers * c.n_heads * c.latent_dim * T
+        else:
+            attn = 3 * c.n_layers * c.n_heads * (c.qk_head_dim + c.v_head_dim) * T
+        return 6 * n_mm + attn
+
+    # --------------------------------------------------------- reference layout I/O
+    def to_reference_state_dict(self) -> Dict[str, torch.Tensor]:
+        """Keys/shapes of the notebook's ``DeepSeekV3.state_dict()`` (ref attention only)."""
+        c = self.c
+        assert c.attention == "ref", "reference layout exists only for attention='ref'"
+        sd = {}
+        sd["embedding.weight"] = self.embed
+        sd["decoder.embeddings.weight"] = self.embed
+        sd["decoder.linear_layer.weight"] = self.embed
+        sd["decoder.norm.rmsnorm_layer.weight"] = self.norm_f
+        sd["norm1.weight"], sd["norm1.bias"] = self.mtp_norm1_w, self.mtp_norm1_b
+        sd["norm2.weight"], sd["norm2.bias"] = self.mtp_norm2_w, self.mtp_norm2_b
+        sd["linear_layer.weight"] = self.mtp_proj
+        for k, h in enumerate(self.mtp_heads):
+            sd[f"heads.{k}.weight"] = h
+        for i, l in enumerate(self.layers):
+            sd.update(_layer_to_ref(l, f"decoder.decoder.{i}."))
+        for k, l in enumerate(self.mtp_layers):
+            sd.update(_layer_to_ref(l, f"unilayer.{k}."))
+        if self.pe is not None:
+            sd["pe"] = self.pe
+        return {k: v.detach().float().cpu().clone() for k, v in sd.items()}
+
+    @torch.no_grad()
+    def from_reference_state_dict(self, sd):
+        self.embed.copy_(sd["decoder.embeddings.weight"])
+        self.norm_f.copy_(sd["decoder.norm.rmsnorm_layer.weight"])
+        self.mtp_norm1_w.copy_(sd["norm1.weight"])
+        self.mtp_norm1_b.copy_(sd["norm1.bias"])
+        self.mtp_norm2_w.copy_(sd["norm2.weight"])
+        self.mtp_norm2_b.copy_(sd["norm2.bias"])
+        self.mtp_proj.copy_(sd["linear_layer.weight"])
+        for k, h in enumerate(self.mtp_heads):
+            h.copy_(sd[f"heads.{k}.weight"])
+        for i, l in enumerate(self.layers):
+            _layer_from_ref(l, sd, f"decoder.decoder.{i}.")
+        for k, l in enumerate(self.mtp_layers):
+            _layer_from_ref(l, sd, f"unilayer.{k}.")
+        return self
+
+
+def _ffn_to_ref(f, F, prefix, sd, e=None):
+    w13 = f.w13 if e is None else f.w13[e]
+    w2 = f.w2 if e is None else f.w2[e]
+    Fp = w13.shape[0] // 2
+    sd[prefix + "w1.weight"] = w13[:F]
+    sd[prefix + "w2.weight"] = w13[Fp:Fp + F]
+    sd[prefix + "w3.weight"] = w2[:, :F]
+
+
+def _ffn_from_ref(w13, w2, F, sd, prefix):
+    Fp = w13.shape[0] // 2
+    w13.zero_()
+    w2.zero_()
+    w13[:F].copy_(sd[prefix + "w1.weight"])
+    w13[Fp:Fp + F].copy_(sd[prefix + "w2.weight"])
+    w2[:, :F].copy_(sd[prefix + "w3.weight"])
+
+
+def _layer_to_ref(l: DSV3Layer, p):
+    sd = {p + "norm1.rmsnorm_layer.weight": l.attn_norm, p + "norm2.rmsnorm_layer.weight": l.ffn_norm}
+    a = l.attn
+    for h in range(l.c.n_heads):
+        q = f"{p}mhla.heads.{h}."
+        sd[q + "W_dkv.weight"] = a.wdkv[h]
+        sd[q + "W_k.weight"] = a.wk[h]
+        sd[q + "W_v.weight"] = a.wv[h]
+        sd[q + "query.weight"] = a.wq[h]
+    sd[p + "mhla.linear.weight"] = a.wo
+    m = l.ffn
+    sd[p + "moe_block.gate.weight"] = m.gate
+    sd[p + "moe_block.routing_bias"] = m.routing_bias
+    for e in range(m.w13.shape[0]):
+        _ffn_to_ref(m, m.F, f"{p}moe_block.experts.{e}.", sd, e)
+    if m.shared is not None:
+        _ffn_to_ref(m.shared, m.shared.F, p + "moe_block.shared_expert.", sd)
+    return sd
+
+
+def _layer_from_ref(l: DSV3Layer, sd, p):
+    l.attn_norm.copy_(sd[p + "norm1.rmsnorm_layer.weight"])
+    l.ffn_norm.copy_(sd[p + "norm2.rmsnorm_layer.weight"])
+    a = l.attn
+    for h in range(l.c.n_heads):
+        q = f"{p}mhla.heads.{h}."
+        a.wdkv[h].copy_(sd[q + "W_dkv.weight"])
+        a.wk[h].copy_(sd[q + "W_k.weight"])
+        a.wv[h].copy_(sd[q + "W_v.weight"])
+        a.wq[h].copy_(sd[q + "query.weight"])
+    a.wo.copy_(sd[p + "mhla.linear.weight"])
+    m = l.ffn
+    m.gate.copy_(sd[p + "moe_block.gate.weight"])
+    m.routing_bias.copy_(sd[p + "moe_block.routing_bias"])
+    for e in range(m.w13.shape[0]):
+        _ffn_from_ref(m.w13[e], m.w2[e], m.F, sd, f"{p}moe_block.experts.{e}.")
+    if m.shared is not None:
+        _ffn_from_ref(m.shared.w13, m.shared.w2, m.shared.F, sd, p + "moe_block.shared_expert.")
+
+
+def estimate_loss(model, batches):
+    """deepseekv3.ipynb:2098-2125 (mean CE over eval batches, eval mode, no grad)."""
+    was = model.training
+    model.eval()
+    with torch.inference_mode():
+        ls = [float(model(x, y)) for x, y in batches]
+    model.train(was)
+    return sum(ls) / max(1, len(ls))

@@ -1,0 +1,240 @@
+"""Mixture-of-Experts ops: router, token permutation, grouped expert GEMMs, combine.
+
+Replaces the reference's Python expert loop (deepseekv3/deepseekv3.ipynb:1059-1079:
+per-expert boolean gather + ``mask.any()`` host sync + ``masked_scatter_``) with a
+fixed sequence of device kernels whose launch count does not depend on E and which
+never synchronise with the host:
+
+    route   -> top-k ids + renormalised softmax weights          (csrc/kernels/moe.hip)
+    permute -> stable counting sort of the N*k assignments by expert, device offsets
+    gather  -> expert-ordered copy of the token rows
+    grouped_linear (x2, + GLU)  -> one MFMA grouped GEMM per projection for all experts
+    combine -> weighted gather-sum back to token order (deterministic, no atomics)
+
+Each op has a pure-PyTorch path for CPU tensors with identical semantics (used by
+the CPU parity tests and the gloo EP tests).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from ..utils.grad import commit
+from ._ext import ops
+
+
+def _gpu(t):
+    return t.is_cuda
+
+
+# --------------------------------------------------------------------------- routing
+class _RouteFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, bias, k, bias_in_w):
+        logits = logits.float()
+        if _gpu(logits):
+            idx, w = ops().moe_route(logits, bias, k, bias_in_w)
+        else:
+            scores = logits + bias if bias is not None else logits
+            vals, idx = torch.topk(scores, k, dim=-1)
+            sel = vals if bias_in_w else logits.gather(-1, idx)
+            w = torch.softmax(sel, dim=-1)
+            idx = idx.int()
+        ctx.save_for_backward(idx, w)
+        ctx.E = logits.shape[-1]
+        ctx.mark_non_differentiable(idx)
+        return idx, w
+
+    @staticmethod
+    def backward(ctx, _didx, dw):
+        idx, w = ctx.saved_tensors
+        if dw is None:
+            return None, None, None, None
+        dw = dw.float()
+        ds = w * (dw - (w * dw).sum(-1, keepdim=True))
+        dl = torch.zeros(w.shape[0], ctx.E, device=w.device, dtype=torch.float32)
+        dl.scatter_add_(1, idx.long(), ds)
+        return dl, None, None, None
+
+
+def route(logits, k, bias=None, bias_in_weights=True):
+    """Top-k expert choice + softmax over the selected logits.
+
+    ``logits`` [N, E]. ``bias`` (aux-free balancing, [E]) shifts the *selection*; with
+    ``bias_in_weights`` the gating weights are softmax(logits + bias) over the top-k
+    (reference semantics, deepseekv3.ipynb:1041-1051), else softmax of the raw logits
+    (DeepSeek-V3 paper: the bias only steers selection). Returns (idx int32 [N,k], w fp32 [N,k]).
+    """
+    if bias is not None:
+        bias = bias.float()
+    return _RouteFn.apply(logits, bias, int(k), bool(bias_in_weights))
+
+
+# --------------------------------------------------------------------------- permutation
+@dataclass
+class MoEPlan:
+    """Expert-sorted layout of N*k token->expert assignments (a = n*k + j)."""
+    perm: torch.Tensor      # [A] int32: sorted position -> assignment
+    inv: torch.Tensor       # [A] int32: assignment -> sorted position
+    offsets: torch.Tensor   # [E+1] int32 (device): expert e owns rows [off[e], off[e+1])
+    counts: torch.Tensor    # [E] int32
+    k: int
+    n_tokens: int
+
+    @property
+    def n_experts(self):
+        return self.counts.numel()
+
+
+def permute(idx, n_experts) -> MoEPlan:
+    idx = idx.contiguous().int()
+    N, k = idx.shape
+    if _gpu(idx):
+        perm, inv, offsets, counts = ops().moe_permute(idx, n_experts)
+    else:
+        flat = idx.reshape(-1).long()
+        perm = torch.sort(flat, stable=True).indices
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(perm.numel())
+        counts = torch.bincount(flat, minlength=n_experts)
+        offsets = torch.cat([counts.new_zeros(1), counts.cumsum(0)])
+        perm, inv, offsets, counts = perm.int(), inv.int(), offsets.int(), counts.int()
+    return MoEPlan(perm, inv, offsets, counts, k, N)
+
+
+class _GatherFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan):
+        ctx.plan = plan
+        if _gpu(x):
+            return ops().moe_gather(x.contiguous(), plan.perm, plan.k)
+        return x[(plan.perm // plan.k).long()]
+
+    @staticmethod
+    def backward(ctx, g):
+        p = ctx.plan
+        if _gpu(g):
+            return ops().moe_combine(g.contiguous(), p.inv, None, p.n_tokens, p.k), None
+        return g[p.inv.long()].view(p.n_tokens, p.k, -1).sum(1), None
+
+
+def gather(x, plan: MoEPlan):
+    """x [N, D] -> expert-ordered rows [N*k, D] (row i = x[perm[i] // k])."""
+    return _GatherFn.apply(x, plan)
+
+
+class _CombineFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, yp, w, plan):
+        ctx.plan = plan
+        ctx.save_for_backward(yp, w)
+        if _gpu(yp):
+            return ops().moe_combine(yp.contiguous(), plan.inv, w.contiguous(), plan.n_tokens, plan.k)
+        rows = yp[plan.inv.long()].view(plan.n_tokens, plan.k, -1)
+        return (rows.float() * w[..., None]).sum(1).to(yp.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        yp, w = ctx.saved_tensors
+        p = ctx.plan
+        if _gpu(g):
+            dyp, dw = ops().moe_combine_bwd(g.contiguous(), yp, p.perm, p.inv, w.contiguous(), p.k)
+            return dyp, dw, None
+        pl = p.perm.long()
+        wa = w.reshape(-1)[pl]
+        dyp = (g[pl // p.k].float() * wa[:, None]).to(yp.dtype)
+        rows = yp[p.inv.long()].view(p.n_tokens, p.k, -1).float()
+        dw = (rows * g.float()[:, None, :]).sum(-1)
+        return dyp, dw, None
+
+
+def combine(yp, w, plan: MoEPlan):
+    """y[n] = sum_j w[n, j] * yp[inv[n*k + j]] (fp32 accumulation)."""
+    return _CombineFn.apply(yp, w, plan)
+
+
+# --------------------------------------------------------------------------- grouped GEMM
+def _cpu_grouped(a, w, offsets, mode):
+    off = offsets.tolist()
+    if mode == 2:
+        out = a.new_zeros(len(off) - 1, a.shape[1], w.shape[1])
+        for e in range(len(off) - 1):
+            if off[e + 1] > off[e]:
+                out[e] = a[off[e]:off[e + 1]].t() @ w[off[e]:off[e + 1]]
+        return out
+    N = w.shape[1] if mode == 0 else w.shape[2]
+    out = a.new_zeros(a.shape[0], N)
+    for e in range(len(off) - 1):
+        if off[e + 1] > off[e]:
+            we = w[e].t() if mode == 0 else w[e]
+            out[off[e]:off[e + 1]] = a[off[e]:off[e + 1]] @ we
+    return out
+
+
+def grouped_gemm(a, w, offsets, mode, out=None, accumulate=False):
+    """mode 0: a_e @ w_e^T ; mode 1: a_e @ w_e ; mode 2: per-expert a_e^T @ w_e (w = X rows)."""
+    if _gpu(a):
+        return ops().grouped_gemm(a.contiguous(), w.contiguous(), offsets, mode, out, accumulate)
+    r = _cpu_grouped(a, w, offsets, mode)
+    if out is None:
+        return r
+    if accumulate:
+        out.add_(r.view_as(out))
+    else:
+        out.copy_(r.view_as(out))
+    return out
+
+
+class _GroupedLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xp, W, plan):
+        ctx.plan, ctx.W = plan, W
+        ctx.save_for_backward(xp)
+        return grouped_gemm(xp, W, plan.offsets, 0)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xp,) = ctx.saved_tensors
+        W, plan = ctx.W, ctx.plan
+        dy = dy.contiguous()
+        dx = grouped_gemm(dy, W, plan.offsets, 1) if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            def _w(out, acc):
+                if out is None:
+                    return grouped_gemm(dy, xp, plan.offsets, 2)
+                if out.dtype == dy.dtype and out.is_contiguous():
+                    grouped_gemm(dy, xp, plan.offsets, 2, out=out.view(W.shape), accumulate=acc)
+                else:
+                    g = grouped_gemm(dy, xp, plan.offsets, 2)
+                    if acc:
+                        out.add_(g.view_as(out))
+                    else:
+                        out.copy_(g.view_as(out))
+            gw = commit(W, _w)
+        return dx, gw, None
+
+
+def grouped_linear(xp, W, plan: MoEPlan):
+    """Per-expert ``xp[rows_e] @ W[e]^T`` for expert-ordered rows; W [E, out, in]."""
+    return _GroupedLinearFn.apply(xp, W, plan)
+
+
+def moe_ffn(x, idx, w, W13, W2, act="silu"):
+    """Routed SwiGLU/GeGLU experts: sum_j w[n,j] * E_{idx[n,j]}(x[n]).
+
+    ``W13`` [E, 2F, D] = per-expert [gate; up], ``W2`` [E, D, F].
+    """
+    from .activation import glu
+    plan = permute(idx, W13.shape[0])
+    xp = gather(x, plan)
+    h = grouped_linear(xp, W13, plan)
+    h = glu(h, act)
+    yp = grouped_linear(h, W2, plan)
+    return combine(yp, w, plan), plan
+
+
+def load_counts(plan: MoEPlan):
+    """Tokens routed to each expert (device int32 [E]) - the aux-free balancing signal."""
+    return plan.counts

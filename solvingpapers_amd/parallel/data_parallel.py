@@ -13,7 +13,12 @@ reduced gradients onto cuda:0. Here:
   GradReadyMarker the moment the layer's backward finishes, so all-reduce of
   layer i overlaps the backward GEMMs of layers i-1..0;
 * ``zero1=True`` switches each bucket to reduce-scatter, shards AdamW state
-  across ranks (optimizer memory/compute / N) and all-gathers updated params.
+  across ranks (optimizer memory/compute / N) and all-gathers updated params;
+* expert-parallel buckets (every param tagged ``expert_parallel``) hold different
+  experts on each EP rank and already contain the gradient contributions of every
+  rank's tokens (the all-to-all backward brought them home): they are summed only
+  over ``expert_dp_group`` (ranks holding the same experts, None = no replicas) and
+  scaled by 1/world so the objective is the same mean-over-ranks as dense params.
 """
 from __future__ import annotations
 
@@ -27,8 +32,13 @@ from ..utils.flat import FlatParams
 
 
 class DataParallel:
-    def __init__(self, model: torch.nn.Module, flat: FlatParams, group=None, zero1: bool = False):
+    def __init__(self, model: torch.nn.Module, flat: FlatParams, group=None, zero1: bool = False,
+                 expert_dp_group=None):
         self.model = model
+        self.expert_dp_group = expert_dp_group
+        self.expert_buckets = {b.index for b in flat.buckets
+                               if b.params and all(getattr(p, "expert_parallel", False) for p in b.params)}
+        assert not (zero1 and self.expert_buckets), "ZeRO-1 with expert-parallel buckets is not supported"
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -60,6 +70,13 @@ class DataParallel:
         self._launched.add(idx)
         b = self.flat.buckets[idx]
         g = self.flat.grad[b.start:b.end]
+        if idx in self.expert_buckets:
+            grp = self.expert_dp_group
+            if grp is not None and dist.get_world_size(grp) > 1:
+                self._works.append(dist.all_reduce(g, group=grp, async_op=True))
+            self._avg_after.append((g, self.world))
+            return
+        group, world = self.group, self.world
         use_avg = self.backend == "nccl"
         op = dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM
         if self.zero1:
@@ -67,11 +84,11 @@ class DataParallel:
             out = g[self.rank * n:(self.rank + 1) * n]
             w = dist.reduce_scatter_tensor(out, g, op=op, group=self.group, async_op=True)
             if not use_avg:
-                self._avg_after.append(out)
+                self._avg_after.append((out, world))
         else:
-            w = dist.all_reduce(g, op=op, group=self.group, async_op=True)
+            w = dist.all_reduce(g, op=op, group=group, async_op=True)
             if not use_avg:
-                self._avg_after.append(g)
+                self._avg_after.append((g, world))
         self._works.append(w)
 
     def _on_ready(self, key):
@@ -96,8 +113,8 @@ class DataParallel:
             self._reduce_bucket(i)
         for w in self._works:
             w.wait()
-        for t in self._avg_after:
-            t.div_(self.world)
+        for t, n in self._avg_after:
+            t.div_(n)
         self._works.clear()
         self._avg_after.clear()
         self._launched.clear()

@@ -1,0 +1,113 @@
+"""Expert parallelism: each rank of an EP group owns E/P experts; tokens travel to
+their experts and back with two variable-size all-to-alls over RCCL (xGMI is a full
+point-to-point mesh inside a node, so one all-to-all uses all 7 links at once).
+
+The reference keeps all 8 experts on every replica and runs them in a Python loop
+(deepseekv3/deepseekv3.ipynb:1018,1059-1079). Dispatch here:
+
+1. local routing + ``permute`` (device counting sort by global expert id);
+2. per-expert counts exchanged with one tiny all-to-all; the split sizes are the only
+   host sync (one D2H copy of 2*E ints per MoE layer);
+3. token rows exchanged (``all_to_all_single`` with uneven splits) — they arrive
+   ordered by (source rank, local expert) and are regrouped to (local expert, source);
+4. the local experts run as ONE grouped GEMM per projection (csrc/kernels/moe.hip);
+5. the inverse regroup + all-to-all return the rows; ``combine`` applies the gate
+   weights in the original token order.
+
+Expert parameters carry ``p.expert_parallel = True``: DataParallel does not
+all-reduce them across the EP group (each rank holds different experts) and the
+optimizer's grad-norm sums their squares over the EP group.
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import torch
+import torch.distributed as dist
+
+from ..ops.activation import glu
+from ..ops.moe import combine, gather, grouped_linear, permute
+
+
+def ep_rank_size(group):
+    if group is None or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+class _AllToAll(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, out_splits, in_splits, group):
+        ctx.splits, ctx.group = (out_splits, in_splits), group
+        out = x.new_empty((sum(out_splits),) + tuple(x.shape[1:]))
+        dist.all_to_all_single(out, x.contiguous(), out_splits, in_splits, group=group)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        out_splits, in_splits = ctx.splits
+        dx = g.new_empty((sum(in_splits),) + tuple(g.shape[1:]))
+        dist.all_to_all_single(dx, g.contiguous(), in_splits, out_splits, group=ctx.group)
+        return dx, None, None, None
+
+
+def all_to_all(x, out_splits, in_splits, group):
+    return _AllToAll.apply(x, list(out_splits), list(in_splits), group)
+
+
+def _regroup_index(rc):
+    """rc [P, El] rows received from (src, local expert), laid out src-major.
+    Returns (idx, offsets): idx[j] = source row of expert-major position j."""
+    P, El = rc.shape
+    starts = torch.cat([rc.new_zeros(1), rc.reshape(-1).cumsum(0)[:-1]]).view(P, El)
+    pieces = []
+    for e in range(El):
+        for s in range(P):
+            n = int(rc[s, e])
+            if n:
+                pieces.append(torch.arange(int(starts[s, e]), int(starts[s, e]) + n))
+    idx = torch.cat(pieces) if pieces else torch.zeros(0, dtype=torch.long)
+    per_e = rc.sum(0)
+    offsets = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
+    return idx, offsets
+
+
+def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu"):
+    """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
+    [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
+    ``W2`` [E/P, D, F] are this rank's experts. Returns (y [N, D], local plan)."""
+    rank, P = ep_rank_size(group)
+    plan = permute(idx, n_experts)
+    if P == 1:
+        xp = gather(x, plan)
+        h = glu(grouped_linear(xp, W13, plan), act)
+        return combine(grouped_linear(h, W2, plan), w, plan), plan
+    El = n_experts // P
+    assert El * P == n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
+    counts = plan.counts.to(torch.int64)
+    recv = torch.empty_like(counts)
+    dist.all_to_all_single(recv, counts, group=group)       # recv[(src, e_local)]
+    both = torch.stack([counts, recv]).cpu()                 # the single host sync
+    send_splits = both[0].view(P, El).sum(1).tolist()
+    rc = both[1].view(P, El)
+    recv_splits = rc.sum(1).tolist()
+    xp = gather(x, plan)                                      # [A, D] sorted by global expert
+    xr = all_to_all(xp, recv_splits, send_splits, group)     # [R, D] (src, e_local) order
+    ridx, loff = _regroup_index(rc)
+    dev = x.device
+    ridx = ridx.to(dev)
+    inv = torch.empty_like(ridx)
+    inv[ridx] = torch.arange(ridx.numel(), device=dev)
+    lplan = SimpleNamespace(offsets=loff.to(device=dev, dtype=torch.int32))
+    xl = xr.index_select(0, ridx)
+    h = glu(grouped_linear(xl, W13, lplan), act)
+    yl = grouped_linear(h, W2, lplan)
+    yr = yl.index_select(0, inv)
+    yp = all_to_all(yr, send_splits, recv_splits, group)
+    return combine(yp, w, plan), plan
+
+
+def shard_experts(full_w, rank, P):
+    """Slice [E, ...] expert weights to this EP rank's [E/P, ...] block."""
+    El = full_w.shape[0] // P
+    return full_w[rank * El:(rank + 1) * El]

@@ -20,8 +20,12 @@ from ..utils.flat import FlatParams
 
 class FlatOptimizer:
     def __init__(self, flat: FlatParams, lr: float, weight_decay: float = 0.0, max_grad_norm: Optional[float] = None,
-                 shard: Optional[Tuple[List[Tuple[int, int]], object]] = None):
+                 shard: Optional[Tuple[List[Tuple[int, int]], object]] = None, ep_group=None):
         self.flat = flat
+        # expert-parallel buckets: their squared-norm partial is summed over the EP group
+        self.ep_group = ep_group
+        self.expert_ranges = [(b.start, b.end) for b in flat.buckets
+                              if b.params and all(getattr(p, "expert_parallel", False) for p in b.params)]
         self.lr = lr
         self.weight_decay = weight_decay
         self.max_grad_norm = max_grad_norm
@@ -95,14 +99,31 @@ class FlatOptimizer:
 
     def grad_norm(self) -> torch.Tensor:
         """Global L2 norm of the (already reduced) gradient, on the device."""
+        import torch.distributed as dist
         tot = None
+        ex = None
         for a, b in self.ranges:
-            s = K.sqsum(self.flat.grad[a:b])
-            tot = s if tot is None else tot + s
-        if self.sharded:
-            import torch.distributed as dist
+            if self.ep_group is not None and self.expert_ranges:
+                # split the owned range into replicated / expert pieces
+                for ea, eb in self.expert_ranges:
+                    lo, hi = max(a, ea), min(b, eb)
+                    if lo < hi:
+                        s = K.sqsum(self.flat.grad[lo:hi])
+                        ex = s if ex is None else ex + s
+                pieces = _subtract([(a, b)], self.expert_ranges)
+            else:
+                pieces = [(a, b)]
+            for lo, hi in pieces:
+                s = K.sqsum(self.flat.grad[lo:hi])
+                tot = s if tot is None else tot + s
+        if tot is None:
+            tot = torch.zeros((), dtype=torch.float32, device=self.flat.device)
+        if self.sharded and dist.is_initialized():
+            dist.all_reduce(tot, group=self.norm_group)
+        if ex is not None:
             if dist.is_initialized():
-                dist.all_reduce(tot, group=self.norm_group)
+                dist.all_reduce(ex, group=self.ep_group)
+            tot = tot + ex
         return tot.sqrt()
 
     def clip_coef(self):
@@ -118,10 +139,25 @@ class FlatOptimizer:
         next_generation()
 
 
+def _subtract(ranges, holes):
+    out = []
+    for a, b in ranges:
+        cur = a
+        for ha, hb in sorted(holes):
+            if hb <= cur or ha >= b:
+                continue
+            if ha > cur:
+                out.append((cur, ha))
+            cur = max(cur, hb)
+        if cur < b:
+            out.append((cur, b))
+    return out
+
+
 class FlatAdamW(FlatOptimizer):
     def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=None,
-                 adam_l2=False, shard=None):
-        super().__init__(flat, lr, weight_decay, max_grad_norm, shard)
+                 adam_l2=False, shard=None, ep_group=None):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, ep_group)
         self.b1, self.b2 = betas
         self.eps = eps
         self.adam_l2 = adam_l2

@@ -163,3 +163,61 @@ def test_tensor_parallel_gemma_matches_unsharded():
                 fl = F2 // world
                 f = torch.cat([f[rank * fl:(rank + 1) * fl], f[F2 + rank * fl:F2 + (rank + 1) * fl]])
             assert torch.allclose(g, f, atol=1e-5, rtol=1e-4), (n, (g - f).abs().max())
+
+
+def _moe_cfg():
+    from solvingpapers_amd.models import deepseekv3 as ds
+    return ds.config("dsv3_tiny", dim=32, n_experts=4, top_k=2, n_shared=1, expert_hidden=24, aux_free=False)
+
+
+def _moe_inputs():
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 2, 6, 32, generator=g)          # [rank, B, T, D]
+    gy = torch.randn(2, 2, 6, 32, generator=g)
+    return x, gy
+
+
+def _ep_worker(rank, world, port, q):
+    _init(rank, world, port)
+    from solvingpapers_amd.models import deepseekv3 as ds
+    from solvingpapers_amd.parallel.expert_parallel import shard_experts
+    c = _moe_cfg()
+    torch.manual_seed(0)
+    full = ds.MoE(c)
+    full.reset_parameters(0.1, torch.Generator().manual_seed(3))
+    grp = dist.new_group([0, 1])
+    m = ds.MoE(c, ep_group=grp)
+    with torch.no_grad():
+        m.gate.copy_(full.gate)
+        m.w13.copy_(shard_experts(full.w13, rank, world))
+        m.w2.copy_(shard_experts(full.w2, rank, world))
+        m.shared.w13.copy_(full.shared.w13)
+        m.shared.w2.copy_(full.shared.w2)
+    x, gy = _moe_inputs()
+    xr = x[rank].clone().requires_grad_(True)
+    y = m(xr)
+    (y * gy[rank]).sum().backward()
+    q.put((rank, y.detach().numpy(), xr.grad.numpy(), m.w13.grad.numpy(), m.w2.grad.numpy(), m.gate.grad.numpy()))
+    dist.destroy_process_group()
+
+
+def test_expert_parallel_moe_matches_local():
+    """EP=2 (all-to-all dispatch/combine, 2 experts per rank) == one process holding all
+    4 experts: outputs, input grads, and each rank's expert grads (which collect the
+    contributions of BOTH ranks' tokens)."""
+    from solvingpapers_amd.models import deepseekv3 as ds
+    c = _moe_cfg()
+    torch.manual_seed(0)
+    full = ds.MoE(c)
+    full.reset_parameters(0.1, torch.Generator().manual_seed(3))
+    x, gy = _moe_inputs()
+    xs = x.clone().requires_grad_(True)
+    ys = [full(xs[r]) for r in range(2)]
+    sum((y * gy[r]).sum() for r, y in enumerate(ys)).backward()
+    out = _run(_ep_worker, 2)
+    for rank, y, gx, g13, g2, gg in out:
+        assert torch.allclose(torch.from_numpy(y), ys[rank].detach(), atol=1e-5)
+        assert torch.allclose(torch.from_numpy(gx), xs.grad[rank], atol=1e-5)
+        assert torch.allclose(torch.from_numpy(g13), full.w13.grad[rank * 2:(rank + 1) * 2], atol=1e-5)
+        assert torch.allclose(torch.from_numpy(g2), full.w2.grad[rank * 2:(rank + 1) * 2], atol=1e-5)
+        # gate grads are rank-local (DP all-reduces them later)
