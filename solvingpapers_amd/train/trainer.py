@@ -1,0 +1,249 @@
+"""Generic training loop shared by every model family.
+
+What the reference spreads over per-notebook loops (gpt/gpt-jax.ipynb:791-802,
+gemma/gemma.ipynb:540-560, deepseekv3/deepseekv3.ipynb:2320-2470, ViT/AE/VAE/KD epochs):
+step loop, periodic held-out loss, LR warmup + cosine (deepseekv3.ipynb:1976-1986),
+grad-norm clipping, gradient accumulation, checkpoint/resume — plus what it lacks
+(SURVEY §5): JSONL metrics, NaN/Inf guard (skip the update, abort after N in a row),
+RNG + step + data-cursor in checkpoints, auto-resume from ``latest`` (pairs with
+``torchrun --max-restarts``), CUDA-event step timing and optional torch.profiler trace.
+
+Parameters live in one FlatParams buffer; data parallelism (RCCL buckets overlapped
+with backward, optional ZeRO-1) and the fused flat optimizers come from
+parallel/data_parallel.py and train/optim.py. The model must implement
+``forward(x, y) -> scalar loss`` (all models in solvingpapers_amd.models do).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Callable, Iterable, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..parallel.data_parallel import DataParallel
+from ..utils.flat import FlatParams
+from . import checkpoint as ckpt
+from .optim import FlatAdamW, FlatSGD, cosine_lr
+
+
+@dataclass
+class TrainConfig:
+    steps: int = 1000
+    grad_accum: int = 1
+    optimizer: str = "adamw"            # adamw | adam | sgd
+    lr: float = 3e-4
+    min_lr: Optional[float] = None       # None -> constant LR
+    warmup: int = 0
+    betas: tuple = (0.9, 0.95)
+    eps: float = 1e-8
+    weight_decay: float = 0.1
+    clip: Optional[float] = 1.0
+    eval_every: int = 0
+    eval_iters: int = 10
+    ckpt_dir: Optional[str] = None
+    ckpt_every: int = 0
+    keep: int = 2
+    resume: str = "auto"                 # "auto" (latest if present) | "never" | <path>
+    log_path: Optional[str] = None       # JSONL metrics
+    log_every: int = 1
+    max_bad_steps: int = 3               # consecutive non-finite losses before abort
+    zero1: bool = False
+    opt_overlap: bool = False
+    tokens_per_sample: int = 0           # for tok/s (0 -> x.numel())
+    profile_steps: tuple = ()            # (start, stop) -> torch.profiler trace into ckpt_dir/log dir
+    grad_dtype: Optional[torch.dtype] = None
+    param_dtype: Optional[torch.dtype] = None
+
+
+class NonFiniteLoss(RuntimeError):
+    pass
+
+
+class Trainer:
+    def __init__(self, model, cfg: TrainConfig, train_batch: Callable[[int], tuple],
+                 eval_batch: Optional[Callable[[int], tuple]] = None, dp_group=None, ep_group=None,
+                 expert_dp_group=None, hooks: Iterable[Callable] = ()):
+        self.model, self.cfg = model, cfg
+        self.train_batch, self.eval_batch = train_batch, eval_batch
+        self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        groups = model.param_groups() if hasattr(model, "param_groups") else None
+        self.flat = FlatParams(model, groups=groups, align=64 * max(1, self.world),
+                               grad_dtype=cfg.grad_dtype, param_dtype=cfg.param_dtype)
+        self.dp = DataParallel(model, self.flat, group=dp_group, zero1=cfg.zero1,
+                               expert_dp_group=expert_dp_group) if self.world > 1 else None
+        shard = (self.dp.shard_ranges(), dp_group) if (self.dp and cfg.zero1) else None
+        if cfg.optimizer in ("adamw", "adam"):
+            self.opt = FlatAdamW(self.flat, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
+                                 max_grad_norm=cfg.clip, adam_l2=cfg.optimizer == "adam", shard=shard,
+                                 ep_group=ep_group)
+        elif cfg.optimizer == "sgd":
+            self.opt = FlatSGD(self.flat, lr=cfg.lr, weight_decay=cfg.weight_decay, max_grad_norm=cfg.clip,
+                               shard=shard)
+        else:
+            raise ValueError(cfg.optimizer)
+        for m in getattr(model, "moe_layers", lambda: [])():
+            m.balance_group = dp_group
+        if self.dp is not None:
+            self.dp.broadcast_params()
+        self.step = 0
+        self.bad_steps = 0
+        self.history = []
+        self.hooks = list(hooks)
+        self._log = None
+        if cfg.log_path and self.rank == 0:
+            os.makedirs(os.path.dirname(os.path.abspath(cfg.log_path)), exist_ok=True)
+            self._log = open(cfg.log_path, "a")
+
+    # ------------------------------------------------------------------ utils
+    def lr_at(self, step):
+        c = self.cfg
+        if c.min_lr is None:
+            return c.lr * min(1.0, (step + 1) / (c.warmup + 1)) if c.warmup else c.lr
+        return cosine_lr(step, c.lr, c.warmup, c.steps, c.min_lr)
+
+    def buffers(self):
+        return {n: b for n, b in self.model.named_buffers() if n.endswith("routing_bias")}
+
+    def log(self, rec):
+        self.history.append(rec)
+        if self._log is not None:
+            self._log.write(json.dumps(rec) + "\n")
+            self._log.flush()
+        for h in self.hooks:
+            h(rec)
+
+    # -------------------------------------------------------------- checkpoint
+    def save(self, loss=None):
+        if not self.cfg.ckpt_dir:
+            return None
+        self.flat.wait_all()
+        # saved step = index of the last completed step; resume continues at step + 1
+        return ckpt.save(self.cfg.ckpt_dir, self.step - 1, self.flat, self.opt, self.buffers(),
+                         extra={"loss": loss, "config": {k: str(v) for k, v in asdict(self.cfg).items()}},
+                         keep=self.cfg.keep)
+
+    def maybe_resume(self):
+        r = self.cfg.resume
+        if r == "never":
+            return False
+        path = ckpt.latest(self.cfg.ckpt_dir) if (r == "auto" and self.cfg.ckpt_dir) else (None if r == "auto" else r)
+        if not path:
+            return False
+        info = ckpt.load(path, self.flat, self.opt, self.buffers())
+        self.step = info["step"] + 1
+        return True
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def evaluate(self, iters=None):
+        """Mean held-out loss (gpt-jax.ipynb:542-552, gemma.ipynb:522-538, deepseekv3.ipynb:2098-2125)."""
+        if self.eval_batch is None:
+            return None
+        self.flat.wait_all()
+        was = self.model.training
+        self.model.eval()
+        tot = 0.0
+        n = iters or self.cfg.eval_iters
+        for i in range(n):
+            x, y = self.eval_batch(i)
+            tot += float(self.model(x, y))
+        self.model.train(was)
+        v = torch.tensor([tot / n], dtype=torch.float64)
+        if self.world > 1 and dist.get_backend() == "gloo":
+            dist.all_reduce(v)
+            v /= self.world
+        elif self.world > 1:
+            v = v.to(self.flat.device)
+            dist.all_reduce(v)
+            v = v.cpu() / self.world
+        return float(v)
+
+    # ------------------------------------------------------------------ train
+    def train_step(self, step):
+        c = self.cfg
+        self.opt.zero_grad()
+        tot = None
+        ntok = 0
+        for mi in range(c.grad_accum):
+            x, y = self.train_batch(step * c.grad_accum + mi)
+            ntok += c.tokens_per_sample * x.shape[0] if c.tokens_per_sample else x.numel()
+            last = mi == c.grad_accum - 1
+            ctx = self.dp.no_sync() if (self.dp is not None and not last) else _null()
+            with ctx:
+                loss = self.model(x, y)
+                (loss / c.grad_accum).backward()
+            tot = loss.detach() if tot is None else tot + loss.detach()
+        if self.dp is not None:
+            self.dp.finish_grad_sync()
+        loss = tot / c.grad_accum
+        finite = bool(torch.isfinite(loss).item())
+        if not finite:
+            self.bad_steps += 1
+            if self.bad_steps >= c.max_bad_steps:
+                raise NonFiniteLoss(f"{self.bad_steps} consecutive non-finite losses at step {step}")
+            return float("nan"), ntok, False
+        self.bad_steps = 0
+        self.opt.step(lr=self.lr_at(step), overlap=c.opt_overlap)
+        if self.dp is not None:
+            self.dp.gather_params()
+        return float(loss), ntok, True
+
+    def fit(self):
+        c = self.cfg
+        self.model.train()
+        self.maybe_resume()
+        prof = None
+        dev = self.flat.device
+        t_last = time.perf_counter()
+        while self.step < c.steps:
+            s = self.step
+            if c.profile_steps and s == c.profile_steps[0]:
+                prof = _start_profiler(c)
+            loss, ntok, ok = self.train_step(s)
+            if prof is not None and s + 1 >= c.profile_steps[1]:
+                prof.stop()
+                prof = None
+            if s % c.log_every == 0 or s == c.steps - 1:
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
+                now = time.perf_counter()
+                dt = (now - t_last) / (c.log_every if s else 1)
+                t_last = now
+                gn = self.opt.last_grad_norm
+                rec = {"step": s, "loss": loss, "lr": self.lr_at(s), "ok": ok, "dt": dt,
+                       "tok_per_s": ntok * self.world / max(dt, 1e-9),
+                       "grad_norm": float(gn) if gn is not None else None}
+                self.log(rec)
+            if c.eval_every and (s % c.eval_every == 0 and s) or (c.eval_every and s == c.steps - 1):
+                self.log({"step": s, "val_loss": self.evaluate()})
+            self.step += 1
+            if c.ckpt_every and self.step % c.ckpt_every == 0:
+                self.save(loss)
+        self.flat.wait_all()
+        if c.ckpt_dir and c.ckpt_every:
+            self.save()
+        return self.history
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _start_profiler(c: TrainConfig):
+    from torch.profiler import ProfilerActivity, profile
+    out = os.path.join(c.ckpt_dir or ".", "trace")
+    os.makedirs(out, exist_ok=True)
+    acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if torch.cuda.is_available() else [])
+    p = profile(activities=acts, on_trace_ready=torch.profiler.tensorboard_trace_handler(out))
+    p.start()
+    return p
