@@ -1,0 +1,67 @@
+#!/usr/bin/env python
+"""DeepSeek-V3-style (MLA + DeepSeekMoE) bf16 training tokens/s (BASELINE.json config #5,
+SURVEY App. C): ``python bench/dsv3_train.py --steps K --warmup W [--layers L]``; under
+torchrun with N>1 ranks the routed experts are expert-parallel over all N GPUs (EP=N,
+all-to-all dispatch) and the dense parameters data-parallel (RCCL buckets)."""
+from __future__ import annotations
+
+import argparse
+
+import torch
+
+from common import PEAK_BF16, report, sdist, timed
+from solvingpapers_amd.models import deepseekv3 as ds
+from solvingpapers_amd.parallel.data_parallel import DataParallel
+from solvingpapers_amd.train.optim import FlatAdamW
+from solvingpapers_amd.utils.flat import FlatParams
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--preset", default="dsv3_style")
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--mb", type=int, default=2)
+    a = ap.parse_args()
+    info = sdist.init_distributed()
+    world, dev = info.world_size, info.device
+    kw = {"block_size": a.seq}
+    if a.layers:
+        kw["n_layers"] = a.layers
+    c = ds.config(a.preset, **kw)
+    ep = torch.distributed.group.WORLD if world > 1 else None
+    m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep)
+    flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16, align=64 * world)
+    dp = DataParallel(m, flat) if world > 1 else None
+    opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, ep_group=ep)
+    for l in m.moe_layers():
+        l.balance_group = None
+    gen = torch.Generator(device=dev).manual_seed(7 + info.rank)
+    B, T = a.mb, a.seq
+    last = [None]
+
+    def step():
+        opt.zero_grad()
+        t = torch.randint(0, c.vocab_size, (B, T + 1), device=dev, generator=gen)
+        loss = m(t[:, :-1], t[:, 1:])
+        loss.backward()
+        if dp is not None:
+            dp.finish_grad_sync()
+        opt.step()
+        last[0] = loss
+
+    el = timed(step, a.steps, a.warmup)
+    tok_s = world * B * T * a.steps / el
+    tf = tok_s * m.flops_per_token(T) / world / 1e12
+    report("training tokens/sec, DeepSeek-V3-style MLA+MoE bf16", tok_s, "tokens/s", a.steps, a.warmup, el,
+           {"model": a.preset + (f"-L{a.layers}" if a.layers else ""), "global_batch": world * B, "seq_len": T,
+            "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu", "params": m.num_params(),
+            "active_params": m.num_params(active=True)},
+           tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0]), 4))
+    sdist.cleanup()
+
+
+if __name__ == "__main__":
+    main()
