@@ -195,70 +195,93 @@ __global__ __launch_bounds__(256) void scatter_grad_kernel(const T* __restrict__
 //                  B_e = B + e * strideB.   (fwd:  X_e W_e^T ; dX: dY_e W_e)
 // GROUP_K = true : groups split K (the token dim): C_e = C + e * strideC, reduction over
 //                  rows [off_e, off_e+1) of the token-major A and B. (dW_e = dY_e^T X_e)
-// Tile 128x128x32, 4 waves as 2x2 of 64x64; MFMA 32x32x16 bf16, computing C^T per wave
-// so the epilogue stores 4 consecutive columns (8 bytes) per lane.
-// LDS: K-contiguous tiles [128][32] with an 8-byte-unit XOR swizzle (u ^ (r>>2)&7);
-// K-strided tiles [32][128] read with ds_read_b64_tr_b16 and the attention image swizzle.
+// Block tile BM x BN x BK, WGM x WGN waves (wave tile TM x TN of 32x32 MFMA sub-tiles,
+// v_mfma_f32_32x32x16_bf16); each wave computes C^T so the epilogue writes 4 consecutive
+// columns (8 bytes) per lane. Register-staged double-buffered LDS, one barrier per k-step.
+// LDS images: K-contiguous tiles [rows][BK] with an 8-byte-unit XOR swizzle
+// (u ^ (r / P) where P rows span the 64 banks); K-strided tiles [BK][cols] read with
+// ds_read_b64_tr_b16 through the attention image swizzle. Zero bank conflicts by design.
+// Tile -> expert: per-block scan of the per-expert tile counts (E <= threads), so launch
+// count and grid are independent of the routing (no host sync); logical tile ids are
+// XCD-remapped so tiles sharing an A panel run on one XCD's L2.
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
-template <bool KC>
-struct OpTile {
-  // element offset of (row r, 8-byte unit u) in a [128][32] K-contiguous tile
-  static __device__ __forceinline__ int kc_off(int r, int u) { return r * 32 + 4 * (u ^ ((r >> 2) & 7)); }
-  // element offset of (k row r, 16B chunk ch) in a [32][128] K-strided tile
-  static __device__ __forceinline__ int ks_off(int r, int ch) {
-    return r * 128 + 8 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
-  }
-};
-
+template <int BK>
+__device__ __forceinline__ int kc_off(int r, int u) {
+  constexpr int P = 128 / BK;              // rows per 256-byte (64-bank) span
+  constexpr int NU = BK / 4;               // 8-byte units per row
+  return r * BK + 4 * (u ^ ((r / P) & (NU - 1)));
+}
+template <int L>
+__device__ __forceinline__ int ks_off(int r, int ch) {   // 16B chunk ch of k-row r, row length L
+  return r * L + 8 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+// MFMA operand with permuted k order: k = 16s + 4hh + {0..3}, 16s + 8 + 4hh + {0..3}
+template <int BK>
 __device__ __forceinline__ bf16x8 ld_kc(const bf16* t, int row, int s, int hh) {
-  // MFMA operand with permuted k order: k = 16s + 4hh + {0..3}, 16s + 8 + 4hh + {0..3}
-  typedef OpTile<true> O;
-  const bf16x4 a = *reinterpret_cast<const bf16x4*>(t + O::kc_off(row, 4 * s + hh));
-  const bf16x4 b = *reinterpret_cast<const bf16x4*>(t + O::kc_off(row, 4 * s + 2 + hh));
+  const bf16x4 a = *reinterpret_cast<const bf16x4*>(t + kc_off<BK>(row, 4 * s + hh));
+  const bf16x4 b = *reinterpret_cast<const bf16x4*>(t + kc_off<BK>(row, 4 * s + 2 + hh));
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+template <int L>
 __device__ __forceinline__ bf16x8 ld_ks(const bf16* t, int col0, int s, int lane) {
-  typedef OpTile<false> O;
   const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3, hh = lane >> 5;
   const int c = col0 + 16 * (g & 1) + 4 * pp;
   const int ra = 16 * s + 4 * hh + q, rb = ra + 8;
-  typedef __attribute__((address_space(3))) s16x4_t L;
-  const s16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((L*)(t + O::ks_off(ra, c >> 3) + (c & 7)));
-  const s16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((L*)(t + O::ks_off(rb, c >> 3) + (c & 7)));
+  typedef __attribute__((address_space(3))) s16x4_t LT;
+  const s16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LT*)(t + ks_off<L>(ra, c >> 3) + (c & 7)));
+  const s16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LT*)(t + ks_off<L>(rb, c >> 3) + (c & 7)));
   const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
   return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <bool A_KC, bool B_KC, bool GROUP_K>
-__global__ __launch_bounds__(256) void grouped_gemm_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                           bf16* __restrict__ C, const int* __restrict__ offsets,
-                                                           int E, int M, int N, int K, long lda, long ldb, long ldc,
-                                                           long strideB, long strideC, int accumulate) {
-  constexpr int BM = 128, BN = 128, BK = 32;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM * BK + BN * BK)];
+template <int BM, int BN, int BK, int WGM, int WGN, bool A_KC, bool B_KC, bool GROUP_K>
+__global__ __launch_bounds__(64 * WGM * WGN, (BM * BN / (WGM * WGN) <= 8192 && WGM * WGN == 4) ? 2 : 1)
+void grouped_gemm_kernel(
+    const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C, const int* __restrict__ offsets,
+    int E, int M, int N, int K, long lda, long ldb, long ldc, long strideB, long strideC, int accumulate) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int TM = BM / WGM, TN = BN / WGN;         // wave tile (m, n)
+  constexpr int IM = TM / 32, IN = TN / 32;
+  constexpr int AEL = BM * BK, BEL = BN * BK;          // elements per stage
+  constexpr int CA = AEL / 8 / NT, CB = BEL / 8 / NT;  // 16B chunks per thread
+  static_assert(CA * 8 * NT == AEL && CB * 8 * NT == BEL, "tile/threads mismatch");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (AEL + BEL)];
+  __shared__ int s_e, s_mt;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;   // 2x2 waves, 64x64 each
+  const int wm = wave / WGN, wn = wave % WGN;
   const int nnt = (N + BN - 1) / BN;
-  const int nt = blockIdx.x % nnt;
-  int mt = blockIdx.x / nnt;
-  // ---- decode (expert, tile) ----
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = lid % nnt;
+  int mt = lid / nnt;
   int e = 0, m0 = 0, mend = M, k0 = 0, kend = K;
   const bf16* Bp = B;
   bf16* Cp = C;
   if (!GROUP_K) {
-    for (e = 0; e < E; ++e) {
-      const int cnt = offsets[e + 1] - offsets[e];
-      const int tiles = (cnt + BM - 1) / BM;
-      if (mt < tiles) break;
-      mt -= tiles;
+    // block-wide exclusive scan of per-expert tile counts; thread e owns expert e
+    __shared__ int wsum[NT / 64];
+    const int cnt = tid < E ? offsets[tid + 1] - offsets[tid] : 0;
+    const int tiles = (cnt + BM - 1) / BM;
+    int inc = tiles;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
     }
-    if (e >= E) return;
+    if (lane == 63) wsum[wave] = inc;
+    if (tid == 0) s_e = -1;
+    __syncthreads();
+    int pre = inc - tiles;
+    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) { s_e = tid; s_mt = mt - pre; }
+    __syncthreads();
+    e = s_e;
+    if (e < 0) return;                                  // beyond the last tile
+    mt = s_mt;
     m0 = offsets[e] + mt * BM;
     mend = offsets[e + 1];
     Bp = B + e * strideB;
   } else {
-    // grid.x = E * (M/BM) * nnt : blocks of one expert cover its whole output C_e
     const int nmt = (M + BM - 1) / BM;
     e = mt / nmt;
     mt = mt % nmt;
@@ -269,61 +292,68 @@ __global__ __launch_bounds__(256) void grouped_gemm_kernel(const bf16* __restric
     Cp = C + e * strideC;
   }
   const int n0 = nt * BN;
-  // ---- staging: 256 threads, A tile 128x32 = 512 chunks of 8, B tile 512 chunks ----
-  bf16x8 ra[2], rb[2];
+  bf16x8 ra[CA], rb[CB];
   auto load_tiles = [&](int kk) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int idx = tid + c * 256;
-      if (A_KC) {  // [128 rows][32 k]: row = idx/4, kchunk = idx%4
-        const int r = idx >> 2, kc = (idx & 3) * 8;
+    for (int c = 0; c < CA; ++c) {
+      const int idx = tid + c * NT;
+      if (A_KC) {  // [BM rows][BK k]
+        const int r = idx / (BK / 8), kc = (idx % (BK / 8)) * 8;
         const int gm = m0 + r, gk = kk + kc;
         ra[c] = (gm < mend && gk < kend) ? *reinterpret_cast<const bf16x8*>(A + (long)gm * lda + gk) : bf16x8{};
-      } else {     // [32 k][128 m]: k = idx/16, mchunk = idx%16
-        const int r = idx >> 4, mc = (idx & 15) * 8;
+      } else {     // [BK k][BM m]
+        const int r = idx / (BM / 8), mc = (idx % (BM / 8)) * 8;
         const int gk = kk + r, gm = m0 + mc;
         ra[c] = (gk < kend && gm < mend) ? *reinterpret_cast<const bf16x8*>(A + (long)gk * lda + gm) : bf16x8{};
       }
-      if (B_KC) {  // [128 n][32 k]
-        const int r = idx >> 2, kc = (idx & 3) * 8;
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int idx = tid + c * NT;
+      if (B_KC) {  // [BN n][BK k]
+        const int r = idx / (BK / 8), kc = (idx % (BK / 8)) * 8;
         const int gn = n0 + r, gk = kk + kc;
         rb[c] = (gn < N && gk < kend) ? *reinterpret_cast<const bf16x8*>(Bp + (long)gn * ldb + gk) : bf16x8{};
-      } else {     // [32 k][128 n]
-        const int r = idx >> 4, nc = (idx & 15) * 8;
+      } else {     // [BK k][BN n]
+        const int r = idx / (BN / 8), nc = (idx % (BN / 8)) * 8;
         const int gk = kk + r, gn = n0 + nc;
         rb[c] = (gk < kend && gn < N) ? *reinterpret_cast<const bf16x8*>(Bp + (long)gk * ldb + gn) : bf16x8{};
       }
     }
   };
   auto store_tiles = [&](int buf) {
-    bf16* At = smem + buf * (BM * BK + BN * BK);
-    bf16* Bt = At + BM * BK;
+    bf16* At = smem + buf * (AEL + BEL);
+    bf16* Bt = At + AEL;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int idx = tid + c * 256;
+    for (int c = 0; c < CA; ++c) {
+      const int idx = tid + c * NT;
       if (A_KC) {
-        const int r = idx >> 2, u = (idx & 3) * 2;
-        *reinterpret_cast<bf16x4*>(At + OpTile<true>::kc_off(r, u)) = __builtin_shufflevector(ra[c], ra[c], 0, 1, 2, 3);
-        *reinterpret_cast<bf16x4*>(At + OpTile<true>::kc_off(r, u + 1)) = __builtin_shufflevector(ra[c], ra[c], 4, 5, 6, 7);
+        const int r = idx / (BK / 8), u = (idx % (BK / 8)) * 2;
+        *reinterpret_cast<bf16x4*>(At + kc_off<BK>(r, u)) = __builtin_shufflevector(ra[c], ra[c], 0, 1, 2, 3);
+        *reinterpret_cast<bf16x4*>(At + kc_off<BK>(r, u + 1)) = __builtin_shufflevector(ra[c], ra[c], 4, 5, 6, 7);
       } else {
-        const int r = idx >> 4, ch = idx & 15;
-        *reinterpret_cast<bf16x8*>(At + OpTile<false>::ks_off(r, ch)) = ra[c];
+        const int r = idx / (BM / 8), ch = idx % (BM / 8);
+        *reinterpret_cast<bf16x8*>(At + ks_off<BM>(r, ch)) = ra[c];
       }
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int idx = tid + c * NT;
       if (B_KC) {
-        const int r = idx >> 2, u = (idx & 3) * 2;
-        *reinterpret_cast<bf16x4*>(Bt + OpTile<true>::kc_off(r, u)) = __builtin_shufflevector(rb[c], rb[c], 0, 1, 2, 3);
-        *reinterpret_cast<bf16x4*>(Bt + OpTile<true>::kc_off(r, u + 1)) = __builtin_shufflevector(rb[c], rb[c], 4, 5, 6, 7);
+        const int r = idx / (BK / 8), u = (idx % (BK / 8)) * 2;
+        *reinterpret_cast<bf16x4*>(Bt + kc_off<BK>(r, u)) = __builtin_shufflevector(rb[c], rb[c], 0, 1, 2, 3);
+        *reinterpret_cast<bf16x4*>(Bt + kc_off<BK>(r, u + 1)) = __builtin_shufflevector(rb[c], rb[c], 4, 5, 6, 7);
       } else {
-        const int r = idx >> 4, ch = idx & 15;
-        *reinterpret_cast<bf16x8*>(Bt + OpTile<false>::ks_off(r, ch)) = rb[c];
+        const int r = idx / (BN / 8), ch = idx % (BN / 8);
+        *reinterpret_cast<bf16x8*>(Bt + ks_off<BN>(r, ch)) = rb[c];
       }
     }
   };
-  f32x16 acc[2][2];  // [n sub-tile][m sub-tile]: C^T tiles (rows = n, cols = m)
+  f32x16 acc[IN][IM];  // [n sub-tile][m sub-tile]: C^T tiles (rows = n, cols = m)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < IN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < IM; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   const int kt = (kend - k0 + BK - 1) / BK;
@@ -340,36 +370,39 @@ __global__ __launch_bounds__(256) void grouped_gemm_kernel(const bf16* __restric
       store_tiles(buf ^ 1);
       if (t + 2 < kt) load_tiles(k0 + (t + 2) * BK);
     }
-    const bf16* At = smem + buf * (BM * BK + BN * BK);
-    const bf16* Bt = At + BM * BK;
+    const bf16* At = smem + buf * (AEL + BEL);
+    const bf16* Bt = At + AEL;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[2], bfr[2];
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[IM], bfr[IN];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int mrow = wm * 64 + j * 32;
-        af[j] = A_KC ? ld_kc(At, mrow + l32, s, hh) : ld_ks(At, mrow, s, lane);
-        const int ncol = wn * 64 + j * 32;
-        bfr[j] = B_KC ? ld_kc(Bt, ncol + l32, s, hh) : ld_ks(Bt, ncol, s, lane);
+      for (int j = 0; j < IM; ++j) {
+        const int mrow = wm * TM + j * 32;
+        af[j] = A_KC ? ld_kc<BK>(At, mrow + l32, s, hh) : ld_ks<BM>(At, mrow, s, lane);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < IN; ++i) {
+        const int ncol = wn * TN + i * 32;
+        bfr[i] = B_KC ? ld_kc<BK>(Bt, ncol + l32, s, hh) : ld_ks<BN>(Bt, ncol, s, lane);
+      }
 #pragma unroll
-        for (int j = 0; j < 2; ++j)  // C^T[n][m] += B^T-frag (rows n) x A-frag^T (cols m)
+      for (int i = 0; i < IN; ++i)
+#pragma unroll
+        for (int j = 0; j < IM; ++j)  // C^T[n][m] += B^T-frag (rows n) x A-frag^T (cols m)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
   // ---- epilogue: lane holds column m = l32 of each C^T tile, rows n = 8g + 4hh + {0..3}
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < IN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int gm = m0 + wm * 64 + j * 32 + l32;
+    for (int j = 0; j < IM; ++j) {
+      const int gm = m0 + wm * TM + j * 32 + l32;
       if (GROUP_K ? gm >= M : gm >= mend) continue;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int gn = n0 + wn * 64 + i * 32 + 8 * g + 4 * hh;
+        const int gn = n0 + wn * TN + i * 32 + 8 * g + 4 * hh;
         if (gn >= N) continue;
         bf16* cp = Cp + (long)gm * ldc + gn;
         float v[4];
@@ -386,6 +419,43 @@ __global__ __launch_bounds__(256) void grouped_gemm_kernel(const bf16* __restric
         *reinterpret_cast<bf16x4*>(cp) = w4;
       }
     }
+}
+
+// tile configurations: id -> (BM, BN, BK, WGM, WGN)
+template <int CFG> struct GG;
+template <> struct GG<0> { static constexpr int BM = 128, BN = 128, BK = 32, WGM = 2, WGN = 2; };
+template <> struct GG<1> { static constexpr int BM = 128, BN = 256, BK = 32, WGM = 2, WGN = 2; };
+template <> struct GG<2> { static constexpr int BM = 256, BN = 256, BK = 32, WGM = 2, WGN = 4; };
+template <> struct GG<3> { static constexpr int BM = 256, BN = 256, BK = 64, WGM = 2, WGN = 2; };
+template <> struct GG<4> { static constexpr int BM = 128, BN = 256, BK = 64, WGM = 2, WGN = 2; };
+template <> struct GG<5> { static constexpr int BM = 256, BN = 128, BK = 32, WGM = 2, WGN = 2; };
+
+template <int CFG, bool A_KC, bool B_KC, bool GROUP_K>
+void launch_gg(int grid_m, const bf16* A, const bf16* B, bf16* C, const int* off, int E, int M, int N, int K, long lda,
+               long ldb, long ldc, long sB, long sC, int acc, hipStream_t st) {
+  using G = GG<CFG>;
+  const int nnt = cdiv(N, G::BN);
+  grouped_gemm_kernel<G::BM, G::BN, G::BK, G::WGM, G::WGN, A_KC, B_KC, GROUP_K>
+      <<<grid_m * nnt, 64 * G::WGM * G::WGN, 0, st>>>(A, B, C, off, E, M, N, K, lda, ldb, ldc, sB, sC, acc);
+}
+
+template <bool A_KC, bool B_KC, bool GROUP_K>
+void dispatch_gg(int cfg, int Mtot, int E, const bf16* A, const bf16* B, bf16* C, const int* off, int M, int N, int K,
+                 long lda, long ldb, long ldc, long sB, long sC, int acc, hipStream_t st) {
+  auto gm = [&](int BM) { return GROUP_K ? E * cdiv(M, BM) : cdiv(Mtot, BM) + E; };
+  switch (cfg) {
+#define GG_CASE(I) \
+  case I: launch_gg<I, A_KC, B_KC, GROUP_K>(gm(GG<I>::BM), A, B, C, off, E, M, N, K, lda, ldb, ldc, sB, sC, acc, st); break;
+    GG_CASE(0) GG_CASE(1) GG_CASE(2) GG_CASE(3) GG_CASE(4) GG_CASE(5)
+#undef GG_CASE
+    default: TORCH_CHECK(false, "grouped_gemm: unknown tile config ", cfg);
+  }
+}
+
+static int default_cfg(int mode) {
+  const char* e = getenv("SPA_GG_CFG");
+  if (e) return atoi(e);
+  return 0;
 }
 
 // --------------------------------------------------------------------------- host
@@ -490,12 +560,14 @@ std::vector<at::Tensor> moe_combine_bwd(const at::Tensor& dy_, const at::Tensor&
 // mode 1: dX[M,K] = dY[M,N] W_e[N,K]   (rows grouped; W [E, N, K])
 // mode 2: dW_e[N,K] = dY_e[.,N]^T X_e[.,K]  (token dim grouped; out [E, N, K]); accumulate -> +=
 at::Tensor grouped_gemm(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t mode,
-                        const c10::optional<at::Tensor>& out_, bool accumulate) {
+                        const c10::optional<at::Tensor>& out_, bool accumulate, int64_t cfg) {
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "grouped_gemm: bf16");
   TORCH_CHECK(a.is_contiguous() && w.is_contiguous() && offsets.scalar_type() == at::kInt);
   const int E = offsets.numel() - 1;
+  TORCH_CHECK(E >= 1 && E <= 256, "grouped_gemm: 1..256 experts");
   DeviceGuard g(a.device());
   auto st = stream();
+  if (cfg < 0) cfg = default_cfg((int)mode);
   if (mode == 0 || mode == 1) {
     TORCH_CHECK(w.dim() == 3 && w.size(0) == E);
     const int M = a.size(0);
@@ -506,16 +578,15 @@ at::Tensor grouped_gemm(const at::Tensor& a, const at::Tensor& w, const at::Tens
     TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "grouped_gemm: dims must be multiples of 8");
     auto out = out_ ? *out_ : at::empty({M, N}, a.options());
     if (M == 0) return out;
-    const int nnt = cdiv(N, 128);
-    const int mtiles = cdiv(M, 128) + E;  // upper bound on per-expert m-tiles
+    const bf16* A = (const bf16*)a.data_ptr();
+    const bf16* W = (const bf16*)w.data_ptr();
+    bf16* C = (bf16*)out.data_ptr();
     if (mode == 0)
-      grouped_gemm_kernel<true, true, false><<<mtiles * nnt, 256, 0, st>>>(
-          (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,
-          N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0);
+      dispatch_gg<true, true, false>(cfg, M, E, A, W, C, offsets.data_ptr<int>(), M, N, K, K, Kw, N,
+                                     (long)Nw * Kw, 0, accumulate ? 1 : 0, st);
     else
-      grouped_gemm_kernel<true, false, false><<<mtiles * nnt, 256, 0, st>>>(
-          (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,
-          N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0);
+      dispatch_gg<true, false, false>(cfg, M, E, A, W, C, offsets.data_ptr<int>(), M, N, K, K, Kw, N,
+                                      (long)Nw * Kw, 0, accumulate ? 1 : 0, st);
     SPA_LAUNCH_CHECK();
     return out;
   }
@@ -525,12 +596,9 @@ at::Tensor grouped_gemm(const at::Tensor& a, const at::Tensor& w, const at::Tens
   TORCH_CHECK(a.size(0) == w.size(0) && N % 8 == 0 && K % 8 == 0);
   auto out = out_ ? *out_ : at::empty({E, N, K}, a.options());
   TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * N * K);
-  if (E == 0) return out;
   // C_e (M=N rows, N=K cols) = A (dY^T, stored [k=token][m]) * B (X, stored [k=token][n])
-  const int nnt = cdiv(K, 128), nmt = cdiv(N, 128);
-  grouped_gemm_kernel<false, false, true><<<E * nmt * nnt, 256, 0, st>>>(
-      (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K,
-      0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0);
+  dispatch_gg<false, false, true>(cfg, 0, E, (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(),
+                                  offsets.data_ptr<int>(), N, K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, st);
   SPA_LAUNCH_CHECK();
   return out;
 }
@@ -543,7 +611,7 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("moe_gather(Tensor x, Tensor perm, int div) -> Tensor");
   m.def("moe_combine(Tensor yp, Tensor inv, Tensor? w, int N, int k) -> Tensor");
   m.def("moe_combine_bwd(Tensor dy, Tensor yp, Tensor perm, Tensor inv, Tensor w, int k) -> Tensor[]");
-  m.def("grouped_gemm(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
+  m.def("grouped_gemm(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate, int cfg=-1) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("moe_route", &spa::moe_route);

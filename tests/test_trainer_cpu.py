@@ -98,3 +98,12 @@ def test_reference_dsv3_checkpoint_roundtrip(tmp_path):
     assert ck.load_reference_dsv3(p, m2) == 42
     for a, b in zip(m.parameters(), m2.parameters()):
         assert torch.equal(a, b)
+
+
+def test_cli_entrypoint_trains_and_checkpoints(tmp_path):
+    from solvingpapers_amd.train.__main__ import main
+    main(["gpt", "--preset", "gpt_tiny_cpu", "--steps", "4", "--set", "num_layers=1", "--device", "cpu",
+          "--ckpt-dir", str(tmp_path), "--ckpt-every", "2", "--log", str(tmp_path / "m.jsonl")])
+    assert (tmp_path / "latest").exists()
+    recs = [json.loads(l) for l in open(tmp_path / "m.jsonl")]
+    assert len(recs) == 4
