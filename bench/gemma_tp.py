@@ -1,0 +1,59 @@
+#!/usr/bin/env python
+"""Gemma-7B-shape (MQA, 1 KV head) bf16 training tokens/s with tensor parallelism over all
+ranks (BASELINE.json config #4: TP=8 on one node). Column-parallel q / GeGLU, row-parallel
+o / down with RCCL all-reduces, replicated K/V, vocab-parallel embedding + CE.
+``[torchrun --nproc-per-node N ...] python bench/gemma_tp.py --steps K --warmup W [--layers L]``"""
+from __future__ import annotations
+
+import argparse
+
+import torch
+import torch.distributed as dist
+
+from common import PEAK_BF16, report, sdist, timed
+from solvingpapers_amd.models import gemma
+from solvingpapers_amd.train.optim import FlatAdamW
+from solvingpapers_amd.utils.flat import FlatParams
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--layers", type=int, default=None)
+    a = ap.parse_args()
+    info = sdist.init_distributed()
+    world, dev = info.world_size, info.device
+    kw = {"max_seq_len": a.seq}
+    if a.layers:
+        kw["n_layers"] = a.layers
+    c = gemma.config("gemma_7b_mqa", **kw)
+    tp = dist.group.WORLD if world > 1 else None
+    m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=tp, seed=1)
+    flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
+    # global grad norm: TP-sharded squares summed over the group, replicated params counted once
+    opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, tp_group=tp)
+    g = torch.Generator(device=dev).manual_seed(11)                 # same tokens on every TP rank
+    last = [None]
+
+    def step():
+        opt.zero_grad()
+        t = torch.randint(0, c.vocab_size, (1, a.seq + 1), device=dev, generator=g)
+        loss = m(t[:, :-1], t[:, 1:])
+        loss.backward()
+        opt.step()
+        last[0] = loss
+
+    el = timed(step, a.steps, a.warmup)
+    tok_s = a.seq * a.steps / el                                     # one sequence per step for the TP group
+    tf = tok_s * m.flops_per_token(a.seq) / world / 1e12
+    report("training tokens/sec, Gemma-7B-shape MQA bf16 (TP)", tok_s, "tokens/s", a.steps, a.warmup, el,
+           {"model": "gemma_7b_mqa" + (f"-L{a.layers}" if a.layers else ""), "global_batch": 1, "seq_len": a.seq,
+            "parallelism": f"tp{world}"}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
+           loss=round(float(last[0].detach()), 4))
+    sdist.cleanup()
+
+
+if __name__ == "__main__":
+    main()

@@ -186,7 +186,8 @@ class GemmaBlock(tnn.Module):
         self.ffn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
         self.w13 = tnn.Parameter(torch.empty(2 * c.ffn_hidden // tp_size, c.dim, **fk))  # column-parallel [gate|up]
         self.w2 = tnn.Parameter(torch.empty(c.dim, c.ffn_hidden // tp_size, **fk))       # row-parallel
-        self.wkv.tp_replicated = True
+        for p in (self.wkv, self.attn_norm, self.ffn_norm):
+            p.tp_replicated = True
 
     @torch.no_grad()
     def reset_parameters(self, g):
@@ -226,6 +227,7 @@ class Gemma(tnn.Module):
         self.embed = tnn.Parameter(torch.empty(c.vocab_size // self.tp, c.dim, **fk))   # vocab-parallel, tied head
         self.layers = tnn.ModuleList([GemmaBlock(c, self.tp, **fk) for _ in range(c.n_layers)])
         self.norm_f = tnn.Parameter(torch.ones(c.dim, **fk))
+        self.norm_f.tp_replicated = True
         self.grad_ready_cb = None
         with torch.no_grad():
             g = torch.Generator(device=self.embed.device).manual_seed(seed + 1000 * self.tp_rank)

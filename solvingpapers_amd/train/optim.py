@@ -20,8 +20,13 @@ from ..utils.flat import FlatParams
 
 class FlatOptimizer:
     def __init__(self, flat: FlatParams, lr: float, weight_decay: float = 0.0, max_grad_norm: Optional[float] = None,
-                 shard: Optional[Tuple[List[Tuple[int, int]], object]] = None, ep_group=None):
+                 shard: Optional[Tuple[List[Tuple[int, int]], object]] = None, ep_group=None, tp_group=None):
         self.flat = flat
+        # tensor parallelism: params tagged ``tp_replicated`` are identical on every TP rank and
+        # counted once; the squared norm of everything else is summed over the TP group
+        self.tp_group = tp_group
+        self.tp_rep_ranges = sorted((flat.offsets[id(p)], flat.offsets[id(p)] + p.numel())
+                                    for b in flat.buckets for p in b.params if getattr(p, "tp_replicated", False))
         # expert-parallel buckets: their squared-norm partial is summed over the EP group
         self.ep_group = ep_group
         self.expert_ranges = [(b.start, b.end) for b in flat.buckets
@@ -118,6 +123,17 @@ class FlatOptimizer:
                 tot = s if tot is None else tot + s
         if tot is None:
             tot = torch.zeros((), dtype=torch.float32, device=self.flat.device)
+        if self.tp_group is not None and dist.is_initialized() and dist.get_world_size(self.tp_group) > 1:
+            rep = None
+            for a, b in self.ranges:
+                for ra, rb in self.tp_rep_ranges:
+                    lo, hi = max(a, ra), min(b, rb)
+                    if lo < hi:
+                        s = K.sqsum(self.flat.grad[lo:hi])
+                        rep = s if rep is None else rep + s
+            sharded = tot - rep if rep is not None else tot
+            dist.all_reduce(sharded, group=self.tp_group)
+            tot = sharded + rep if rep is not None else sharded
         if self.sharded and dist.is_initialized():
             dist.all_reduce(tot, group=self.norm_group)
         if ex is not None:
@@ -156,8 +172,8 @@ def _subtract(ranges, holes):
 
 class FlatAdamW(FlatOptimizer):
     def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=None,
-                 adam_l2=False, shard=None, ep_group=None):
-        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, ep_group)
+                 adam_l2=False, shard=None, ep_group=None, tp_group=None):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, ep_group, tp_group)
         self.b1, self.b2 = betas
         self.eps = eps
         self.adam_l2 = adam_l2

@@ -128,7 +128,9 @@ def _tp_worker(rank, world, port, q):
     loss = local(ids[:, :-1], ids[:, 1:])
     loss.backward()
     grads = {n: p.main_grad.clone().numpy() for n, p in local.named_parameters()}
-    q.put((rank, loss.item(), grads))
+    from solvingpapers_amd.train.optim import FlatAdamW
+    gn = FlatAdamW(flat, max_grad_norm=1.0, tp_group=grp).grad_norm().item()
+    q.put((rank, loss.item(), (grads, gn)))
     dist.destroy_process_group()
 
 
@@ -144,8 +146,10 @@ def test_tensor_parallel_gemma_matches_unsharded():
     fg = {n: p.main_grad for n, p in full.named_parameters()}
     out = _run(_tp_worker, 2, )
     world = 2
-    for rank, l, grads in out:
+    full_norm = torch.sqrt(sum((g.float() ** 2).sum() for g in fg.values())).item()
+    for rank, l, (grads, gn) in out:
         assert abs(l - loss.item()) < 1e-5
+        assert abs(gn - full_norm) < 1e-4 * full_norm, (gn, full_norm)   # TP-aware global grad norm
         for n, g in grads.items():
             g = torch.from_numpy(g)
             f = fg[n]
