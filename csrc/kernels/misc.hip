@@ -31,15 +31,18 @@ __device__ __forceinline__ float u01(uint64_t seed, uint64_t i) {  // (0, 1]
 // --------------------------------------------------------------------------- dropout
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, float p,
-                                                      uint64_t seed) {
+                                                      uint64_t seed, const int64_t* __restrict__ seed_ptr) {
+  if (seed_ptr) seed = (uint64_t)*seed_ptr;   // device seed: fresh mask per HIP-graph replay
   const float scale = 1.f / (1.f - p);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const bool keep = u01(seed, i) > p;
     y[i] = (T)(keep ? (float)x[i] * scale : 0.f);
   }
 }
-at::Tensor dropout_apply(const at::Tensor& x_, double p, int64_t seed) {
+at::Tensor dropout_apply(const at::Tensor& x_, double p, int64_t seed, const c10::optional<at::Tensor>& seed_t) {
   SPA_CHECK_CUDA(x_);
+  if (seed_t) TORCH_CHECK(seed_t->scalar_type() == at::kLong && seed_t->is_cuda() && seed_t->numel() >= 1);
+  const int64_t* sp = seed_t ? seed_t->data_ptr<int64_t>() : nullptr;
   auto x = x_.contiguous();
   auto y = at::empty_like(x);
   const long n = x.numel();
@@ -47,9 +50,9 @@ at::Tensor dropout_apply(const at::Tensor& x_, double p, int64_t seed) {
   DeviceGuard g(x.device());
   const int grid = (int)std::min<long>((n + 255) / 256, 8192);
   if (x.scalar_type() == at::kBFloat16)
-    dropout_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), n, (float)p, seed);
+    dropout_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), n, (float)p, seed, sp);
   else if (x.scalar_type() == at::kFloat)
-    dropout_kernel<float><<<grid, 256, 0, stream()>>>(x.data_ptr<float>(), y.data_ptr<float>(), n, (float)p, seed);
+    dropout_kernel<float><<<grid, 256, 0, stream()>>>(x.data_ptr<float>(), y.data_ptr<float>(), n, (float)p, seed, sp);
   else TORCH_CHECK(false, "dropout: bf16/fp32 only");
   SPA_LAUNCH_CHECK();
   return y;
@@ -586,7 +589,7 @@ std::vector<at::Tensor> luong_bwd(const at::Tensor& dctx_, const at::Tensor& st_
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
-  m.def("dropout_apply(Tensor x, float p, int seed) -> Tensor");
+  m.def("dropout_apply(Tensor x, float p, int seed, Tensor? seed_t=None) -> Tensor");
   m.def("kd_loss_fwd(Tensor s, Tensor t, Tensor y, float T, float alpha, bool want_grad) -> Tensor[]");
   m.def("vae_reparam(Tensor mu, Tensor logvar, Tensor? dz, int seed) -> Tensor");
   m.def("vae_loss_fwd(Tensor r, Tensor x, Tensor mu, Tensor logvar) -> Tensor[]");

@@ -22,8 +22,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* _
                                                     const GT* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, long n, float lr, float b1, float b2,
                                                     float eps, float wd, float inv_bc1, float inv_sqrt_bc2,
-                                                    const float* __restrict__ coef_ptr, int adam_l2) {
+                                                    const float* __restrict__ coef_ptr, int adam_l2,
+                                                    const float* __restrict__ hyper) {
   const float coef = coef_ptr ? *coef_ptr : 1.f;
+  if (hyper) {  // graph-safe: lr and step read from the device (hyper = [lr, step])
+    lr = hyper[0];
+    inv_bc1 = 1.f / (1.f - __powf(b1, hyper[1]));
+    inv_sqrt_bc2 = rsqrtf(1.f - __powf(b2, hyper[1]));
+  }
   const long nv = n / 8;
   const long stride = (long)gridDim.x * 256;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < nv + (n % 8 ? 1 : 0); i += stride) {
@@ -79,8 +85,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* _
 template <typename PT, typename GT, bool MASTER>
 __global__ __launch_bounds__(256) void sgd_kernel(PT* __restrict__ p, float* __restrict__ master,
                                                   const GT* __restrict__ g, float* __restrict__ buf, long n, float lr,
-                                                  float momentum, float wd, const float* __restrict__ coef_ptr) {
+                                                  float momentum, float wd, const float* __restrict__ coef_ptr,
+                                                  const float* __restrict__ hyper) {
   const float coef = coef_ptr ? *coef_ptr : 1.f;
+  if (hyper) lr = hyper[0];
   for (long j = blockIdx.x * 256L + threadIdx.x; j < n; j += (long)gridDim.x * 256) {
     float pv = MASTER ? master[j] : (float)p[j];
     float gr = (float)g[j] * coef + wd * pv;
@@ -123,7 +131,7 @@ static int opt_grid(long n) { return (int)std::max<long>(1, std::min<long>((n / 
 
 void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g, const at::Tensor& m,
             const at::Tensor& v, double lr, double b1, double b2, double eps, double wd, int64_t step,
-            const c10::optional<at::Tensor>& coef, bool adam_l2) {
+            const c10::optional<at::Tensor>& coef, bool adam_l2, const c10::optional<at::Tensor>& hyper) {
   SPA_CHECK_CUDA(p);
   for (auto* t : {&p, &g, &m, &v}) TORCH_CHECK(t->is_contiguous(), "adamw: flat contiguous buffers required");
   const long n = p.numel();
@@ -137,11 +145,13 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   const float inv_bc1 = 1.f / (1.f - std::pow((float)b1, (float)step));
   const float inv_sqrt_bc2 = 1.f / std::sqrt(1.f - std::pow((float)b2, (float)step));
   const float* cp = coef ? coef->data_ptr<float>() : nullptr;
+  if (hyper) TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->numel() >= 2 && hyper->is_cuda());
+  const float* hp = hyper ? hyper->data_ptr<float>() : nullptr;
 #define AL(PT, GT, MS)                                                                                           \
   adamw_kernel<PT, GT, MS><<<opt_grid(n), 256, 0, st>>>(                                                         \
       (PT*)p.data_ptr(), MS ? master->data_ptr<float>() : nullptr, (const GT*)g.data_ptr(), m.data_ptr<float>(), \
       v.data_ptr<float>(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cp,  \
-      adam_l2 ? 1 : 0)
+      adam_l2 ? 1 : 0, hp)
   const bool pb = p.scalar_type() == at::kBFloat16, gb = g.scalar_type() == at::kBFloat16;
   if (pb && gb) { TORCH_CHECK(master.has_value(), "bf16 params need an fp32 master"); AL(bf16, bf16, true); }
   else if (pb && !gb) { TORCH_CHECK(master.has_value(), "bf16 params need an fp32 master"); AL(bf16, float, true); }
@@ -153,7 +163,7 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
 
 void sgd_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g,
           const c10::optional<at::Tensor>& buf, double lr, double momentum, double wd,
-          const c10::optional<at::Tensor>& coef) {
+          const c10::optional<at::Tensor>& coef, const c10::optional<at::Tensor>& hyper) {
   const long n = p.numel();
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && g.numel() == n);
   if (n == 0) return;
@@ -165,7 +175,7 @@ void sgd_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at
 #define SL(PT, GT, MS)                                                                                          \
   sgd_kernel<PT, GT, MS><<<grid, 256, 0, st>>>((PT*)p.data_ptr(), MS ? master->data_ptr<float>() : nullptr,     \
                                                (const GT*)g.data_ptr(), bp, n, (float)lr, (float)momentum,       \
-                                               (float)wd, cp)
+                                               (float)wd, cp, hyper ? hyper->data_ptr<float>() : nullptr)
   const bool pb = p.scalar_type() == at::kBFloat16, gb = g.scalar_type() == at::kBFloat16;
   if (pb) { TORCH_CHECK(master.has_value()); if (gb) SL(bf16, bf16, true); else SL(bf16, float, true); }
   else { if (gb) { if (master) SL(float, bf16, true); else SL(float, bf16, false); }
@@ -198,9 +208,9 @@ at::Tensor sqsum(const at::Tensor& g) {
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("adamw_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!) m, Tensor(d!) v, float lr, float b1, "
-        "float b2, float eps, float wd, int step, Tensor? coef, bool adam_l2) -> ()");
+        "float b2, float eps, float wd, int step, Tensor? coef, bool adam_l2, Tensor? hyper=None) -> ()");
   m.def("sgd_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!)? buf, float lr, float momentum, float wd, "
-        "Tensor? coef) -> ()");
+        "Tensor? coef, Tensor? hyper=None) -> ()");
   m.def("sqsum(Tensor g) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {

@@ -22,23 +22,29 @@ def _seed():
 
 
 # ------------------------------------------------------------------------------- dropout
+def _device_seed(device):
+    """Seed drawn by torch's (graph-capture-safe) device generator: inside a captured HIP
+    graph every replay gets a fresh seed, so dropout masks differ step to step."""
+    return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
+
+
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
-        ctx.p, ctx.seed = p, seed
-        return _ext.ops().dropout_apply(x, p, seed)
+    def forward(ctx, x, p, seed_t):
+        ctx.p, ctx.seed_t = p, seed_t
+        return _ext.ops().dropout_apply(x, p, 0, seed_t)
 
     @staticmethod
     def backward(ctx, g):
         # same mask (regenerated from the seed), same 1/(1-p) scale
-        return _ext.ops().dropout_apply(g.contiguous(), ctx.p, ctx.seed), None, None
+        return _ext.ops().dropout_apply(g.contiguous(), ctx.p, 0, ctx.seed_t), None, None
 
 
 def dropout(x, p=0.1, training=True):
     if not training or p == 0.0:
         return x
     if _hip(x):
-        return _DropoutFn.apply(x, float(p), _seed())
+        return _DropoutFn.apply(x, float(p), _device_seed(x.device))
     return F.dropout(x, p, training)
 
 

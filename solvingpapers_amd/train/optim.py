@@ -20,8 +20,13 @@ from ..utils.flat import FlatParams
 
 class FlatOptimizer:
     def __init__(self, flat: FlatParams, lr: float, weight_decay: float = 0.0, max_grad_norm: Optional[float] = None,
-                 shard: Optional[Tuple[List[Tuple[int, int]], object]] = None, ep_group=None, tp_group=None):
+                 shard: Optional[Tuple[List[Tuple[int, int]], object]] = None, ep_group=None, tp_group=None,
+                 graph_safe: bool = False):
         self.flat = flat
+        # graph_safe: lr and step live on the device ([lr, step] fp32) so a captured HIP graph of
+        # the whole training step replays with the right bias correction / schedule (set_lr)
+        self.hyper = (torch.tensor([lr, 0.0], dtype=torch.float32, device=flat.device)
+                      if graph_safe and flat.device.type == "cuda" else None)
         # tensor parallelism: params tagged ``tp_replicated`` are identical on every TP rank and
         # counted once; the squared norm of everything else is summed over the TP group
         self.tp_group = tp_group
@@ -73,6 +78,10 @@ class FlatOptimizer:
         memory-bound optimizer overlaps the compute-bound forward of the next
         step (see FlatParams.wait_bucket)."""
         self.step_count += 1
+        if self.hyper is not None:
+            if not torch.cuda.is_current_stream_capturing():
+                self.hyper[0].fill_(lr)
+            self.hyper[1].add_(1.0)
         coef = self.clip_coef()
         segs = self._segments()
         if overlap and self.flat.device.type == "cuda":
@@ -154,6 +163,15 @@ class FlatOptimizer:
         from ..utils.grad import next_generation
         next_generation()
 
+    def set_lr(self, lr: float):
+        """Update the learning rate (also for an already captured graph_safe step)."""
+        self.lr = lr
+        if self.hyper is not None:
+            self.hyper[0].fill_(lr)
+
+    def device_step(self) -> int:
+        return int(self.hyper[1].item()) if self.hyper is not None else self.step_count
+
 
 def _subtract(ranges, holes):
     out = []
@@ -172,8 +190,8 @@ def _subtract(ranges, holes):
 
 class FlatAdamW(FlatOptimizer):
     def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=None,
-                 adam_l2=False, shard=None, ep_group=None, tp_group=None):
-        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, ep_group, tp_group)
+                 adam_l2=False, shard=None, ep_group=None, tp_group=None, graph_safe=False):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, ep_group, tp_group, graph_safe)
         self.b1, self.b2 = betas
         self.eps = eps
         self.adam_l2 = adam_l2
@@ -189,13 +207,15 @@ class FlatAdamW(FlatOptimizer):
         n = b - a
         K.adamw_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
                  self.m[so:so + n], self.v[so:so + n], lr, self.b1, self.b2, self.eps,
-                 self.weight_decay if dec else 0.0, self.step_count, coef, self.adam_l2)
+                 self.weight_decay if dec else 0.0, self.step_count, coef, self.adam_l2, self.hyper)
 
     def state_dict(self):
-        return {"step": self.step_count, "m": self.m, "v": self.v, "master": self.master, "lr": self.lr}
+        return {"step": self.device_step(), "m": self.m, "v": self.v, "master": self.master, "lr": self.lr}
 
     def load_state_dict(self, sd):
         self.step_count = int(sd["step"])
+        if self.hyper is not None:
+            self.hyper[1].fill_(float(self.step_count))
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         if self.master is not None and sd.get("master") is not None:
@@ -208,8 +228,9 @@ def FlatAdam(flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_
 
 
 class FlatSGD(FlatOptimizer):
-    def __init__(self, flat, lr=1e-3, momentum=0.0, weight_decay=0.0, max_grad_norm=None, shard=None):
-        super().__init__(flat, lr, weight_decay, max_grad_norm, shard)
+    def __init__(self, flat, lr=1e-3, momentum=0.0, weight_decay=0.0, max_grad_norm=None, shard=None,
+                 graph_safe=False):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, graph_safe=graph_safe)
         self.momentum = momentum
         self.buf = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device) if momentum else None
 
@@ -222,7 +243,7 @@ class FlatSGD(FlatOptimizer):
         n = b - a
         K.sgd_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
                self.buf[so:so + n] if self.buf is not None else None, lr, self.momentum,
-               self.weight_decay if dec else 0.0, coef)
+               self.weight_decay if dec else 0.0, coef, self.hyper)
 
     def state_dict(self):
         return {"step": self.step_count, "buf": self.buf, "master": self.master, "lr": self.lr}

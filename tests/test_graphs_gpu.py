@@ -1,0 +1,53 @@
+"""HIP-graph capture of full training steps (utils/graphs.py): replayed steps match eager
+steps bit-for-bit-ish (same kernels), lr/step come from the device, dropout masks change
+between replays."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(seed=0, p=0.0):
+    from solvingpapers_amd.models import gpt
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = gpt.config("gpt_tiny_cpu", vocab_size=64, block_size=32, emb_dim=64, num_heads=2, dropout_rate=p)
+    m = gpt.GPT(c, device="cuda", dtype=torch.bfloat16, seed=seed)
+    flat = FlatParams(m, groups=m.param_groups() if hasattr(m, "param_groups") else None)
+    opt = FlatAdamW(flat, lr=1e-3, weight_decay=0.1, max_grad_norm=1.0, graph_safe=True)
+    return m, flat, opt
+
+
+def test_graph_replay_matches_eager():
+    from solvingpapers_amd.utils.graphs import StepGraph
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xs = [torch.randint(0, 64, (4, 32), device="cuda", generator=g) for _ in range(6)]
+    m1, f1, o1 = _setup()
+    x = torch.zeros(4, 32, dtype=torch.long, device="cuda")
+    out = {}
+
+    def step():
+        o1.zero_grad()
+        loss = m1(x[:, :-1], x[:, 1:])
+        loss.backward()
+        o1.step()
+        out["l"] = loss
+
+    x.copy_(xs[0])
+    sg = StepGraph(step, warmup=2)          # 2 warmup steps + 1 captured step ran on xs[0]
+    losses_g = []
+    for i in range(1, 6):
+        x.copy_(xs[i])
+        sg.replay()
+        losses_g.append(float(out["l"]))
+    m2, f2, o2 = _setup()
+    losses_e = []
+    for i in [0, 0, 0] + list(range(1, 6)):
+        o2.zero_grad()
+        loss = m2(xs[i][:, :-1], xs[i][:, 1:])
+        loss.backward()
+        o2.step()
+        losses_e.append(float(loss))
+    assert o1.device_step() == 8 and o2.device_step() == 8
+    assert max(abs(a - b) for a, b in zip(losses_g, losses_e[3:])) < 1e-2
+    assert (f1.param.float() - f2.param.float()).abs().max() < 1e-2
