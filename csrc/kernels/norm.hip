@@ -202,6 +202,23 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   __syncthreads();
   if (rs == 0 && c < D) out[c] = (OT)(s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
 }
+// First level of a two-level deterministic column sum: block (bx, by) reduces rows
+// [by*chunk, (by+1)*chunk) of 64 columns -> part2[by, c]. Enough blocks to fill the chip
+// (a single-level sum over thousands of partial rows ran on D/64 blocks: latency bound).
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ part, float* __restrict__ part2,
+                                                             int P, int D, int chunk) {
+  __shared__ float s[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rs = threadIdx.x >> 6;
+  const int p0 = blockIdx.y * chunk, p1 = min(P, p0 + chunk);
+  float acc = 0.f;
+  if (c < D)
+    for (int p = p0 + rs; p < p1; p += 4) acc += part[(size_t)p * D + c];
+  s[rs][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rs == 0 && c < D)
+    part2[(size_t)blockIdx.y * D + c] = s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x];
+}
 
 #define NORM_FWD_DISPATCH(NT, MAXV)                                                              \
   do {                                                                                           \
@@ -317,10 +334,21 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& h, cons
 #undef ARGS
     SPA_LAUNCH_CHECK();
     auto colsum = [&](const at::Tensor& part, const at::Tensor& out) {
+      const float* src = part.data_ptr<float>();
+      int P = nparts;
+      at::Tensor p2;
+      if (P > 64) {
+        const int Y = std::min(64, cdiv(P, 16));
+        const int chunk = cdiv(P, Y);
+        p2 = at::empty({Y, D}, opts);
+        colsum_partial_kernel<<<dim3(cdiv(D, 64), Y), 256, 0, st>>>(src, p2.data_ptr<float>(), P, D, chunk);
+        src = p2.data_ptr<float>();
+        P = Y;
+      }
       if (out.scalar_type() == at::kFloat)
-        colsum_kernel<float><<<cdiv(D, 64), 256, 0, st>>>(part.data_ptr<float>(), out.data_ptr<float>(), nparts, D);
+        colsum_kernel<float><<<cdiv(D, 64), 256, 0, st>>>(src, out.data_ptr<float>(), P, D);
       else
-        colsum_kernel<bf16><<<cdiv(D, 64), 256, 0, st>>>(part.data_ptr<float>(), (bf16*)out.data_ptr(), nparts, D);
+        colsum_kernel<bf16><<<cdiv(D, 64), 256, 0, st>>>(src, (bf16*)out.data_ptr(), P, D);
     };
     colsum(dw_part, dw);
     if (is_ln) colsum(db_part, db);

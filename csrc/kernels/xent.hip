@@ -29,11 +29,16 @@ __global__ __launch_bounds__(256) void xent_kernel(T* __restrict__ logits, const
     else s += __expf(v - m);
     sx += v;
   };
+  // vector body over 16-byte-aligned elements [h0, h0 + 8*nv); scalar head/tail (odd V,
+  // e.g. GPT-2's 50257, leaves every row start misaligned)
+  int h0 = 0, nv = 0;
   if constexpr (VEC) {
-    const int nv = V / 8;
+    h0 = (int)(((16 - ((uintptr_t)x & 15)) & 15) / sizeof(T));
+    h0 = min(h0, V);
+    nv = (V - h0) / 8;
     for (int i = threadIdx.x; i < nv; i += 256) {
       float v[8];
-      load8(x + i * 8, v);
+      load8(x + h0 + i * 8, v);
       float lm = v[0];
 #pragma unroll
       for (int k = 1; k < 8; ++k) lm = fmaxf(lm, v[k]);
@@ -44,6 +49,8 @@ __global__ __launch_bounds__(256) void xent_kernel(T* __restrict__ logits, const
       s = s * __expf(m - nm) + acc;
       m = nm;
     }
+    for (int i = threadIdx.x; i < h0; i += 256) upd((float)x[i]);
+    for (int i = h0 + nv * 8 + threadIdx.x; i < V; i += 256) upd((float)x[i]);
   } else {
     for (int i = threadIdx.x; i < V; i += 256) upd((float)x[i]);
   }
@@ -74,18 +81,23 @@ __global__ __launch_bounds__(256) void xent_kernel(T* __restrict__ logits, const
     __syncthreads();  // thread 0 has read x[y] before anyone overwrites it
     const float sc = valid ? (scale_ptr ? *scale_ptr : 1.f) : 0.f;
     const float onv = 1.f - smoothing, off = smoothing / V;
+    auto g1 = [&](int i) {
+      const float v = (float)x[i];
+      x[i] = (T)(sc * (__expf(v - lse) - off - (i == y ? onv : 0.f)));
+    };
     if constexpr (VEC) {
-      const int nv = V / 8;
       for (int i = threadIdx.x; i < nv; i += 256) {
         float v[8];
-        load8(x + i * 8, v);
+        load8(x + h0 + i * 8, v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int c = i * 8 + k;
+          const int c = h0 + i * 8 + k;
           v[k] = sc * (__expf(v[k] - lse) - off - (c == y ? onv : 0.f));
         }
-        store8(x + i * 8, v);
+        store8(x + h0 + i * 8, v);
       }
+      for (int i = threadIdx.x; i < h0; i += 256) g1(i);
+      for (int i = h0 + nv * 8 + threadIdx.x; i < V; i += 256) g1(i);
     } else {
       for (int i = threadIdx.x; i < V; i += 256) {
         const float v = (float)x[i];
@@ -110,7 +122,9 @@ std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& tar
   auto lse = at::empty({N}, opts);
   if (N == 0) return {loss, lse};
   if (scale) TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1);
-  const bool vec = (V % 8 == 0) && (ld % 8 == 0) && ((uintptr_t)logits.data_ptr() % 16 == 0);
+  // every row start is 2-byte (bf16) / 4-byte (fp32) aligned: the kernel peels a scalar head
+  // to reach 16-byte alignment, so the vector path works for any V and row stride
+  const bool vec = ((uintptr_t)logits.data_ptr() % logits.element_size() == 0);
   auto st = stream();
   const float* sp = scale ? scale->data_ptr<float>() : nullptr;
 #define XL(T, VEC, GR)                                                                                     \

@@ -34,20 +34,20 @@ def test_graph_replay_matches_eager():
         out["l"] = loss
 
     x.copy_(xs[0])
-    sg = StepGraph(step, warmup=2)          # 2 warmup steps + 1 captured step ran on xs[0]
+    sg = StepGraph(step, warmup=2)          # 2 eager warmup steps on xs[0]; capture does not execute
     losses_g = []
     for i in range(1, 6):
         x.copy_(xs[i])
         sg.replay()
-        losses_g.append(float(out["l"]))
+        losses_g.append(float(out["l"].detach()))
     m2, f2, o2 = _setup()
     losses_e = []
-    for i in [0, 0, 0] + list(range(1, 6)):
+    for i in [0, 0] + list(range(1, 6)):
         o2.zero_grad()
         loss = m2(xs[i][:, :-1], xs[i][:, 1:])
         loss.backward()
         o2.step()
         losses_e.append(float(loss))
-    assert o1.device_step() == 8 and o2.device_step() == 8
-    assert max(abs(a - b) for a, b in zip(losses_g, losses_e[3:])) < 1e-2
+    assert o1.device_step() == 7 and o2.device_step() == 7
+    assert max(abs(a - b) for a, b in zip(losses_g, losses_e[2:])) < 1e-2
     assert (f1.param.float() - f2.param.float()).abs().max() < 1e-2
