@@ -47,13 +47,25 @@ class _LinearXentFn(torch.autograd.Function):
     def forward(ctx, h, w, b, target, ignore_index, smoothing):
         D = h.shape[-1]
         h2 = h.reshape(-1, D)
-        logits = torch.addmm(b, h2, w.t()) if b is not None else torch.mm(h2, w.t())
+        V = w.shape[0]
+        # odd vocabularies (GPT-2's 50257) make every GEMM leading dimension misaligned;
+        # run the head on a zero-padded copy (multiple of 128 rows: padded logits are exactly
+        # 0 and are excluded from the softmax through the row stride), slice the results
+        Vp = (V + 127) // 128 * 128 if V % 64 else V
+        wp, bp = w, b
+        if Vp != V:
+            wp = w.new_zeros(Vp, D)
+            wp[:V].copy_(w)
+            if b is not None:
+                bp = b.new_zeros(Vp)
+                bp[:V].copy_(b)
+        logits = torch.addmm(bp, h2, wp.t()) if bp is not None else torch.mm(h2, wp.t())
         t = target.reshape(-1).contiguous()
         valid = (t != ignore_index).sum().clamp_min(1).float()
         inv = (1.0 / valid).reshape(1)
-        loss, _ = _ext.ops().xent_fwd(logits, t, ignore_index, smoothing, True, inv)
+        loss, _ = _ext.ops().xent_fwd(logits[:, :V], t, ignore_index, smoothing, True, inv)
         ctx.save_for_backward(h2)
-        ctx.grad_buf, ctx.w, ctx.b, ctx.hshape = logits, w, b, h.shape
+        ctx.grad_buf, ctx.w, ctx.wp, ctx.b, ctx.hshape, ctx.V = logits, w, wp, b, h.shape, V
         return loss.sum() * inv[0]
 
     @staticmethod
@@ -61,9 +73,11 @@ class _LinearXentFn(torch.autograd.Function):
         (h2,) = ctx.saved_tensors
         G = ctx.grad_buf
         ctx.grad_buf = None
-        G.mul_(g.to(G.dtype))
-        w, b = ctx.w, ctx.b
-        dh = torch.mm(G, w).view(ctx.hshape) if ctx.needs_input_grad[0] else None
+        G.mul_(g.to(G.dtype))                 # padded columns are exactly 0
+        w, b, wp = ctx.w, ctx.b, ctx.wp
+        ctx.wp = None
+        dh = torch.mm(G, wp).view(ctx.hshape) if ctx.needs_input_grad[0] else None
+        G = G[:, :ctx.V]
         gw = gb = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):
