@@ -177,3 +177,35 @@ def test_kd_and_vit_training_cpu():
     _, accs = vit.train(vit.config("vit_mnist_ref"), epochs=2, device="cpu", n_train=1024, n_test=256,
                         log=lambda *a: None)
     assert accs[-1] > 30.0
+
+
+def test_reference_named_api(tmp_path):
+    """Reference entry-point names (solvingpapers_amd/api.py): pickle-free LLaMA pytree I/O,
+    DSV3 get_lr / compute_mtp_loss / topk_sampling / checkpoint, estimate_loss."""
+    import torch.nn.functional as F
+    from solvingpapers_amd import api
+    from solvingpapers_amd.models import deepseekv3 as ds, llama3
+    m = llama3.Llama3(llama3.config("llama3_ref", vocab_size=64, dim=32, n_heads=4, n_kv_heads=2, ffn_hidden=64))
+    tree = m.to_reference_params()
+    p = str(tmp_path / "params.safetensors")
+    api.save_params(tree, p)
+    back = api.load_params(p)
+    m2 = llama3.Llama3(llama3.config("llama3_ref", vocab_size=64, dim=32, n_heads=4, n_kv_heads=2, ffn_hidden=64), seed=3)
+    m2.from_reference_params(back)
+    for a, b in zip(m.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+    assert abs(api.get_lr(0) - 6e-4 / 401) < 1e-12 and abs(api.get_lr(20000) - 6e-5) < 1e-12
+    # compute_mtp_loss vs the notebook's double loop
+    B, T, D, C = 2, 5, 2, 7
+    lg = torch.randn(B, T, D, C)
+    tg = torch.randint(0, C, (B, T))
+    idx = [min(i + k + 1, T - 1) for i in range(T) for k in range(D)]
+    ref = F.cross_entropy(lg.reshape(-1, C), tg[:, idx].reshape(-1))
+    assert torch.allclose(api.compute_mtp_loss(lg, tg), ref)
+    dm = ds.DeepSeekV3(ds.config("dsv3_tiny", vocab_size=64, n_layers=1))
+    out = api.topk_sampling(dm, torch.zeros(1, 3, dtype=torch.long), max_length=8, top_k=5,
+                            generator=torch.Generator().manual_seed(0))
+    assert out.shape == (1, 8)
+    data = torch.randint(0, 64, (500,))
+    est = api.estimate_loss(m, {"train": data, "val": data}, 2, 4, 16)
+    assert set(est) == {"train", "val"} and all(v > 0 for v in est.values())
