@@ -26,7 +26,8 @@
 //    masks only on straddling tiles.
 //  * Backward = two deterministic kernels (no float atomics): dq (query-parallel,
 //    also produces delta = rowsum(dO*O)) then dkdv (key-parallel, loops the GQA
-//    group's q-heads so dK/dV of a kv-head are summed in registers).
+//    group's q-heads so dK/dV of a kv-head are summed in registers). An optional
+//    fused variant (dkdv<..., FUSEDQ>) adds dQ += dS K with fp32 atomics.
 // q/k/v/o and grads are addressed with (batch, seq, head) strides so the kernels
 // read/write a fused [B, T, H + 2*Hkv, hd] qkv buffer in place.
 #include "spa_common.h"
@@ -37,7 +38,7 @@ namespace spa {
 struct AttnParams {
   const bf16* q; const bf16* k; const bf16* v; const bf16* o; const bf16* dout;
   bf16* out; bf16* dq; bf16* dk; bf16* dv;
-  float* lse; const float* lse_in; float* delta;
+  float* lse; const float* lse_in; float* delta; float* dqacc;  // dqacc: fused bwd fp32 dQ [B,Tq,H,HD]
   int B, H, Hkv, Tq, Tk;
   long sqb, sqt, sqh, skb, skt, skh, svb, svt, svh, sob, sot, soh;
   long sdob, sdot, sdoh;
@@ -431,12 +432,18 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 //   dV^T += dO^T P, dK^T += Q^T dS   (A = tr reads of the Q / dO images, B = accumulators)
 // Loops over the q-heads sharing this kv-head (GQA) so the group sum stays in regs.
 // ---------------------------------------------------------------------------
-template <int HD, bool CAUSAL, int MT>
+template <int HD, bool CAUSAL, int MT, bool FUSEDQ>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   // MT 32-row q sub-tiles per iteration (more MFMA work per barrier / LDS fill)
   constexpr int BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 256;
   constexpr int TILE = BMQ * HD;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][Q|dO]
+  // FUSEDQ: dQ computed here too (dQ += dS K over this block's 128 keys, fp32 atomics into
+  // p.dqacc) -> 5 MFMA products per tile instead of 7 for the split dq + dkdv kernels.
+  // dS crosses LDS once ([key][q] image, transposed reads), K sits in a [key][d] image.
+  constexpr int KIMG = FUSEDQ ? BNK * HD : 8, DSIMG = FUSEDQ ? BNK * 64 : 8;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE + KIMG + DSIMG];  // [buf][Q|dO] | K | dS
+  bf16* kimg = smem + 4 * TILE;
+  bf16* dsimg = kimg + KIMG;
   __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];  // [buf][lse2 | delta]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lk = lane & 31, hh = lane >> 5;
@@ -457,6 +464,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     for (int s = 0; s < KS; ++s) {
       kf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(kp + 16 * s) : zero8();
       vf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(vp + 16 * s) : zero8();
+      if constexpr (FUSEDQ)   // row = this lane's key; chunk 2s+hh holds d = 16s + 8hh .. +8
+        *reinterpret_cast<bf16x8*>(kimg + img_off<HD>(wave * 32 + lk, 2 * s + hh)) = kf[s];
     }
   }
   f32x16 dkt[DT], dvt[DT];
@@ -547,6 +556,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
       bf16x8 pf[2 * MT], sf[2 * MT];
 #pragma unroll
       for (int kk = 0; kk < 2 * MT; ++kk) { pf[kk] = pack_acc(s[kk >> 1], kk & 1); sf[kk] = pack_acc(dp[kk >> 1], kk & 1); }
+      if constexpr (FUSEDQ) {
+        // dS rows of this wave's 32 keys -> [key][q] image (registers 4g..4g+3 = 4 consecutive q)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 w4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w4[i] = (bf16)dp[t][4 * g + i];
+            *reinterpret_cast<bf16x4*>(dsimg + img_off<64>(wave * 32 + lk, 4 * t + g) + 4 * hh) = w4;
+          }
+      }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -554,6 +575,38 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
           dvt[dt] = mfma32(ld_tr(Ds + 16 * kk * HD, off.tra[dt], off.trb[dt]), pf[kk], dvt[dt]);
           dkt[dt] = mfma32(ld_tr(Qs + 16 * kk * HD, off.tra[dt], off.trb[dt]), sf[kk], dkt[dt]);
         }
+    } else if constexpr (FUSEDQ) {
+      // masked-out wave: its keys contribute nothing to dQ this tile
+      bf16x4 z4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) z4[i] = (bf16)0.f;
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<bf16x4*>(dsimg + img_off<64>(wave * 32 + lk, 4 * t + g) + 4 * hh) = z4;
+    }
+    if constexpr (FUSEDQ) {
+      __syncthreads();  // dS image complete
+      const int h = hk * G + it / nper;
+#pragma unroll
+      for (int tile = wave; tile < MT * DT; tile += 4) {
+        const int tq = tile / DT, td = tile % DT;
+        const int q0 = qq0 + 32 * tq;
+        if (CAUSAL && q0 + 31 + p.causal_off < kb * BNK) continue;   // every key of the block is masked
+        if (q0 >= p.Tq) continue;
+        f32x16 acc;
+        zero16(acc);
+#pragma unroll
+        for (int kk = 0; kk < BNK / 16; ++kk)
+          acc = mfma32(rd_tr<64>(dsimg, 16 * kk, 32 * tq, lane), rd_tr<HD>(kimg, 16 * kk, 32 * td, lane), acc);
+        float* dst = p.dqacc + ((long)b * p.Tq * p.H + h) * HD + 32 * td + lk;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qq = q0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (qq < p.Tq) atomicAdd(dst + (long)qq * p.H * HD, acc[r]);
+        }
+      }
     }
     __syncthreads();
   };
@@ -577,6 +630,46 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
         *reinterpret_cast<bf16x4*>(kp + 32 * dt + 8 * g + 4 * hh) = wk;
         *reinterpret_cast<bf16x4*>(vp + 32 * dt + 8 * g + 4 * hh) = wv;
       }
+  }
+}
+
+// delta[b,h,q] = sum_d dO*O (fp32); TPR = HD/8 threads per row
+template <int HD>
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p) {
+  constexpr int TPR = HD / 8, RPB = 256 / TPR;
+  const long row = (long)blockIdx.x * RPB + threadIdx.x / TPR;
+  const int t = threadIdx.x % TPR;
+  const long nrows = (long)p.B * p.Tq * p.H;
+  float acc = 0.f;
+  long b = 0, q = 0, h = 0;
+  if (row < nrows) {
+    h = row % p.H;
+    q = (row / p.H) % p.Tq;
+    b = row / ((long)p.H * p.Tq);
+    float a[8], c[8];
+    load8(p.dout + b * p.sdob + q * p.sdot + h * p.sdoh + 8 * t, a);
+    load8(p.o + b * p.sob + q * p.sot + h * p.soh + 8 * t, c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += a[i] * c[i];
+  }
+#pragma unroll
+  for (int o = TPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, TPR);
+  if (row < nrows && t == 0) p.delta[(b * p.H + h) * p.Tq + q] = acc;
+}
+// dq (strided bf16) = scale * dqacc
+template <int HD>
+__global__ __launch_bounds__(256) void attn_dq_store_kernel(AttnParams p) {
+  constexpr int TPR = HD / 8;
+  const long n = (long)p.B * p.Tq * p.H * TPR;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int t = i % TPR;
+    const long row = i / TPR;
+    const long h = row % p.H, q = (row / p.H) % p.Tq, b = row / ((long)p.H * p.Tq);
+    float a[8];
+    load8(p.dqacc + row * HD + 8 * t, a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] *= p.scale;
+    store8(p.dq + b * p.sdqb + q * p.sdqt + h * p.sdqh + 8 * t, a);
   }
 }
 
@@ -669,16 +762,37 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   if (B * H == 0) return;
   auto st = stream();
   if (Tq == 0) { dk.zero_(); dv.zero_(); return; }
+  // default: the deterministic two-kernel path (dq kernel + dkdv kernel, no atomics).
+  // SPA_ATTN_BWD_FUSED=1: one pass computing dQ too (5 MFMA products per tile instead of 7)
+  // with fp32 dQ atomics. Measured on MI355X at LLaMA3-8B shape (B1 T8192 H32/8 hd128):
+  // fused 3.87 ms vs split 2.74 ms -- with 128-key blocks each dQ row receives T/128 atomic
+  // adds (~4 GB of adds per call), past the chip-wide atomic rate; kept as an option.
+  static const bool want_fused = getenv("SPA_ATTN_BWD_FUSED") && atoi(getenv("SPA_ATTN_BWD_FUSED")) != 0;
+  const bool fused = want_fused && Tk > 0 && HD <= 128;
+  at::Tensor dqacc;
+  if (fused) {
+    dqacc = at::zeros({B, Tq, H, HD}, q.options().dtype(at::kFloat));
+    p.dqacc = dqacc.data_ptr<float>();
+  }
   HD_SWITCH(HD, {
     constexpr int NW = fwd_waves<HD_>();
-    const int grid = cdiv(Tq, 32 * NW) * H * B;
-    if (causal) attn_bwd_dq_kernel<HD_, NW, true><<<grid, NW * 64, 0, st>>>(p);
-    else attn_bwd_dq_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
-    if (Tk > 0) {
-      const int g2 = cdiv(Tk, 128) * Hkv * B;
-      constexpr int MT = HD_ == 128 ? 2 : 1;
-      if (causal) attn_bwd_dkdv_kernel<HD_, true, MT><<<g2, 256, 0, st>>>(p);
-      else attn_bwd_dkdv_kernel<HD_, false, MT><<<g2, 256, 0, st>>>(p);
+    constexpr int MT = HD_ == 128 ? 2 : 1;
+    const int g2 = cdiv(Tk, 128) * Hkv * B;
+    if (fused && HD_ <= 128) {   // hd 256: the fused body exceeds the register file (spills)
+      const long rows = (long)B * Tq * H;
+      attn_delta_kernel<HD_><<<(int)cdiv(rows, 256 / (HD_ / 8)), 256, 0, st>>>(p);
+      if (causal) attn_bwd_dkdv_kernel<HD_, true, MT, true><<<g2, 256, 0, st>>>(p);
+      else attn_bwd_dkdv_kernel<HD_, false, MT, true><<<g2, 256, 0, st>>>(p);
+      const long n = rows * (HD_ / 8);
+      attn_dq_store_kernel<HD_><<<(int)std::min<long>((n + 255) / 256, 65536), 256, 0, st>>>(p);
+    } else {
+      const int grid = cdiv(Tq, 32 * NW) * H * B;
+      if (causal) attn_bwd_dq_kernel<HD_, NW, true><<<grid, NW * 64, 0, st>>>(p);
+      else attn_bwd_dq_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
+      if (Tk > 0) {
+        if (causal) attn_bwd_dkdv_kernel<HD_, true, MT, false><<<g2, 256, 0, st>>>(p);
+        else attn_bwd_dkdv_kernel<HD_, false, MT, false><<<g2, 256, 0, st>>>(p);
+      }
     }
   });
   SPA_LAUNCH_CHECK();

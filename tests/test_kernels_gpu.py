@@ -222,3 +222,37 @@ def test_packed_attention_matches_split():
     o2.backward(g)
     assert torch.equal(o, o2)
     assert rel(qkv.grad, q2.grad.reshape(B, T, -1)) < 1e-3
+
+
+def test_attention_fused_bwd_matches_split():
+    """The optional fused backward (dQ via fp32 atomics inside the dK/dV kernel) against the
+    default split kernels, run in a subprocess because the mode is read once per process."""
+    import os, subprocess, sys, textwrap
+    code = textwrap.dedent("""
+        import math, torch, sys
+        from solvingpapers_amd.ops import _ext
+        ops = _ext.ops()
+        torch.manual_seed(0)
+        for (T, H, Hkv, hd, causal) in [(300, 4, 2, 128, True), (256, 4, 4, 64, False), (129, 2, 1, 128, True)]:
+            q = torch.randn(2, T, H, hd, device='cuda', dtype=torch.bfloat16)
+            k = torch.randn(2, T, Hkv, hd, device='cuda', dtype=torch.bfloat16)
+            v = torch.randn(2, T, Hkv, hd, device='cuda', dtype=torch.bfloat16)
+            sc = 1 / math.sqrt(hd)
+            o, lse = ops.attn_fwd(q, k, v, sc, causal)
+            do = torch.randn_like(o)
+            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            ops.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, sc, causal)
+            torch.save([dq.cpu(), dk.cpu(), dv.cpu()], sys.argv[1] + f'_{T}.pt')
+    """)
+    outs = {}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for mode in ("0", "1"):
+        env = dict(os.environ, SPA_ATTN_BWD_FUSED=mode, PYTHONPATH=root)
+        pref = f"/tmp/spa_attn_fused_{mode}"
+        subprocess.run([sys.executable, "-c", code, pref], check=True, env=env, cwd=root)
+        outs[mode] = pref
+    for T in (300, 256, 129):
+        a = torch.load(outs["0"] + f"_{T}.pt", weights_only=True)
+        b = torch.load(outs["1"] + f"_{T}.pt", weights_only=True)
+        for x, y in zip(a, b):
+            assert (x.float() - y.float()).norm() / x.float().norm() < 2e-2
