@@ -1,0 +1,72 @@
+// Layout kernels: bf16/fp32 2-D transpose through a padded LDS tile.
+//
+// Used to feed the weight-gradient GEMM dW = dY^T X in the layout hipBLASLt runs fastest
+// on gfx950: with both operands transposed to K(token)-contiguous rows the product is the
+// "NT" form x @ w^T, measured at LLaMA3-8B shapes (T = 8192) at 1.2-1.63 PF vs 0.94-1.13 PF
+// for the "TN" form (tools/bench_gemm_layouts.py) -- the transposes cost far less than that.
+//
+// Tile 64 x 64, 256 threads: 16-byte global loads of rows -> LDS [64][72] (row pad keeps the
+// column gathers on distinct banks) -> 8 column elements per thread -> 16-byte global stores.
+#include "spa_common.h"
+
+namespace spa {
+
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int R, int C,
+                                                        long ldx, long ldy) {
+  constexpr int TS = 64, PAD = 16 / sizeof(T), LD = TS + PAD, VE = 16 / sizeof(T);  // VE elements per 16 B
+  __shared__ __attribute__((aligned(16))) T tile[TS * LD];
+  const int r0 = blockIdx.y * TS, c0 = blockIdx.x * TS;
+  constexpr int CPR = TS / VE;                  // 16-byte chunks per tile row
+  constexpr int NCH = TS * CPR;                 // chunks per tile
+#pragma unroll
+  for (int c = 0; c < NCH / 256; ++c) {
+    const int idx = threadIdx.x + 256 * c;
+    const int r = idx / CPR, ch = idx % CPR;
+    const int gr = r0 + r, gc = c0 + ch * VE;
+    uint4 v = {0, 0, 0, 0};
+    if (gr < R && gc < C) v = *reinterpret_cast<const uint4*>(x + (long)gr * ldx + gc);
+    *reinterpret_cast<uint4*>(tile + r * LD + ch * VE) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NCH / 256; ++c) {
+    const int idx = threadIdx.x + 256 * c;
+    const int j = idx / CPR, ch = idx % CPR;     // output row j (= input column), chunk of input rows
+    const int orow = c0 + j, ocol = r0 + ch * VE;
+    if (orow < C && ocol < R) {
+      T o[VE];
+#pragma unroll
+      for (int e = 0; e < VE; ++e) o[e] = tile[(ch * VE + e) * LD + j];
+      *reinterpret_cast<uint4*>(y + (long)orow * ldy + ocol) = *reinterpret_cast<uint4*>(o);
+    }
+  }
+}
+
+// x [R, C] (row stride ldx, unit column stride) -> y [C, R] contiguous
+at::Tensor transpose2d(const at::Tensor& x) {
+  SPA_CHECK_CUDA(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "transpose2d: [R, C] with unit column stride");
+  const int R = x.size(0), C = x.size(1);
+  const int ve = 16 / (int)x.element_size();
+  TORCH_CHECK(R % ve == 0 && C % ve == 0 && x.stride(0) % ve == 0 && (uintptr_t)x.data_ptr() % 16 == 0,
+              "transpose2d: rows/cols must be 16-byte multiples");
+  DeviceGuard g(x.device());
+  auto y = at::empty({C, R}, x.options());
+  if (R == 0 || C == 0) return y;
+  dim3 grid(cdiv(C, 64), cdiv(R, 64));
+  if (x.scalar_type() == at::kBFloat16)
+    transpose_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), R, C,
+                                                       x.stride(0), R);
+  else if (x.scalar_type() == at::kFloat)
+    transpose_kernel<float><<<grid, 256, 0, stream()>>>(x.data_ptr<float>(), y.data_ptr<float>(), R, C, x.stride(0), R);
+  else
+    TORCH_CHECK(false, "transpose2d: bf16/fp32");
+  SPA_LAUNCH_CHECK();
+  return y;
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) { m.def("transpose2d(Tensor x) -> Tensor"); }
+TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("transpose2d", &spa::transpose2d); }

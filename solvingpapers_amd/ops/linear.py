@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from ..utils.grad import commit
+from .layout import wgrad
 
 
 class _LinearFn(torch.autograd.Function):
@@ -36,12 +37,14 @@ class _LinearFn(torch.autograd.Function):
         gw = gb = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):
-                if out is None:
-                    return torch.mm(dy2.t(), x2)
-                if acc:
-                    out.addmm_(dy2.t(), x2)
-                else:
-                    torch.mm(dy2.t(), x2, out=out)
+                if out is not None and out.dtype != dy2.dtype:
+                    g = wgrad(dy2, x2)
+                    if acc:
+                        out.add_(g)
+                    else:
+                        out.copy_(g)
+                    return None
+                return wgrad(dy2, x2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
             def _b(out, acc):

@@ -9,7 +9,9 @@ from __future__ import annotations
 
 import torch
 
-from . import _ext, reference
+from . import _ext
+from . import reference
+from .layout import wgrad
 from ..utils.grad import commit, commit_tensor
 
 
@@ -81,12 +83,14 @@ class _LinearXentFn(torch.autograd.Function):
         gw = gb = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):
-                if out is None:
-                    return torch.mm(G.t(), h2)
-                if acc:
-                    out.addmm_(G.t(), h2)
-                else:
-                    torch.mm(G.t(), h2, out=out)
+                if out is not None and out.dtype != G.dtype:
+                    g = wgrad(G, h2)
+                    if acc:
+                        out.add_(g)
+                    else:
+                        out.copy_(g)
+                    return None
+                return wgrad(G, h2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
             gb = commit_tensor(b, G.float().sum(0).to(b.dtype))

@@ -256,3 +256,24 @@ def test_attention_fused_bwd_matches_split():
         b = torch.load(outs["1"] + f"_{T}.pt", weights_only=True)
         for x, y in zip(a, b):
             assert (x.float() - y.float()).norm() / x.float().norm() < 2e-2
+
+
+@pytest.mark.parametrize("R,C,dt", [(8192, 4096, torch.bfloat16), (200, 136, torch.bfloat16), (64, 4100, torch.float32)])
+def test_transpose2d(R, C, dt):
+    from solvingpapers_amd.ops.layout import transpose2d
+    x = torch.randn(R, C, device="cuda", dtype=dt)
+    assert torch.equal(transpose2d(x), x.t().contiguous())
+    xs = torch.randn(R, C + 16, device="cuda", dtype=dt)[:, 8:C + 8]
+    assert torch.equal(transpose2d(xs), xs.t().contiguous())
+
+
+def test_wgrad_nt_matches_tn():
+    from solvingpapers_amd.ops.layout import wgrad
+    dy = torch.randn(4096, 1024, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(4096, 512, device="cuda", dtype=torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    out = wgrad(dy, x)
+    assert ((out.float() - ref).norm() / ref.norm()) < 1e-2
+    acc = out.clone()
+    wgrad(dy, x, acc, True)
+    assert ((acc.float() - 2 * ref).norm() / ref.norm()) < 1e-2
