@@ -13,7 +13,9 @@ namespace spa {
 
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int R, int C,
-                                                        long ldx, long ldy) {
+                                                        long ldx, long ldy, long bsx, long bsy) {
+  x += blockIdx.z * bsx;   // batch (e.g. one expert's [N, K] weight per z)
+  y += blockIdx.z * bsy;
   constexpr int TS = 64, PAD = 16 / sizeof(T), LD = TS + PAD, VE = 16 / sizeof(T);  // VE elements per 16 B
   __shared__ __attribute__((aligned(16))) T tile[TS * LD];
   const int r0 = blockIdx.y * TS, c0 = blockIdx.x * TS;
@@ -43,23 +45,28 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ x,
   }
 }
 
-// x [R, C] (row stride ldx, unit column stride) -> y [C, R] contiguous
-at::Tensor transpose2d(const at::Tensor& x) {
-  SPA_CHECK_CUDA(x);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "transpose2d: [R, C] with unit column stride");
-  const int R = x.size(0), C = x.size(1);
+// x [R, C] or [Bt, R, C] (row stride ldx, unit column stride) -> y [C, R] / [Bt, C, R] contiguous
+at::Tensor transpose2d(const at::Tensor& x_) {
+  SPA_CHECK_CUDA(x_);
+  TORCH_CHECK((x_.dim() == 2 || x_.dim() == 3) && x_.stride(-1) == 1, "transpose2d: [(Bt,) R, C], unit column stride");
+  const bool batched = x_.dim() == 3;
+  const at::Tensor x = batched ? x_.contiguous() : x_;
+  const int Bt = batched ? x.size(0) : 1;
+  const int R = x.size(-2), C = x.size(-1);
   const int ve = 16 / (int)x.element_size();
-  TORCH_CHECK(R % ve == 0 && C % ve == 0 && x.stride(0) % ve == 0 && (uintptr_t)x.data_ptr() % 16 == 0,
+  TORCH_CHECK(R % ve == 0 && C % ve == 0 && x.stride(-2) % ve == 0 && (uintptr_t)x.data_ptr() % 16 == 0,
               "transpose2d: rows/cols must be 16-byte multiples");
   DeviceGuard g(x.device());
-  auto y = at::empty({C, R}, x.options());
-  if (R == 0 || C == 0) return y;
-  dim3 grid(cdiv(C, 64), cdiv(R, 64));
+  auto y = batched ? at::empty({Bt, C, R}, x.options()) : at::empty({C, R}, x.options());
+  if (R == 0 || C == 0 || Bt == 0) return y;
+  dim3 grid(cdiv(C, 64), cdiv(R, 64), Bt);
+  const long ld = x.stride(-2), bsx = batched ? x.stride(0) : 0, bsy = (long)R * C;
   if (x.scalar_type() == at::kBFloat16)
-    transpose_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), R, C,
-                                                       x.stride(0), R);
+    transpose_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), R, C, ld, R,
+                                                       bsx, bsy);
   else if (x.scalar_type() == at::kFloat)
-    transpose_kernel<float><<<grid, 256, 0, stream()>>>(x.data_ptr<float>(), y.data_ptr<float>(), R, C, x.stride(0), R);
+    transpose_kernel<float><<<grid, 256, 0, stream()>>>(x.data_ptr<float>(), y.data_ptr<float>(), R, C, ld, R, bsx,
+                                                        bsy);
   else
     TORCH_CHECK(false, "transpose2d: bf16/fp32");
   SPA_LAUNCH_CHECK();

@@ -71,6 +71,7 @@ class DSV3Config:
     expert_hidden: int = 0          # 0 -> (2*D*4)//3 (reference SWiGLUExpert)
     n_dense_layers: int = 0         # leading layers with a dense SwiGLU FFN
     dense_hidden: int = 0
+    moe_fp8: bool = False           # routed-expert fwd/dX GEMMs in OCP e4m3 (BASELINE config #5)
     aux_free: bool = True
     bias_update_rate: float = 1e-3
     bias_in_weights: bool = True    # ref: softmax over (logits + bias); paper: bias steers selection only
@@ -325,7 +326,8 @@ class MoE(tnn.Module):
         x2 = x.reshape(-1, D)
         logits = torch.mm(x2.float(), self.gate.float().t())
         idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
-        y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group)
+        y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group,
+                             fp8=c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0)
         if self.shared is not None:
             y = y + self.shared(x2)
         self.last_counts = plan.counts

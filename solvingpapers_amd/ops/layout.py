@@ -14,10 +14,10 @@ WGRAD_NT_MIN_TOKENS = 2048
 
 
 def transpose2d(x: torch.Tensor) -> torch.Tensor:
-    """[R, C] -> contiguous [C, R]."""
+    """[R, C] -> contiguous [C, R] (or batched [Bt, R, C] -> [Bt, C, R])."""
     if x.is_cuda and x.dtype in (torch.bfloat16, torch.float32):
         return _ext.ops().transpose2d(x)
-    return x.t().contiguous()
+    return x.transpose(-1, -2).contiguous()
 
 
 def wgrad_nt_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:

@@ -216,12 +216,80 @@ class _GroupedLinearFn(torch.autograd.Function):
         return dx, gw, None
 
 
-def grouped_linear(xp, W, plan: MoEPlan):
-    """Per-expert ``xp[rows_e] @ W[e]^T`` for expert-ordered rows; W [E, out, in]."""
+def grouped_linear(xp, W, plan: MoEPlan, fp8: bool = False):
+    """Per-expert ``xp[rows_e] @ W[e]^T`` for expert-ordered rows; W [E, out, in].
+    ``fp8``: forward and dX products in OCP e4m3 on the block-scaled MFMA (per-row scales,
+    csrc/kernels/moe_fp8.hip); dW stays bf16."""
+    if fp8:
+        return _GroupedLinearFP8Fn.apply(xp, W, plan)
     return _GroupedLinearFn.apply(xp, W, plan)
 
 
-def moe_ffn(x, idx, w, W13, W2, act="silu"):
+# --------------------------------------------------------------------------- fp8 path
+def quant_rows_fp8(x):
+    """Row-wise e4m3 quantization: (q, scale) with x ~= q * scale[:, None], scale = amax/448."""
+    if x.is_cuda:
+        q, s = ops().quant_rows_fp8(x.contiguous())
+        return q, s
+    x2 = x.reshape(-1, x.shape[-1]).float()
+    s = (x2.abs().amax(-1) / 448.0).clamp_min(0)
+    s = torch.where(s > 0, s, torch.ones_like(s))
+    q = (x2 / s[:, None]).to(torch.float8_e4m3fn).view(x.shape)
+    return q, s
+
+
+def grouped_gemm_fp8(xq, sx, wq, sw, offsets):
+    if xq.is_cuda:
+        return ops().grouped_gemm_fp8(xq, sx, wq, sw.reshape(wq.shape[0], wq.shape[1]), offsets)
+    x = xq.float() * sx[:, None]
+    w = wq.float() * sw.reshape(wq.shape[0], wq.shape[1], 1)
+    return _cpu_grouped(x, w, offsets, 0).to(torch.bfloat16)
+
+
+def _quant_weight(W):
+    E, N, K = W.shape
+    q, s = quant_rows_fp8(W.reshape(E * N, K))
+    return q.view(E, N, K), s.view(E, N)
+
+
+class _GroupedLinearFP8Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xp, W, plan):
+        ctx.plan, ctx.W = plan, W
+        ctx.save_for_backward(xp)
+        xq, sx = quant_rows_fp8(xp)
+        wq, sw = _quant_weight(W)
+        return grouped_gemm_fp8(xq, sx, wq, sw, plan.offsets).to(xp.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .layout import transpose2d
+        (xp,) = ctx.saved_tensors
+        W, plan = ctx.W, ctx.plan
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dq, sd = quant_rows_fp8(dy)
+            wtq, swt = _quant_weight(transpose2d(W))          # [E, in, out]
+            dx = grouped_gemm_fp8(dq, sd, wtq, swt, plan.offsets).to(xp.dtype)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            def _w(out, acc):
+                if out is None:
+                    return grouped_gemm(dy, xp, plan.offsets, 2)
+                if out.dtype == dy.dtype and out.is_contiguous():
+                    grouped_gemm(dy, xp, plan.offsets, 2, out=out.view(W.shape), accumulate=acc)
+                else:
+                    g = grouped_gemm(dy, xp, plan.offsets, 2)
+                    if acc:
+                        out.add_(g.view_as(out))
+                    else:
+                        out.copy_(g.view_as(out))
+            gw = commit(W, _w)
+        return dx, gw, None
+
+
+def moe_ffn(x, idx, w, W13, W2, act="silu", fp8=False):
     """Routed SwiGLU/GeGLU experts: sum_j w[n,j] * E_{idx[n,j]}(x[n]).
 
     ``W13`` [E, 2F, D] = per-expert [gate; up], ``W2`` [E, D, F].
@@ -229,9 +297,9 @@ def moe_ffn(x, idx, w, W13, W2, act="silu"):
     from .activation import glu
     plan = permute(idx, W13.shape[0])
     xp = gather(x, plan)
-    h = grouped_linear(xp, W13, plan)
+    h = grouped_linear(xp, W13, plan, fp8)
     h = glu(h, act)
-    yp = grouped_linear(h, W2, plan)
+    yp = grouped_linear(h, W2, plan, fp8)
     return combine(yp, w, plan), plan
 
 

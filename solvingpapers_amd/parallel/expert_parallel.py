@@ -72,7 +72,7 @@ def _regroup_index(rc):
     return idx, offsets
 
 
-def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu"):
+def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
     [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
     ``W2`` [E/P, D, F] are this rank's experts. Returns (y [N, D], local plan)."""
@@ -80,8 +80,8 @@ def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu"):
     plan = permute(idx, n_experts)
     if P == 1:
         xp = gather(x, plan)
-        h = glu(grouped_linear(xp, W13, plan), act)
-        return combine(grouped_linear(h, W2, plan), w, plan), plan
+        h = glu(grouped_linear(xp, W13, plan, fp8), act)
+        return combine(grouped_linear(h, W2, plan, fp8), w, plan), plan
     El = n_experts // P
     assert El * P == n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
     counts = plan.counts.to(torch.int64)
@@ -100,8 +100,8 @@ def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu"):
     inv[ridx] = torch.arange(ridx.numel(), device=dev)
     lplan = SimpleNamespace(offsets=loff.to(device=dev, dtype=torch.int32))
     xl = xr.index_select(0, ridx)
-    h = glu(grouped_linear(xl, W13, lplan), act)
-    yl = grouped_linear(h, W2, lplan)
+    h = glu(grouped_linear(xl, W13, lplan, fp8), act)
+    yl = grouped_linear(h, W2, lplan, fp8)
     yr = yl.index_select(0, inv)
     yp = all_to_all(yr, send_splits, recv_splits, group)
     return combine(yp, w, plan), plan

@@ -66,9 +66,12 @@ class FlatOptimizer:
         for (a, b), so in zip(self.ranges, self.state_off):
             for sa, sb, dec in self.flat.decay_segments:
                 lo, hi = max(a, sa), min(b, sb)
-                if lo < hi:
-                    bi = next(i for i, bk in enumerate(self.flat.buckets) if bk.start <= lo < bk.end)
-                    out.append((lo, hi, so + lo - a, dec, bi))
+                # split at bucket boundaries: one update (and one ready event) per bucket, so
+                # an overlapped optimizer releases layer i's params as soon as they are done
+                for bi, bk in enumerate(self.flat.buckets):
+                    l2, h2 = max(lo, bk.start), min(hi, bk.end)
+                    if l2 < h2:
+                        out.append((l2, h2, so + l2 - a, dec, bi))
         out.sort(key=lambda x: x[0])
         return out
 

@@ -152,3 +152,46 @@ def test_deepseek_gpu_matches_cpu(preset):
         assert _rel(b.grad.cpu(), a.grad) < tol, n
     out = gpu.generate(ids[:, :8].to(dev), 8, greedy=True)
     assert out.shape == (2, 16)
+
+
+def test_quant_rows_fp8_matches_torch():
+    x = torch.randn(777, 1408, device=dev, dtype=torch.bfloat16) * 3
+    q, s = M.quant_rows_fp8(x)
+    s_ref = x.float().abs().amax(-1) / 448.0
+    assert torch.allclose(s, s_ref, rtol=1e-6)
+    q_ref = (x.float() / s_ref[:, None]).to(torch.float8_e4m3fn)
+    mism = (q.view(torch.uint8) != q_ref.view(torch.uint8)).float().mean().item()
+    assert mism < 5e-3, mism   # x*(1/s) vs x/s rounding moves a few values by one fp8 step
+    deq = q.float() * s[:, None]
+    assert ((deq - x.float()).norm() / x.float().norm()) < 0.04
+
+
+@pytest.mark.parametrize("counts", [[300, 0, 129, 1, 64, 700, 0, 33], [512] * 4])
+def test_grouped_gemm_fp8_exact_on_dequantized(counts):
+    torch.manual_seed(5)
+    E, K, N = len(counts), 2048, 1408
+    Mt = sum(counts)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    x = torch.randn(Mt, K, device=dev, dtype=torch.bfloat16)
+    W = torch.randn(E, N, K, device=dev, dtype=torch.bfloat16) * 0.02
+    xq, sx = M.quant_rows_fp8(x)
+    wq, sw = M.quant_rows_fp8(W.view(E * N, K))
+    y = M.grouped_gemm_fp8(xq, sx, wq.view(E, N, K), sw, off)
+    ref = M._cpu_grouped((xq.float() * sx[:, None]).cpu(), (wq.float() * sw[:, None]).view(E, N, K).cpu(), off.cpu(), 0)
+    assert _rel(y.cpu(), ref) < 1e-2
+
+
+def test_moe_ffn_fp8_close_to_bf16():
+    torch.manual_seed(6)
+    N, D, F, E, k = 2048, 512, 256, 16, 4
+    x = (torch.randn(N, D, device=dev) * 0.5).bfloat16().requires_grad_(True)
+    W13 = (torch.randn(E, 2 * F, D, device=dev) / D ** 0.5).bfloat16().requires_grad_(True)
+    W2 = (torch.randn(E, D, F, device=dev) / F ** 0.5).bfloat16().requires_grad_(True)
+    idx, w = M.route(torch.randn(N, E, device=dev), k)
+    outs = []
+    for fp8 in (False, True):
+        y, _ = M.moe_ffn(x, idx, w, W13, W2, fp8=fp8)
+        g = torch.autograd.grad((y.float() ** 2).sum(), [x, W13, W2])
+        outs.append([y.float()] + [t.float() for t in g])
+    for a, b in zip(outs[1], outs[0]):
+        assert _rel(a, b) < 0.1

@@ -56,6 +56,13 @@ for name, (fn, fl) in cases.items():
         ms = tm(lambda: fn(c))
         row.append(f"c{c}:{fl / ms / 1e9:6.0f}TF{'' if err < 1e-2 else ' ERR%.2e' % err}")
     print(f"{name:8s} " + " ".join(row))
+xq, sx = M.quant_rows_fp8(x)
+wq, sw = M.quant_rows_fp8(W13.view(E * 2 * F, D))
+wq = wq.view(E, 2 * F, D)
+ms = tm(lambda: ops.grouped_gemm_fp8(xq, sx, wq, sw.view(E, 2 * F), plan.offsets))
+print(f"fp8 fwd W13 grouped GEMM: {2 * A * 2 * F * D / ms / 1e9:.0f} TF (e4m3, block-scaled MFMA)")
+msq = tm(lambda: M.quant_rows_fp8(x))
+print(f"quant_rows_fp8 [{A}x{D}]: {msq*1e3:.3f} ms = {A * D * 3 / msq / 1e9:.0f} GB/s")
 a = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
 b = torch.randn(2 * F, D, device=dev, dtype=torch.bfloat16)
 ms = tm(lambda: torch.mm(a, b.t()))
