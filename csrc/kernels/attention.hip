@@ -19,11 +19,18 @@
 //    stores. Images use 16-byte-chunk XOR swizzles chosen so both read kinds are
 //    bank-conflict free (HD>=128: ch ^ ((r&3)<<2 | (r>>2)&3); HD=64: ch ^ ((r>>1&1)<<2 | (r>>2)&3)).
 //  * Double-buffered K/V (or Q/dO) LDS tiles with register prefetch two tiles
-//    ahead: one barrier per tile.
-//  * Forward: 8 waves x 32 query rows (2 waves / SIMD) for HD <= 128; the O
-//    rescale is skipped whenever no row max moved (wave-uniform test).
-//  * Causal: heavy blocks first; waves skip tiles entirely above their diagonal;
-//    masks only on straddling tiles.
+//    ahead: one barrier per tile. Tiles come in through buffer loads whose
+//    descriptor range ends at the last valid row, so ragged tails read zeros from
+//    the hardware range check instead of per-lane branches.
+//  * VALU budget (the loops are VALU-issue bound at 2 waves/SIMD, measured
+//    SQ_INSTS_VALU ~10x SQ_INSTS_MFMA before this layout): bare v_exp_f32
+//    (__builtin_amdgcn_exp2f, no denormal range reduction), one v_fma per score
+//    (scale and max folded), masks only on the diagonal / tail tiles, the row max
+//    combined across the two lane halves with v_permlane32_swap, the online-softmax
+//    rescale deferred until some row max grew by more than 2^8 (T13: P <= 256 in
+//    bf16, l and O in fp32), and the bwd row constants (-lse, -delta) preloaded
+//    into the accumulators instead of zeros.
+//  * Causal: heavy blocks first; waves skip tiles entirely above their diagonal.
 //  * Backward = two deterministic kernels (no float atomics): dq (query-parallel,
 //    also produces delta = rowsum(dO*O)) then dkdv (key-parallel, loops the GQA
 //    group's q-heads so dK/dV of a kv-head are summed in registers). An optional
@@ -49,9 +56,23 @@ struct AttnParams {
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// deferred-rescale threshold in log2 units (T13): P = 2^(s*c - m) <= 2^8
+constexpr float kRescaleThr = 8.f;
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// max of x over lanes l and l^32 (one v_permlane32_swap, no LDS)
+__device__ __forceinline__ float halfmax(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halfsum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -59,9 +80,11 @@ __device__ __forceinline__ bf16x8 zero8() {
   for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
   return z;
 }
-__device__ __forceinline__ void zero16(f32x16& a) {
+__device__ __forceinline__ f32x16 splat16(float v) {
+  f32x16 a;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) a[r] = 0.f;
+  for (int r = 0; r < 16; ++r) a[r] = v;
+  return a;
 }
 // accumulator registers 8s..8s+7 -> bf16 operand fragment (permuted k order)
 __device__ __forceinline__ bf16x8 pack_acc(const f32x16& a, int s) {
@@ -80,11 +103,6 @@ __device__ __forceinline__ int swz(int r) {
 template <int HD>
 __device__ __forceinline__ int img_off(int r, int ch) {  // element offset of 16B chunk ch of row r
   return r * HD + 8 * (ch ^ swz<HD>(r));
-}
-// 16-byte row fragment: row r, elements [8ch, 8ch+8)
-template <int HD>
-__device__ __forceinline__ bf16x8 rd_row(const bf16* img, int r, int ch) {
-  return *reinterpret_cast<const bf16x8*>(img + img_off<HD>(r, ch));
 }
 // A/B operand "X^T" for one 16-deep k-step, where X is the row-major image with
 // rows = k index, columns = output index. Lane l gets X[r0 + 16s + perm(j)][c0 + (l&31)].
@@ -139,27 +157,52 @@ __device__ __forceinline__ bf16x8 ld_tr(const bf16* img, int offa, int offb) {
 template <int V> using IC = std::integral_constant<int, V>;
 
 // Register-staged tile loader: ROWS x HD bf16 tile of a strided tensor -> regs -> LDS image.
+// Global side: one buffer descriptor per tile (scalar work), its range ending at the
+// tensor's last valid row, so rows >= nrows load as zeros without a branch. The per-lane
+// byte offsets and LDS offsets are loop invariant (computed once).
+// Thread -> chunk map: W = min(HD/8, 16) lanes share a row, a lane takes the chunk
+// columns ch, ch+16, ... of its row (HD = 256: two) and rows rr, rr+R, ... (R = NT/W,
+// a multiple of 16). The XOR swizzle only touches the low 4 chunk bits and repeats
+// every 16 rows, so all of a lane's LDS offsets are one register + immediates; on the
+// global side each row pass gets its own scalar descriptor and the column step is the
+// instruction offset.
 template <int HD, int ROWS, int NT>
 struct TileLoader {
-  static constexpr int CH = ROWS * HD / 8 / NT;  // 16B chunks per thread
-  static_assert(CH >= 1 && ROWS * HD / 8 % NT == 0, "tile/threads mismatch");
+  static constexpr int CPR = HD / 8;                   // 16B chunks per row
+  static constexpr int W = CPR < 16 ? CPR : 16;        // lanes per row
+  static constexpr int NC = CPR / W;                   // column chunks per lane (16 apart)
+  static constexpr int R = NT / W;                     // rows between a lane's row passes
+  static constexpr int NP = ROWS / R;                  // row passes
+  static constexpr int CH = NP * NC;
+  static_assert(R % 16 == 0 && ROWS % R == 0 && NP >= 1, "tile/threads mismatch");
   bf16x8 r[CH];
-  __device__ __forceinline__ void load(const bf16* base, long stride, int row0, int nrows, int tid) {
+  int voff;  // byte offset of this lane's first chunk within its row pass
+  int loff;  // element offset of this lane's first chunk in the LDS image
+  __device__ __forceinline__ void init(long stride, int tid) {
+    const int rr = tid / W, ch = tid % W;
+    voff = (int)(((long)rr * stride + ch * 8) * 2);
+    loff = img_off<HD>(rr, ch);
+  }
+  __device__ __forceinline__ void load(const bf16* base, long stride, int row0, int nrows) {
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = tid + c * NT;
-      const int rr = idx / (HD / 8), ch = idx % (HD / 8);
-      const int row = row0 + rr;
-      r[c] = row < nrows ? *reinterpret_cast<const bf16x8*>(base + (long)row * stride + ch * 8) : zero8();
+    for (int ps = 0; ps < NP; ++ps) {
+      const int r0 = row0 + ps * R;
+      const int left = nrows - r0;
+      const int bytes = left > 0 ? (int)(((long)(left - 1) * stride + HD) * 2) : 0;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)r0 * stride), 0, bytes, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        r[ps * NC + j] =
+            __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 256 * j, 0, 0));
     }
   }
-  __device__ __forceinline__ void store(bf16* img, int tid) const {
+  __device__ __forceinline__ void store(bf16* img) const {
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = tid + c * NT;
-      const int rr = idx / (HD / 8), ch = idx % (HD / 8);
-      *reinterpret_cast<bf16x8*>(img + img_off<HD>(rr, ch)) = r[c];
-    }
+    for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        *reinterpret_cast<bf16x8*>(img + loff + ps * R * HD + 128 * j) = r[ps * NC + j];
   }
 };
 
@@ -168,7 +211,7 @@ struct TileLoader {
 // ---------------------------------------------------------------------------
 template <int HD, int NW, bool CAUSAL>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
-  constexpr int BN = 64, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
+  constexpr int BN = HD >= 256 ? 32 : 64, NSUB = BN / 32, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
   constexpr int TILE = BN * HD;
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][K|V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -180,8 +223,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   if (CAUSAL) qb = nqb - 1 - qb;  // heaviest q-blocks first
   const int h = bh % p.H, b = bh / p.H;
   const int hk = h / (p.H / p.Hkv);
-  const int q0 = qb * BM + wave * 32;
+  const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
+  const float c = p.scale_log2;
 
   bf16x8 qf[KS];
   {
@@ -191,7 +235,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   }
   f32x16 o[DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) zero16(o[i]);
+  for (int i = 0; i < DT; ++i) o[i] = splat16(0.f);
   float m = -1e30f, l = 0.f;
 
   int kend = p.Tk;
@@ -202,16 +246,55 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
   const bf16* vbase = p.v + b * p.svb + hk * p.svh;
   TileLoader<HD, BN, NT> lk, lv;
+  lk.init(p.skt, tid);
+  lv.init(p.svt, tid);
   if (ntiles > 0) {
-    lk.load(kbase, p.skt, 0, p.Tk, tid);
-    lv.load(vbase, p.svt, 0, p.Tk, tid);
-    lk.store(smem, tid);
-    lv.store(smem + TILE, tid);
-    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk, tid); lv.load(vbase, p.svt, BN, p.Tk, tid); }
+    lk.load(kbase, p.skt, 0, p.Tk);
+    lv.load(vbase, p.svt, 0, p.Tk);
+    lk.store(smem);
+    lv.store(smem + TILE);
+    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk); lv.load(vbase, p.svt, BN, p.Tk); }
   }
   __syncthreads();
   LdsOff<HD> off;
   off.init(lane);
+  // causal / tail mask of one 32-key sub-tile (keys k0..k0+31): only on diagonal / tail
+  // tiles, and kept apart from the softmax so the O-rescale code exists once (two merged
+  // copies made hipcc re-home all of O with 64 v_mov per sub-tile)
+  auto mask = [&](f32x16& s, const int k0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (key >= p.Tk || (CAUSAL && key > q + p.causal_off)) s[r] = -INFINITY;
+    }
+  };
+  // scores -> probabilities for one 32-key sub-tile: each sub-tile is its own online-softmax step
+  auto softmax = [&](f32x16& s) {
+    float mx = s[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
+    const float mxs = halfmax(mx) * c;
+    // per-lane (exec-masked) rescale: both lane halves of a row take the same decision.
+    // A wave-uniform branch here made hipcc re-home all of O (64 v_mov per sub-tile).
+    if (mxs > m + kRescaleThr) {
+      const float alpha = fexp2(m - mxs);
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < DT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      m = mxs;
+    }
+    const float nm = -m;
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = fexp2(fmaf(s[r], c, nm));
+      s[r] = e;
+      ls += e;
+    }
+    l += ls;
+  };
   // body(j, buffer) with the buffer a compile-time constant (loop unrolled x2) so
   // every LDS address is a precomputed lane offset + an immediate
   auto body = [&](const int j, auto bufc) {
@@ -221,60 +304,27 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     const bf16* Vs = Ks + TILE;
     if (j + 1 < ntiles) {
       bf16* Kn = smem + (1 - BUF) * 2 * TILE;
-      lk.store(Kn, tid);
-      lv.store(Kn + TILE, tid);
-      if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk, tid); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk, tid); }
+      lk.store(Kn);
+      lv.store(Kn + TILE);
+      if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk); }
     }
-    if (k0 < wave_kend) {
-      f32x16 s[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        zero16(s[t]);
+    for (int t = 0; t < NSUB; ++t) {
+      const int ks0 = k0 + 32 * t;
+      if (ks0 < wave_kend) {
+        f32x16 s = mfma32(ld_row(Ks + 32 * t * HD, off.row[0]), qf[0], splat16(0.f));
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[t] = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s[t]);
-      }
-      const bool need_mask = (k0 + BN > p.Tk) || (CAUSAL && k0 + BN - 1 > q0 + p.causal_off);
-      float mx = -1e30f;
+        for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s);
+        const bool need_mask = (ks0 + 32 > p.Tk) || (CAUSAL && ks0 + 31 > q0 + p.causal_off);
+        if (need_mask) mask(s, ks0);
+        softmax(s);
+        const bf16x8 pa = pack_acc(s, 0), pb = pack_acc(s, 1);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = s[t][r] * p.scale_log2;
-          if (need_mask) {
-            const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (key >= p.Tk || (CAUSAL && key > q + p.causal_off)) v = -INFINITY;
-          }
-          s[t][r] = v;
-          mx = fmaxf(mx, v);
+        for (int dt = 0; dt < DT; ++dt) {
+          o[dt] = mfma32(ld_tr(Vs + 32 * t * HD, off.tra[dt], off.trb[dt]), pa, o[dt]);
+          o[dt] = mfma32(ld_tr(Vs + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), pb, o[dt]);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      if (__any(mnew > m)) {  // wave-uniform: rescale only when some row max moved
-        const float alpha = exp2f(m - mnew);
-        l *= alpha;
-#pragma unroll
-        for (int i = 0; i < DT; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-        m = mnew;
       }
-      float ls = 0.f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = exp2f(s[t][r] - m);
-          s[t][r] = e;
-          ls += e;
-        }
-      l += ls;
-      bf16x8 pf[4];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) pf[kk] = pack_acc(s[kk >> 1], kk & 1);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) o[dt] = mfma32(ld_tr(Vs + 16 * kk * HD, off.tra[dt], off.trb[dt]), pf[kk], o[dt]);
     }
     __syncthreads();
   };
@@ -282,7 +332,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     body(j, IC<0>{});
     if (j + 1 < ntiles) body(j + 1, IC<1>{});
   }
-  l += __shfl_xor(l, 32, 64);
+  l = halfsum(l);
   const float inv = l > 0.f ? 1.f / l : 0.f;
   if (q < p.Tq) {
     bf16* op = p.out + b * p.sob + (long)q * p.sot + h * p.soh;
@@ -296,18 +346,18 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
         *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * hh) = w;
       }
     if (hh == 0 && p.lse)
-      p.lse[((long)b * p.H + h) * p.Tq + q] = (l > 0.f) ? (m + log2f(l)) * 0.69314718055994531f : INFINITY;
+      p.lse[((long)b * p.H + h) * p.Tq + q] = (l > 0.f) ? (m + __log2f(l)) * 0.69314718055994531f : INFINITY;
   }
 }
 
 // ---------------------------------------------------------------------------
 // Backward dQ (query-parallel; also writes delta = rowsum(dO*O)).
-//   S^T = K Q^T ; P^T = exp2(S^T*c - lse2) ; dP^T = V dO^T ; dS^T = P^T (dP^T - delta)
+//   S^T = K Q^T ; P^T = exp2(S^T*c - lse2) ; dP^T = V dO^T - delta ; dS^T = P^T dP^T
 //   dQ^T += K^T dS^T   (K^T via tr reads of the K image)
 // ---------------------------------------------------------------------------
 template <int HD, int NW, bool CAUSAL>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
-  constexpr int BN = 64, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
+  constexpr int BN = HD >= 256 ? 32 : 64, NSUB = BN / 32, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
   constexpr int TILE = BN * HD;
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -319,9 +369,10 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   if (CAUSAL) qb = nqb - 1 - qb;
   const int h = bh % p.H, b = bh / p.H;
   const int hk = h / (p.H / p.Hkv);
-  const int q0 = qb * BM + wave * 32;
+  const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
   const bool qvalid = q < p.Tq;
+  const float c = p.scale_log2;
 
   bf16x8 qf[KS], df[KS];
   float dlt = 0.f;
@@ -337,14 +388,14 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) dlt += (float)ov[j] * (float)df[s][j];
     }
-    dlt += __shfl_xor(dlt, 32, 64);
+    dlt = halfsum(dlt);
   }
   const long srow = ((long)b * p.H + h) * p.Tq + q;
   if (qvalid && hh == 0) p.delta[srow] = dlt;
-  const float lse2 = qvalid ? p.lse_in[srow] * 1.4426950408889634f : INFINITY;
+  const float nlse2 = qvalid ? -p.lse_in[srow] * 1.4426950408889634f : -INFINITY;
   f32x16 acc[DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) zero16(acc[i]);
+  for (int i = 0; i < DT; ++i) acc[i] = splat16(0.f);
 
   int kend = p.Tk;
   if (CAUSAL) kend = min(p.Tk, qb * BM + BM + p.causal_off);
@@ -353,16 +404,30 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
   const bf16* vbase = p.v + b * p.svb + hk * p.svh;
   TileLoader<HD, BN, NT> lk, lv;
+  lk.init(p.skt, tid);
+  lv.init(p.svt, tid);
   if (ntiles > 0) {
-    lk.load(kbase, p.skt, 0, p.Tk, tid);
-    lv.load(vbase, p.svt, 0, p.Tk, tid);
-    lk.store(smem, tid);
-    lv.store(smem + TILE, tid);
-    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk, tid); lv.load(vbase, p.svt, BN, p.Tk, tid); }
+    lk.load(kbase, p.skt, 0, p.Tk);
+    lv.load(vbase, p.svt, 0, p.Tk);
+    lk.store(smem);
+    lv.store(smem + TILE);
+    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk); lv.load(vbase, p.svt, BN, p.Tk); }
   }
   __syncthreads();
   LdsOff<HD> off;
   off.init(lane);
+  auto mask = [&](f32x16& s, const int k0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (key >= p.Tk || (CAUSAL && key > q + p.causal_off)) s[r] = -INFINITY;
+    }
+  };
+  // one 32-key sub-tile: s <- dS^T = P^T (dP^T - delta)   (dp already carries -delta)
+  auto dsoft = [&](f32x16& s, const f32x16& dp) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = fexp2(fmaf(s[r], c, nlse2)) * dp[r];
+  };
   auto body = [&](const int j, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     const int k0 = j * BN;
@@ -370,41 +435,31 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     const bf16* Vs = Ks + TILE;
     if (j + 1 < ntiles) {
       bf16* Kn = smem + (1 - BUF) * 2 * TILE;
-      lk.store(Kn, tid);
-      lv.store(Kn + TILE, tid);
-      if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk, tid); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk, tid); }
+      lk.store(Kn);
+      lv.store(Kn + TILE);
+      if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk); }
     }
-    if (k0 < wave_kend) {
-      f32x16 s[2], dp[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        zero16(s[t]);
-        zero16(dp[t]);
+    for (int t = 0; t < NSUB; ++t) {
+      const int ks0 = k0 + 32 * t;
+      if (ks0 < wave_kend) {
+        f32x16 s = mfma32(ld_row(Ks + 32 * t * HD, off.row[0]), qf[0], splat16(0.f));
+        f32x16 dp = mfma32(ld_row(Vs + 32 * t * HD, off.row[0]), df[0], splat16(-dlt));
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          s[t] = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s[t]);
-          dp[t] = mfma32(ld_row(Vs + 32 * t * HD, off.row[ks]), df[ks], dp[t]);
+        for (int ks = 1; ks < KS; ++ks) {
+          s = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s);
+          dp = mfma32(ld_row(Vs + 32 * t * HD, off.row[ks]), df[ks], dp);
+        }
+        const bool need_mask = (ks0 + 32 > p.Tk) || (CAUSAL && ks0 + 31 > q0 + p.causal_off);
+        if (need_mask) mask(s, ks0);
+        dsoft(s, dp);
+        const bf16x8 sa = pack_acc(s, 0), sb = pack_acc(s, 1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          acc[dt] = mfma32(ld_tr(Ks + 32 * t * HD, off.tra[dt], off.trb[dt]), sa, acc[dt]);
+          acc[dt] = mfma32(ld_tr(Ks + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), sb, acc[dt]);
         }
       }
-      const bool need_mask = (k0 + BN > p.Tk) || (CAUSAL && k0 + BN - 1 > q0 + p.causal_off);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float pr = exp2f(s[t][r] * p.scale_log2 - lse2);
-          if (need_mask) {
-            const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (key >= p.Tk || (CAUSAL && key > q + p.causal_off)) pr = 0.f;
-          }
-          s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
-        }
-      bf16x8 sf[4];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) sf[kk] = pack_acc(s[kk >> 1], kk & 1);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) acc[dt] = mfma32(ld_tr(Ks + 16 * kk * HD, off.tra[dt], off.trb[dt]), sf[kk], acc[dt]);
     }
     __syncthreads();
   };
@@ -428,7 +483,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 
 // ---------------------------------------------------------------------------
 // Backward dK/dV: key-block parallel (4 waves x 32 keys), key on the lane.
-//   S = Q K^T, dP = dO V^T     (A = Q / dO row reads, B = K / V fragments in regs)
+//   S = Q K^T, dP = dO V^T - delta   (A = Q / dO row reads, B = K / V fragments in regs;
+//                                     the dP accumulator starts at -delta of its row)
 //   dV^T += dO^T P, dK^T += Q^T dS   (A = tr reads of the Q / dO images, B = accumulators)
 // Loops over the q-heads sharing this kv-head (GQA) so the group sum stays in regs.
 // ---------------------------------------------------------------------------
@@ -444,7 +500,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE + KIMG + DSIMG];  // [buf][Q|dO] | K | dS
   bf16* kimg = smem + 4 * TILE;
   bf16* dsimg = kimg + KIMG;
-  __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];  // [buf][lse2 | delta]
+  __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];  // [buf][-lse2 | -delta]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lk = lane & 31, hh = lane >> 5;
   const int nbh = p.Hkv * p.B;
@@ -452,9 +508,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int bh = blockIdx.x % nbh;
   const int hk = bh % p.Hkv, b = bh / p.Hkv;
   const int G = p.H / p.Hkv;
-  const int kw0 = kb * BNK + wave * 32;
+  const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + wave * 32);
   const int key = kw0 + lk;
   const bool kvalid = key < p.Tk;
+  const float c = p.scale_log2;
 
   bf16x8 kf[KS], vf[KS];
   {
@@ -470,7 +527,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   }
   f32x16 dkt[DT], dvt[DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) { zero16(dkt[i]); zero16(dvt[i]); }
+  for (int i = 0; i < DT; ++i) { dkt[i] = splat16(0.f); dvt[i] = splat16(0.f); }
 
   int qstart = 0, wave_qstart = 0;
   if (CAUSAL) {
@@ -482,23 +539,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int nper = ntq - t0 > 0 ? ntq - t0 : 0;  // q-tiles per head
   const int total = nper * G;                      // (head, q-tile) iterations
   TileLoader<HD, BMQ, NT> lq_, ld_;
+  lq_.init(p.sqt, tid);
+  ld_.init(p.sdot, tid);
   float rl = 0.f, rd = 0.f;  // per-thread row constants for the prefetched tile (tid < BMQ)
   auto fetch = [&](int it) {
     const int hg = it / nper, tq = t0 + it % nper;
     const int h = hk * G + hg;
     const int qq0 = tq * BMQ;
-    lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq, tid);
-    ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq, tid);
+    lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq);
+    ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq);
     if (tid < BMQ) {
       const int qq = qq0 + tid;
       const long rbase = ((long)b * p.H + h) * p.Tq;
-      rl = qq < p.Tq ? p.lse_in[rbase + qq] * 1.4426950408889634f : INFINITY;
-      rd = qq < p.Tq ? p.delta[rbase + qq] : 0.f;
+      rl = qq < p.Tq ? -p.lse_in[rbase + qq] * 1.4426950408889634f : -INFINITY;
+      rd = qq < p.Tq ? -p.delta[rbase + qq] : 0.f;
     }
   };
   auto commit_tile = [&](int buf) {
-    lq_.store(smem + buf * 2 * TILE, tid);
-    ld_.store(smem + buf * 2 * TILE + TILE, tid);
+    lq_.store(smem + buf * 2 * TILE);
+    ld_.store(smem + buf * 2 * TILE + TILE);
     if (tid < BMQ) { rowc[buf][tid] = rl; rowc[buf][BMQ + tid] = rd; }
   };
   if (total > 0) {
@@ -509,6 +568,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   __syncthreads();
   LdsOff<HD> off;
   off.init(lane);
+  // rows of s/dp[t] are queries qq0 + 32t + 8g + 4hh + i (r = 4g + i); column = key (lane)
+  // one 32-query sub-tile (rows qt0 + 8g + 4hh + i): s <- P, dp <- dS = P (dP - delta)
+  auto mask = [&](f32x16& s, const int qt0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qq = qt0 + 8 * (r >> 2) + 4 * hh + (r & 3);
+      if (key > qq + p.causal_off) s[r] = -INFINITY;
+    }
+  };
+  auto dsoft = [&](f32x16& s, f32x16& dp, const float* rc) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 8 * g + 4 * hh);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * g + i;
+        const float pr = fexp2(fmaf(s[r], c, lv[i]));  // rows >= Tq: -lse2 = -inf -> 0
+        s[r] = pr;
+        dp[r] = pr * dp[r];
+      }
+    }
+  };
   auto body = [&](const int it, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     const int tq = t0 + it % nper;
@@ -522,59 +603,46 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     }
     const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
     if (active) {
-      f32x16 s[MT], dp[MT];
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
-        zero16(s[t]);
-        zero16(dp[t]);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          s[t] = mfma32(ld_row(Qs + 32 * t * HD, off.row[ks]), kf[ks], s[t]);
-          dp[t] = mfma32(ld_row(Ds + 32 * t * HD, off.row[ks]), vf[ks], dp[t]);
-        }
-      }
-      // rows of s/dp[t] are queries qq0 + 32t + 8g + 4hh + i (r = 4g + i); column = key (lane)
-      const bool need_mask = CAUSAL && qq0 + p.causal_off < kw0 + 31;
-#pragma unroll
-      for (int t = 0; t < MT; ++t)
+        // dP accumulator starts at -delta of each row (register r <-> query row 8g+4hh+i)
+        f32x16 dp;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 32 * t + 8 * g + 4 * hh);
           const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            float pr = exp2f(s[t][r] * p.scale_log2 - lv[i]);  // rows >= Tq: lse=inf -> 0
-            if (need_mask) {
-              const int qq = qq0 + 32 * t + 8 * g + 4 * hh + i;
-              if (key > qq + p.causal_off) pr = 0.f;
-            }
-            s[t][r] = pr;
-            dp[t][r] = pr * (dp[t][r] - dv[i]);
-          }
+          for (int i = 0; i < 4; ++i) dp[4 * g + i] = dv[i];
         }
-      bf16x8 pf[2 * MT], sf[2 * MT];
+        f32x16 s = mfma32(ld_row(Qs + 32 * t * HD, off.row[0]), kf[0], splat16(0.f));
+        dp = mfma32(ld_row(Ds + 32 * t * HD, off.row[0]), vf[0], dp);
 #pragma unroll
-      for (int kk = 0; kk < 2 * MT; ++kk) { pf[kk] = pack_acc(s[kk >> 1], kk & 1); sf[kk] = pack_acc(dp[kk >> 1], kk & 1); }
-      if constexpr (FUSEDQ) {
-        // dS rows of this wave's 32 keys -> [key][q] image (registers 4g..4g+3 = 4 consecutive q)
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
+        for (int ks = 1; ks < KS; ++ks) {
+          s = mfma32(ld_row(Qs + 32 * t * HD, off.row[ks]), kf[ks], s);
+          dp = mfma32(ld_row(Ds + 32 * t * HD, off.row[ks]), vf[ks], dp);
+        }
+        const int qt0 = qq0 + 32 * t;
+        const bool need_mask = CAUSAL && qt0 + p.causal_off < kw0 + 31;
+        if (need_mask) mask(s, qt0);
+        dsoft(s, dp, rc + 32 * t);
+        const bf16x8 pa = pack_acc(s, 0), pb = pack_acc(s, 1), sa = pack_acc(dp, 0), sb = pack_acc(dp, 1);
+        if constexpr (FUSEDQ) {
+          // dS rows of this wave's 32 keys -> [key][q] image (registers 4g..4g+3 = 4 consecutive q)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             bf16x4 w4;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) w4[i] = (bf16)dp[t][4 * g + i];
+            for (int i = 0; i < 4; ++i) w4[i] = (bf16)dp[4 * g + i];
             *reinterpret_cast<bf16x4*>(dsimg + img_off<64>(wave * 32 + lk, 4 * t + g) + 4 * hh) = w4;
           }
-      }
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int kk = 0; kk < 2 * MT; ++kk) {
-          dvt[dt] = mfma32(ld_tr(Ds + 16 * kk * HD, off.tra[dt], off.trb[dt]), pf[kk], dvt[dt]);
-          dkt[dt] = mfma32(ld_tr(Qs + 16 * kk * HD, off.tra[dt], off.trb[dt]), sf[kk], dkt[dt]);
         }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dvt[dt] = mfma32(ld_tr(Ds + 32 * t * HD, off.tra[dt], off.trb[dt]), pa, dvt[dt]);
+          dkt[dt] = mfma32(ld_tr(Qs + 32 * t * HD, off.tra[dt], off.trb[dt]), sa, dkt[dt]);
+          dvt[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), pb, dvt[dt]);
+          dkt[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), sb, dkt[dt]);
+        }
+      }
     } else if constexpr (FUSEDQ) {
       // masked-out wave: its keys contribute nothing to dQ this tile
       bf16x4 z4;
@@ -595,8 +663,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
         const int q0 = qq0 + 32 * tq;
         if (CAUSAL && q0 + 31 + p.causal_off < kb * BNK) continue;   // every key of the block is masked
         if (q0 >= p.Tq) continue;
-        f32x16 acc;
-        zero16(acc);
+        f32x16 acc = splat16(0.f);
 #pragma unroll
         for (int kk = 0; kk < BNK / 16; ++kk)
           acc = mfma32(rd_tr<64>(dsimg, 16 * kk, 32 * tq, lane), rd_tr<HD>(kimg, 16 * kk, 32 * td, lane), acc);

@@ -210,6 +210,32 @@ def test_flash_lse_and_spike():
     assert (lse - lf).abs().max().item() < 5e-2
 
 
+@pytest.mark.parametrize("step", [0.3, 0.735, 2.0])
+def test_flash_deferred_rescale(step):
+    """Scores that grow along the key axis so the running row max creeps up tile after
+    tile by less than (0.3, 0.735: ~1 and ~3 log2 units per 32-key sub-tile) and more
+    than (2.0) the 2^8 deferral threshold: exercises the deferred-rescale path, whose
+    branch random data almost never takes (guide rule 26)."""
+    from solvingpapers_amd.ops import flash_attention
+    torch.manual_seed(3)
+    B, T, H, hd = 1, 640, 2, 128
+    q = (torch.randn(B, T, H, hd, device=DEV) * 0.2)
+    k = (torch.randn(B, T, H, hd, device=DEV) * 0.2)
+    q[..., 0] = 1.0
+    k[..., 0] = step * torch.arange(T, device=DEV, dtype=torch.float32).view(1, T, 1) / 32
+    q, k = q.bfloat16().requires_grad_(), k.bfloat16().requires_grad_()
+    v = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attention(q, k, v, causal=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qf, kf, vf = (t.detach().float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention(qf, kf, vf, True)
+    of.backward(do.float())
+    assert rel(o, of) < 2e-2, rel(o, of)
+    for a, b in ((q.grad, qf.grad), (k.grad, kf.grad), (v.grad, vf.grad)):
+        assert rel(a, b) < 3e-2, rel(a, b)
+
+
 def test_packed_attention_matches_split():
     from solvingpapers_amd.ops import attention_packed, flash_attention
     B, T, H, Hkv, hd = 2, 150, 8, 2, 128
