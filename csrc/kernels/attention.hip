@@ -53,6 +53,10 @@ struct AttnParams {
   float scale;       // softmax scale (natural)
   float scale_log2;  // scale * log2(e)
   int causal_off;    // key j visible to query i iff j <= i + causal_off
+  // dK/dV q-head split (small Hkv x key-block grids, e.g. MQA): hsplit blocks per key block,
+  // each summing G/hsplit q-heads into fp32 partials dkacc/dvacc [hsplit, B, Tk, Hkv, HD]
+  int hsplit;
+  float* dkacc; float* dvacc;
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -481,6 +485,41 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   }
 }
 
+// dK^T / dV^T accumulator (rows d = 32dt + (r&3) + 8(r>>2) + 4hh, column = key) -> global:
+// bf16 (dk scaled) when the block owns all q-heads of its kv-head, else fp32 partials.
+template <int HD>
+__device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 (&acc)[HD / 32], bool is_k,
+                                              int b, int hk, int key, int split, int hh) {
+  if (key >= p.Tk) return;
+  constexpr int DT = HD / 32;
+  if (p.hsplit == 1) {
+    bf16* dst = is_k ? p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh
+                     : p.dv + b * p.sdvb + (long)key * p.sdvt + hk * p.sdvh;
+    const float sc = is_k ? p.scale : 1.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = (bf16)(acc[dt][4 * g + i] * sc);
+        *reinterpret_cast<bf16x4*>(dst + 32 * dt + 8 * g + 4 * hh) = w;
+      }
+  } else {
+    float* dst = (is_k ? p.dkacc : p.dvacc) +
+                 ((((long)split * p.B + b) * p.Tk + key) * p.Hkv + hk) * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = acc[dt][4 * g + i];
+        *reinterpret_cast<f32x4*>(dst + 32 * dt + 8 * g + 4 * hh) = w;
+      }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Backward dK/dV: key-block parallel (4 waves x 32 keys), key on the lane.
 //   S = Q K^T, dP = dO V^T - delta   (A = Q / dO row reads, B = K / V fragments in regs;
@@ -504,10 +543,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lk = lane & 31, hh = lane >> 5;
   const int nbh = p.Hkv * p.B;
-  const int kb = blockIdx.x / nbh;  // causal: low key blocks are heaviest, launched first
   const int bh = blockIdx.x % nbh;
+  const int rest = blockIdx.x / nbh;  // causal: low key blocks are heaviest, launched first
+  const int split = rest % p.hsplit, kb = rest / p.hsplit;
   const int hk = bh % p.Hkv, b = bh / p.Hkv;
-  const int G = p.H / p.Hkv;
+  const int G = p.H / p.Hkv / p.hsplit;  // q-heads handled by this block
+  const int h0 = hk * (p.H / p.Hkv) + split * G;
   const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + wave * 32);
   const int key = kw0 + lk;
   const bool kvalid = key < p.Tk;
@@ -544,7 +585,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   float rl = 0.f, rd = 0.f;  // per-thread row constants for the prefetched tile (tid < BMQ)
   auto fetch = [&](int it) {
     const int hg = it / nper, tq = t0 + it % nper;
-    const int h = hk * G + hg;
+    const int h = h0 + hg;
     const int qq0 = tq * BMQ;
     lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq);
     ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq);
@@ -656,7 +697,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     }
     if constexpr (FUSEDQ) {
       __syncthreads();  // dS image complete
-      const int h = hk * G + it / nper;
+      const int h = h0 + it / nper;
 #pragma unroll
       for (int tile = wave; tile < MT * DT; tile += 4) {
         const int tq = tile / DT, td = tile % DT;
@@ -681,22 +722,216 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     body(it, IC<0>{});
     if (it + 1 < total) body(it + 1, IC<1>{});
   }
-  if (kvalid) {
-    bf16* kp = p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh;
-    bf16* vp = p.dv + b * p.sdvb + (long)key * p.sdvt + hk * p.sdvh;
+  store_kv_grad<HD>(p, dkt, true, b, hk, key, split, hh);
+  store_kv_grad<HD>(p, dvt, false, b, hk, key, split, hh);
+}
+
+// ---------------------------------------------------------------------------
+// Backward dK/dV with paired waves (HD <= 128): 8 waves = 4 pairs x 32 keys (128 keys per
+// block); key on the lane. Splitting the four products of a key column over two waves
+// halves each wave's live registers (one of K/V fragments, one of dK^T/dV^T), which puts
+// two waves on every SIMD (one wave per SIMD in the single-wave kernel above), and the
+// two roles' matrix and vector work interleave on the SIMD:
+//   role A (waves 0-3):  S = Q K^T -> P = exp2(S c - lse2) -> P to LDS (fp32);  | dV^T += dO^T P
+//   role B (waves 4-7):  dP = dO V^T - delta (kept in registers)                | dS = P dP; dK^T += Q^T dS
+// '|' is a block barrier: phase 1 = the left column, phase 2 = the right column, so the
+// pair's P crosses LDS once per 32x32 sub-tile ([pair][t][j][lane][4] fp32 image,
+// conflict-free 16-byte rows). Q / dO tiles of 64 rows are double-buffered as before.
+// ---------------------------------------------------------------------------
+template <int HD, bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
+  constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 512;
+  constexpr int TILE = BMQ * HD;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];               // [buf][Q|dO]
+  __shared__ __attribute__((aligned(16))) float pimg[4 * MT * 4 * 64 * 4];  // [pair][t][j][lane][4]
+  __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];           // [buf][-lse2 | -delta]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pair = wave & 3, role = wave >> 2;
+  const int lk = lane & 31, hh = lane >> 5;
+  const int nbh = p.Hkv * p.B;
+  const int bh = blockIdx.x % nbh;
+  const int rest = blockIdx.x / nbh;             // causal: low key blocks are heaviest, launched first
+  const int split = rest % p.hsplit, kb = rest / p.hsplit;
+  const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  const int Gs = p.H / p.Hkv / p.hsplit;         // q-heads handled by this block
+  const int h0 = hk * (p.H / p.Hkv) + split * Gs;
+  const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + pair * 32);
+  const int key = kw0 + lk;
+  const bool kvalid = key < p.Tk;
+  const float c = p.scale_log2;
+
+  bf16x8 xf[KS];  // A: K fragments, B: V fragments of this lane's key
+  {
+    const bf16* xp = role == 0 ? p.k + b * p.skb + (long)key * p.skt + hk * p.skh + 8 * hh
+                               : p.v + b * p.svb + (long)key * p.svt + hk * p.svh + 8 * hh;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+    for (int s = 0; s < KS; ++s) xf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
+  }
+  f32x16 acc[DT];  // A: dV^T, B: dK^T
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 wk, wv;
+  for (int i = 0; i < DT; ++i) acc[i] = splat16(0.f);
+
+  int qstart = 0, wave_qstart = 0;
+  if (CAUSAL) {
+    qstart = max(0, kb * BNK - p.causal_off);
+    wave_qstart = max(0, kw0 - p.causal_off);
+  }
+  const int t0 = qstart / BMQ;
+  const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
+  const int nper = ntq - t0 > 0 ? ntq - t0 : 0;
+  const int total = nper * Gs;
+  TileLoader<HD, BMQ, NT> lq_, ld_;
+  lq_.init(p.sqt, tid);
+  ld_.init(p.sdot, tid);
+  float rl = 0.f, rd = 0.f;
+  auto fetch = [&](int it) {
+    const int h = h0 + it / nper;
+    const int qq0 = (t0 + it % nper) * BMQ;
+    lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq);
+    ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq);
+    if (tid < BMQ) {
+      const int qq = qq0 + tid;
+      const long rbase = ((long)b * p.H + h) * p.Tq;
+      rl = qq < p.Tq ? -p.lse_in[rbase + qq] * 1.4426950408889634f : -INFINITY;
+      rd = qq < p.Tq ? -p.delta[rbase + qq] : 0.f;
+    }
+  };
+  auto commit_tile = [&](int buf) {
+    lq_.store(smem + buf * 2 * TILE);
+    ld_.store(smem + buf * 2 * TILE + TILE);
+    if (tid < BMQ) { rowc[buf][tid] = rl; rowc[buf][BMQ + tid] = rd; }
+  };
+  if (total > 0) {
+    fetch(0);
+    commit_tile(0);
+    if (total > 1) fetch(1);
+  }
+  __syncthreads();
+  LdsOff<HD> off;
+  off.init(lane);
+  float* pme = pimg + pair * (MT * 4 * 64 * 4) + lane * 4;  // + (t*4 + j) * 256
+  auto body = [&](const int it, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    const int qq0 = (t0 + it % nper) * BMQ;
+    const bf16* Qs = smem + BUF * 2 * TILE;
+    const bf16* Ds = Qs + TILE;
+    const float* rc = rowc[BUF];
+    if (it + 1 < total) {
+      commit_tile(1 - BUF);
+      if (it + 2 < total) fetch(it + 2);
+    }
+    const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
+    bf16x8 pk[2 * MT];  // A: packed P of both sub-tiles (kept over the barrier)
+    f32x16 dp[MT];      // B: dP - delta of both sub-tiles (kept over the barrier)
+    // ---- phase 1
+    if (active) {
+      if (role == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          wk[i] = (bf16)(dkt[dt][4 * g + i] * p.scale);
-          wv[i] = (bf16)(dvt[dt][4 * g + i]);
+        for (int t = 0; t < MT; ++t) {
+          f32x16 s = mfma32(ld_row(Qs + 32 * t * HD, off.row[0]), xf[0], splat16(0.f));
+#pragma unroll
+          for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Qs + 32 * t * HD, off.row[ks]), xf[ks], s);
+          const int qt0 = qq0 + 32 * t;
+          if (CAUSAL && qt0 + p.causal_off < kw0 + 31) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (key > qt0 + 8 * (r >> 2) + 4 * hh + (r & 3) + p.causal_off) s[r] = -INFINITY;
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 32 * t + 8 * g + 4 * hh);
+            f32x4 pv;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              pv[i] = fexp2(fmaf(s[4 * g + i], c, lv[i]));  // rows >= Tq: -lse2 = -inf -> 0
+              s[4 * g + i] = pv[i];
+            }
+            *reinterpret_cast<f32x4*>(pme + (t * 4 + g) * 256) = pv;
+          }
+          pk[2 * t] = pack_acc(s, 0);
+          pk[2 * t + 1] = pack_acc(s, 1);
         }
-        *reinterpret_cast<bf16x4*>(kp + 32 * dt + 8 * g + 4 * hh) = wk;
-        *reinterpret_cast<bf16x4*>(vp + 32 * dt + 8 * g + 4 * hh) = wv;
+      } else {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dp[t][4 * g + i] = dv[i];
+          }
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) dp[t] = mfma32(ld_row(Ds + 32 * t * HD, off.row[ks]), xf[ks], dp[t]);
+        }
       }
+    }
+    __syncthreads();  // P images complete
+    // ---- phase 2
+    if (active) {
+      if (role == 0) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            acc[dt] = mfma32(ld_tr(Ds + 32 * t * HD, off.tra[dt], off.trb[dt]), pk[2 * t], acc[dt]);
+            acc[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), pk[2 * t + 1], acc[dt]);
+          }
+      } else {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          f32x16 ds;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 pv = *reinterpret_cast<const f32x4*>(pme + (t * 4 + g) * 256);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ds[4 * g + i] = pv[i] * dp[t][4 * g + i];
+          }
+          const bf16x8 sa = pack_acc(ds, 0), sb = pack_acc(ds, 1);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            acc[dt] = mfma32(ld_tr(Qs + 32 * t * HD, off.tra[dt], off.trb[dt]), sa, acc[dt]);
+            acc[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), sb, acc[dt]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  };
+  for (int it = 0; it < total; it += 2) {
+    body(it, IC<0>{});
+    if (it + 1 < total) body(it + 1, IC<1>{});
+  }
+  store_kv_grad<HD>(p, acc, role == 1, b, hk, key, split, hh);
+}
+
+// sum the q-head-split fp32 partials -> bf16 dK (scaled) / dV
+template <int HD>
+__global__ __launch_bounds__(256) void attn_kv_reduce_kernel(AttnParams p) {
+  constexpr int TPR = HD / 8;
+  const long rows = (long)p.B * p.Tk * p.Hkv;
+  const long n = rows * TPR * 2;
+  const long slab = rows * HD;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const bool is_k = i < rows * TPR;
+    const long j = is_k ? i : i - rows * TPR;
+    const int t = j % TPR;
+    const long row = j / TPR;  // (b, key, hk)
+    const long hk = row % p.Hkv, key = (row / p.Hkv) % p.Tk, b = row / ((long)p.Hkv * p.Tk);
+    const float* src = (is_k ? p.dkacc : p.dvacc) + row * HD + 8 * t;
+    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < p.hsplit; ++s) {
+      float x[8];
+      load8(src + s * slab, x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += x[k];
+    }
+    const float sc = is_k ? p.scale : 1.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] *= sc;
+    bf16* dst = is_k ? p.dk + b * p.sdkb + key * p.sdkt + hk * p.sdkh + 8 * t
+                     : p.dv + b * p.sdvb + key * p.sdvt + hk * p.sdvh + 8 * t;
+    store8(dst, a);
   }
 }
 
@@ -787,6 +1022,7 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
   p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal_off = Tk - Tq;
+  p.hsplit = 1;
   if (B * Tq * H == 0) return {out, lse};
   auto st = stream();
   HD_SWITCH(HD, {
@@ -841,10 +1077,33 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
     dqacc = at::zeros({B, Tq, H, HD}, q.options().dtype(at::kFloat));
     p.dqacc = dqacc.data_ptr<float>();
   }
+  // dK/dV grid: key blocks x kv-heads x batch, times a q-head split when that grid cannot
+  // fill the chip (MQA: Hkv = 1 launched 32 blocks at T = 4096); partials are summed by
+  // attn_kv_reduce_kernel. dK/dV kernel: paired-wave (2) for hd 128, single-wave (1) else;
+  // SPA_ATTN_DKDV overrides (read per call, so one process can A/B them). Measured in one
+  // process on MI355X: LLaMA3-8B shape bwd 2.22 ms paired vs 2.45 ms single-wave; ViT-B
+  // hd 64 (T 197, B 64) 0.121 ms paired vs 0.097 ms single-wave.
+  const int dkdv_mode = getenv("SPA_ATTN_DKDV") ? atoi(getenv("SPA_ATTN_DKDV")) : (HD == 128 ? 2 : 1);
+  const int G = H / Hkv;
+  const int nkv = cdiv(Tk, 128) * Hkv * B;
+  int hsplit = 1;
+  if (!fused)
+    while (nkv * hsplit < 512 && hsplit < G) {
+      int d = hsplit + 1;
+      while (G % d) ++d;
+      hsplit = d;
+    }
+  p.hsplit = hsplit;
+  at::Tensor kvacc;
+  if (hsplit > 1) {
+    kvacc = at::empty({2, hsplit, B, Tk, Hkv, HD}, q.options().dtype(at::kFloat));
+    p.dkacc = kvacc.data_ptr<float>();
+    p.dvacc = p.dkacc + (long)hsplit * B * Tk * Hkv * HD;
+  }
   HD_SWITCH(HD, {
     constexpr int NW = fwd_waves<HD_>();
     constexpr int MT = HD_ == 128 ? 2 : 1;
-    const int g2 = cdiv(Tk, 128) * Hkv * B;
+    const int g2 = nkv * hsplit;
     if (fused && HD_ <= 128) {   // hd 256: the fused body exceeds the register file (spills)
       const long rows = (long)B * Tq * H;
       attn_delta_kernel<HD_><<<(int)cdiv(rows, 256 / (HD_ / 8)), 256, 0, st>>>(p);
@@ -857,8 +1116,17 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
       if (causal) attn_bwd_dq_kernel<HD_, NW, true><<<grid, NW * 64, 0, st>>>(p);
       else attn_bwd_dq_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
       if (Tk > 0) {
-        if (causal) attn_bwd_dkdv_kernel<HD_, true, MT, false><<<g2, 256, 0, st>>>(p);
-        else attn_bwd_dkdv_kernel<HD_, false, MT, false><<<g2, 256, 0, st>>>(p);
+        if (HD_ <= 128 && dkdv_mode != 1) {
+          if (causal) attn_bwd_dkdv2_kernel<(HD_ <= 128 ? HD_ : 128), true><<<g2, 512, 0, st>>>(p);
+          else attn_bwd_dkdv2_kernel<(HD_ <= 128 ? HD_ : 128), false><<<g2, 512, 0, st>>>(p);
+        } else {
+          if (causal) attn_bwd_dkdv_kernel<HD_, true, MT, false><<<g2, 256, 0, st>>>(p);
+          else attn_bwd_dkdv_kernel<HD_, false, MT, false><<<g2, 256, 0, st>>>(p);
+        }
+        if (hsplit > 1) {
+          const long n = (long)B * Tk * Hkv * (HD_ / 8) * 2;
+          attn_kv_reduce_kernel<HD_><<<(int)std::min<long>((n + 255) / 256, 65536), 256, 0, st>>>(p);
+        }
       }
     }
   });

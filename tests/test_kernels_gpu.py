@@ -250,16 +250,19 @@ def test_packed_attention_matches_split():
     assert rel(qkv.grad, q2.grad.reshape(B, T, -1)) < 1e-3
 
 
-def test_attention_fused_bwd_matches_split():
-    """The optional fused backward (dQ via fp32 atomics inside the dK/dV kernel) against the
-    default split kernels, run in a subprocess because the mode is read once per process."""
+@pytest.mark.parametrize("env", [{"SPA_ATTN_BWD_FUSED": "1"}, {"SPA_ATTN_DKDV": "1"}, {"SPA_ATTN_DKDV": "2"}])
+def test_attention_bwd_variants_match_default(env):
+    """The optional backward variants -- fused (dQ via fp32 atomics inside the dK/dV kernel)
+    and the paired-wave dK/dV kernel -- against the default kernels, each run in a subprocess
+    because the mode is read once per process. Shapes cover the q-head split (MQA / GQA
+    grids too small for the chip) and the unsplit path."""
     import os, subprocess, sys, textwrap
     code = textwrap.dedent("""
         import math, torch, sys
         from solvingpapers_amd.ops import _ext
         ops = _ext.ops()
         torch.manual_seed(0)
-        for (T, H, Hkv, hd, causal) in [(300, 4, 2, 128, True), (256, 4, 4, 64, False), (129, 2, 1, 128, True)]:
+        for (T, H, Hkv, hd, causal) in CASES:
             q = torch.randn(2, T, H, hd, device='cuda', dtype=torch.bfloat16)
             k = torch.randn(2, T, Hkv, hd, device='cuda', dtype=torch.bfloat16)
             v = torch.randn(2, T, Hkv, hd, device='cuda', dtype=torch.bfloat16)
@@ -270,16 +273,21 @@ def test_attention_fused_bwd_matches_split():
             ops.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, sc, causal)
             torch.save([dq.cpu(), dk.cpu(), dv.cpu()], sys.argv[1] + f'_{T}.pt')
     """)
+    cases = [(300, 4, 2, 128, True), (256, 4, 4, 64, False), (129, 2, 1, 128, True), (1100, 8, 8, 128, True)]
+    code = code.replace("CASES", repr(cases))
     outs = {}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for mode in ("0", "1"):
-        env = dict(os.environ, SPA_ATTN_BWD_FUSED=mode, PYTHONPATH=root)
-        pref = f"/tmp/spa_attn_fused_{mode}"
-        subprocess.run([sys.executable, "-c", code, pref], check=True, env=env, cwd=root)
-        outs[mode] = pref
-    for T in (300, 256, 129):
-        a = torch.load(outs["0"] + f"_{T}.pt", weights_only=True)
-        b = torch.load(outs["1"] + f"_{T}.pt", weights_only=True)
+    for name, extra in (("default", {}), ("variant", env)):
+        e = dict(os.environ, PYTHONPATH=root, **extra)
+        for key in ("SPA_ATTN_BWD_FUSED", "SPA_ATTN_DKDV"):
+            if key not in extra:
+                e.pop(key, None)
+        pref = f"/tmp/spa_attn_bwd_{name}_{'_'.join(env)}"
+        subprocess.run([sys.executable, "-c", code, pref], check=True, env=e, cwd=root, timeout=100)
+        outs[name] = pref
+    for T, *_ in cases:
+        a = torch.load(outs["default"] + f"_{T}.pt", weights_only=True)
+        b = torch.load(outs["variant"] + f"_{T}.pt", weights_only=True)
         for x, y in zip(a, b):
             assert (x.float() - y.float()).norm() / x.float().norm() < 2e-2
 
