@@ -1,0 +1,241 @@
+// Split-K decode attention for KV-cached generation on gfx950.
+//
+// The reference re-runs the whole prefix for every generated token (gpt/gpt-jax.ipynb:821-829,
+// llama3/LLaMA-jax.ipynb:499-511, gemma/gemma.ipynb:608-630, deepseekv3/deepseekv3.ipynb:
+// 1849-1873); the framework keeps a KV cache, so each step is a few query rows against a
+// long cache: memory-bound, and with B * Hkv far below the CU count a per-head kernel would
+// leave most of the chip idle. This kernel splits the KEY axis instead:
+//
+//   grid = (B * Hkv, nsplit); block = 4 waves. A block takes the R = G * Tq query rows that
+//   share kv-head hk (G = H / Hkv: GQA / MQA rows are processed together, so every K/V byte
+//   is read once per block) against keys [s * chunk, (s + 1) * chunk).
+//   Lanes: hd / 4 lanes per key (4 bf16 of the head dim each: one 8-byte load per lane per
+//   key row, 64 / (hd/4) keys per wave step). Each lane group keeps its own online-softmax
+//   state (m, l, o[4]) per row; groups are merged with v_permlane32_swap / LDS at the end.
+//   The split's (m, l, o) go to fp32 partials; attn_decode_combine merges the splits and
+//   writes bf16 out + lse.
+// Causal: query row t sits at position Tk - Tq + t (the cache holds the prefix plus the new
+// tokens); keys beyond a row's position are masked.
+#include "spa_common.h"
+
+namespace spa {
+
+struct DecodeParams {
+  const bf16* q; const bf16* k; const bf16* v;
+  float* opart; float* mpart; float* lpart;  // [nsplit][B][Tq][H][hd], [nsplit][B][Tq][H]
+  bf16* out; float* lse;
+  int B, Tq, Tk, H, Hkv, nsplit, chunk;
+  long sqb, sqt, sqh, skb, skt, skh, svb, svt, svh, sob, sot, soh;
+  float scale_log2;
+  bool causal;
+};
+
+constexpr int kMaxRows = 16;
+
+template <int HD, int R>
+__global__ __launch_bounds__(256) void attn_decode_kernel(DecodeParams p) {
+  constexpr int KL = HD / 4;        // lanes per key
+  constexpr int KPW = 64 / KL;      // keys per wave step
+  constexpr int NG = 4 * KPW;       // lane groups per block
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane % KL, grp = wave * KPW + lane / KL;
+  const int bh = blockIdx.x, split = blockIdx.y;
+  const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  const int G = p.H / p.Hkv;
+  const int rows = G * p.Tq;
+  const int k0 = split * p.chunk, k1 = min(p.Tk, k0 + p.chunk);
+
+  // query slices (pre-scaled to log2 units), rows r = t * G + g  (head hk*G + g, token t)
+  float qv[R][4];
+  int qpos[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = r / G, g = r % G;
+    qpos[r] = p.causal ? p.Tk - p.Tq + t : p.Tk;
+    if (r < rows) {
+      const bf16* qp = p.q + b * p.sqb + (long)t * p.sqt + (long)(hk * G + g) * p.sqh + 4 * sub;
+      const bf16x4 x = *reinterpret_cast<const bf16x4*>(qp);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qv[r][j] = (float)x[j] * p.scale_log2;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qv[r][j] = 0.f;
+      qpos[r] = -1;  // never visible
+    }
+  }
+  float m[R], l[R], o[R][4];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    m[r] = -INFINITY; l[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[r][j] = 0.f;
+  }
+  const bf16* kb = p.k + b * p.skb + hk * p.skh + 4 * sub;
+  const bf16* vb = p.v + b * p.svb + hk * p.svh + 4 * sub;
+  for (int key = k0 + grp; key < k1; key += NG) {
+    const bf16x4 kx = *reinterpret_cast<const bf16x4*>(kb + (long)key * p.skt);
+    const bf16x4 vx = *reinterpret_cast<const bf16x4*>(vb + (long)key * p.svt);
+    float kf[4], vf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { kf[j] = (float)kx[j]; vf[j] = (float)vx[j]; }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float s = qv[r][0] * kf[0];
+#pragma unroll
+      for (int j = 1; j < 4; ++j) s = fmaf(qv[r][j], kf[j], s);
+#pragma unroll
+      for (int w = KL / 2; w > 0; w >>= 1) s += __shfl_xor(s, w, KL);
+      if (key > qpos[r]) s = -INFINITY;
+      const float mn = fmaxf(m[r], s);
+      if (mn == -INFINITY) continue;  // nothing visible yet for this row
+      const float alpha = __builtin_amdgcn_exp2f(m[r] - mn);
+      const float e = __builtin_amdgcn_exp2f(s - mn);
+      m[r] = mn;
+      l[r] = l[r] * alpha + e;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[r][j] = fmaf(o[r][j], alpha, e * vf[j]);
+    }
+  }
+  // merge the NG lane groups: in-wave groups through shuffles, then waves through LDS
+  __shared__ float sm[4][R], sl[4][R], so[4][R][HD];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+#pragma unroll
+    for (int w = KL; w < 64; w <<= 1) {
+      const float m2 = __shfl_xor(m[r], w, 64), l2 = __shfl_xor(l[r], w, 64);
+      const float mn = fmaxf(m[r], m2);
+      const float a1 = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[r] - mn);
+      const float a2 = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2 - mn);
+      l[r] = l[r] * a1 + l2 * a2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[r][j] = o[r][j] * a1 + __shfl_xor(o[r][j], w, 64) * a2;
+      m[r] = mn;
+    }
+    if (lane < KL) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) so[wave][r][4 * sub + j] = o[r][j];
+      if (sub == 0) { sm[wave][r] = m[r]; sl[wave][r] = l[r]; }
+    }
+  }
+  __syncthreads();
+  // rows x hd outputs of this split: thread -> (row, 4-element slice)
+  for (int i = tid; i < rows * KL; i += 256) {
+    const int r = i / KL, s4 = i % KL;
+    float mn = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mn = fmaxf(mn, sm[w][r]);
+    float lt = 0.f, ot[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float a = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sm[w][r] - mn);
+      lt += sl[w][r] * a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ot[j] += so[w][r][4 * s4 + j] * a;
+    }
+    const int t = r / G, hq = hk * G + r % G;
+    const long row = (((long)split * p.B + b) * p.Tq + t) * p.H + hq;
+    f32x4 w4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w4[j] = ot[j];
+    *reinterpret_cast<f32x4*>(p.opart + row * HD + 4 * s4) = w4;
+    if (s4 == 0) { p.mpart[row] = mn; p.lpart[row] = lt; }
+  }
+}
+
+// merge the splits of one (b, t, h) row: thread -> 4 elements of hd
+template <int HD>
+__global__ __launch_bounds__(256) void attn_decode_combine_kernel(DecodeParams p) {
+  constexpr int TPR = HD / 4;
+  const long nrows = (long)p.B * p.Tq * p.H;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nrows * TPR) return;
+  const long row = i / TPR;
+  const int s4 = i % TPR;
+  float mn = -INFINITY;
+  for (int s = 0; s < p.nsplit; ++s) mn = fmaxf(mn, p.mpart[s * nrows + row]);
+  float lt = 0.f, ot[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < p.nsplit; ++s) {
+    const float ms = p.mpart[s * nrows + row];
+    const float a = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - mn);
+    lt += p.lpart[s * nrows + row] * a;
+    const f32x4 x = *reinterpret_cast<const f32x4*>(p.opart + (s * nrows + row) * HD + 4 * s4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ot[j] += x[j] * a;
+  }
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const long h = row % p.H, t = (row / p.H) % p.Tq, b = row / ((long)p.H * p.Tq);
+  bf16x4 w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = (bf16)(ot[j] * inv);
+  *reinterpret_cast<bf16x4*>(p.out + b * p.sob + t * p.sot + h * p.soh + 4 * s4) = w;
+  if (s4 == 0) p.lse[(b * p.H + h) * p.Tq + t] = lt > 0.f ? (mn + __log2f(lt)) * 0.69314718055994531f : INFINITY;
+}
+
+// q [B, Tq, H, hd] (Tq * H / Hkv <= 16), k/v [B, Tk, Hkv, hd] strided (cache views).
+// Returns (out [B, Tq, H, hd] bf16, lse [B, H, Tq] fp32).
+std::vector<at::Tensor> attn_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
+                                    bool causal, int64_t nsplit_req) {
+  for (auto* t : {&q, &k, &v}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 4, "attn_decode: bf16 [B,T,H,hd]");
+    TORCH_CHECK(t->stride(3) == 1 && t->stride(2) % 4 == 0 && t->stride(1) % 4 == 0 && t->stride(0) % 4 == 0 &&
+                    ((uintptr_t)t->data_ptr() % 8) == 0,
+                "attn_decode: rows must be 8-byte aligned and contiguous in hd");
+  }
+  const int B = q.size(0), Tq = q.size(1), H = q.size(2), HD = q.size(3);
+  const int Tk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Tk && v.size(2) == Hkv && k.size(3) == HD &&
+              v.size(3) == HD && H % Hkv == 0, "attn_decode: shape mismatch");
+  TORCH_CHECK(Tq <= Tk, "attn_decode: the cache must hold the query tokens");
+  const int rows = Tq * (H / Hkv);
+  TORCH_CHECK(rows <= kMaxRows, "attn_decode: Tq * H / Hkv must be <= 16 (use flash attention for prefill)");
+  DeviceGuard g(q.device());
+  auto out = at::empty({B, Tq, H, HD}, q.options());
+  auto lse = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
+  if (B * Tq * H == 0) return {out, lse};
+  // split the keys so the grid covers the chip ~2x, but keep >= 128 keys per split
+  int nsplit = (int)nsplit_req;
+  if (nsplit <= 0) {
+    const int want = std::max(1, 512 / std::max(1, B * Hkv));
+    nsplit = std::max(1, std::min(want, cdiv(Tk, 128)));
+  }
+  const int chunk = cdiv(Tk, nsplit);
+  nsplit = cdiv(Tk, chunk);
+  auto part = at::empty({(long)nsplit * B * Tq * H * (HD + 2)}, q.options().dtype(at::kFloat));
+  DecodeParams p{};
+  p.q = (const bf16*)q.data_ptr(); p.k = (const bf16*)k.data_ptr(); p.v = (const bf16*)v.data_ptr();
+  p.opart = part.data_ptr<float>();
+  p.mpart = p.opart + (long)nsplit * B * Tq * H * HD;
+  p.lpart = p.mpart + (long)nsplit * B * Tq * H;
+  p.out = (bf16*)out.data_ptr(); p.lse = lse.data_ptr<float>();
+  p.B = B; p.Tq = Tq; p.Tk = Tk; p.H = H; p.Hkv = Hkv; p.nsplit = nsplit; p.chunk = chunk;
+  p.sqb = q.stride(0); p.sqt = q.stride(1); p.sqh = q.stride(2);
+  p.skb = k.stride(0); p.skt = k.stride(1); p.skh = k.stride(2);
+  p.svb = v.stride(0); p.svt = v.stride(1); p.svh = v.stride(2);
+  p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.causal = causal;
+  auto st = stream();
+  const dim3 grid(B * Hkv, nsplit);
+  const long nthr = (long)B * Tq * H * (HD / 4);
+#define SPA_DECODE_LAUNCH(HDV)                                                                      \
+  {                                                                                                \
+    if (rows <= 4) attn_decode_kernel<HDV, 4><<<grid, 256, 0, st>>>(p);                            \
+    else if (rows <= 8) attn_decode_kernel<HDV, 8><<<grid, 256, 0, st>>>(p);                       \
+    else attn_decode_kernel<HDV, 16><<<grid, 256, 0, st>>>(p);                                     \
+    attn_decode_combine_kernel<HDV><<<(int)((nthr + 255) / 256), 256, 0, st>>>(p);                  \
+  }
+  if (HD == 64) SPA_DECODE_LAUNCH(64)
+  else if (HD == 128) SPA_DECODE_LAUNCH(128)
+  else if (HD == 256) SPA_DECODE_LAUNCH(256)
+  else TORCH_CHECK(false, "attn_decode: head dim must be 64, 128 or 256");
+#undef SPA_DECODE_LAUNCH
+  SPA_LAUNCH_CHECK();
+  return {out, lse};
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("attn_decode(Tensor q, Tensor k, Tensor v, float scale, bool causal, int nsplit) -> Tensor[]");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("attn_decode", &spa::attn_decode); }

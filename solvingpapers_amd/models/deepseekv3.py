@@ -44,7 +44,7 @@ from ..ops.attention import FLASH_HD, attention_dropout, flash_attention
 from ..ops.misc import dropout
 from ..ops.moe import route
 from ..utils.grad import mark_ready
-from .llama3 import sample
+from ..infer.sampling import sample
 
 FP32_EPS = float(torch.finfo(torch.float32).eps)
 
@@ -515,29 +515,23 @@ class DeepSeekV3(tnn.Module):
         return [(torch.zeros(B, Tmax, c.kv_lora_rank, device=dev, dtype=dt),
                  torch.zeros(B, Tmax, c.qk_rope_dim, device=dev, dtype=dt)) for _ in self.layers]
 
+    @property
+    def max_context(self):
+        return self.c.block_size if self.c.pos_emb == "sinusoidal" else None
+
+    def step(self, ids, cache, pos):
+        """Write ids' latents at cache rows [pos, pos+T), return the last position's logits [B, V]."""
+        n, _ = self.hidden(ids, cache, pos)
+        return self.logits(n[:, -1:]).float()[:, -1]
+
     @torch.no_grad()
-    def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None):
+    def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None,
+                 top_p=None, eos_token_id=None, stats=None):
         """Cached decoding (ref: one latent cache, Q1; mla: per-layer compressed cache).
         Reference sampling (deepseekv3.ipynb:1850-1873) recomputes the whole prefix per token
         with top-k + temperature; results are identical, the cache removes the recompute."""
-        c = self.c
-        was = self.training
-        self.eval()
-        B, T0 = ids.shape
-        Tmax = min(c.block_size, T0 + max_new_tokens) if c.pos_emb == "sinusoidal" else T0 + max_new_tokens
-        caches = self.new_cache(B, Tmax)
-        out, cur, pos = ids, ids[:, -Tmax:], 0
-        for _ in range(max_new_tokens):
-            if pos + cur.shape[1] > Tmax:
-                break
-            n, _ = self.hidden(cur, caches, pos)
-            lg = self.logits(n[:, -1:]).float()[:, -1]
-            pos += cur.shape[1]
-            nxt = sample(lg, temperature, top_k, greedy, generator)
-            out = torch.cat([out, nxt], 1)
-            cur = nxt
-        self.train(was)
-        return out
+        from ..infer.generate import generate
+        return generate(self, ids, max_new_tokens, temperature, top_k, top_p, greedy, eos_token_id, generator, stats)
 
     # ------------------------------------------------------------------- metrics
     def num_params(self, active=False):

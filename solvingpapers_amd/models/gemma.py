@@ -26,7 +26,7 @@ import torch.nn as tnn
 
 from .. import nn as snn
 from ..ops import attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
-from ..ops.attention import flash_attention
+from ..ops.attention import decode_attention, flash_attention
 from ..ops.misc import dropout
 from ..ops.rope import gemma_ref_rotate
 from ..utils.grad import mark_ready
@@ -194,7 +194,7 @@ class GemmaBlock(tnn.Module):
         for w in (self.wq, self.wkv, self.wo, self.w13, self.w2):
             w.normal_(0.0, 0.02, generator=g)
 
-    def forward(self, res, delta, tp_group=None):
+    def forward(self, res, delta, tp_group=None, cache=None, pos=0):
         from ..parallel.tensor_parallel import copy_to_tp, reduce_from_tp, reduce_grad_tp
         c = self.c
         if res is None:
@@ -207,8 +207,16 @@ class GemmaBlock(tnn.Module):
         q = linear(n1p, self.wq)                                         # [B, T, hl*hd]
         kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)              # replicated K/V, grads summed over TP
         qkv = torch.cat([q, kv], dim=-1)
-        qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, 0, interleaved=False, head_dim=hd)
-        o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
+        qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, pos, interleaved=False, head_dim=hd)
+        if cache is None:
+            o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
+        else:  # KV-cached inference: write this step's K/V, attend over the cache
+            x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
+            kc, vc = cache
+            kc[:, pos:pos + T] = x4[:, :, self.hl:self.hl + KV]
+            vc[:, pos:pos + T] = x4[:, :, self.hl + KV:]
+            o = decode_attention(x4[:, :, :self.hl], kc[:, :pos + T], vc[:, :pos + T], causal=True)
+            o = o.reshape(B, T, self.hl * hd)
         a = reduce_from_tp(linear(o, self.wo), tp_group)
         n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
         f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
@@ -239,20 +247,48 @@ class Gemma(tnn.Module):
     def param_groups(self):
         return [[self.embed]] + [list(l.parameters()) for l in self.layers] + [[self.norm_f]]
 
-    def forward(self, ids, targets=None):
-        from ..parallel.tensor_parallel import vocab_parallel_cross_entropy, vocab_parallel_embedding
+    def hidden(self, ids, cache=None, pos=0):
+        from ..parallel.tensor_parallel import vocab_parallel_embedding
         c = self.c
         x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim))
         res, delta = None, x
         for i, l in enumerate(self.layers):
             delta = mark_ready(delta, self.grad_ready_cb, i + 1)
-            res, delta = l(res, delta, self.tp_group)
+            res, delta = l(res, delta, self.tp_group, None if cache is None else cache[i], pos)
         delta = mark_ready(delta, self.grad_ready_cb, len(self.layers) + 1)
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
+        return n
+
+    def forward(self, ids, targets=None):
+        from ..parallel.tensor_parallel import vocab_parallel_cross_entropy
+        c = self.c
+        n = self.hidden(ids)
         if targets is None:
             from ..parallel.tensor_parallel import gather_vocab_logits
             return gather_vocab_logits(linear(n, self.embed), self.tp_group)
         return vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, targets.reshape(-1), self.tp_group)
+
+    # ---------------------------------------------------------------- inference
+    @property
+    def max_context(self):
+        return self.c.max_seq_len
+
+    def new_cache(self, B, Tmax):
+        from ..infer.cache import KVCache
+        c = self.c
+        return KVCache(c.n_layers, B, Tmax, c.n_kv_heads, c.head_dim, device=self.embed.device, dtype=self.embed.dtype)
+
+    def step(self, ids, cache, pos):
+        from ..parallel.tensor_parallel import gather_vocab_logits
+        n = self.hidden(ids, cache, pos)
+        return gather_vocab_logits(linear(n[:, -1:], self.embed), self.tp_group).float()[:, -1]
+
+    @torch.no_grad()
+    def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None,
+                 top_p=None, eos_token_id=None, stats=None):
+        """KV-cached MQA decoding (the reference re-runs the window per token, gemma.ipynb:608-630)."""
+        from ..infer.generate import generate
+        return generate(self, ids, max_new_tokens, temperature, top_k, top_p, greedy, eos_token_id, generator, stats)
 
     def flops_per_token(self, T):
         c = self.c

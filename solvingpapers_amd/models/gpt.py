@@ -144,7 +144,7 @@ class GPT(tnn.Module):
     @torch.no_grad()
     def generate(self, idx, max_new_tokens, greedy=True, temperature=1.0, top_k=None, generator=None):
         """gpt-jax.ipynb:821-829: crop to block_size, argmax (greedy by default)."""
-        from .llama3 import sample
+        from ..infer.sampling import sample
         was = self.training
         self.eval()
         for _ in range(max_new_tokens):

@@ -25,8 +25,10 @@ from typing import List, Optional
 import torch
 import torch.nn as nn
 
+from ..infer.cache import KVCache
+from ..infer.sampling import sample  # noqa: F401  (re-exported: reference-style sampling)
 from ..ops import attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
-from ..ops.attention import flash_attention
+from ..ops.attention import decode_attention
 from ..ops.rope import apply_rope
 from ..utils.grad import mark_ready
 
@@ -114,7 +116,8 @@ class LlamaBlock(nn.Module):
             kc, vc = kv_cache
             kc[:, pos:pos + T] = k
             vc[:, pos:pos + T] = v
-            o = flash_attention(q.contiguous(), kc[:, :pos + T], vc[:, :pos + T], causal=True)
+            # decode steps: split-K decode kernel; prompt prefill: flash (decode_attention routes)
+            o = decode_attention(q, kc[:, :pos + T], vc[:, :pos + T], causal=True)
         return linear(o.reshape(B, T, c.n_heads * hd), self.wo)
 
     def forward(self, res, delta, kv_cache=None, pos=0):
@@ -210,28 +213,27 @@ class Llama3(nn.Module):
         return 6 * n_mm + attn
 
     # ---------------------------------------------------------------- inference
-    @torch.no_grad()
-    def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None):
-        """KV-cached sampling (reference: llama3/LLaMA-jax.ipynb:499-511 categorical at T=1)."""
+    @property
+    def max_context(self):
+        return self.c.max_seq_len
+
+    def new_cache(self, B, Tmax):
         c = self.c
-        B, T0 = ids.shape
-        Tmax = min(c.max_seq_len, T0 + max_new_tokens) if c.max_seq_len else T0 + max_new_tokens
-        dev, dt = self.tok_embeddings.device, self.tok_embeddings.dtype
-        caches = [(torch.zeros(B, Tmax, c.n_kv_heads, c.head_dim, device=dev, dtype=dt),
-                   torch.zeros(B, Tmax, c.n_kv_heads, c.head_dim, device=dev, dtype=dt)) for _ in self.layers]
-        out = ids
-        pos = 0
-        cur = ids[:, -Tmax:]
-        for _ in range(max_new_tokens):
-            if pos + cur.shape[1] > Tmax:
-                break
-            n = self.hidden(cur, caches, pos)
-            lg = self.logits(n[:, -1:]).float()[:, -1]
-            pos += cur.shape[1]
-            nxt = sample(lg, temperature, top_k, greedy, generator)
-            out = torch.cat([out, nxt], dim=1)
-            cur = nxt
-        return out
+        return KVCache(c.n_layers, B, Tmax, c.n_kv_heads, c.head_dim, device=self.tok_embeddings.device,
+                       dtype=self.tok_embeddings.dtype)
+
+    def step(self, ids, cache, pos):
+        """Write ids' K/V at cache rows [pos, pos+T), return the last position's logits [B, V]."""
+        n = self.hidden(ids, cache, pos)
+        return self.logits(n[:, -1:]).float()[:, -1]
+
+    @torch.no_grad()
+    def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None,
+                 top_p=None, eos_token_id=None, stats=None):
+        """KV-cached sampling (reference: llama3/LLaMA-jax.ipynb:499-511, categorical at T=1,
+        full re-forward per token; its cache path :816-819 was never exercised)."""
+        from ..infer.generate import generate
+        return generate(self, ids, max_new_tokens, temperature, top_k, top_p, greedy, eos_token_id, generator, stats)
 
     # ------------------------------------------------------- reference layout I/O
     def to_reference_params(self):
@@ -274,17 +276,3 @@ class Llama3(nn.Module):
             l.attention_norm.copy_(t(b["attention_norm"]))
             l.ffn_norm.copy_(t(b["ffn_norm"]))
         return self
-
-
-def sample(logits, temperature=1.0, top_k=None, greedy=False, generator=None):
-    """argmax / categorical / top-k + temperature (GPT :827, LLaMA :508, DSV3 :1861-1866)."""
-    if greedy:
-        return logits.argmax(-1, keepdim=True)
-    logits = logits / max(temperature, 1e-6)
-    if top_k is not None:
-        v, ix = torch.topk(logits, min(top_k, logits.shape[-1]), dim=-1)
-        p = torch.softmax(v, dim=-1)
-        j = torch.multinomial(p, 1, generator=generator)
-        return ix.gather(-1, j)
-    p = torch.softmax(logits, dim=-1)
-    return torch.multinomial(p, 1, generator=generator)

@@ -132,3 +132,27 @@ def attention_dropout(q, k, v, causal=True, scale=None, p=0.0, training=True, ne
         s = s.masked_fill(j > i + (Tk - Tq), neg)
     pr = dropout(torch.softmax(s, dim=-1).to(q.dtype), p, training)
     return torch.matmul(pr, vh).transpose(1, 2)
+
+
+DECODE_MAX_ROWS = 16
+
+
+def _decode_ok(q, k, v):
+    if not (q.is_cuda and q.dtype == torch.bfloat16 and q.dim() == 4 and q.shape[-1] in FLASH_HD):
+        return False
+    B, Tq, H, hd = q.shape
+    Hkv = k.shape[2]
+    if H % Hkv or Tq * (H // Hkv) > DECODE_MAX_ROWS or Tq > k.shape[1]:
+        return False
+    return all(t.stride(3) == 1 and t.stride(0) % 4 == 0 and t.stride(1) % 4 == 0 and t.stride(2) % 4 == 0
+               and t.data_ptr() % 8 == 0 for t in (q, k, v))
+
+
+def decode_attention(q, k, v, causal=True, scale=None, nsplit=0):
+    """Few new query rows against a KV cache: q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd] (cache views,
+    the last Tq cache rows are the query tokens). Split-K HIP kernel (csrc/kernels/decode.hip)
+    when Tq * H / Hkv <= 16, else the flash kernel. Inference only (no autograd)."""
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if _decode_ok(q, k, v):
+        return _ext.ops().attn_decode(q, k, v, scale, causal, int(nsplit))[0]
+    return flash_attention(q.contiguous(), k, v, causal, scale)
