@@ -34,14 +34,21 @@ def main(argv=None):
     ap.add_argument("--prompt", type=int, default=1024)
     ap.add_argument("--new", type=int, default=128)
     ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--graph", action="store_true", help="HIP-graph decode (one replay per token)")
     a = ap.parse_args(argv)
     m = build(a.model, a.layers).eval()
     ids = torch.randint(0, m.c.vocab_size, (a.batch, a.prompt), device="cuda")
-    m.generate(ids[:, :64], 4, greedy=True)  # warm-up (kernels, allocator)
     st = GenerationStats()
-    out = m.generate(ids, a.new, greedy=True, stats=st)
+    if a.graph:
+        from solvingpapers_amd.infer import GraphDecoder
+        dec = GraphDecoder(m, a.batch, a.prompt + a.new)
+        dec.generate(ids[:, :64], 4)  # warm-up of the eager prefill path
+        out = dec.generate(ids, a.new, stats=st)
+    else:
+        m.generate(ids[:, :64], 4, greedy=True)  # warm-up (kernels, allocator)
+        out = m.generate(ids, a.new, greedy=True, stats=st)
     torch.cuda.synchronize()
-    print(json.dumps({"metric": "decode tokens/s", "model": a.model, "batch": a.batch, "prompt": a.prompt,
+    print(json.dumps({"metric": "decode tokens/s", "model": a.model, "graph": a.graph, "batch": a.batch, "prompt": a.prompt,
                       "new_tokens": st.new_tokens, "prefill_tok_s": round(st.prefill_tok_s, 1),
                       "decode_tok_s": round(st.decode_tok_s, 2),
                       "ms_per_token": round(1e3 * st.decode_s / max(1, st.new_tokens // a.batch), 3),

@@ -24,6 +24,7 @@ struct DecodeParams {
   const bf16* q; const bf16* k; const bf16* v;
   float* opart; float* mpart; float* lpart;  // [nsplit][B][Tq][H][hd], [nsplit][B][Tq][H]
   bf16* out; float* lse;
+  const int* kv_len;  // optional device-side cache length (HIP-graph replay); else Tk
   int B, Tq, Tk, H, Hkv, nsplit, chunk;
   long sqb, sqt, sqh, skb, skt, skh, svb, svt, svh, sob, sot, soh;
   float scale_log2;
@@ -43,7 +44,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeParams p) {
   const int hk = bh % p.Hkv, b = bh / p.Hkv;
   const int G = p.H / p.Hkv;
   const int rows = G * p.Tq;
-  const int k0 = split * p.chunk, k1 = min(p.Tk, k0 + p.chunk);
+  const int Tk = p.kv_len ? min(*p.kv_len, p.Tk) : p.Tk;
+  const int k0 = split * p.chunk, k1 = min(Tk, k0 + p.chunk);
 
   // query slices (pre-scaled to log2 units), rows r = t * G + g  (head hk*G + g, token t)
   float qv[R][4];
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeParams p) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int t = r / G, g = r % G;
-    qpos[r] = p.causal ? p.Tk - p.Tq + t : p.Tk;
+    qpos[r] = p.causal ? Tk - p.Tq + t : Tk;
     if (r < rows) {
       const bf16* qp = p.q + b * p.sqb + (long)t * p.sqt + (long)(hk * G + g) * p.sqh + 4 * sub;
       const bf16x4 x = *reinterpret_cast<const bf16x4*>(qp);
@@ -171,10 +173,12 @@ __global__ __launch_bounds__(256) void attn_decode_combine_kernel(DecodeParams p
   if (s4 == 0) p.lse[(b * p.H + h) * p.Tq + t] = lt > 0.f ? (mn + __log2f(lt)) * 0.69314718055994531f : INFINITY;
 }
 
-// q [B, Tq, H, hd] (Tq * H / Hkv <= 16), k/v [B, Tk, Hkv, hd] strided (cache views).
+// q [B, Tq, H, hd] (Tq * H / Hkv <= 16), k/v [B, Tk, Hkv, hd] strided (cache views); with
+// kv_len (device int32) k/v are the full cache buffers and only rows [0, *kv_len) count, so a
+// decode step can be captured once in a hipGraph and replayed at every position.
 // Returns (out [B, Tq, H, hd] bf16, lse [B, H, Tq] fp32).
 std::vector<at::Tensor> attn_decode(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
-                                    bool causal, int64_t nsplit_req) {
+                                    bool causal, int64_t nsplit_req, const c10::optional<at::Tensor>& kv_len) {
   for (auto* t : {&q, &k, &v}) {
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 4, "attn_decode: bf16 [B,T,H,hd]");
     TORCH_CHECK(t->stride(3) == 1 && t->stride(2) % 4 == 0 && t->stride(1) % 4 == 0 && t->stride(0) % 4 == 0 &&
@@ -214,6 +218,11 @@ std::vector<at::Tensor> attn_decode(const at::Tensor& q, const at::Tensor& k, co
   p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
   p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal = causal;
+  if (kv_len.has_value()) {  // k/v are the whole cache; the valid length lives on the device
+    TORCH_CHECK(kv_len->is_cuda() && kv_len->scalar_type() == at::kInt && kv_len->numel() >= 1,
+                "attn_decode: kv_len must be a device int32 tensor");
+    p.kv_len = kv_len->data_ptr<int>();
+  }
   auto st = stream();
   const dim3 grid(B * Hkv, nsplit);
   const long nthr = (long)B * Tq * H * (HD / 4);
@@ -236,6 +245,6 @@ std::vector<at::Tensor> attn_decode(const at::Tensor& q, const at::Tensor& k, co
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
-  m.def("attn_decode(Tensor q, Tensor k, Tensor v, float scale, bool causal, int nsplit) -> Tensor[]");
+  m.def("attn_decode(Tensor q, Tensor k, Tensor v, float scale, bool causal, int nsplit, Tensor? kv_len=None) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("attn_decode", &spa::attn_decode); }

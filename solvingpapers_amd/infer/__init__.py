@@ -12,6 +12,7 @@ deepseekv3/deepseekv3.ipynb:1849-1873.
 """
 from .cache import KVCache
 from .generate import GenerationStats, generate
+from .graph import DecodeState, GraphDecoder
 from .sampling import sample
 
-__all__ = ["KVCache", "GenerationStats", "generate", "sample"]
+__all__ = ["KVCache", "DecodeState", "GenerationStats", "GraphDecoder", "generate", "sample"]

@@ -26,10 +26,11 @@ import torch
 import torch.nn as nn
 
 from ..infer.cache import KVCache
+from ..infer.graph import DecodeState
 from ..infer.sampling import sample  # noqa: F401  (re-exported: reference-style sampling)
-from ..ops import attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
+from ..ops import _ext, attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
 from ..ops.attention import decode_attention
-from ..ops.rope import apply_rope
+from ..ops.rope import RopeCache, apply_rope
 from ..utils.grad import mark_ready
 
 
@@ -105,6 +106,16 @@ class LlamaBlock(nn.Module):
         B, T, _ = n1.shape
         hd = c.head_dim
         qkv = linear(n1, self.wqkv)  # [B, T, (H+2Hkv)*hd]
+        if isinstance(pos, DecodeState):  # graph-capturable decode step: positions on the device
+            H, KV = c.n_heads, c.n_kv_heads
+            x4 = qkv.view(B, T, H + 2 * KV, hd)
+            cos, sin = RopeCache.get(pos.max_len, hd, c.rope_theta, qkv.device, c.ref_freqs)
+            _ext.ops().rope_(x4, cos, sin, pos.positions, H + KV, 0, 0, False)
+            kc, vc = kv_cache
+            kc.index_copy_(1, pos.index, x4[:, :, H:H + KV])
+            vc.index_copy_(1, pos.index, x4[:, :, H + KV:])
+            o = decode_attention(x4[:, :, :H], kc, vc, causal=True, kv_len=pos.kv_len)
+            return linear(o.reshape(B, T, H * hd), self.wo)
         if kv_cache is None:
             qkv = rope_packed_(qkv, c.n_heads + c.n_kv_heads, c.rope_theta, 0, head_dim=hd, ref_freqs=c.ref_freqs)
             o = attention_packed(qkv, c.n_heads, c.n_kv_heads, causal=True, head_dim=hd)
@@ -226,6 +237,13 @@ class Llama3(nn.Module):
         """Write ids' K/V at cache rows [pos, pos+T), return the last position's logits [B, V]."""
         n = self.hidden(ids, cache, pos)
         return self.logits(n[:, -1:]).float()[:, -1]
+
+    def step_graph(self, ids, cache, state: DecodeState):
+        """One-token decode step with every position on the device (HIP-graph capturable;
+        infer/graph.py): cache rows are written with index_copy_, RoPE reads device
+        positions, the decode kernel reads the cache length from ``state.kv_len``."""
+        n = self.hidden(ids, cache, state)
+        return self.logits(n).float()[:, -1]
 
     @torch.no_grad()
     def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None,

@@ -148,11 +148,16 @@ def _decode_ok(q, k, v):
                and t.data_ptr() % 8 == 0 for t in (q, k, v))
 
 
-def decode_attention(q, k, v, causal=True, scale=None, nsplit=0):
+def decode_attention(q, k, v, causal=True, scale=None, nsplit=0, kv_len=None):
     """Few new query rows against a KV cache: q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd] (cache views,
     the last Tq cache rows are the query tokens). Split-K HIP kernel (csrc/kernels/decode.hip)
-    when Tq * H / Hkv <= 16, else the flash kernel. Inference only (no autograd)."""
+    when Tq * H / Hkv <= 16, else the flash kernel. Inference only (no autograd).
+
+    ``kv_len`` (device int32 [1]): k/v are whole cache buffers and only the first *kv_len
+    rows are valid -- the form a captured hipGraph decode step replays at every position."""
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if _decode_ok(q, k, v):
-        return _ext.ops().attn_decode(q, k, v, scale, causal, int(nsplit))[0]
+        return _ext.ops().attn_decode(q, k, v, scale, causal, int(nsplit), kv_len)[0]
+    if kv_len is not None:
+        raise ValueError("decode_attention: kv_len needs the decode kernel (Tq * H / Hkv <= 16, bf16 on the GPU)")
     return flash_attention(q.contiguous(), k, v, causal, scale)

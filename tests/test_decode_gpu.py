@@ -76,3 +76,26 @@ def test_gemma_mqa_cached_steps_match_full_forward():
         cache = m.new_cache(1, 24)
         lg = [m.step(ids[:, :16], cache, 0)] + [m.step(ids[:, t:t + 1], cache, t) for t in range(16, 24)]
     assert rel(torch.stack(lg[1:], 1), full[:, 16:24]) < 2e-2
+
+
+def test_graph_decoder_matches_eager_logits():
+    """HIP-graph decode (device-side positions, index_copy_ cache writes, kv_len decode
+    kernel, state advanced inside the graph) == full forward, teacher-forced."""
+    from solvingpapers_amd.infer import GraphDecoder
+    from solvingpapers_amd.models import llama3
+    torch.manual_seed(0)
+    m = llama3.Llama3(llama3.config("llama3_tiny"), device=DEV, dtype=torch.bfloat16).eval()
+    ids = torch.randint(0, m.c.vocab_size, (2, 40), device=DEV)
+    with torch.no_grad():
+        full = m(ids).float()
+        dec = GraphDecoder(m, 2, 48)
+        lg = [dec.prefill(ids[:, :24])]
+        for t in range(24, 40):
+            dec.ids.copy_(ids[:, t:t + 1])
+            dec.graph.replay()
+            lg.append(dec.logits.clone())
+    assert rel(lg[0], full[:, 23]) < 2e-2
+    assert rel(torch.stack(lg[1:], 1), full[:, 24:40]) < 2e-2
+    out = dec.generate(ids[:, :10], 6)
+    ref = m.generate(ids[:, :10], 6, greedy=True)
+    assert out.shape == ref.shape and torch.equal(out[:, :11], ref[:, :11])

@@ -6,4 +6,6 @@ timeout -k 10 200 python -u -m pytest tests/test_decode_gpu.py -x -q --timeout 1
 timeout -k 10 200 python bench/decode.py --prompt 1024 --new 128 > gpurun_out/decode.log 2>&1 || exit 2
 timeout -k 10 200 python bench/decode.py --prompt 7936 --new 128 >> gpurun_out/decode.log 2>&1 || exit 2
 timeout -k 10 200 python bench/decode.py --prompt 1024 --new 128 --batch 16 >> gpurun_out/decode.log 2>&1 || exit 2
+timeout -k 10 200 python bench/decode.py --prompt 1024 --new 128 --graph >> gpurun_out/decode.log 2>&1 || exit 3
+timeout -k 10 200 python bench/decode.py --prompt 1024 --new 128 --batch 16 --graph >> gpurun_out/decode.log 2>&1 || exit 3
 cat gpurun_out/decode.log | grep metric
