@@ -30,6 +30,7 @@ from solvingpapers_amd.parallel import dist as sdist  # noqa: E402
 from solvingpapers_amd.parallel.data_parallel import DataParallel  # noqa: E402
 from solvingpapers_amd.train.optim import FlatAdamW  # noqa: E402
 from solvingpapers_amd.utils.flat import FlatParams  # noqa: E402
+from solvingpapers_amd.utils.tuning import load_gemm_tuning  # noqa: E402
 
 BASELINE_TOKS = None  # BASELINE.json "published": {} -> no reference number for this config
 PEAK_BF16 = 2.5e15
@@ -47,6 +48,8 @@ def main(argv=None):
     ap.add_argument("--zero1", action="store_true")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (NOT for headline runs)")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
+    ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (default tuning/tunableop_llama8b.csv; "
+                    "SPA_GEMM_TUNING=0 disables)")
     a = ap.parse_args(argv)
 
     info = sdist.init_distributed()
@@ -55,6 +58,7 @@ def main(argv=None):
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dev = info.device
     torch.backends.cuda.matmul.allow_tf32 = False
+    tuned = load_gemm_tuning(a.gemm_table)
 
     kw = {} if a.layers is None else {"n_layers": a.layers}
     cfg = llama3.config(a.model, max_seq_len=a.seq, **kw)
@@ -138,6 +142,7 @@ def main(argv=None):
             },
             "tflops_per_gpu": round(tflops_gpu, 1),
             "mfu_vs_2.5PF": round(tflops_gpu * 1e12 / PEAK_BF16, 4),
+            "gemm_table": tuned,
             "loss": round(loss_v, 4),
             "mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
         }

@@ -143,7 +143,9 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args(argv)
     from ..parallel import dist as sdist
+    from ..utils.tuning import load_gemm_tuning
     info = sdist.init_distributed()
+    load_gemm_tuning()  # tuned hipBLASLt/rocBLAS solutions for the shapes in tuning/*.csv
     try:
         if args.model in ("vit", "ae", "vae", "kd"):
             _images(args, info)
