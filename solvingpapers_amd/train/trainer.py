@@ -203,6 +203,7 @@ class Trainer:
         t_last = time.perf_counter()
         while self.step < c.steps:
             s = self.step
+            _maybe_inject_fault(s, self.rank)  # test hook: no-op unless SPA_FAULT_STEP is set
             if c.profile_steps and s == c.profile_steps[0]:
                 prof = _start_profiler(c)
             loss, ntok, ok = self.train_step(s)
@@ -229,6 +230,24 @@ class Trainer:
         if c.ckpt_dir and c.ckpt_every:
             self.save()
         return self.history
+
+
+def _maybe_inject_fault(step: int, rank: int):
+    """Fault injection for the elastic-restart test (SURVEY §5 'Failure detection'):
+    ``SPA_FAULT_STEP=s`` (+ ``SPA_FAULT_RANK=r``, default 0) makes rank r die abruptly --
+    ``os._exit``, no cleanup, no checkpoint -- when it reaches step s. With
+    ``SPA_FAULT_MARKER=<file>`` it fires once (the marker survives the restart), so a run
+    under ``torchrun --max-restarts`` crashes, restarts and auto-resumes."""
+    at = os.environ.get("SPA_FAULT_STEP")
+    if at is None or int(at) != step or int(os.environ.get("SPA_FAULT_RANK", "0")) != rank:
+        return
+    marker = os.environ.get("SPA_FAULT_MARKER")
+    if marker:
+        if os.path.exists(marker):
+            return
+        with open(marker, "w") as f:
+            f.write(f"rank {rank} killed at step {step}\n")
+    os._exit(17)
 
 
 class _null:
