@@ -194,18 +194,29 @@ class GemmaBlock(tnn.Module):
         for w in (self.wq, self.wkv, self.wo, self.w13, self.w2):
             w.normal_(0.0, 0.02, generator=g)
 
-    def forward(self, res, delta, tp_group=None, cache=None, pos=0):
-        from ..parallel.tensor_parallel import copy_to_tp, reduce_from_tp, reduce_grad_tp
+    def forward(self, res, delta, tp_group=None, cache=None, pos=0, sp=False):
+        """``sp``: sequence parallel -- res/delta are [B, T/tp, D] shards; the TP regions
+        open with an all-gather over T and close with a reduce-scatter over T."""
+        from ..parallel.tensor_parallel import (copy_to_tp, gather_seq, reduce_from_tp, reduce_grad_tp,
+                                                reduce_scatter_seq, scale_grad)
         c = self.c
         if res is None:
             n1, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
         else:
             n1, h = rms_norm(delta, self.attn_norm, c.norm_eps, residual=res)
-        B, T, _ = n1.shape
         hd, KV = c.head_dim, c.n_kv_heads
-        n1p = copy_to_tp(n1, tp_group)
-        q = linear(n1p, self.wq)                                         # [B, T, hl*hd]
-        kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)              # replicated K/V, grads summed over TP
+        if sp:
+            assert cache is None, "sequence parallelism is a training layout"
+            n1f = gather_seq(n1, tp_group)                               # [B, T, D]
+            q = linear(n1f, self.wq)
+            # the K/V activation grad is summed over TP below, so its input grad is complete on
+            # every rank: scale by 1/tp before gather_seq's reduce-scatter sums the copies
+            kv = reduce_grad_tp(linear(scale_grad(n1f, 1.0 / self.tp), self.wkv), tp_group)
+        else:
+            n1p = copy_to_tp(n1, tp_group)
+            q = linear(n1p, self.wq)                                     # [B, T, hl*hd]
+            kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)          # replicated K/V, grads summed over TP
+        B, T = q.shape[0], q.shape[1]
         qkv = torch.cat([q, kv], dim=-1)
         qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, pos, interleaved=False, head_dim=hd)
         if cache is None:
@@ -217,19 +228,22 @@ class GemmaBlock(tnn.Module):
             vc[:, pos:pos + T] = x4[:, :, self.hl + KV:]
             o = decode_attention(x4[:, :, :self.hl], kc[:, :pos + T], vc[:, :pos + T], causal=True)
             o = o.reshape(B, T, self.hl * hd)
-        a = reduce_from_tp(linear(o, self.wo), tp_group)
+        close = reduce_scatter_seq if sp else reduce_from_tp
+        a = close(linear(o, self.wo), tp_group)
         n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
-        f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
-        return h2, reduce_from_tp(linear(f, self.w2), tp_group)
+        f = glu(linear(gather_seq(n2, tp_group) if sp else copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
+        return h2, close(linear(f, self.w2), tp_group)
 
 
 class Gemma(tnn.Module):
-    def __init__(self, c: GemmaConfig, device=None, dtype=torch.float32, tp_group=None, seed=0):
+    def __init__(self, c: GemmaConfig, device=None, dtype=torch.float32, tp_group=None, seed=0,
+                 sequence_parallel=False):
         super().__init__()
         from ..parallel.tensor_parallel import tp_rank_size
         self.c = c
         self.tp_group = tp_group
         self.tp_rank, self.tp = tp_rank_size(tp_group)
+        self.sp = bool(sequence_parallel) and self.tp > 1
         assert c.vocab_size % self.tp == 0
         fk = dict(device=device, dtype=dtype)
         self.embed = tnn.Parameter(torch.empty(c.vocab_size // self.tp, c.dim, **fk))   # vocab-parallel, tied head
@@ -248,25 +262,37 @@ class Gemma(tnn.Module):
         return [[self.embed]] + [list(l.parameters()) for l in self.layers] + [[self.norm_f]]
 
     def hidden(self, ids, cache=None, pos=0):
+        """Final-norm hidden states; a [B, T/tp, D] sequence shard under sequence parallelism."""
         from ..parallel.tensor_parallel import vocab_parallel_embedding
         c = self.c
-        x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim))
+        sp = self.sp and cache is None
+        x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim), sequence_parallel=sp)
         res, delta = None, x
         for i, l in enumerate(self.layers):
             delta = mark_ready(delta, self.grad_ready_cb, i + 1)
-            res, delta = l(res, delta, self.tp_group, None if cache is None else cache[i], pos)
+            res, delta = l(res, delta, self.tp_group, None if cache is None else cache[i], pos, sp)
         delta = mark_ready(delta, self.grad_ready_cb, len(self.layers) + 1)
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
         return n
 
     def forward(self, ids, targets=None):
-        from ..parallel.tensor_parallel import vocab_parallel_cross_entropy
+        from ..parallel.tensor_parallel import gather_seq, scale_grad, vocab_parallel_cross_entropy
         c = self.c
         n = self.hidden(ids)
+        if self.sp:  # the vocab-parallel head needs every token on every rank; its input grad is
+            n = scale_grad(gather_seq(n, self.tp_group), 1.0 / self.tp)  # complete on each rank
         if targets is None:
             from ..parallel.tensor_parallel import gather_vocab_logits
             return gather_vocab_logits(linear(n, self.embed), self.tp_group)
         return vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, targets.reshape(-1), self.tp_group)
+
+    def sync_sequence_parallel_grads(self):
+        """Norm weights see only their sequence shard under SP: sum their grads over TP
+        (call after backward, before the optimizer)."""
+        if self.sp:
+            from ..parallel.tensor_parallel import sync_sequence_parallel_grads
+            ps = [self.norm_f] + [p for l in self.layers for p in (l.attn_norm, l.ffn_norm)]
+            sync_sequence_parallel_grads(ps, self.tp_group)
 
     # ---------------------------------------------------------------- inference
     @property

@@ -64,8 +64,104 @@ def reduce_from_tp(x, group):
 reduce_grad_tp = copy_to_tp  # identity fwd, sum of activation grads over the TP group bwd
 
 
-def vocab_parallel_embedding(w_local, ids, group, scale=1.0):
-    """Rows [r*V/tp, (r+1)*V/tp) live on TP rank r; out-of-shard ids contribute zeros."""
+# ----------------------------------------------------------- sequence parallelism
+# Megatron sequence parallelism: between the TP regions the residual stream is sharded
+# along the sequence ([B, T/tp, D] per rank), so norms, residual adds and their
+# activations are computed and stored once per token instead of tp times. Each
+# row-parallel all-reduce becomes a reduce-scatter (over T) and each replicated input of
+# a column-parallel region an all-gather (over T): same bytes on the wire as one
+# all-reduce (RS + AG), split into two calls that bracket the local work.
+
+def _gather_seq_raw(x, group):
+    rank, tp = tp_rank_size(group)
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(x) for _ in range(tp)]
+        dist.all_gather(parts, x.contiguous(), group=group)
+        return torch.cat(parts, dim=1)
+    xt = x.transpose(0, 1).contiguous()                                 # [T/tp, B, ...]
+    out = torch.empty((xt.shape[0] * tp,) + tuple(xt.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, xt, group=group)
+    return out.transpose(0, 1).contiguous()
+
+
+def _reduce_scatter_seq_raw(x, group):
+    rank, tp = tp_rank_size(group)
+    assert x.shape[1] % tp == 0, "sequence parallelism needs T divisible by the TP size"
+    if dist.get_backend(group) == "gloo":                               # gloo has no reduce-scatter
+        y = x.contiguous().clone()
+        dist.all_reduce(y, group=group)
+        return y.chunk(tp, dim=1)[rank].contiguous()
+    xt = x.transpose(0, 1).contiguous()                                 # [T, B, ...]
+    out = torch.empty((xt.shape[0] // tp,) + tuple(xt.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, xt, group=group)
+    return out.transpose(0, 1).contiguous()
+
+
+class _GatherSeq(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return _gather_seq_raw(x, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _reduce_scatter_seq_raw(g, ctx.group), None
+
+
+class _ReduceScatterSeq(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return _reduce_scatter_seq_raw(x, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _gather_seq_raw(g, ctx.group), None
+
+
+class _ScaleGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.s = s
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * ctx.s, None
+
+
+def gather_seq(x, group):
+    """[B, T/tp, ...] -> [B, T, ...]: all-gather fwd, reduce-scatter bwd."""
+    return x if tp_rank_size(group)[1] == 1 else _GatherSeq.apply(x, group)
+
+
+def reduce_scatter_seq(x, group):
+    """Partial [B, T, ...] -> summed local shard [B, T/tp, ...]: reduce-scatter fwd, all-gather bwd."""
+    return x if tp_rank_size(group)[1] == 1 else _ReduceScatterSeq.apply(x, group)
+
+
+def scale_grad(x, s):
+    """Identity forward, gradient times ``s``: a replicated consumer whose input gradient is
+    already complete on every rank, feeding a gather_seq whose backward sums over ranks."""
+    return x if s == 1 else _ScaleGrad.apply(x, s)
+
+
+def sync_sequence_parallel_grads(params, group):
+    """Replicated parameters used on sequence shards (norm weights) see only their shard's
+    tokens: sum their gradients over the TP group (main_grad when present, else .grad)."""
+    if tp_rank_size(group)[1] == 1:
+        return
+    for p in params:
+        g = getattr(p, "main_grad", None)
+        g = g if g is not None else p.grad
+        if g is not None:
+            dist.all_reduce(g, group=group)
+
+
+def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=False):
+    """Rows [r*V/tp, (r+1)*V/tp) live on TP rank r; out-of-shard ids contribute zeros.
+    With ``sequence_parallel`` the partial rows are reduce-scattered over T (the output is
+    this rank's [B, T/tp, D] shard) instead of all-reduced."""
     rank, tp = tp_rank_size(group)
     if tp == 1:
         return embedding(w_local, ids, scale=scale)
@@ -74,7 +170,7 @@ def vocab_parallel_embedding(w_local, ids, group, scale=1.0):
     mask = (ids >= lo) & (ids < lo + vl)
     local = torch.where(mask, ids - lo, torch.zeros_like(ids))
     x = embedding(w_local, local, scale=scale) * mask.unsqueeze(-1).to(w_local.dtype)
-    return reduce_from_tp(x, group)
+    return reduce_scatter_seq(x, group) if sequence_parallel else reduce_from_tp(x, group)
 
 
 class _VocabParallelXent(torch.autograd.Function):

@@ -113,7 +113,7 @@ def test_zero1_matches_dp():
         assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
 
 
-def _tp_worker(rank, world, port, q):
+def _tp_worker(rank, world, port, q, sp=False):
     _init(rank, world, port)
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.parallel.tensor_parallel import shard_gemma_from_full
@@ -121,12 +121,13 @@ def _tp_worker(rank, world, port, q):
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     grp = dist.new_group([0, 1])
-    local = gemma.Gemma(c, tp_group=grp, seed=5)
+    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=sp)
     shard_gemma_from_full(full, local, rank, world)
     flat = FlatParams(local)
     ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
-    loss = local(ids[:, :-1], ids[:, 1:])
+    loss = local(ids[:, :-1], ids[:, 1:]) if not sp else local(ids[:, :-2], ids[:, 1:-1])
     loss.backward()
+    local.sync_sequence_parallel_grads()
     grads = {n: p.main_grad.clone().numpy() for n, p in local.named_parameters()}
     from solvingpapers_amd.train.optim import FlatAdamW
     gn = FlatAdamW(flat, max_grad_norm=1.0, tp_group=grp).grad_norm().item()
@@ -134,17 +135,20 @@ def _tp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_tensor_parallel_gemma_matches_unsharded():
+@pytest.mark.parametrize("sp", [False, True])
+def test_tensor_parallel_gemma_matches_unsharded(sp):
+    """TP=2 (and TP=2 with Megatron sequence parallelism: reduce-scatter / all-gather over T,
+    norms on sequence shards, norm-weight grads summed over TP) == the unsharded model."""
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.utils.flat import FlatParams
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     FlatParams(full)
     ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
-    loss = full(ids[:, :-1], ids[:, 1:])
+    loss = full(ids[:, :-1], ids[:, 1:]) if not sp else full(ids[:, :-2], ids[:, 1:-1])  # SP: T even
     loss.backward()
     fg = {n: p.main_grad for n, p in full.named_parameters()}
-    out = _run(_tp_worker, 2, )
+    out = _run(_tp_worker, 2, sp)
     world = 2
     full_norm = torch.sqrt(sum((g.float() ** 2).sum() for g in fg.values())).item()
     for rank, l, (grads, gn) in out:
