@@ -16,6 +16,7 @@ V128256), seq 8192, micro-batch 1 per GPU (weak scaling: global batch = N).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -30,6 +31,7 @@ from solvingpapers_amd.parallel import dist as sdist  # noqa: E402
 from solvingpapers_amd.parallel.data_parallel import DataParallel  # noqa: E402
 from solvingpapers_amd.train.optim import FlatAdamW  # noqa: E402
 from solvingpapers_amd.utils.flat import FlatParams  # noqa: E402
+from solvingpapers_amd.utils.prof import annotate  # noqa: E402
 from solvingpapers_amd.utils.tuning import load_gemm_tuning  # noqa: E402
 
 BASELINE_TOKS = None  # BASELINE.json "published": {} -> no reference number for this config
@@ -87,16 +89,16 @@ def main(argv=None):
         for i in range(a.accum):
             x, y = batch()
             sync = (i == a.accum - 1)
-            if dp is not None and not sync:
-                with dp.no_sync():
+            with (dp.no_sync() if (dp is not None and not sync) else contextlib.nullcontext()):
+                with annotate("forward"):
                     loss = model(x, y) / a.accum
+                with annotate("backward"):
                     loss.backward()
-            else:
-                loss = model(x, y) / a.accum
-                loss.backward()
         if dp is not None:
-            dp.finish_grad_sync()
-        opt.step(overlap=overlap)
+            with annotate("grad_sync"):
+                dp.finish_grad_sync()
+        with annotate("optimizer"):
+            opt.step(overlap=overlap)
         if dp is not None:
             dp.gather_params()
         last_loss[0] = loss

@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 from ..parallel.data_parallel import DataParallel
 from ..utils.flat import FlatParams
+from ..utils.prof import annotate
 from . import checkpoint as ckpt
 from .optim import FlatAdamW, FlatSGD, cosine_lr
 
@@ -176,11 +177,17 @@ class Trainer:
             last = mi == c.grad_accum - 1
             ctx = self.dp.no_sync() if (self.dp is not None and not last) else _null()
             with ctx:
-                loss = self.model(x, y)
-                (loss / c.grad_accum).backward()
+                with annotate("forward"):
+                    loss = self.model(x, y)
+                with annotate("backward"):
+                    (loss / c.grad_accum).backward()
             tot = loss.detach() if tot is None else tot + loss.detach()
         if self.dp is not None:
-            self.dp.finish_grad_sync()
+            with annotate("grad_sync"):
+                self.dp.finish_grad_sync()
+        sync_sp = getattr(self.model, "sync_sequence_parallel_grads", None)
+        if sync_sp is not None:
+            sync_sp()
         loss = tot / c.grad_accum
         finite = bool(torch.isfinite(loss).item())
         if not finite:
@@ -189,7 +196,8 @@ class Trainer:
                 raise NonFiniteLoss(f"{self.bad_steps} consecutive non-finite losses at step {step}")
             return float("nan"), ntok, False
         self.bad_steps = 0
-        self.opt.step(lr=self.lr_at(step), overlap=c.opt_overlap)
+        with annotate("optimizer"):
+            self.opt.step(lr=self.lr_at(step), overlap=c.opt_overlap)
         if self.dp is not None:
             self.dp.gather_params()
         return float(loss), ntok, True
