@@ -51,6 +51,13 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> Di
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl" and cuda:
             kw["device_id"] = device
+        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if restart is not None and int(restart) > 0:
+            # after an elastic restart the workers share the agent's store with the dead round:
+            # namespace this round's keys, or a new rank can read a dead peer's address
+            # (gloo: 'connectFullMesh ... Connection refused') and the restart fails
+            store, _, _ = next(dist.rendezvous("env://", rank, world, timeout=kw["timeout"]))
+            kw["store"] = dist.PrefixStore(f"spa_restart{restart}", store)
         dist.init_process_group(**kw)
     _INFO = DistInfo(rank, world, local, backend if world > 1 else "none", device)
     return _INFO

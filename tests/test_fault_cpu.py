@@ -30,8 +30,10 @@ def _run(tmp, name, fault):
         env.pop(k, None)
     if fault:
         env.update(SPA_FAULT_STEP="6", SPA_FAULT_RANK="1", SPA_FAULT_MARKER=os.path.join(tmp, name + ".fault"))
+    # dynamic c10d rendezvous: each restart round re-rendezvouses under a fresh round id
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-           "--max-restarts", "1", "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "--max-restarts", "1", "--rdzv-backend", "c10d", "--rdzv-endpoint", f"127.0.0.1:{_port()}",
+           "--rdzv-id", f"spa-{name}-{os.getpid()}",
            "-m", "solvingpapers_amd.train", "llama3", "--preset", "llama3_ref", "--device", "cpu",
            "--set", "vocab_size=128", "--set", "dim=64", "--set", "ffn_hidden=128", "--set", "init='std'",
            "--batch", "2", "--seq", "16", "--steps", "10", "--ckpt-dir", ck, "--ckpt-every", "4", "--lr", "1e-2"]
