@@ -21,8 +21,11 @@ def transpose2d(x: torch.Tensor) -> torch.Tensor:
 
 
 def wgrad_nt_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    # the transpose kernel moves 16-byte units along both axes: token count, N and K all % 8
+    # (MTP heads feed T - k tokens, e.g. 8190)
     return (WGRAD_NT and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
-            and dy2.shape[0] >= WGRAD_NT_MIN_TOKENS and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0
+            and dy2.shape[0] >= WGRAD_NT_MIN_TOKENS and dy2.shape[0] % 8 == 0
+            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0)
 
 

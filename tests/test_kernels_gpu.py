@@ -311,3 +311,16 @@ def test_wgrad_nt_matches_tn():
     acc = out.clone()
     wgrad(dy, x, acc, True)
     assert ((acc.float() - 2 * ref).norm() / ref.norm()) < 1e-2
+
+
+def test_wgrad_odd_token_count_falls_back():
+    """dW = dY^T X for a token count that is not a multiple of 8 (MTP heads: T - k rows) takes
+    the direct product instead of the transposed-operand path."""
+    from solvingpapers_amd.ops.layout import wgrad, wgrad_nt_ok
+    dy = torch.randn(4095, 256, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(4095, 512, device="cuda", dtype=torch.bfloat16)
+    assert not wgrad_nt_ok(dy, x)
+    assert rel(wgrad(dy, x), dy.float().t() @ x.float()) < 1e-2
+    dy8, x8 = dy[:4088], x[:4088]
+    assert wgrad_nt_ok(dy8, x8)
+    assert rel(wgrad(dy8, x8), dy8.float().t() @ x8.float()) < 1e-2
