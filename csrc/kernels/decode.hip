@@ -32,12 +32,16 @@ struct DecodeParams {
 };
 
 constexpr int kMaxRows = 16;
+constexpr int kKeysPerLoad = 8;
+// keys one 4-wave block covers per load batch: 4 waves x (64 / (hd / 4)) lane groups x 8
+constexpr int keys_per_batch(int hd) { return 4 * (256 / hd) * kKeysPerLoad; }
 
 template <int HD, int R>
 __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeParams p) {
   constexpr int KL = HD / 4;        // lanes per key
   constexpr int KPW = 64 / KL;      // keys per wave step
   constexpr int NG = 4 * KPW;       // lane groups per block
+  constexpr int KPL = kKeysPerLoad; // keys per lane group per load batch
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int sub = lane % KL, grp = wave * KPW + lane / KL;
   const int bh = blockIdx.x, split = blockIdx.y;
@@ -74,28 +78,47 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeParams p) {
   }
   const bf16* kb = p.k + b * p.skb + hk * p.skh + 4 * sub;
   const bf16* vb = p.v + b * p.svb + hk * p.svh + 4 * sub;
-  for (int key = k0 + grp; key < k1; key += NG) {
-    const bf16x4 kx = *reinterpret_cast<const bf16x4*>(kb + (long)key * p.skt);
-    const bf16x4 vx = *reinterpret_cast<const bf16x4*>(vb + (long)key * p.svt);
-    float kf[4], vf[4];
+  // Batches of KPL keys per lane group: every K/V load of a batch is issued before any is
+  // consumed (one HBM round trip per batch, 2 * KPL loads in flight per lane), and the batch
+  // shares one online-softmax rescale per row. Keys past the split end are clamped on load
+  // and masked in the softmax. (One key per round trip measured 24.6 us per layer at a
+  // 1K-token cache: pure latency.)
+  for (int base = k0; base < k1; base += NG * KPL) {
+    bf16x4 kx[KPL], vx[KPL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { kf[j] = (float)kx[j]; vf[j] = (float)vx[j]; }
+    for (int j = 0; j < KPL; ++j) {
+      const long kk = min(base + j * NG + grp, k1 - 1);
+      kx[j] = *reinterpret_cast<const bf16x4*>(kb + kk * p.skt);
+      vx[j] = *reinterpret_cast<const bf16x4*>(vb + kk * p.svt);
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      float s = qv[r][0] * kf[0];
+      float s[KPL];
+      float mx = m[r];
 #pragma unroll
-      for (int j = 1; j < 4; ++j) s = fmaf(qv[r][j], kf[j], s);
+      for (int j = 0; j < KPL; ++j) {
+        float d = qv[r][0] * (float)kx[j][0];
 #pragma unroll
-      for (int w = KL / 2; w > 0; w >>= 1) s += __shfl_xor(s, w, KL);
-      if (key > qpos[r]) s = -INFINITY;
-      const float mn = fmaxf(m[r], s);
-      if (mn == -INFINITY) continue;  // nothing visible yet for this row
-      const float alpha = __builtin_amdgcn_exp2f(m[r] - mn);
-      const float e = __builtin_amdgcn_exp2f(s - mn);
-      m[r] = mn;
-      l[r] = l[r] * alpha + e;
+        for (int e = 1; e < 4; ++e) d = fmaf(qv[r][e], (float)kx[j][e], d);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[r][j] = fmaf(o[r][j], alpha, e * vf[j]);
+        for (int w = KL / 2; w > 0; w >>= 1) d += __shfl_xor(d, w, KL);
+        const int key = base + j * NG + grp;
+        s[j] = (key >= k1 || key > qpos[r]) ? -INFINITY : d;
+        mx = fmaxf(mx, s[j]);
+      }
+      if (mx == -INFINITY) continue;  // nothing visible yet for this row
+      const float alpha = __builtin_amdgcn_exp2f(m[r] - mx);  // m = -inf -> 0
+      l[r] *= alpha;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[r][e] *= alpha;
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        const float pj = __builtin_amdgcn_exp2f(s[j] - mx);
+        l[r] += pj;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[r][e] = fmaf(pj, (float)vx[j][e], o[r][e]);
+      }
+      m[r] = mx;
     }
   }
   // merge the NG lane groups: in-wave groups through shuffles, then waves through LDS
@@ -196,13 +219,18 @@ std::vector<at::Tensor> attn_decode(const at::Tensor& q, const at::Tensor& k, co
   auto out = at::empty({B, Tq, H, HD}, q.options());
   auto lse = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
   if (B * Tq * H == 0) return {out, lse};
-  // split the keys so the grid covers the chip ~2x, but keep >= 128 keys per split
+  // split the keys so the grid covers the chip ~2x, each split a whole number of load
+  // batches (hd 128: 64 keys = 8 lane groups x 8 keys in flight)
+  const int kpb = keys_per_batch(HD);
   int nsplit = (int)nsplit_req;
+  int chunk;
   if (nsplit <= 0) {
     const int want = std::max(1, 512 / std::max(1, B * Hkv));
-    nsplit = std::max(1, std::min(want, cdiv(Tk, 128)));
+    nsplit = std::max(1, std::min(want, cdiv(Tk, kpb)));
+    chunk = cdiv(cdiv(Tk, nsplit), kpb) * kpb;
+  } else {
+    chunk = cdiv(Tk, nsplit);
   }
-  const int chunk = cdiv(Tk, nsplit);
   nsplit = cdiv(Tk, chunk);
   auto part = at::empty({(long)nsplit * B * Tq * H * (HD + 2)}, q.options().dtype(at::kFloat));
   DecodeParams p{};

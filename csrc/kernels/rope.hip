@@ -118,10 +118,91 @@ void rope_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, co
   SPA_LAUNCH_CHECK();
 }
 
+// Decode-step prologue in one launch (interleaved RoPE, MODE 0): for a packed qkv buffer
+// [B, T, H + 2 Hkv, hd], rotate the q heads in place, rotate the k heads into the KV cache and
+// copy the v heads into it, at cache row *index + t. The row and the RoPE positions are read
+// from device memory, so a captured hipGraph replays it at every position (replaces rope_ +
+// two index_copy_ launches per layer). Rows past the cache end are dropped.
+__global__ __launch_bounds__(256) void rope_kv_write_kernel(bf16* __restrict__ x, const float* __restrict__ cosT,
+                                                            const float* __restrict__ sinT,
+                                                            const int* __restrict__ pos,
+                                                            const long* __restrict__ index, bf16* __restrict__ kc,
+                                                            bf16* __restrict__ vc, long sb, long st, long sh,
+                                                            long kcb, long kct, long kch, long vcb, long vct,
+                                                            long vch, int B, int T, int H, int Hkv, int hd,
+                                                            int Tmax) {
+  const int vpr = hd / 8;
+  const int NH = H + 2 * Hkv;
+  const long total = (long)B * T * NH * vpr;
+  const long row0 = *index;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int v = i % vpr;
+    long r = i / vpr;
+    const int hh = r % NH;
+    r /= NH;
+    const int t = r % T;
+    const int b = r / T;
+    float a[8];
+    load8(x + b * sb + t * st + hh * sh + v * 8, a);
+    if (hh < H + Hkv) {
+      const int ps = pos[b * T + t];
+      const f32x4 cv = *reinterpret_cast<const f32x4*>(cosT + (long)ps * (hd / 2) + v * 4);
+      const f32x4 sv = *reinterpret_cast<const f32x4*>(sinT + (long)ps * (hd / 2) + v * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x0 = a[2 * k], x1 = a[2 * k + 1];
+        a[2 * k] = x0 * cv[k] - x1 * sv[k];
+        a[2 * k + 1] = x0 * sv[k] + x1 * cv[k];
+      }
+    }
+    const long row = row0 + t;
+    if (hh < H) store8(x + b * sb + t * st + hh * sh + v * 8, a);
+    else if (row < Tmax && hh < H + Hkv) store8(kc + b * kcb + row * kct + (hh - H) * kch + v * 8, a);
+    else if (row < Tmax) store8(vc + b * vcb + row * vct + (hh - H - Hkv) * vch + v * 8, a);
+  }
+}
+
+void rope_kv_write_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const at::Tensor& pos,
+                    const at::Tensor& index, const at::Tensor& kc, const at::Tensor& vc, int64_t H, int64_t Hkv) {
+  for (auto* t : {&x, &kc, &vc}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 4 && t->stride(3) == 1,
+                "rope_kv_write: bf16 [B, T, heads, hd] tensors with contiguous hd");
+    TORCH_CHECK(t->stride(0) % 8 == 0 && t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0 &&
+                    (uintptr_t)t->data_ptr() % 16 == 0,
+                "rope_kv_write: 16-byte aligned rows");
+  }
+  const int B = x.size(0), T = x.size(1), hd = x.size(3);
+  TORCH_CHECK(x.size(2) == H + 2 * Hkv && hd % 16 == 0, "rope_kv_write: x must be packed [B, T, H + 2 Hkv, hd]");
+  TORCH_CHECK(kc.size(0) == B && vc.size(0) == B && kc.size(2) == Hkv && vc.size(2) == Hkv && kc.size(3) == hd &&
+                  vc.size(3) == hd && vc.size(1) == kc.size(1),
+              "rope_kv_write: cache shape mismatch");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous() && cos.size(1) == hd / 2,
+              "rope_kv_write: fp32 [Tmax, hd/2] tables");
+  TORCH_CHECK(pos.is_cuda() && pos.scalar_type() == at::kInt && pos.is_contiguous() && pos.numel() == (int64_t)B * T,
+              "rope_kv_write: pos must be device int32 [B, T]");
+  TORCH_CHECK(index.is_cuda() && index.scalar_type() == at::kLong && index.numel() >= 1,
+              "rope_kv_write: index must be a device int64 tensor");
+  DeviceGuard g(x.device());
+  const long total = (long)B * T * (H + 2 * Hkv) * (hd / 8);
+  if (total == 0) return;
+  const int grid = (int)std::min<long>((total + 255) / 256, 4096);
+  rope_kv_write_kernel<<<grid, 256, 0, stream()>>>(
+      (bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(),
+      index.data_ptr<int64_t>(), (bf16*)kc.data_ptr(), (bf16*)vc.data_ptr(), x.stride(0), x.stride(1), x.stride(2),
+      kc.stride(0), kc.stride(1), kc.stride(2), vc.stride(0), vc.stride(1), vc.stride(2), B, T, (int)H, (int)Hkv, hd,
+      (int)kc.size(1));
+  SPA_LAUNCH_CHECK();
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int nrot, int pos_off, int mode, "
         "bool inverse) -> ()");
+  m.def("rope_kv_write_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor pos, Tensor index, Tensor(b!) kc, "
+        "Tensor(c!) vc, int n_heads, int n_kv_heads) -> ()");
 }
-TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("rope_", &spa::rope_); }
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("rope_", &spa::rope_);
+  m.impl("rope_kv_write_", &spa::rope_kv_write_);
+}

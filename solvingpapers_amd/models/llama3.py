@@ -110,10 +110,9 @@ class LlamaBlock(nn.Module):
             H, KV = c.n_heads, c.n_kv_heads
             x4 = qkv.view(B, T, H + 2 * KV, hd)
             cos, sin = RopeCache.get(pos.max_len, hd, c.rope_theta, qkv.device, c.ref_freqs)
-            _ext.ops().rope_(x4, cos, sin, pos.positions, H + KV, 0, 0, False)
             kc, vc = kv_cache
-            kc.index_copy_(1, pos.index, x4[:, :, H:H + KV])
-            vc.index_copy_(1, pos.index, x4[:, :, H + KV:])
+            # one launch: RoPE on q (in place) and k, k/v rows into the cache at pos.index
+            _ext.ops().rope_kv_write_(x4, cos, sin, pos.positions, pos.index, kc, vc, H, KV)
             o = decode_attention(x4[:, :, :H], kc, vc, causal=True, kv_len=pos.kv_len)
             return linear(o.reshape(B, T, H * hd), self.wo)
         if kv_cache is None:

@@ -7,10 +7,17 @@ no per-parameter grad allocation and no extra accumulate pass.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..utils.grad import commit
+from . import _ext
 from .layout import wgrad
+
+# decode-time products with <= 4 token rows go to the GEMV kernel; SPA_GEMV=0 -> torch.mm
+GEMV = os.environ.get("SPA_GEMV", "1") != "0"
+GEMV_MAX_ROWS = 4
 
 
 class _LinearFn(torch.autograd.Function):
@@ -59,7 +66,26 @@ class _LinearFn(torch.autograd.Function):
         return dx, gw, gb
 
 
+def _gemv_ok(x, w, b) -> bool:
+    """Decode-shaped inference product (<= GEMV_MAX_ROWS token rows, no autograd): routed to
+    the weight-streaming GEMV kernel (csrc/kernels/gemv.hip) instead of a library GEMM."""
+    if not (GEMV and b is None and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
+        return False
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    return (1 <= rows <= GEMV_MAX_ROWS and K % 8 == 0 and w.dim() == 2 and w.stride(1) == 1
+            and w.stride(0) % 8 == 0 and w.data_ptr() % 16 == 0 and x.stride(-1) == 1
+            and x.data_ptr() % 16 == 0)
+
+
 def linear(x, w, b=None):
+    if _gemv_ok(x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.stride(0) % 8:
+            x2 = x2.contiguous()
+        return _ext.ops().gemv(x2, w).view(*x.shape[:-1], w.shape[0])
     return _LinearFn.apply(x, w, b)
 
 
