@@ -12,11 +12,15 @@
 //   Lanes: hd / 4 lanes per key (4 bf16 of the head dim each: one 8-byte load per lane per
 //   key row, 64 / (hd/4) keys per wave step). Each lane group keeps its own online-softmax
 //   state (m, l, o[4]) per row; groups are merged with v_permlane32_swap / LDS at the end.
-//   The split's (m, l, o) go to fp32 partials; attn_decode_combine merges the splits and
-//   writes bf16 out + lse.
+//   The split's (m, l, o) go to fp32 partials; attn_decode_combine_kernel merges the splits
+//   and writes bf16 out + lse (an in-launch merge by the last-arriving split block is kept
+//   behind SPA_DECODE_FUSED=1: its cross-XCD release/acquire fences measured slower).
 // Causal: query row t sits at position Tk - Tq + t (the cache holds the prefix plus the new
 // tokens); keys beyond a row's position are masked.
 #include "spa_common.h"
+
+#include <map>
+#include <mutex>
 
 namespace spa {
 
@@ -25,6 +29,7 @@ struct DecodeParams {
   float* opart; float* mpart; float* lpart;  // [nsplit][B][Tq][H][hd], [nsplit][B][Tq][H]
   bf16* out; float* lse;
   const int* kv_len;  // optional device-side cache length (HIP-graph replay); else Tk
+  int* arrivals;      // [B * Hkv] split-arrival counters (zero between launches)
   int B, Tq, Tk, H, Hkv, nsplit, chunk;
   long sqb, sqt, sqh, skb, skt, skh, svb, svt, svh, sob, sot, soh;
   float scale_log2;
@@ -36,7 +41,7 @@ constexpr int kKeysPerLoad = 8;
 // keys one 4-wave block covers per load batch: 4 waves x (64 / (hd / 4)) lane groups x 8
 constexpr int keys_per_batch(int hd) { return 4 * (256 / hd) * kKeysPerLoad; }
 
-template <int HD, int R>
+template <int HD, int R, bool FUSED>
 __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeParams p) {
   constexpr int KL = HD / 4;        // lanes per key
   constexpr int KPW = 64 / KL;      // keys per wave step
@@ -165,35 +170,119 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeParams p) {
     *reinterpret_cast<f32x4*>(p.opart + row * HD + 4 * s4) = w4;
     if (s4 == 0) { p.mpart[row] = mn; p.lpart[row] = lt; }
   }
+  if constexpr (!FUSED) return;  // attn_decode_combine_kernel merges the splits
+  // Split-K fix-up in the same launch: the last of the nsplit blocks of this (b, kv head) to
+  // arrive merges every split's partials (saves the separate combine launch, which measured
+  // 10.4 us per layer at a 1K cache -- a latency chain over the splits with 4 blocks in flight).
+  // Release (L2 write-back only) by every wave after its partial stores, before the arrival
+  // counter moves; acquire (L2 invalidate only) in the last block before it reads partials
+  // written through other XCDs' L2s. Measured (LLaMA3-8B graph decode, B=1, same box):
+  // 252 tok/s fused vs 278 with the separate combine launch -- the L2 write-back / invalidate
+  // cost more than the launch it saves; hence off by default.
+  __shared__ int last;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = atomicAdd(p.arrivals + bh, 1);
+    last = old == p.nsplit - 1;
+    if (last) p.arrivals[bh] = 0;  // every split has arrived: re-arm for the next launch
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const long nrows = (long)p.B * p.Tq * p.H;
+  for (int i = tid; i < rows * KL; i += 256) {
+    const int r = i / KL, s4 = i % KL;
+    const int t = r / G, hq = hk * G + r % G;
+    const long row = ((long)b * p.Tq + t) * p.H + hq;
+    float mn = -INFINITY;
+    for (int s = 0; s < p.nsplit; ++s) mn = fmaxf(mn, __builtin_nontemporal_load(p.mpart + s * nrows + row));
+    float lt = 0.f, ot[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < p.nsplit; ++s) {
+      const float ms = __builtin_nontemporal_load(p.mpart + s * nrows + row);
+      const float a = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - mn);
+      lt += __builtin_nontemporal_load(p.lpart + s * nrows + row) * a;
+      const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.opart + (s * nrows + row) * HD + 4 * s4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ot[j] += x[j] * a;
+    }
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16x4 w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = (bf16)(ot[j] * inv);
+    *reinterpret_cast<bf16x4*>(p.out + b * p.sob + t * p.sot + hq * p.soh + 4 * s4) = w;
+    if (s4 == 0)
+      p.lse[((long)b * p.H + hq) * p.Tq + t] = lt > 0.f ? (mn + __log2f(lt)) * 0.69314718055994531f : INFINITY;
+  }
 }
 
-// merge the splits of one (b, t, h) row: thread -> 4 elements of hd
+// Split merge, one block per (b, t, h) row: the block max of the split maxima first, then each
+// of the 4 waves folds every 4th split (hd spread over the lanes, 4 splits' loads in flight),
+// and the waves are summed through LDS. The latency chain is ~nsplit / 16 round trips; the
+// first version (one thread per 4 outputs, all splits in sequence) measured 10.4 us per layer
+// at 17 splits.
 template <int HD>
 __global__ __launch_bounds__(256) void attn_decode_combine_kernel(DecodeParams p) {
-  constexpr int TPR = HD / 4;
+  constexpr int E = HD / 64;  // outputs per lane
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long nrows = (long)p.B * p.Tq * p.H;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nrows * TPR) return;
-  const long row = i / TPR;
-  const int s4 = i % TPR;
-  float mn = -INFINITY;
-  for (int s = 0; s < p.nsplit; ++s) mn = fmaxf(mn, p.mpart[s * nrows + row]);
-  float lt = 0.f, ot[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < p.nsplit; ++s) {
-    const float ms = p.mpart[s * nrows + row];
-    const float a = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - mn);
-    lt += p.lpart[s * nrows + row] * a;
-    const f32x4 x = *reinterpret_cast<const f32x4*>(p.opart + (s * nrows + row) * HD + 4 * s4);
+  const long row = blockIdx.x;
+  __shared__ float red[4];
+  __shared__ float sacc[4][HD + 1];
+  float mx = -INFINITY;
+  for (int s = tid; s < p.nsplit; s += 256) mx = fmaxf(mx, p.mpart[s * nrows + row]);
+  mx = block_max<256>(mx, red);
+  float lt = 0.f, acc[E];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ot[j] += x[j] * a;
+  for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  if (mx != -INFINITY) {
+#pragma unroll 4
+    for (int s = wave; s < p.nsplit; s += 4) {
+      const float ms = p.mpart[s * nrows + row];
+      const float a = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - mx);
+      lt += p.lpart[s * nrows + row] * a;
+      const float* src = p.opart + (s * nrows + row) * HD + lane * E;
+      if constexpr (E == 1) {
+        acc[0] += src[0] * a;
+      } else if constexpr (E == 2) {
+        const f32x2 x = *reinterpret_cast<const f32x2*>(src);
+        acc[0] += x[0] * a; acc[1] += x[1] * a;
+      } else {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += x[e] * a;
+      }
+    }
   }
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  const long h = row % p.H, t = (row / p.H) % p.Tq, b = row / ((long)p.H * p.Tq);
-  bf16x4 w;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) w[j] = (bf16)(ot[j] * inv);
-  *reinterpret_cast<bf16x4*>(p.out + b * p.sob + t * p.sot + h * p.soh + 4 * s4) = w;
-  if (s4 == 0) p.lse[(b * p.H + h) * p.Tq + t] = lt > 0.f ? (mn + __log2f(lt)) * 0.69314718055994531f : INFINITY;
+  for (int e = 0; e < E; ++e) sacc[wave][lane * E + e] = acc[e];
+  if (lane == 0) sacc[wave][HD] = lt;
+  __syncthreads();
+  if (wave != 0) return;
+  const float L = sacc[0][HD] + sacc[1][HD] + sacc[2][HD] + sacc[3][HD];
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const long h = row % p.H, t = (row / p.H) % p.Tq, b = row / ((long)p.H * p.Tq);
+  bf16* dst = p.out + b * p.sob + t * p.sot + h * p.soh + lane * E;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int d = lane * E + e;
+    dst[e] = (bf16)((sacc[0][d] + sacc[1][d] + sacc[2][d] + sacc[3][d]) * inv);
+  }
+  if (lane == 0) p.lse[(b * p.H + h) * p.Tq + t] = L > 0.f ? (mx + __log2f(L)) * 0.69314718055994531f : INFINITY;
+}
+
+// Split-arrival counters, one set per (device, stream): zeroed once, left at zero by every
+// launch (the last block of each kv group re-arms its counter), so no per-call memset and a
+// captured hipGraph can replay the kernel as is. Launches on one stream are serialised, so
+// they never share a counter concurrently.
+static int* arrival_counters(const at::Tensor& like, hipStream_t st, int n) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, at::Tensor> bufs;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& t = bufs[{like.get_device(), st}];
+  if (!t.defined() || t.numel() < n)
+    t = at::zeros({std::max(n, 4096)}, like.options().dtype(at::kInt));
+  return t.data_ptr<int>();
 }
 
 // q [B, Tq, H, hd] (Tq * H / Hkv <= 16), k/v [B, Tk, Hkv, hd] strided (cache views); with
@@ -252,20 +341,31 @@ std::vector<at::Tensor> attn_decode(const at::Tensor& q, const at::Tensor& k, co
     p.kv_len = kv_len->data_ptr<int>();
   }
   auto st = stream();
+  const char* env = getenv("SPA_DECODE_FUSED");
+  const bool fused = env ? atoi(env) != 0 : false;  // in-launch merge measured slower (see kernel)
+  if (fused) p.arrivals = arrival_counters(q, st, B * Hkv);
   const dim3 grid(B * Hkv, nsplit);
-  const long nthr = (long)B * Tq * H * (HD / 4);
+  const int nrows = B * Tq * H;
+#define SPA_DECODE_ROWS(HDV, F)                                                                    \
+  {                                                                                                \
+    if (rows <= 4) attn_decode_kernel<HDV, 4, F><<<grid, 256, 0, st>>>(p);                         \
+    else if (rows <= 8) attn_decode_kernel<HDV, 8, F><<<grid, 256, 0, st>>>(p);                    \
+    else attn_decode_kernel<HDV, 16, F><<<grid, 256, 0, st>>>(p);                                  \
+  }
 #define SPA_DECODE_LAUNCH(HDV)                                                                      \
   {                                                                                                \
-    if (rows <= 4) attn_decode_kernel<HDV, 4><<<grid, 256, 0, st>>>(p);                            \
-    else if (rows <= 8) attn_decode_kernel<HDV, 8><<<grid, 256, 0, st>>>(p);                       \
-    else attn_decode_kernel<HDV, 16><<<grid, 256, 0, st>>>(p);                                     \
-    attn_decode_combine_kernel<HDV><<<(int)((nthr + 255) / 256), 256, 0, st>>>(p);                  \
+    if (fused) SPA_DECODE_ROWS(HDV, true)                                                          \
+    else {                                                                                         \
+      SPA_DECODE_ROWS(HDV, false)                                                                  \
+      attn_decode_combine_kernel<HDV><<<nrows, 256, 0, st>>>(p);                \
+    }                                                                                              \
   }
   if (HD == 64) SPA_DECODE_LAUNCH(64)
   else if (HD == 128) SPA_DECODE_LAUNCH(128)
   else if (HD == 256) SPA_DECODE_LAUNCH(256)
   else TORCH_CHECK(false, "attn_decode: head dim must be 64, 128 or 256");
 #undef SPA_DECODE_LAUNCH
+#undef SPA_DECODE_ROWS
   SPA_LAUNCH_CHECK();
   return {out, lse};
 }

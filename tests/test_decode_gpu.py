@@ -42,6 +42,23 @@ def test_decode_attention_matches_oracle(B, Tq, Tk, H, Hkv, hd, ns):
     assert (lse - lf).abs().max().item() < 1e-2
 
 
+def test_decode_attention_repeated_launches_rearm_split_counters():
+    """The in-launch split combine relies on per-(b, kv head) arrival counters that every
+    launch must leave at zero: back-to-back launches with different split counts and grids
+    (and a device kv_len that leaves trailing splits empty) must all match the oracle."""
+    torch.manual_seed(1)
+    sc = 1 / math.sqrt(128)
+    for it, (B, Tk, ns) in enumerate([(1, 2000, 0), (2, 2000, 5), (1, 2000, 31), (2, 700, 0), (1, 2000, 0)]):
+        q = torch.randn(B, 1, 32, 128, device=DEV, dtype=torch.bfloat16)
+        k = torch.randn(B, Tk, 8, 128, device=DEV, dtype=torch.bfloat16)
+        v = torch.randn(B, Tk, 8, 128, device=DEV, dtype=torch.bfloat16)
+        n = Tk - 300 * (it % 2)
+        kv_len = torch.tensor([n], device=DEV, dtype=torch.int32)
+        out, _ = _ext.ops().attn_decode(q, k, v, sc, True, ns, kv_len)
+        of, _ = R.attention(q.float(), k[:, :n].float(), v[:, :n].float(), True, sc)
+        assert rel(out, of) < 1e-2, (it, rel(out, of))
+
+
 def test_decode_attention_routes_prefill_to_flash():
     from solvingpapers_amd.ops import decode_attention, flash_attention
     q = torch.randn(1, 64, 8, 128, device=DEV, dtype=torch.bfloat16)  # 64 * 4 rows > 16 -> flash
