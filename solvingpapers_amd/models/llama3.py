@@ -239,8 +239,9 @@ class Llama3(nn.Module):
 
     def step_graph(self, ids, cache, state: DecodeState):
         """One-token decode step with every position on the device (HIP-graph capturable;
-        infer/graph.py): cache rows are written with index_copy_, RoPE reads device
-        positions, the decode kernel reads the cache length from ``state.kv_len``."""
+        infer/graph.py): one fused launch rotates q/k and writes the cache row at
+        ``state.index``, RoPE reads device positions, the decode kernel reads the cache
+        length from ``state.kv_len``."""
         n = self.hidden(ids, cache, state)
         return self.logits(n).float()[:, -1]
 
