@@ -118,11 +118,13 @@ void rope_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, co
   SPA_LAUNCH_CHECK();
 }
 
-// Decode-step prologue in one launch (interleaved RoPE, MODE 0): for a packed qkv buffer
-// [B, T, H + 2 Hkv, hd], rotate the q heads in place, rotate the k heads into the KV cache and
-// copy the v heads into it, at cache row *index + t. The row and the RoPE positions are read
-// from device memory, so a captured hipGraph replays it at every position (replaces rope_ +
-// two index_copy_ launches per layer). Rows past the cache end are dropped.
+// Decode-step prologue in one launch: for a packed qkv buffer [B, T, H + 2 Hkv, hd], rotate
+// the q heads in place, rotate the k heads into the KV cache and copy the v heads into it, at
+// cache row *index + t. MODE 0: interleaved pairs (LLaMA), MODE 1: rotate_half (Gemma). The
+// row and the RoPE positions are read from device memory, so a captured hipGraph replays it
+// at every position (replaces rope_ + two index_copy_ launches per layer). Rows past the
+// cache end are dropped.
+template <int MODE>
 __global__ __launch_bounds__(256) void rope_kv_write_kernel(bf16* __restrict__ x, const float* __restrict__ cosT,
                                                             const float* __restrict__ sinT,
                                                             const int* __restrict__ pos,
@@ -142,28 +144,54 @@ __global__ __launch_bounds__(256) void rope_kv_write_kernel(bf16* __restrict__ x
     r /= NH;
     const int t = r % T;
     const int b = r / T;
+    const long row = row0 + t;
+    if (hh >= H && row >= Tmax) continue;
+    const bf16* src = x + b * sb + t * st + hh * sh;
+    bf16* dst = hh < H ? x + b * sb + t * st + hh * sh
+                       : (hh < H + Hkv ? kc + b * kcb + row * kct + (hh - H) * kch
+                                       : vc + b * vcb + row * vct + (hh - H - Hkv) * vch);
     float a[8];
-    load8(x + b * sb + t * st + hh * sh + v * 8, a);
-    if (hh < H + Hkv) {
-      const int ps = pos[b * T + t];
-      const f32x4 cv = *reinterpret_cast<const f32x4*>(cosT + (long)ps * (hd / 2) + v * 4);
-      const f32x4 sv = *reinterpret_cast<const f32x4*>(sinT + (long)ps * (hd / 2) + v * 4);
+    if (hh >= H + Hkv) {  // v: plain copy into the cache
+      load8(src + v * 8, a);
+      store8(dst + v * 8, a);
+      continue;
+    }
+    const int ps = pos[b * T + t];
+    const float* c = cosT + (long)ps * (hd / 2);
+    const float* s = sinT + (long)ps * (hd / 2);
+    if constexpr (MODE == 0) {
+      load8(src + v * 8, a);
+      const f32x4 cv = *reinterpret_cast<const f32x4*>(c + v * 4);
+      const f32x4 sv = *reinterpret_cast<const f32x4*>(s + v * 4);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float x0 = a[2 * k], x1 = a[2 * k + 1];
         a[2 * k] = x0 * cv[k] - x1 * sv[k];
         a[2 * k + 1] = x0 * sv[k] + x1 * cv[k];
       }
+      store8(dst + v * 8, a);
+    } else {  // rotate_half: thread v < vpr/2 owns elements [8v, 8v+8) and their partners at +hd/2
+      if (v >= vpr / 2) continue;
+      float bq[8], cv[8], sv[8];
+      load8(src + v * 8, a);
+      load8(src + hd / 2 + v * 8, bq);
+      load8(c + v * 8, cv);
+      load8(s + v * 8, sv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float x0 = a[k], x1 = bq[k];
+        a[k] = x0 * cv[k] - x1 * sv[k];
+        bq[k] = x0 * sv[k] + x1 * cv[k];
+      }
+      store8(dst + v * 8, a);
+      store8(dst + hd / 2 + v * 8, bq);
     }
-    const long row = row0 + t;
-    if (hh < H) store8(x + b * sb + t * st + hh * sh + v * 8, a);
-    else if (row < Tmax && hh < H + Hkv) store8(kc + b * kcb + row * kct + (hh - H) * kch + v * 8, a);
-    else if (row < Tmax) store8(vc + b * vcb + row * vct + (hh - H - Hkv) * vch + v * 8, a);
   }
 }
 
 void rope_kv_write_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const at::Tensor& pos,
-                    const at::Tensor& index, const at::Tensor& kc, const at::Tensor& vc, int64_t H, int64_t Hkv) {
+                    const at::Tensor& index, const at::Tensor& kc, const at::Tensor& vc, int64_t H, int64_t Hkv,
+                    int64_t mode) {
   for (auto* t : {&x, &kc, &vc}) {
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 4 && t->stride(3) == 1,
                 "rope_kv_write: bf16 [B, T, heads, hd] tensors with contiguous hd");
@@ -182,15 +210,21 @@ void rope_kv_write_(const at::Tensor& x, const at::Tensor& cos, const at::Tensor
               "rope_kv_write: pos must be device int32 [B, T]");
   TORCH_CHECK(index.is_cuda() && index.scalar_type() == at::kLong && index.numel() >= 1,
               "rope_kv_write: index must be a device int64 tensor");
+  TORCH_CHECK(mode == 0 || mode == 1, "rope_kv_write: mode 0 (interleaved) or 1 (rotate_half)");
   DeviceGuard g(x.device());
   const long total = (long)B * T * (H + 2 * Hkv) * (hd / 8);
   if (total == 0) return;
   const int grid = (int)std::min<long>((total + 255) / 256, 4096);
-  rope_kv_write_kernel<<<grid, 256, 0, stream()>>>(
-      (bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(),
-      index.data_ptr<int64_t>(), (bf16*)kc.data_ptr(), (bf16*)vc.data_ptr(), x.stride(0), x.stride(1), x.stride(2),
-      kc.stride(0), kc.stride(1), kc.stride(2), vc.stride(0), vc.stride(1), vc.stride(2), B, T, (int)H, (int)Hkv, hd,
-      (int)kc.size(1));
+  auto launch = [&](auto modec) {
+    constexpr int M = decltype(modec)::value;
+    rope_kv_write_kernel<M><<<grid, 256, 0, stream()>>>(
+        (bf16*)x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(),
+        index.data_ptr<int64_t>(), (bf16*)kc.data_ptr(), (bf16*)vc.data_ptr(), x.stride(0), x.stride(1),
+        x.stride(2), kc.stride(0), kc.stride(1), kc.stride(2), vc.stride(0), vc.stride(1), vc.stride(2), B, T,
+        (int)H, (int)Hkv, hd, (int)kc.size(1));
+  };
+  if (mode == 0) launch(std::integral_constant<int, 0>{});
+  else launch(std::integral_constant<int, 1>{});
   SPA_LAUNCH_CHECK();
 }
 
@@ -200,7 +234,7 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int nrot, int pos_off, int mode, "
         "bool inverse) -> ()");
   m.def("rope_kv_write_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor pos, Tensor index, Tensor(b!) kc, "
-        "Tensor(c!) vc, int n_heads, int n_kv_heads) -> ()");
+        "Tensor(c!) vc, int n_heads, int n_kv_heads, int mode=0) -> ()");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("rope_", &spa::rope_);

@@ -25,10 +25,11 @@ import torch
 import torch.nn as tnn
 
 from .. import nn as snn
-from ..ops import attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
+from ..infer.graph import DecodeState
+from ..ops import _ext, attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
 from ..ops.attention import decode_attention, flash_attention
 from ..ops.misc import dropout
-from ..ops.rope import gemma_ref_rotate
+from ..ops.rope import RopeCache, gemma_ref_rotate
 from ..utils.grad import mark_ready
 
 
@@ -218,6 +219,17 @@ class GemmaBlock(tnn.Module):
             kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)          # replicated K/V, grads summed over TP
         B, T = q.shape[0], q.shape[1]
         qkv = torch.cat([q, kv], dim=-1)
+        if isinstance(pos, DecodeState):  # graph-capturable decode step: positions on the device
+            x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
+            cos, sin = RopeCache.get(pos.max_len, hd, c.rope_theta, qkv.device)
+            kc, vc = cache
+            # one launch: rotate_half RoPE on q (in place) and k, k/v rows into the cache
+            _ext.ops().rope_kv_write_(x4, cos, sin, pos.positions, pos.index, kc, vc, self.hl, KV, 1)
+            o = decode_attention(x4[:, :, :self.hl], kc, vc, causal=True, kv_len=pos.kv_len)
+            a = reduce_from_tp(linear(o.reshape(B, T, self.hl * hd), self.wo), tp_group)
+            n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
+            f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
+            return h2, reduce_from_tp(linear(f, self.w2), tp_group)
         qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, pos, interleaved=False, head_dim=hd)
         if cache is None:
             o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
@@ -308,6 +320,15 @@ class Gemma(tnn.Module):
         from ..parallel.tensor_parallel import gather_vocab_logits
         n = self.hidden(ids, cache, pos)
         return gather_vocab_logits(linear(n[:, -1:], self.embed), self.tp_group).float()[:, -1]
+
+    def step_graph(self, ids, cache, state):
+        """One-token decode step with every position on the device (HIP-graph capturable,
+        infer/graph.py): fused rotate_half RoPE + cache write at ``state.index``, MQA decode
+        kernel over ``state.kv_len`` rows. Single TP rank (a captured step holds no collectives)."""
+        if self.tp != 1:
+            raise NotImplementedError("graph decode runs on one TP rank; use step() under tensor parallelism")
+        n = self.hidden(ids, cache, state)
+        return linear(n, self.embed).float()[:, -1]
 
     @torch.no_grad()
     def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None,

@@ -112,7 +112,7 @@ class LlamaBlock(nn.Module):
             cos, sin = RopeCache.get(pos.max_len, hd, c.rope_theta, qkv.device, c.ref_freqs)
             kc, vc = kv_cache
             # one launch: RoPE on q (in place) and k, k/v rows into the cache at pos.index
-            _ext.ops().rope_kv_write_(x4, cos, sin, pos.positions, pos.index, kc, vc, H, KV)
+            _ext.ops().rope_kv_write_(x4, cos, sin, pos.positions, pos.index, kc, vc, H, KV, 0)
             o = decode_attention(x4[:, :, :H], kc, vc, causal=True, kv_len=pos.kv_len)
             return linear(o.reshape(B, T, H * hd), self.wo)
         if kv_cache is None:

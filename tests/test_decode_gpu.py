@@ -43,9 +43,9 @@ def test_decode_attention_matches_oracle(B, Tq, Tk, H, Hkv, hd, ns):
 
 
 def test_decode_attention_repeated_launches_rearm_split_counters():
-    """The in-launch split combine relies on per-(b, kv head) arrival counters that every
-    launch must leave at zero: back-to-back launches with different split counts and grids
-    (and a device kv_len that leaves trailing splits empty) must all match the oracle."""
+    """Back-to-back launches with different split counts and grids, and a device kv_len that
+    leaves trailing splits empty, must all match the oracle (with SPA_DECODE_FUSED=1 this also
+    checks that every launch re-arms the per-(b, kv head) arrival counters)."""
     torch.manual_seed(1)
     sc = 1 / math.sqrt(128)
     for it, (B, Tk, ns) in enumerate([(1, 2000, 0), (2, 2000, 5), (1, 2000, 31), (2, 700, 0), (1, 2000, 0)]):
@@ -96,7 +96,7 @@ def test_gemma_mqa_cached_steps_match_full_forward():
 
 
 def test_graph_decoder_matches_eager_logits():
-    """HIP-graph decode (device-side positions, index_copy_ cache writes, kv_len decode
+    """HIP-graph decode (device-side positions, fused RoPE + KV cache write, kv_len decode
     kernel, state advanced inside the graph) == full forward, teacher-forced."""
     from solvingpapers_amd.infer import GraphDecoder
     from solvingpapers_amd.models import llama3
@@ -116,3 +116,23 @@ def test_graph_decoder_matches_eager_logits():
     out = dec.generate(ids[:, :10], 6)
     ref = m.generate(ids[:, :10], 6, greedy=True)
     assert out.shape == ref.shape and torch.equal(out[:, :11], ref[:, :11])
+
+
+def test_gemma_graph_decoder_matches_full_forward():
+    """MQA graph decode: rotate_half RoPE + cache write fused, hd 64 decode kernel, == the
+    full forward teacher-forced."""
+    from solvingpapers_amd.infer import GraphDecoder
+    from solvingpapers_amd.models import gemma
+    torch.manual_seed(0)
+    m = gemma.Gemma(gemma.config("gemma_tiny"), device=DEV, dtype=torch.bfloat16).eval()
+    ids = torch.randint(0, m.c.vocab_size, (2, 30), device=DEV)
+    with torch.no_grad():
+        full = m(ids).float()
+        dec = GraphDecoder(m, 2, 40)
+        lg = [dec.prefill(ids[:, :20])]
+        for t in range(20, 30):
+            dec.ids.copy_(ids[:, t:t + 1])
+            dec.graph.replay()
+            lg.append(dec.logits.clone())
+    assert rel(lg[0], full[:, 19]) < 2e-2
+    assert rel(torch.stack(lg[1:], 1), full[:, 20:30]) < 2e-2

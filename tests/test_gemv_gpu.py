@@ -80,3 +80,22 @@ def test_rope_kv_write_matches_unfused():
     k0, v0 = kc.clone(), vc.clone()
     _ext.ops().rope_kv_write_(x, cos, sin, positions, torch.tensor([Tmax], device=DEV), kc, vc, H, KV)
     assert torch.equal(kc, k0) and torch.equal(vc, v0)
+
+
+def test_rope_kv_write_rotate_half_matches_unfused():
+    from solvingpapers_amd.ops.rope import RopeCache
+    torch.manual_seed(4)
+    B, T, H, KV, hd, Tmax = 1, 1, 16, 1, 256, 24
+    x = torch.randn(B, T, H + 2 * KV, hd, device=DEV, dtype=torch.bfloat16)
+    cos, sin = RopeCache.get(Tmax, hd, 10000.0, x.device)
+    index = torch.tensor([5], device=DEV, dtype=torch.long)
+    positions = torch.full((B, T), 5, device=DEV, dtype=torch.int32)
+    kc = torch.zeros(B, Tmax, KV, hd, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros(B, Tmax, KV, hd, device=DEV, dtype=torch.bfloat16)
+    xr, kr, vr = x.clone(), kc.clone(), vc.clone()
+    _ext.ops().rope_(xr, cos, sin, positions, H + KV, 0, 1, False)
+    kr.index_copy_(1, index, xr[:, :, H:H + KV])
+    vr.index_copy_(1, index, xr[:, :, H + KV:])
+    _ext.ops().rope_kv_write_(x, cos, sin, positions, index, kc, vc, H, KV, 1)
+    assert torch.equal(x[:, :, :H], xr[:, :, :H])
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)

@@ -14,3 +14,7 @@ timeout -k 10 300 python bench/vit_train.py > gpurun_out/vit.log 2>&1 || echo "v
 grep -o '"metric": "[^"]*"\|"value": [0-9.]*' gpurun_out/vit.log | tr '\n' ' '; echo
 timeout -k 10 300 python bench/gemma_tp.py --layers 4 --seq 4096 > gpurun_out/gemma.log 2>&1 || echo "gemma FAILED"
 grep -o '"metric": "[^"]*"\|"value": [0-9.]*' gpurun_out/gemma.log | tr '\n' ' '; echo
+timeout -k 10 300 python bench/decode.py --prompt 1024 --new 128 --graph > gpurun_out/decode_llama.log 2>&1 || echo "llama decode FAILED"
+grep -o '"decode_tok_s": [0-9.]*' gpurun_out/decode_llama.log
+timeout -k 10 300 python bench/decode.py --model gemma_7b_mqa --prompt 1024 --new 128 --graph > gpurun_out/decode_gemma.log 2>&1 || echo "gemma decode FAILED"
+grep -o '"decode_tok_s": [0-9.]*' gpurun_out/decode_gemma.log
