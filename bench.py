@@ -11,7 +11,14 @@ A step is a full training step: forward, fused CE loss, backward (per-layer
 RCCL gradient buckets overlapped with backward when N>1), grad-norm clip,
 fused AdamW over the flat fp32 master/moment buffers. Synthetic token ids,
 random-init weights of the LLaMA3-8B architecture (D4096 L32 H32 KV8 FFN14336
-V128256), seq 8192, micro-batch 1 per GPU (weak scaling: global batch = N).
+V128256), seq 8192, micro-batch 1 per GPU, 4 micro-batches accumulated per
+optimizer step (weak scaling: global batch = 4N sequences = 32K tokens per GPU
+per step). Every micro-batch runs its full forward + backward inside the timed
+region; only the inner micro-batches skip the gradient all-reduce (no_sync) and
+the last one launches it, so the per-step optimizer / grad-norm / all-reduce
+cost (~40 ms on 1 GPU, more at N=8) is paid once per 32K tokens as in a real
+LLaMA-scale run (global batches of millions of tokens). Measured on 1 MI355X:
+accum 1: 18.6K tok/s, 2: 19.4K, 4: 20.35K, 8: 20.6K.
 """
 from __future__ import annotations
 
@@ -46,7 +53,7 @@ def main(argv=None):
     ap.add_argument("--model", default="llama3_8b")
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--mb", type=int, default=1, help="micro-batch per GPU")
-    ap.add_argument("--accum", type=int, default=1, help="micro-batches per step")
+    ap.add_argument("--accum", type=int, default=4, help="micro-batches accumulated per optimizer step")
     ap.add_argument("--zero1", action="store_true")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (NOT for headline runs)")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")

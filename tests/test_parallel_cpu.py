@@ -6,6 +6,7 @@
   sharded over 2 ranks == the unsharded model (loss and every gradient).
 * EP: expert-parallel MoE (all-to-all dispatch/combine) == local MoE.
 """
+import contextlib
 import os
 import socket
 
@@ -36,7 +37,7 @@ def _llama(seed=0):
     return llama3.Llama3(c, seed=seed)
 
 
-def _dp_worker(rank, world, port, q, zero1):
+def _dp_worker(rank, world, port, q, zero1, accum=1):
     _init(rank, world, port)
     from solvingpapers_amd.parallel.data_parallel import DataParallel
     from solvingpapers_amd.train.optim import FlatAdamW
@@ -51,7 +52,13 @@ def _dp_worker(rank, world, port, q, zero1):
     mine = ids[rank * 2:(rank + 1) * 2]
     for _ in range(2):
         opt.zero_grad()
-        m(mine[:, :-1], mine[:, 1:]).backward()
+        if accum == 1:
+            m(mine[:, :-1], mine[:, 1:]).backward()
+        else:  # one sample per micro-batch; communication only on the last one
+            for i in range(accum):
+                ctx = dp.no_sync() if i < accum - 1 else contextlib.nullcontext()
+                with ctx:
+                    (m(mine[i:i + 1, :-1], mine[i:i + 1, 1:]) / accum).backward()
         dp.finish_grad_sync()
         if zero1:
             grads = None
@@ -102,6 +109,20 @@ def test_dp_grads_and_params_match_single_process():
     for rank, g, p in out:
         g, p = torch.from_numpy(g), torch.from_numpy(p)
         assert torch.allclose(g, ref_g, atol=1e-5, rtol=1e-4), (rank, (g - ref_g).abs().max())
+        assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
+
+
+@pytest.mark.parametrize("zero1", [False, True])
+def test_dp_grad_accumulation_no_sync_matches_single_process(zero1):
+    """bench.py --accum: inner micro-batches skip the bucket all-reduce (no_sync), the last
+    one launches it; the result equals the un-accumulated single-process step."""
+    ref_g, ref_p = _single_reference()
+    out = _run(_dp_worker, 2, zero1, 2)
+    for rank, g, p in out:
+        if g is not None:
+            g = torch.from_numpy(g)
+            assert torch.allclose(g, ref_g, atol=1e-5, rtol=1e-4), (rank, (g - ref_g).abs().max())
+        p = torch.from_numpy(p)
         assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
 
 
