@@ -147,6 +147,7 @@ def main(argv=None):
                 "seq_len": T,
                 "parallelism": f"dp{world}" + ("-zero1" if a.zero1 else ""),
                 "micro_batch": B,
+                "grad_accum": a.accum,
                 "params": model.num_params(),
             },
             "tflops_per_gpu": round(tflops_gpu, 1),

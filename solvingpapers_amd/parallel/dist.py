@@ -39,10 +39,13 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> Di
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if cuda else "gloo"
+        # SPA_DIST_BACKEND=gloo: rehearse the multi-rank paths on a box with fewer GPUs than ranks
+        backend = os.environ.get("SPA_DIST_BACKEND") or ("nccl" if cuda else "gloo")
     if cuda:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        ndev = torch.cuda.device_count()
+        dev_idx = local if (backend == "nccl" or local < ndev) else local % ndev
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
