@@ -12,7 +12,8 @@ from pathlib import Path
 
 import torch
 
-_SO = Path(__file__).resolve().parent.parent / "_C.so"
+# SPA_EXT_SO: load another build of the extension (kernel A/B experiments on one box)
+_SO = Path(os.environ.get("SPA_EXT_SO") or Path(__file__).resolve().parent.parent / "_C.so")
 _loaded = False
 _err: str | None = None
 
