@@ -24,12 +24,21 @@ def main():
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--mb", type=int, default=2)
+    ap.add_argument("--experts", type=int, default=None, help="routed experts (whole job; EP splits them)")
+    ap.add_argument("--dense-layers", type=int, default=None)
+    ap.add_argument("--fp8", action="store_true", help="fp8 (OCP e4m3) routed-expert GEMMs")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
     kw = {"block_size": a.seq}
     if a.layers:
         kw["n_layers"] = a.layers
+    if a.experts:
+        kw["n_experts"] = a.experts
+    if a.dense_layers is not None:
+        kw["n_dense_layers"] = a.dense_layers
+    if a.fp8:
+        kw["moe_fp8"] = True
     c = ds.config(a.preset, **kw)
     ep = torch.distributed.group.WORLD if world > 1 else None
     m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep)
@@ -56,10 +65,11 @@ def main():
     tok_s = world * B * T * a.steps / el
     tf = tok_s * m.flops_per_token(T) / world / 1e12
     report("training tokens/sec, DeepSeek-V3-style MLA+MoE bf16", tok_s, "tokens/s", a.steps, a.warmup, el,
-           {"model": a.preset + (f"-L{a.layers}" if a.layers else ""), "global_batch": world * B, "seq_len": T,
+           {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
+            + ("-fp8" if a.fp8 else ""), "global_batch": world * B, "seq_len": T,
             "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu", "params": m.num_params(),
             "active_params": m.num_params(active=True)},
-           tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0]), 4))
+           tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4))
     sdist.cleanup()
 
 

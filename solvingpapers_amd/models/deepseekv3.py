@@ -40,7 +40,7 @@ import torch.distributed as dist
 import torch.nn as tnn
 
 from ..ops import apply_rope, embedding, glu, layer_norm, linear, linear_cross_entropy, rms_norm
-from ..ops.attention import FLASH_HD, attention_dropout, flash_attention
+from ..ops.attention import attention_dropout, flash_attention
 from ..ops.misc import dropout
 from ..ops.moe import route
 from ..utils.grad import mark_ready
@@ -124,6 +124,16 @@ PRESETS = {
                              n_dense_layers=1, dense_hidden=10944, pos_emb="none", bias_in_weights=False,
                              balance_stat="counts", final_scale=False, norm_eps=1e-6, dropout=0.0,
                              attn_dropout=0.0, mtp_heads=1, batch_size=1),
+    # DeepSeek-V3 (arXiv 2412.19437) widths: D7168, 128 heads, q_lora 1536, kv_lora 512,
+    # qk 128 nope + 64 rope = 192 and v 128 (flash kernel via zero-padding to 256), 256 routed
+    # experts top-8 + 1 shared of hidden 2048, 3 dense layers of 18432, V 129280. 61 layers is
+    # the model card; benches override depth and (for 1 GPU) the expert count.
+    "dsv3_v3": DSV3Config(vocab_size=129280, block_size=4096, dim=7168, n_layers=61, n_heads=128,
+                          attention="mla", q_lora_rank=1536, kv_lora_rank=512, qk_nope_dim=128,
+                          qk_rope_dim=64, v_head_dim=128, n_experts=256, top_k=8, n_shared=1,
+                          expert_hidden=2048, n_dense_layers=3, dense_hidden=18432, pos_emb="none",
+                          bias_in_weights=False, balance_stat="counts", final_scale=False, norm_eps=1e-6,
+                          dropout=0.0, attn_dropout=0.0, mtp_heads=1, batch_size=1),
 }
 
 
@@ -232,10 +242,8 @@ class MLA(tnn.Module):
         qf = torch.cat([q[..., :dn], qr], dim=-1)
         k = torch.cat([kv[..., :dn], kr.expand(B, T, H, dr)], dim=-1)
         v = kv[..., dn:]
-        if dv == dn + dr and dv in FLASH_HD:
-            o = flash_attention(qf, k, v.contiguous(), causal=True, scale=scale)
-        else:
-            o = attention_dropout(qf, k, v, causal=True, scale=scale, p=0.0)
+        # dv == dn + dr runs the flash kernel directly; V3's 192/128 heads are zero-padded onto it
+        o = flash_attention(qf, k, v.contiguous() if dv == dn + dr else v, causal=True, scale=scale)
         return linear(o.reshape(B, T, H * dv), self.wo)
 
     def _decode(self, qn, qr, ckv, kr, cache, pos, scale):

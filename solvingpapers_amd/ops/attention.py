@@ -3,8 +3,9 @@
 Tensors are [B, T, H, hd] views (hd contiguous); the kernels take (b, t, h)
 strides, so q/k/v may be slices of one packed qkv projection output and the
 gradients can be written into slices of one dqkv buffer (``attention_packed``).
-Head dims 64/128/256 run the MFMA flash kernel; other head dims fall back to a
-materialised GEMM + softmax path (used only by reference-parity presets such
+Head dims 64/128/256 run the MFMA flash kernel; other q/k and v head dims up to
+256 (DeepSeek-V3 MLA's 192/128) are zero-padded onto it; wider heads fall back to
+a materialised GEMM + softmax path (used only by reference-parity presets such
 as Gemma-ref's 768-wide heads).
 """
 from __future__ import annotations
@@ -86,11 +87,31 @@ def _materialised(q, k, v, causal, scale):
     return torch.matmul(p, vh).transpose(1, 2)
 
 
+def _flash_pad_dim(dqk, dv):
+    """Smallest flash head dim that holds both the q/k and the v head dim (None: none does)."""
+    return next((h for h in FLASH_HD if h >= max(dqk, dv)), None)
+
+
+def _pad_last(x, n):
+    return x if x.shape[-1] == n else torch.nn.functional.pad(x, (0, n - x.shape[-1]))
+
+
 def flash_attention(q, k, v, causal=True, scale=None):
-    """softmax(q k^T * scale [+causal]) v.  q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd]."""
+    """softmax(q k^T * scale [+causal]) v.  q/k [B,T,H(kv),dqk], v [B,Tk,Hkv,dv].
+
+    dqk == dv in FLASH_HD runs the MFMA kernel directly. Other head dims up to 256
+    (DeepSeek-V3 MLA: dqk = 128 nope + 64 rope = 192, dv = 128) are zero-padded to
+    the next kernel head dim: zero q/k columns leave every score unchanged, zero v
+    columns give zero output columns that are sliced off, and the pad's backward
+    slices the gradients. O(T) memory instead of the materialised O(T^2) path."""
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    if _flash_ok(q):
+    if _flash_ok(q) and v.shape[-1] == q.shape[-1]:
         return _FlashFn.apply(q, k, v, causal, scale)
+    if q.is_cuda and q.dtype == torch.bfloat16 and q.dim() == 4:
+        P = _flash_pad_dim(q.shape[-1], v.shape[-1])
+        if P is not None:
+            o = _FlashFn.apply(_pad_last(q, P), _pad_last(k, P), _pad_last(v, P), causal, scale)
+            return o[..., :v.shape[-1]]
     if q.is_cuda:
         return _materialised(q, k, v, causal, scale)
     if torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad):
@@ -103,7 +124,7 @@ def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None):
     hd = head_dim if head_dim is not None else qkv.shape[-1]
     B, T = qkv.shape[0], qkv.shape[1]
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
-    if _flash_ok(qkv) and hd in FLASH_HD:
+    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and hd in FLASH_HD:
         return _PackedFn.apply(qkv, H, Hkv, hd, causal, scale)
     x4 = qkv.view(B, T, H + 2 * Hkv, hd)
     q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]

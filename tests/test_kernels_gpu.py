@@ -196,6 +196,27 @@ def test_flash_attention(B, Tq, Tk, H, Hkv, hd, causal):
     assert rel(v.grad, vf.grad) < 3e-2, rel(v.grad, vf.grad)
 
 
+@pytest.mark.parametrize("Hkv,dqk,dv", [(4, 192, 128), (1, 96, 64), (2, 128, 64)])
+def test_flash_attention_mixed_head_dims(Hkv, dqk, dv):
+    """MLA-shaped heads (q/k 128 nope + 64 rope, v 128) zero-padded onto the flash kernel."""
+    from solvingpapers_amd.ops import flash_attention
+    torch.manual_seed(3)
+    B, T, H = 2, 300, 4
+    q = torch.randn(B, T, H, dqk, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, T, Hkv, dqk, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, T, Hkv, dv, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attention(q, k, v, causal=True)
+    assert o.shape == (B, T, H, dv)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qf, kf, vf = (t.detach().float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention(qf, kf, vf, True)
+    of.backward(do.float())
+    assert rel(o, of) < 2e-2, rel(o, of)
+    for a, b in ((q.grad, qf.grad), (k.grad, kf.grad), (v.grad, vf.grad)):
+        assert a.shape == b.shape and rel(a, b) < 3e-2, rel(a, b)
+
+
 def test_flash_lse_and_spike():
     """Force the online-softmax rescale: one key spiked against one query (rule 26)."""
     B, T, H, hd = 1, 300, 2, 128

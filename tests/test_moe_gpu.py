@@ -124,12 +124,18 @@ def test_moe_ffn_gpu_matches_cpu():
         assert _rel(a, b) < 3e-2
 
 
-@pytest.mark.parametrize("preset", ["dsv3_ref", "dsv3_tiny"])
+@pytest.mark.parametrize("preset", ["dsv3_ref", "dsv3_tiny", "dsv3_tiny_v3heads"])
 def test_deepseek_gpu_matches_cpu(preset):
     from solvingpapers_amd.models import deepseekv3 as ds
     kw = dict(dropout=0.0, attn_dropout=0.0)
+    norm_tol = 0.15
     if preset == "dsv3_ref":
         kw.update(vocab_size=512, n_layers=2, block_size=64)
+    if preset == "dsv3_tiny_v3heads":      # V3 MLA head dims: qk 128 + 64 rope, v 128 (padded flash)
+        preset = "dsv3_tiny"
+        # no MTP head here (dsv3_tiny covers it): behind the extra low-rank bf16 projections its
+        # tiny router / norm-weight grads measured rel 0.29-0.31 against fp32
+        kw.update(qk_nope_dim=128, qk_rope_dim=64, v_head_dim=128, q_lora_rank=96, mtp_heads=0)
     c = ds.config(preset, **kw)
     cpu = ds.DeepSeekV3(c, seed=0)
     gpu = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=0)
@@ -148,8 +154,9 @@ def test_deepseek_gpu_matches_cpu(preset):
         if a.grad is None or a.grad.abs().max() == 0:
             continue
         # router / norm-weight grads are long bf16 reductions of small terms
-        tol = 0.3 if n.endswith("gate") else 0.15 if n.endswith("norm") or "norm_" in n else 8e-2
-        assert _rel(b.grad.cpu(), a.grad) < tol, n
+        tol = 0.3 if n.endswith("gate") else norm_tol if n.endswith("norm") or "norm_" in n else 8e-2
+        r = _rel(b.grad.cpu(), a.grad)
+        assert r < tol, (n, r)
     out = gpu.generate(ids[:, :8].to(dev), 8, greedy=True)
     assert out.shape == (2, 16)
 
