@@ -21,7 +21,7 @@ import argparse
 import ast
 import dataclasses
 import json
-import sys
+import os
 
 import torch
 
@@ -37,21 +37,40 @@ def _parse_sets(items):
     return out
 
 
+def _tokenizer(spec: str, text: str):
+    """char | bpe:<vocab> (train a byte-level BPE on the text) | gpt2:<dir with vocab.json +
+    merges.txt> | <path to a saved tokenizer.json>."""
+    from ..data.bpe import BPETokenizer
+    from ..data.text import CharTokenizer
+    if spec == "char":
+        return CharTokenizer(text)
+    if spec.startswith("bpe:"):
+        chunk = 1 << 16
+        return BPETokenizer.train((text[i:i + chunk] for i in range(0, len(text), chunk)), int(spec[4:]))
+    if spec.startswith("gpt2:"):
+        d = spec[5:]
+        return BPETokenizer.from_gpt2_files(os.path.join(d, "vocab.json"), os.path.join(d, "merges.txt"))
+    return BPETokenizer.load(spec)
+
+
 def _lm(args, info):
     from ..data.loader import NativeTokenLoader
-    from ..data.text import CharTokenizer, synthetic_corpus
+    from ..data.text import synthetic_corpus
     from ..models import deepseekv3, gemma, gpt, llama3
     from .trainer import TrainConfig, Trainer
     dev = info.device if args.device is None else torch.device(args.device)
     dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.dtype or ("bf16" if dev.type == "cuda" else "fp32")]
     sets = _parse_sets(args.set)
     char = args.preset in ("gpt_ref", "gpt_tiny_cpu", "gemma_ref")
-    if char:
-        text = synthetic_corpus(400_000, seed=args.seed)
-        tok = CharTokenizer(text)
+    stream = files = None
+    if args.data:
+        files = args.data.split(",")
+    elif args.text or char:
+        text = open(args.text, encoding="utf-8").read() if args.text else synthetic_corpus(400_000, seed=args.seed)
+        tok = _tokenizer(args.tokenizer or ("char" if char else "bpe:8192"), text)
         stream = torch.tensor(tok.encode(text), dtype=torch.int32)
-        key = "vocab_size"
-        sets.setdefault(key, tok.vocab_size)
+        sets.setdefault("vocab_size", tok.vocab_size)
+        char = True
     fam = args.model
     if fam == "gpt":
         c = gpt.config(args.preset or "gpt_ref", **sets)
@@ -78,12 +97,23 @@ def _lm(args, info):
         raise SystemExit(f"unknown model {fam}")
     T = args.seq or T
     B = args.batch or B
-    if not char:
-        stream = torch.randint(0, V, (max(200_000, 4 * B * (T + 1)),), generator=torch.Generator().manual_seed(args.seed),
-                               dtype=torch.int32)
-    n = int(stream.numel() * 0.9)
-    tr = NativeTokenLoader(stream[:n], B, T, seed=args.seed, rank=info.rank, world=info.world_size, device=dev)
-    ev = NativeTokenLoader(stream[n:], B, T, seed=args.seed + 1, rank=info.rank, world=info.world_size, device=dev)
+    if files:
+        # token files (data/bpe.encode_to_token_file) memory-mapped by the native loader; without a
+        # second file the eval batches are drawn from the training file with another seed
+        from ..data.bpe import token_file_dtype
+        fd = [torch.int32 if token_file_dtype(f) == "int32" else torch.uint16 for f in files]
+        tr = NativeTokenLoader(files[0], B, T, seed=args.seed, rank=info.rank, world=info.world_size, device=dev,
+                               file_dtype=fd[0])
+        ev = NativeTokenLoader(files[-1], B, T, seed=args.seed + 1, rank=info.rank, world=info.world_size,
+                               device=dev, file_dtype=fd[-1])
+    else:
+        if not char:
+            stream = torch.randint(0, V, (max(200_000, 4 * B * (T + 1)),),
+                                   generator=torch.Generator().manual_seed(args.seed), dtype=torch.int32)
+        n = int(stream.numel() * 0.9)
+        tr = NativeTokenLoader(stream[:n], B, T, seed=args.seed, rank=info.rank, world=info.world_size, device=dev)
+        ev = NativeTokenLoader(stream[n:], B, T, seed=args.seed + 1, rank=info.rank, world=info.world_size,
+                               device=dev)
     tc = TrainConfig(steps=args.steps, lr=args.lr, min_lr=args.min_lr, warmup=args.warmup,
                      weight_decay=args.weight_decay, clip=args.clip, eval_every=args.eval_every,
                      eval_iters=args.eval_iters, ckpt_dir=args.ckpt_dir, ckpt_every=args.ckpt_every,
@@ -140,6 +170,9 @@ def main(argv=None):
     ap.add_argument("--device", default=None)
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"])
     ap.add_argument("--mnist-root", default=None)
+    ap.add_argument("--data", default=None, help="token file(s) TRAIN[,EVAL] written by data.bpe.encode_to_token_file")
+    ap.add_argument("--text", default=None, help="UTF-8 text file to tokenize (LM models)")
+    ap.add_argument("--tokenizer", default=None, help="char | bpe:<vocab> | gpt2:<dir> | <tokenizer.json>")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args(argv)
     from ..parallel import dist as sdist
@@ -148,12 +181,11 @@ def main(argv=None):
     load_gemm_tuning()  # tuned hipBLASLt/rocBLAS solutions for the shapes in tuning/*.csv
     try:
         if args.model in ("vit", "ae", "vae", "kd"):
-            _images(args, info)
-        else:
-            _lm(args, info)
+            return _images(args, info)
+        return _lm(args, info)
     finally:
         sdist.cleanup()
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    main()
