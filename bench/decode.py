@@ -18,8 +18,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from solvingpapers_amd.infer import GenerationStats  # noqa: E402
 
 
-def build(model, layers):
+def build(model, layers, sets=()):
     kw = {} if layers is None else {"n_layers": layers}
+    for kv in sets:                      # --set n_experts=32 etc. (int/float/str)
+        k, v = kv.split("=", 1)
+        for cast in (int, float):
+            try:
+                v = cast(v)
+                break
+            except ValueError:
+                pass
+        kw[k] = v
+    if model.startswith("dsv3"):
+        # MLA decode attends over the per-layer compressed latent cache (kv_lora + rope values
+        # per token) with W_uk absorbed into q and W_uv applied after
+        from solvingpapers_amd.models import deepseekv3
+        return deepseekv3.DeepSeekV3(deepseekv3.config(model, **kw), device="cuda", dtype=torch.bfloat16, seed=1)
     if model.startswith("llama3"):
         from solvingpapers_amd.models import llama3
         return llama3.Llama3(llama3.config(model, **kw), device="cuda", dtype=torch.bfloat16, seed=1)
@@ -35,8 +49,9 @@ def main(argv=None):
     ap.add_argument("--new", type=int, default=128)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--graph", action="store_true", help="HIP-graph decode (one replay per token)")
+    ap.add_argument("--set", action="append", default=[], help="config override key=value")
     a = ap.parse_args(argv)
-    m = build(a.model, a.layers).eval()
+    m = build(a.model, a.layers, a.set).eval()
     ids = torch.randint(0, m.c.vocab_size, (a.batch, a.prompt), device="cuda")
     st = GenerationStats()
     if a.graph:
