@@ -6,6 +6,7 @@ all-to-all dispatch) and the dense parameters data-parallel (RCCL buckets)."""
 from __future__ import annotations
 
 import argparse
+import contextlib
 
 import torch
 
@@ -26,6 +27,7 @@ def main():
     ap.add_argument("--mb", type=int, default=2)
     ap.add_argument("--experts", type=int, default=None, help="routed experts (whole job; EP splits them)")
     ap.add_argument("--dense-layers", type=int, default=None)
+    ap.add_argument("--accum", type=int, default=1, help="micro-batches accumulated per optimizer step")
     ap.add_argument("--fp8", action="store_true", help="fp8 (OCP e4m3) routed-expert GEMMs")
     a = ap.parse_args()
     info = sdist.init_distributed()
@@ -53,20 +55,23 @@ def main():
 
     def step():
         opt.zero_grad()
-        t = torch.randint(0, c.vocab_size, (B, T + 1), device=dev, generator=gen)
-        loss = m(t[:, :-1], t[:, 1:])
-        loss.backward()
+        for i in range(a.accum):
+            t = torch.randint(0, c.vocab_size, (B, T + 1), device=dev, generator=gen)
+            inner = dp is not None and i < a.accum - 1
+            with (dp.no_sync() if inner else contextlib.nullcontext()):
+                loss = m(t[:, :-1], t[:, 1:]) / a.accum
+                loss.backward()
         if dp is not None:
             dp.finish_grad_sync()
         opt.step()
-        last[0] = loss
+        last[0] = loss * a.accum
 
     el = timed(step, a.steps, a.warmup)
-    tok_s = world * B * T * a.steps / el
+    tok_s = world * B * T * a.accum * a.steps / el
     tf = tok_s * m.flops_per_token(T) / world / 1e12
     report("training tokens/sec, DeepSeek-V3-style MLA+MoE bf16", tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
-            + ("-fp8" if a.fp8 else ""), "global_batch": world * B, "seq_len": T,
+            + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum,
             "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu", "params": m.num_params(),
             "active_params": m.num_params(active=True)},
            tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4))
