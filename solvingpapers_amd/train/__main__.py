@@ -120,6 +120,9 @@ def _lm(args, info):
                      log_path=args.log, grad_accum=args.accum, zero1=args.zero1, optimizer=args.optimizer,
                      grad_dtype=dtype)
     hooks = [lambda r: print(json.dumps(r), flush=True)] if info.rank == 0 else []
+    if info.rank == 0 and args.wandb:
+        from .metrics import WandbHook
+        hooks.append(WandbHook(args.wandb, config=vars(args), tokens_per_step=B * T * args.accum * info.world_size))
     trainer = Trainer(model, tc, tr, ev.batch_at, hooks=hooks)
     trainer.fit()
     return trainer
@@ -174,6 +177,7 @@ def main(argv=None):
     ap.add_argument("--text", default=None, help="UTF-8 text file to tokenize (LM models)")
     ap.add_argument("--tokenizer", default=None, help="char | bpe:<vocab> | gpt2:<dir> | <tokenizer.json>")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--wandb", default=None, help="W&B project (reference metric names; needs the wandb package)")
     args = ap.parse_args(argv)
     from ..parallel import dist as sdist
     from ..utils.tuning import load_gemm_tuning

@@ -107,3 +107,27 @@ def test_cli_entrypoint_trains_and_checkpoints(tmp_path):
     assert (tmp_path / "latest").exists()
     recs = [json.loads(l) for l in open(tmp_path / "m.jsonl")]
     assert len(recs) == 4
+
+
+def test_metric_hooks_use_reference_wandb_names(tmp_path):
+    import json
+    import math
+
+    import pytest
+
+    from solvingpapers_amd.train.metrics import JsonlHook, WandbHook, reference_names
+    r = reference_names({"step": 3, "loss": 2.0, "lr": 1e-3, "grad_norm": 0.5, "ok": True}, tokens_per_step=4096)
+    assert r == {"step": 3, "train_loss": 2.0, "train_perplexity": math.exp(2.0), "lr": 1e-3, "grad_norm": 0.5,
+                 "tokens": 4 * 4096}
+    v = reference_names({"step": 9, "val_loss": 1.5})
+    assert v["val_perplexity"] == pytest.approx(math.exp(1.5))
+    p = tmp_path / "m.jsonl"
+    h = JsonlHook(str(p), tokens_per_step=10)
+    h({"step": 0, "loss": 1.0, "lr": 0.1})
+    h.close()
+    assert json.loads(p.read_text())["train_loss"] == 1.0
+    try:
+        import wandb  # noqa: F401
+    except ImportError:
+        with pytest.raises(RuntimeError, match="wandb"):
+            WandbHook("proj")
