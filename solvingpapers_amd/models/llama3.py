@@ -80,6 +80,7 @@ class LlamaBlock(nn.Module):
         super().__init__()
         hd = c.head_dim
         self.c = c
+        self.cp_group = None  # context parallelism: this rank holds a T/P slice of the sequence
         self.attention_norm = nn.Parameter(torch.ones(c.dim, **fk))
         self.wqkv = nn.Parameter(torch.empty((c.n_heads + 2 * c.n_kv_heads) * hd, c.dim, **fk))
         self.wo = nn.Parameter(torch.empty(c.dim, c.n_heads * hd, **fk))
@@ -115,7 +116,17 @@ class LlamaBlock(nn.Module):
             _ext.ops().rope_kv_write_(x4, cos, sin, pos.positions, pos.index, kc, vc, H, KV, 0)
             o = decode_attention(x4[:, :, :H], kc, vc, causal=True, kv_len=pos.kv_len)
             return linear(o.reshape(B, T, H * hd), self.wo)
-        if kv_cache is None:
+        if kv_cache is None and self.cp_group is not None:
+            # sequence slice at offset rank*T: RoPE at global positions, attention over all
+            # ranks' tokens via the all-to-all sequence <-> head exchange
+            import torch.distributed as dist
+            from ..parallel.context_parallel import context_parallel_attention
+            H, KV = c.n_heads, c.n_kv_heads
+            off = dist.get_rank(self.cp_group) * T
+            qkv = rope_packed_(qkv, H + KV, c.rope_theta, off, head_dim=hd, ref_freqs=c.ref_freqs)
+            x4 = qkv.view(B, T, H + 2 * KV, hd)
+            o = context_parallel_attention(x4[:, :, :H], x4[:, :, H:H + KV], x4[:, :, H + KV:], self.cp_group)
+        elif kv_cache is None:
             qkv = rope_packed_(qkv, c.n_heads + c.n_kv_heads, c.rope_theta, 0, head_dim=hd, ref_freqs=c.ref_freqs)
             o = attention_packed(qkv, c.n_heads, c.n_kv_heads, causal=True, head_dim=hd)
         else:
@@ -195,6 +206,15 @@ class Llama3(nn.Module):
         delta = mark_ready(delta, cb, len(self.layers) + 1)
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
         return n
+
+    def set_context_parallel(self, group):
+        """Train on sequence slices: rank r of ``group`` feeds tokens [r*T, (r+1)*T) of each
+        sequence. Gradients are then summed over ``group`` like data parallelism (e.g.
+        ``DataParallel(model, flat, group=group)``): the mean of the ranks' local losses is the
+        full-sequence loss."""
+        for l in self.layers:
+            l.cp_group = group
+        return self
 
     def logits(self, n):
         w = self.output if self.output is not None else self.tok_embeddings

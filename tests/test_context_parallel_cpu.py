@@ -64,3 +64,50 @@ def test_context_parallel_attention_matches_full(Hkv, causal):
     cat = lambda i: torch.cat([r[i] for r in res], dim=1)  # noqa: E731
     for i, want in ((1, o.detach()), (2, q.grad), (3, k.grad), (4, v.grad)):
         assert torch.allclose(cat(i), want, atol=1e-5, rtol=1e-4), i
+
+
+def _llama_worker(rank, world, port, q_out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from solvingpapers_amd.models import llama3
+    c = llama3.config("llama3_ref", vocab_size=64, dim=64, n_heads=4, n_kv_heads=2, ffn_hidden=128, init="std")
+    m = llama3.Llama3(c, seed=0).set_context_parallel(dist.group.WORLD)
+    ids = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(1))
+    Tl = 16 // world
+    sl = slice(rank * Tl, (rank + 1) * Tl)
+    loss = m(ids[:, :-1][:, sl], ids[:, 1:][:, sl])
+    loss.backward()
+    grads = {}
+    for n, p in m.named_parameters():
+        g = p.grad.clone()
+        dist.all_reduce(g)
+        grads[n] = g / world
+    lt = loss.detach().clone()
+    dist.all_reduce(lt)
+    q_out.put((rank, float(lt) / world, grads))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_llama_context_parallel_matches_single_process():
+    from solvingpapers_amd.models import llama3
+    world = 2
+    ctx = mp.get_context("spawn")
+    q_out = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_llama_worker, args=(r, world, port, q_out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q_out.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = llama3.config("llama3_ref", vocab_size=64, dim=64, n_heads=4, n_kv_heads=2, ffn_hidden=128, init="std")
+    m = llama3.Llama3(c, seed=0)
+    ids = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(1))
+    loss = m(ids[:, :-1], ids[:, 1:])
+    loss.backward()
+    _, l_cp, grads = res[0]
+    assert abs(l_cp - loss.item()) < 1e-5
+    for n, p in m.named_parameters():
+        assert torch.allclose(grads[n], p.grad, atol=1e-5, rtol=1e-4), n
