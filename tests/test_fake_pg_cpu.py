@@ -76,3 +76,29 @@ def test_llama_8b_zero1_dp8_partition():
     print("ok")
     """)
     assert out.startswith("ok")
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_dsv3_v3_ep8_expert_shards(rank):
+    """DeepSeek-V3 layout (256 routed experts top-8, MLA qk 128+64 / v 128 heads), EP=8 at a
+    CPU-sized width: each rank holds 32 of the 256 routed experts and every other weight; the
+    expert-parallel layout (the routed forward is covered by the gloo EP test)."""
+    out = _run(PRELUDE.format(rank=rank) + """
+    from solvingpapers_amd.models import deepseekv3 as ds
+    c = ds.config("dsv3_v3", vocab_size=512, dim=256, n_heads=8, q_lora_rank=64, kv_lora_rank=32,
+                  expert_hidden=64, dense_hidden=128, n_layers=2, n_dense_layers=1, block_size=16)
+    assert (c.n_experts, c.top_k, c.qk_nope_dim, c.qk_rope_dim, c.v_head_dim) == (256, 8, 128, 64, 128)
+    m = ds.DeepSeekV3(c, ep_group=dist.group.WORLD)
+    moe = m.moe_layers()
+    assert moe and all(l.w13.shape[0] == 256 // WORLD for l in moe), [l.w13.shape for l in moe]
+    # shape-only: the fake group's all-to-all leaves the exchanged token counts uninitialised,
+    # so the routed forward is covered by the gloo EP test instead
+    n_local = sum(p.numel() for p in m.parameters())
+    full = ds.DeepSeekV3(ds.config("dsv3_v3", vocab_size=512, dim=256, n_heads=8, q_lora_rank=64,
+                                   kv_lora_rank=32, expert_hidden=64, dense_hidden=128, n_layers=2,
+                                   n_dense_layers=1, block_size=16))
+    per_expert = 3 * 64 * 256
+    assert sum(p.numel() for p in full.parameters()) - n_local == len(moe) * (256 - 32) * per_expert
+    print("ok", tuple(moe[0].w13.shape))
+    """)
+    assert "ok (32," in out
