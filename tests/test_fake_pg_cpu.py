@@ -81,8 +81,8 @@ def test_llama_8b_zero1_dp8_partition():
 @pytest.mark.parametrize("rank", [0, 7])
 def test_dsv3_v3_ep8_expert_shards(rank):
     """DeepSeek-V3 layout (256 routed experts top-8, MLA qk 128+64 / v 128 heads), EP=8 at a
-    CPU-sized width: each rank holds 32 of the 256 routed experts and every other weight; the
-    expert-parallel layout (the routed forward is covered by the gloo EP test)."""
+    CPU-sized width: each rank holds 32 of the 256 routed experts and every other weight
+    (layout only; the routed forward is covered by the gloo EP test)."""
     out = _run(PRELUDE.format(rank=rank) + """
     from solvingpapers_amd.models import deepseekv3 as ds
     c = ds.config("dsv3_v3", vocab_size=512, dim=256, n_heads=8, q_lora_rank=64, kv_lora_rank=32,
