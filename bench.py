@@ -2,7 +2,12 @@
 """Headline benchmark: LLaMA3-8B-shape bf16 training tokens/s on 1..8 MI355X.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
-is launched under ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI).
+runs one rank per GPU (RCCL over xGMI). Launched under ``torch.distributed.run`` it
+uses that process group; launched directly with ``--gpus N > 1`` (no WORLD_SIZE in
+the env) it starts ``torch.distributed.run --nproc-per-node N`` itself as a CHILD
+process before anything touches the GPU, and exits with the child's exit code
+(non-zero if any rank failed). ``n_gpus`` in the JSON is the live process group's
+world size, next to the backend and the visible device count.
 W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
 torch.cuda.synchronize() on both sides; the max elapsed over ranks is used and
 rank 0 prints one JSON line. ``value`` = whole-job tokens/s (all GPUs).
@@ -26,26 +31,41 @@ import argparse
 import contextlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from solvingpapers_amd.models import llama3  # noqa: E402
-from solvingpapers_amd.parallel import dist as sdist  # noqa: E402
-from solvingpapers_amd.parallel.data_parallel import DataParallel  # noqa: E402
-from solvingpapers_amd.train.optim import FlatAdamW  # noqa: E402
-from solvingpapers_amd.utils.flat import FlatParams  # noqa: E402
-from solvingpapers_amd.utils.prof import annotate  # noqa: E402
-from solvingpapers_amd.utils.tuning import load_gemm_tuning  # noqa: E402
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 BASELINE_TOKS = None  # BASELINE.json "published": {} -> no reference number for this config
 PEAK_BF16 = 2.5e15
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n: int, argv) -> int:
+    """Start ``torch.distributed.run`` with n ranks of this script as a child process (no
+    exec: nothing here has touched the GPU, and the parent only waits) and return its exit
+    code. Rendezvous on 127.0.0.1 (the container hostname may not resolve)."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    env["SPA_BENCH_SELF"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env, cwd=ROOT)
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -60,25 +80,48 @@ def main(argv=None):
     ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (default tuning/tunableop_llama8b.csv; "
                     "SPA_GEMM_TUNING=0 disables)")
     a = ap.parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(a.gpus, argv)
+    return run(a)
+
+
+def run(a):
+    import torch
+    import torch.distributed as tdist
+
+    from solvingpapers_amd.models import llama3
+    from solvingpapers_amd.parallel import dist as sdist
+    from solvingpapers_amd.parallel.data_parallel import DataParallel
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    from solvingpapers_amd.utils.prof import annotate
+    from solvingpapers_amd.utils.tuning import load_gemm_tuning
 
     info = sdist.init_distributed()
-    world = info.world_size
+    world = tdist.get_world_size() if tdist.is_initialized() else 1   # the LIVE group
     if world != a.gpus and info.is_main:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        print(f"warning: --gpus {a.gpus} but the process group has {world} ranks; reporting {world}",
+              file=sys.stderr)
     dev = info.device
+    cuda = dev.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
     torch.backends.cuda.matmul.allow_tf32 = False
-    tuned = load_gemm_tuning(a.gemm_table)
+    tuned = load_gemm_tuning(a.gemm_table) if cuda else False
 
     kw = {} if a.layers is None else {"n_layers": a.layers}
     cfg = llama3.config(a.model, max_seq_len=a.seq, **kw)
-    model = llama3.Llama3(cfg, device=dev, dtype=torch.bfloat16, seed=1234)
-    flat = FlatParams(model, groups=model.param_groups(), grad_dtype=torch.bfloat16, align=64)
+    dtype = torch.bfloat16 if cuda else torch.float32
+    model = llama3.Llama3(cfg, device=dev, dtype=dtype, seed=1234)
+    flat = FlatParams(model, groups=model.param_groups(), grad_dtype=dtype, align=64 * world)
     dp = DataParallel(model, flat, zero1=a.zero1) if world > 1 else None
     if dp is not None:
         dp.broadcast_params(0)
     shard = (dp.shard_ranges(), None) if (dp is not None and a.zero1) else None
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0, shard=shard)
-    overlap = not a.no_opt_overlap and not a.zero1
+    overlap = cuda and not a.no_opt_overlap and not a.zero1
     if overlap:
         model.param_wait_cb = flat.wait_bucket
 
@@ -113,11 +156,11 @@ def main(argv=None):
     for _ in range(a.warmup):
         step()
     sdist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     sdist.barrier()
     t1 = time.perf_counter()
     elapsed = sdist.all_reduce_max(t1 - t0)
@@ -139,7 +182,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (tok_s / BASELINE_TOKS) if BASELINE_TOKS else None,
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic (random token ids, random-init weights)",
             "config": {
                 "model": a.model if a.layers is None else f"{a.model}-L{a.layers}",
@@ -154,11 +197,17 @@ def main(argv=None):
             "mfu_vs_2.5PF": round(tflops_gpu * 1e12 / PEAK_BF16, 4),
             "gemm_table": tuned,
             "loss": round(loss_v, 4),
-            "mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
+            "mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,
+            "world_size": world,
+            "backend": tdist.get_backend() if tdist.is_initialized() else "none",
+            "device_count": torch.cuda.device_count() if cuda else 0,
+            "launcher": "bench.py self-launch" if os.environ.get("SPA_BENCH_SELF") else
+                        ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "direct"),
         }
         print(json.dumps(out), flush=True)
     sdist.cleanup()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

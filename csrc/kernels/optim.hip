@@ -25,6 +25,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* _
                                                     const float* __restrict__ coef_ptr, int adam_l2,
                                                     const float* __restrict__ hyper) {
   const float coef = coef_ptr ? *coef_ptr : 1.f;
+  // non-finite global grad norm -> the coefficient is NaN: skip the whole update. The norm is
+  // reduced over every group that holds gradients, so all ranks take the same decision
+  // without a host sync (train/optim.py FlatOptimizer.clip_coef).
+  if (!(coef == coef)) return;
   if (hyper) {  // graph-safe: lr and step read from the device (hyper = [lr, step])
     lr = hyper[0];
     inv_bc1 = 1.f / (1.f - __powf(b1, hyper[1]));
@@ -88,6 +92,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(PT* __restrict__ p, float* __r
                                                   float momentum, float wd, const float* __restrict__ coef_ptr,
                                                   const float* __restrict__ hyper) {
   const float coef = coef_ptr ? *coef_ptr : 1.f;
+  if (!(coef == coef)) return;  // non-finite grad norm: skip (see adamw_kernel)
   if (hyper) lr = hyper[0];
   for (long j = blockIdx.x * 256L + threadIdx.x; j < n; j += (long)gridDim.x * 256) {
     float pv = MASTER ? master[j] : (float)p[j];

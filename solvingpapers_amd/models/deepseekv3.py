@@ -316,11 +316,21 @@ class MoE(tnn.Module):
     def reset_parameters(self, std, g):
         F, Fp = self.F, self.Fp
         self.gate.normal_(0, std, generator=g)
-        self.w13.zero_()
-        self.w2.zero_()
-        self.w13[:, :F].normal_(0, std, generator=g)
-        self.w13[:, Fp:Fp + F].normal_(0, std, generator=g)
-        self.w2[:, :, :F].normal_(0, std, generator=g)
+        # under EP draw all E experts exactly as the unsharded model does and keep this rank's
+        # slice: every EP rank then holds distinct experts, and rank r's shard equals
+        # shard_experts(unsharded init, r, P) (a per-rank E/P draw from the shared generator
+        # sequence would give every rank the same experts)
+        w13 = self.w13 if self.ep == 1 else self.w13.new_zeros((self.c.n_experts,) + tuple(self.w13.shape[1:]))
+        w2 = self.w2 if self.ep == 1 else self.w2.new_zeros((self.c.n_experts,) + tuple(self.w2.shape[1:]))
+        w13.zero_()
+        w2.zero_()
+        w13[:, :F].normal_(0, std, generator=g)
+        w13[:, Fp:Fp + F].normal_(0, std, generator=g)
+        w2[:, :, :F].normal_(0, std, generator=g)
+        if self.ep > 1:
+            El = self.w13.shape[0]
+            self.w13.copy_(w13[self.ep_rank * El:(self.ep_rank + 1) * El])
+            self.w2.copy_(w2[self.ep_rank * El:(self.ep_rank + 1) * El])
         if self.shared is not None:
             self.shared.reset_parameters(std, g)
 

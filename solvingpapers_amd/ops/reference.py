@@ -138,7 +138,10 @@ def embedding(W, idx, pos=None, scale=1.0):
 
 
 def adamw_(p, master, g, m, v, lr, b1, b2, eps, wd, step, coef=None, adam_l2=False):
-    """torch.optim.AdamW / Adam math on flat fp32 state (in place)."""
+    """torch.optim.AdamW / Adam math on flat fp32 state (in place). A NaN ``coef``
+    (non-finite global grad norm) skips the update, as the HIP kernel does."""
+    if coef is not None and bool(torch.isnan(coef).any()):
+        return
     src = master if master is not None else p
     pf = src.float()
     gf = g.float() * (coef.float() if coef is not None else 1.0)
@@ -158,6 +161,8 @@ def adamw_(p, master, g, m, v, lr, b1, b2, eps, wd, step, coef=None, adam_l2=Fal
 
 
 def sgd_(p, master, g, buf, lr, momentum, wd, coef=None):
+    if coef is not None and bool(torch.isnan(coef).any()):
+        return
     src = master if master is not None else p
     pf = src.float()
     gf = g.float() * (coef.float() if coef is not None else 1.0) + wd * pf

@@ -133,6 +133,22 @@ class DataParallel:
             w.wait()
 
     def broadcast_params(self, src: int = 0):
-        """Make every rank start from rank ``src``'s parameters."""
-        if self.world > 1:
-            dist.broadcast(self.flat.param, src=src, group=self.group)
+        """Make every replica start from the same parameters: dense buckets from rank ``src``
+        of the DP group (a group-local rank), expert-parallel buckets only over
+        ``expert_dp_group`` -- each EP rank holds DIFFERENT experts, so broadcasting those
+        over the whole DP group would overwrite every rank's experts with rank 0's."""
+        if self.world <= 1:
+            return
+        gsrc = dist.get_global_rank(self.group, src) if self.group is not None else src
+        dense = [b for b in self.flat.buckets if b.index not in self.expert_buckets]
+        if not self.expert_buckets:
+            dist.broadcast(self.flat.param, src=gsrc, group=self.group)
+        else:
+            for b in dense:
+                dist.broadcast(self.flat.param[b.start:b.end], src=gsrc, group=self.group)
+            grp = self.expert_dp_group
+            if grp is not None and dist.get_world_size(grp) > 1:
+                esrc = dist.get_global_rank(grp, 0)
+                for b in self.flat.buckets:
+                    if b.index in self.expert_buckets:
+                        dist.broadcast(self.flat.param[b.start:b.end], src=esrc, group=grp)

@@ -21,7 +21,7 @@ def reference_names(rec: dict, tokens_per_step: Optional[int] = None) -> dict:
     if "loss" in rec and rec["loss"] is not None:
         out["train_loss"] = float(rec["loss"])
         out["train_perplexity"] = math.exp(min(float(rec["loss"]), 80.0))
-    if "val_loss" in rec:
+    if rec.get("val_loss") is not None:
         out["val_loss"] = float(rec["val_loss"])
         out["val_perplexity"] = math.exp(min(float(rec["val_loss"]), 80.0))
     for k in ("lr", "grad_norm", "tok_per_s"):

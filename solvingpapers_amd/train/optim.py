@@ -21,8 +21,11 @@ from ..utils.flat import FlatParams
 class FlatOptimizer:
     def __init__(self, flat: FlatParams, lr: float, weight_decay: float = 0.0, max_grad_norm: Optional[float] = None,
                  shard: Optional[Tuple[List[Tuple[int, int]], object]] = None, ep_group=None, tp_group=None,
-                 graph_safe: bool = False):
+                 graph_safe: bool = False, skip_nonfinite: bool = True):
         self.flat = flat
+        # skip_nonfinite: compute the global grad norm even without clipping so a non-finite
+        # gradient skips the update on every rank alike (clip_coef)
+        self.skip_nonfinite = skip_nonfinite
         # graph_safe: lr and step live on the device ([lr, step] fp32) so a captured HIP graph of
         # the whole training step replays with the right bias correction / schedule (set_lr)
         self.hyper = (torch.tensor([lr, 0.0], dtype=torch.float32, device=flat.device)
@@ -155,12 +158,28 @@ class FlatOptimizer:
         return tot.sqrt()
 
     def clip_coef(self):
-        if self.max_grad_norm is None:
+        """Device-resident update coefficient: the clip factor, or NaN when the global grad
+        norm is not finite -- the fused kernels then skip the update. The norm is already
+        reduced over every DP/ZeRO/TP/EP group, so every rank reaches the same skip decision
+        with no host sync and no mismatched collectives (a rank-local loss check would
+        desynchronise the ranks)."""
+        if self.max_grad_norm is None and not self.skip_nonfinite:
             self.last_grad_norm = None
             return None
         n = self.grad_norm()
         self.last_grad_norm = n
-        return torch.clamp(self.max_grad_norm / (n + 1e-6), max=1.0).float().reshape(1)
+        nan = torch.full_like(n, float("nan"))
+        if self.max_grad_norm is None:
+            c = torch.where(torch.isfinite(n), torch.ones_like(n), nan)
+        else:
+            c = torch.where(torch.isfinite(n), torch.clamp(self.max_grad_norm / (n + 1e-6), max=1.0), nan)
+        return c.float().reshape(1)
+
+    def last_step_ok(self):
+        """Device bool: did the last step apply an update (finite global grad norm)?"""
+        if self.last_grad_norm is None:
+            return None
+        return torch.isfinite(self.last_grad_norm)
 
     def zero_grad(self):
         from ..utils.grad import next_generation

@@ -52,7 +52,10 @@ class TrainConfig:
     resume: str = "auto"                 # "auto" (latest if present) | "never" | <path>
     log_path: Optional[str] = None       # JSONL metrics
     log_every: int = 1
-    max_bad_steps: int = 3               # consecutive non-finite losses before abort
+    # device values (loss, grad norm, skip flag, step time) are read back in batches of
+    # ``sync_every`` steps: one host sync per batch instead of one per step (GPU only)
+    sync_every: int = 16
+    max_bad_steps: int = 3               # consecutive non-finite grad norms before abort
     zero1: bool = False
     opt_overlap: bool = False
     tokens_per_sample: int = 0           # for tok/s (0 -> x.numel())
@@ -78,6 +81,10 @@ class Trainer:
                                grad_dtype=cfg.grad_dtype, param_dtype=cfg.param_dtype)
         self.dp = DataParallel(model, self.flat, group=dp_group, zero1=cfg.zero1,
                                expert_dp_group=expert_dp_group) if self.world > 1 else None
+        if self.dp is not None:
+            # before the optimizer is built: FlatOptimizer copies its fp32 master from the
+            # params at construction, so a later broadcast would be undone by the first step
+            self.dp.broadcast_params()
         shard = (self.dp.shard_ranges(), dp_group) if (self.dp and cfg.zero1) else None
         if cfg.optimizer in ("adamw", "adam"):
             self.opt = FlatAdamW(self.flat, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
@@ -90,12 +97,11 @@ class Trainer:
             raise ValueError(cfg.optimizer)
         for m in getattr(model, "moe_layers", lambda: [])():
             m.balance_group = dp_group
-        if self.dp is not None:
-            self.dp.broadcast_params()
         self.step = 0
         self.bad_steps = 0
         self.history = []
         self.hooks = list(hooks)
+        self._pending = []      # per-step device values awaiting one batched host read
         self._log = None
         if cfg.log_path and self.rank == 0:
             os.makedirs(os.path.dirname(os.path.abspath(cfg.log_path)), exist_ok=True)
@@ -167,6 +173,9 @@ class Trainer:
 
     # ------------------------------------------------------------------ train
     def train_step(self, step):
+        """One optimizer step over ``grad_accum`` micro-batches. Returns (loss, ntok, ok) as
+        DEVICE tensors (no host sync): ``ok`` is False when the global grad norm was not
+        finite and the update was skipped on every rank (FlatOptimizer.clip_coef)."""
         c = self.cfg
         self.opt.zero_grad()
         tot = None
@@ -188,19 +197,41 @@ class Trainer:
         sync_sp = getattr(self.model, "sync_sequence_parallel_grads", None)
         if sync_sp is not None:
             sync_sp()
-        loss = tot / c.grad_accum
-        finite = bool(torch.isfinite(loss).item())
-        if not finite:
-            self.bad_steps += 1
-            if self.bad_steps >= c.max_bad_steps:
-                raise NonFiniteLoss(f"{self.bad_steps} consecutive non-finite losses at step {step}")
-            return float("nan"), ntok, False
-        self.bad_steps = 0
         with annotate("optimizer"):
             self.opt.step(lr=self.lr_at(step), overlap=c.opt_overlap)
         if self.dp is not None:
             self.dp.gather_params()
-        return float(loss), ntok, True
+        ok = self.opt.last_step_ok()
+        return tot / c.grad_accum, ntok, ok
+
+    def _flush(self):
+        """Read back the pending steps' device values with one sync, log them, and apply
+        the consecutive-bad-step abort."""
+        if not self._pending:
+            return
+        dev = self.flat.device
+        if dev.type == "cuda":
+            self._pending[-1]["ev"].synchronize()
+        for r in self._pending:
+            ok = bool(r["ok"]) if r["ok"] is not None else True
+            if ok:
+                self.bad_steps = 0
+            else:
+                self.bad_steps += 1
+            if r["log"]:
+                if dev.type == "cuda" and r["ev0"] is not None:
+                    dt = r["ev0"].elapsed_time(r["ev"]) / 1e3
+                else:
+                    dt = r["dt"]
+                gn = r["gn"]
+                rec = {"step": r["step"], "loss": float(r["loss"]) if ok else float("nan"), "lr": r["lr"],
+                       "ok": ok, "dt": dt, "tok_per_s": r["ntok"] * self.world / max(dt, 1e-9),
+                       "grad_norm": float(gn) if gn is not None else None}
+                self.log(rec)
+            if self.bad_steps >= self.cfg.max_bad_steps:
+                self._pending.clear()
+                raise NonFiniteLoss(f"{self.bad_steps} consecutive non-finite gradient norms at step {r['step']}")
+        self._pending.clear()
 
     def fit(self):
         c = self.cfg
@@ -208,32 +239,42 @@ class Trainer:
         self.maybe_resume()
         prof = None
         dev = self.flat.device
-        t_last = time.perf_counter()
+        cuda = dev.type == "cuda"
+        flush_every = max(1, c.sync_every) if cuda else 1
         while self.step < c.steps:
             s = self.step
             _maybe_inject_fault(s, self.rank)  # test hook: no-op unless SPA_FAULT_STEP is set
             if c.profile_steps and s == c.profile_steps[0]:
                 prof = _start_profiler(c)
+            ev0 = None
+            if cuda:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            t0 = time.perf_counter()
             loss, ntok, ok = self.train_step(s)
+            ev = None
+            if cuda:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
             if prof is not None and s + 1 >= c.profile_steps[1]:
                 prof.stop()
                 prof = None
-            if s % c.log_every == 0 or s == c.steps - 1:
-                if dev.type == "cuda":
-                    torch.cuda.synchronize(dev)
-                now = time.perf_counter()
-                dt = (now - t_last) / (c.log_every if s else 1)
-                t_last = now
-                gn = self.opt.last_grad_norm
-                rec = {"step": s, "loss": loss, "lr": self.lr_at(s), "ok": ok, "dt": dt,
-                       "tok_per_s": ntok * self.world / max(dt, 1e-9),
-                       "grad_norm": float(gn) if gn is not None else None}
-                self.log(rec)
-            if c.eval_every and (s % c.eval_every == 0 and s) or (c.eval_every and s == c.steps - 1):
-                self.log({"step": s, "val_loss": self.evaluate()})
+            gn = self.opt.last_grad_norm
+            self._pending.append({"step": s, "loss": loss, "ok": ok, "gn": gn, "lr": self.lr_at(s), "ntok": ntok,
+                                  "ev0": ev0, "ev": ev, "dt": time.perf_counter() - t0,
+                                  "log": s % c.log_every == 0 or s == c.steps - 1})
+            evals = c.eval_every and ((s % c.eval_every == 0 and s) or s == c.steps - 1)
             self.step += 1
-            if c.ckpt_every and self.step % c.ckpt_every == 0:
-                self.save(loss)
+            ckpt_now = c.ckpt_every and self.step % c.ckpt_every == 0
+            if len(self._pending) >= flush_every or evals or ckpt_now or self.step >= c.steps:
+                self._flush()
+            if evals:
+                v = self.evaluate()
+                if v is not None:
+                    self.log({"step": s, "val_loss": v})
+            if ckpt_now:
+                self.save(float(loss))
+        self._flush()
         self.flat.wait_all()
         if c.ckpt_dir and c.ckpt_every:
             self.save()

@@ -38,7 +38,9 @@ def _worker(rank, world, port, Hkv, causal, q_out):
     ql, kl, vl = (t[:, sl].clone().requires_grad_() for t in (q, k, v))
     o = context_parallel_attention(ql, kl, vl, causal=causal)
     o.backward(do[:, sl])
-    q_out.put((rank, o.detach(), ql.grad, kl.grad, vl.grad))
+    # numpy, not torch tensors: a torch tensor on an mp queue is a shared-memory handle whose
+    # backing file can vanish when this worker exits before the parent reads it
+    q_out.put((rank, o.detach().numpy(), ql.grad.numpy(), kl.grad.numpy(), vl.grad.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -61,7 +63,7 @@ def test_context_parallel_attention_matches_full(Hkv, causal):
     q, k, v = (t.clone().requires_grad_() for t in (q, k, v))
     o = flash_attention(q, k, v, causal=causal)
     o.backward(do)
-    cat = lambda i: torch.cat([r[i] for r in res], dim=1)  # noqa: E731
+    cat = lambda i: torch.cat([torch.from_numpy(r[i]) for r in res], dim=1)  # noqa: E731
     for i, want in ((1, o.detach()), (2, q.grad), (3, k.grad), (4, v.grad)):
         assert torch.allclose(cat(i), want, atol=1e-5, rtol=1e-4), i
 
@@ -81,7 +83,7 @@ def _llama_worker(rank, world, port, q_out):
     for n, p in m.named_parameters():
         g = p.grad.clone()
         dist.all_reduce(g)
-        grads[n] = g / world
+        grads[n] = (g / world).numpy()
     lt = loss.detach().clone()
     dist.all_reduce(lt)
     q_out.put((rank, float(lt) / world, grads))
@@ -110,4 +112,4 @@ def test_llama_context_parallel_matches_single_process():
     _, l_cp, grads = res[0]
     assert abs(l_cp - loss.item()) < 1e-5
     for n, p in m.named_parameters():
-        assert torch.allclose(grads[n], p.grad, atol=1e-5, rtol=1e-4), n
+        assert torch.allclose(torch.from_numpy(grads[n]), p.grad, atol=1e-5, rtol=1e-4), n

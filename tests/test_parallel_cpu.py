@@ -216,12 +216,12 @@ def _ep_worker(rank, world, port, q):
     full.reset_parameters(0.1, torch.Generator().manual_seed(3))
     grp = dist.new_group([0, 1])
     m = ds.MoE(c, ep_group=grp)
-    with torch.no_grad():
-        m.gate.copy_(full.gate)
-        m.w13.copy_(shard_experts(full.w13, rank, world))
-        m.w2.copy_(shard_experts(full.w2, rank, world))
-        m.shared.w13.copy_(full.shared.w13)
-        m.shared.w2.copy_(full.shared.w2)
+    # the EP constructor's own init: rank r holds shard_experts(unsharded init, r, P), i.e.
+    # distinct experts on every rank (not E/P experts drawn again from the shared sequence)
+    m.reset_parameters(0.1, torch.Generator().manual_seed(3))
+    assert torch.equal(m.w13, shard_experts(full.w13, rank, world))
+    assert torch.equal(m.w2, shard_experts(full.w2, rank, world))
+    assert torch.equal(m.gate, full.gate) and torch.equal(m.shared.w13, full.shared.w13)
     x, gy = _moe_inputs()
     xr = x[rank].clone().requires_grad_(True)
     y = m(xr)
@@ -250,3 +250,62 @@ def test_expert_parallel_moe_matches_local():
         assert torch.allclose(torch.from_numpy(g13), full.w13.grad[rank * 2:(rank + 1) * 2], atol=1e-5)
         assert torch.allclose(torch.from_numpy(g2), full.w2.grad[rank * 2:(rank + 1) * 2], atol=1e-5)
         # gate grads are rank-local (DP all-reduces them later)
+
+
+class _NanOnRank(torch.nn.Module):
+    """Wraps a model; rank ``bad_rank`` returns a NaN loss at training step ``bad_step``."""
+
+    def __init__(self, inner, bad_rank, bad_step):
+        super().__init__()
+        self.inner, self.bad_rank, self.bad_step, self.calls = inner, bad_rank, bad_step, 0
+
+    def param_groups(self):
+        return self.inner.param_groups()
+
+    def forward(self, x, y):
+        loss = self.inner(x, y)
+        if self.training:
+            if dist.get_rank() == self.bad_rank and self.calls == self.bad_step:
+                loss = loss * float("nan")
+            self.calls += 1
+        return loss
+
+
+def _nan_worker(rank, world, port, q, zero1):
+    _init(rank, world, port)
+    from solvingpapers_amd.train.trainer import TrainConfig, Trainer
+    m = _NanOnRank(_llama(seed=rank), bad_rank=1, bad_step=1)   # different seeds: broadcast must fix
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, 64, (8, 17), generator=g)
+
+    def batch(i):
+        j = (2 * i + rank) % 4
+        return ids[2 * j:2 * j + 2, :-1], ids[2 * j:2 * j + 2, 1:]
+    tr = Trainer(m, TrainConfig(steps=4, lr=1e-2, zero1=zero1, max_bad_steps=3), batch)
+    snap = {}
+    orig = tr.train_step
+
+    def spy(s):
+        out = orig(s)
+        snap[s] = tr.flat.param.clone()
+        return out
+    tr.train_step = spy
+    tr.fit()
+    oks = [h["ok"] for h in tr.history if "loss" in h]
+    q.put((rank, oks, {k: v.numpy() for k, v in snap.items()}))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("zero1", [False, True])
+def test_nan_on_one_rank_skips_update_on_every_rank(zero1):
+    """a NaN on ONE rank must make EVERY rank skip the same step (no
+    mismatched collectives, no divergence). The skip is decided on the globally reduced grad
+    norm inside the fused optimizer kernel; ranks also start identical (broadcast before the
+    optimizer copies its fp32 master)."""
+    out = _run(_nan_worker, 2, zero1)
+    (_, ok0, s0), (_, ok1, s1) = out
+    assert ok0 == ok1 == [True, False, True, True]
+    for s in range(4):
+        assert (s0[s] == s1[s]).all(), s                  # replicas never diverge
+    assert (s0[1] == s0[0]).all()                          # step 1 applied no update
+    assert not (s0[2] == s0[1]).all()                      # later steps do
