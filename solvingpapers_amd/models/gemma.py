@@ -191,9 +191,23 @@ class GemmaBlock(tnn.Module):
             p.tp_replicated = True
 
     @torch.no_grad()
-    def reset_parameters(self, g):
-        for w in (self.wq, self.wkv, self.wo, self.w13, self.w2):
-            w.normal_(0.0, 0.02, generator=g)
+    def reset_parameters(self, g, tp_rank: int = 0):
+        """Draw the UNSHARDED tensors and keep this TP rank's slice, so a TP=n model starts
+        as the exact shards of the TP=1 model (shard_gemma_from_full); drawing only the local
+        shard from the shared generator would give every rank identical heads / FFN columns
+        that stay symmetric through training."""
+        c, tp = self.c, self.tp
+        H, hd, F, D = c.n_heads, c.head_dim, c.ffn_hidden, c.dim
+        full = {n: torch.empty(shape, device=self.wq.device, dtype=self.wq.dtype).normal_(0.0, 0.02, generator=g)
+                for n, shape in (("wq", (H * hd, D)), ("wkv", tuple(self.wkv.shape)), ("wo", (D, H * hd)),
+                                 ("w13", (2 * F, D)), ("w2", (D, F)))}
+        hl, fl = self.hl * hd, F // tp
+        r = tp_rank
+        self.wq.copy_(full["wq"][r * hl:(r + 1) * hl])
+        self.wkv.copy_(full["wkv"])
+        self.wo.copy_(full["wo"][:, r * hl:(r + 1) * hl])
+        self.w13.copy_(torch.cat([full["w13"][r * fl:(r + 1) * fl], full["w13"][F + r * fl:F + (r + 1) * fl]]))
+        self.w2.copy_(full["w2"][:, r * fl:(r + 1) * fl])
 
     def forward(self, res, delta, tp_group=None, cache=None, pos=0, sp=False):
         """``sp``: sequence parallel -- res/delta are [B, T/tp, D] shards; the TP regions
@@ -264,11 +278,18 @@ class Gemma(tnn.Module):
         self.norm_f.tp_replicated = True
         self.grad_ready_cb = None
         with torch.no_grad():
-            g = torch.Generator(device=self.embed.device).manual_seed(seed + 1000 * self.tp_rank)
-            self.embed.normal_(0.0, 0.02, generator=g)
-            gl = torch.Generator(device=self.embed.device).manual_seed(seed)  # replicated params identical
+            # unsharded draws sliced per TP rank: TP=n init == shards of the TP=1 init
+            g = torch.Generator(device=self.embed.device).manual_seed(seed)
+            vl = c.vocab_size // self.tp
+            if self.tp == 1:
+                self.embed.normal_(0.0, 0.02, generator=g)
+            else:
+                full = torch.empty(c.vocab_size, c.dim, **fk).normal_(0.0, 0.02, generator=g)
+                self.embed.copy_(full[self.tp_rank * vl:(self.tp_rank + 1) * vl])
+                del full
+            gl = torch.Generator(device=self.embed.device).manual_seed(seed)
             for l in self.layers:
-                l.reset_parameters(gl)
+                l.reset_parameters(gl, self.tp_rank)
 
     def param_groups(self):
         return [[self.embed]] + [list(l.parameters()) for l in self.layers] + [[self.norm_f]]

@@ -9,7 +9,8 @@ The reference keeps all 8 experts on every replica and runs them in a Python loo
 2. per-expert counts exchanged with one tiny all-to-all; the split sizes are the only
    host sync (one D2H copy of 2*E ints per MoE layer);
 3. token rows exchanged (``all_to_all_single`` with uneven splits) — they arrive
-   ordered by (source rank, local expert) and are regrouped to (local expert, source);
+   ordered by (source rank, local expert) and are regrouped to (local expert, source)
+   by one device kernel (``regroup_rows``, csrc/kernels/ep.hip; no host loop);
 4. the local experts run as ONE grouped GEMM per projection (csrc/kernels/moe.hip);
 5. the inverse regroup + all-to-all return the rows; ``combine`` applies the gate
    weights in the original token order.
@@ -25,6 +26,7 @@ from types import SimpleNamespace
 import torch
 import torch.distributed as dist
 
+from ..ops._ext import ops
 from ..ops.activation import glu
 from ..ops.moe import combine, gather, grouped_linear, permute
 
@@ -55,21 +57,44 @@ def all_to_all(x, out_splits, in_splits, group):
     return _AllToAll.apply(x, list(out_splits), list(in_splits), group)
 
 
-def _regroup_index(rc):
-    """rc [P, El] rows received from (src, local expert), laid out src-major.
-    Returns (idx, offsets): idx[j] = source row of expert-major position j."""
+def _em_dest(rc):
+    """rc [P, El] rows received from (src, local expert), laid out src-major. Returns, for
+    every received row j, its position in the (local expert, src)-major order (CPU path of
+    the ``ep_regroup`` kernel; vectorised, no per-segment host loop)."""
     P, El = rc.shape
-    starts = torch.cat([rc.new_zeros(1), rc.reshape(-1).cumsum(0)[:-1]]).view(P, El)
-    pieces = []
-    for e in range(El):
-        for s in range(P):
-            n = int(rc[s, e])
-            if n:
-                pieces.append(torch.arange(int(starts[s, e]), int(starts[s, e]) + n))
-    idx = torch.cat(pieces) if pieces else torch.zeros(0, dtype=torch.long)
-    per_e = rc.sum(0)
-    offsets = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
-    return idx, offsets
+    flat = rc.reshape(-1).long()
+    R = int(flat.sum())
+    seg = torch.repeat_interleave(torch.arange(P * El, device=rc.device), flat, output_size=R)
+    sm = torch.cumsum(flat, 0) - flat
+    emc = rc.t().reshape(-1).long()
+    em = (torch.cumsum(emc, 0) - emc).view(El, P).t().reshape(-1)
+    return em[seg] + (torch.arange(R, device=rc.device) - sm[seg])
+
+
+def regroup_rows(x, rc, to_em: bool):
+    """(src, expert)-major rows -> (expert, src)-major (``to_em``) or back. One HIP launch
+    (csrc/kernels/ep.hip) that builds the segment prefix sums on chip from the device count
+    matrix ``rc`` and copies whole rows; CPU tensors use the vectorised index path."""
+    P, El = rc.shape
+    if x.is_cuda:
+        return ops().ep_regroup(x.contiguous(), rc.reshape(-1).long().contiguous(), P, El, bool(to_em))
+    dest = _em_dest(rc)
+    if to_em:
+        y = torch.empty_like(x)
+        y[dest] = x
+        return y
+    return x[dest]
+
+
+class _Regroup(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rc, to_em):
+        ctx.rc, ctx.to_em = rc, to_em
+        return regroup_rows(x, rc, to_em)
+
+    @staticmethod
+    def backward(ctx, g):
+        return regroup_rows(g.contiguous(), ctx.rc, not ctx.to_em), None, None
 
 
 def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
@@ -93,16 +118,15 @@ def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     recv_splits = rc.sum(1).tolist()
     xp = gather(x, plan)                                      # [A, D] sorted by global expert
     xr = all_to_all(xp, recv_splits, send_splits, group)     # [R, D] (src, e_local) order
-    ridx, loff = _regroup_index(rc)
+    per_e = rc.sum(0)
+    loff = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
     dev = x.device
-    ridx = ridx.to(dev)
-    inv = torch.empty_like(ridx)
-    inv[ridx] = torch.arange(ridx.numel(), device=dev)
+    rc_dev = recv.view(P, El)                                # device copy of the counts
     lplan = SimpleNamespace(offsets=loff.to(device=dev, dtype=torch.int32))
-    xl = xr.index_select(0, ridx)
+    xl = _Regroup.apply(xr, rc_dev, True)                    # (src, e) -> (e, src) rows
     h = glu(grouped_linear(xl, W13, lplan, fp8), act)
     yl = grouped_linear(h, W2, lplan, fp8)
-    yr = yl.index_select(0, inv)
+    yr = _Regroup.apply(yl, rc_dev, False)
     yp = all_to_all(yr, send_splits, recv_splits, group)
     return combine(yp, w, plan), plan
 

@@ -18,6 +18,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import embedding, linear_cross_entropy
+from ..ops.xent import chunked_linear_cross_entropy
 
 
 def tp_rank_size(group):
@@ -173,53 +174,18 @@ def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=F
     return reduce_scatter_seq(x, group) if sequence_parallel else reduce_from_tp(x, group)
 
 
-class _VocabParallelXent(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, h, w_local, target, group):
-        rank, tp = tp_rank_size(group)
-        vl = w_local.shape[0]
-        lo = rank * vl
-        logits = torch.mm(h, w_local.t()).float()                        # [N, V/tp]
-        lmax = logits.amax(-1)
-        dist.all_reduce(lmax, op=dist.ReduceOp.MAX, group=group)
-        sexp = torch.exp(logits - lmax[:, None]).sum(-1)
-        dist.all_reduce(sexp, group=group)
-        lse = lmax + sexp.log()
-        inside = (target >= lo) & (target < lo + vl)
-        tl = torch.where(inside, target - lo, torch.zeros_like(target))
-        tlogit = logits.gather(1, tl[:, None]).squeeze(1) * inside
-        dist.all_reduce(tlogit, group=group)
-        N = h.shape[0]
-        loss = (lse - tlogit).mean()
-        G = torch.exp(logits - lse[:, None])
-        G[torch.arange(N, device=h.device)[inside], tl[inside]] -= 1.0
-        G = (G / N).to(h.dtype)
-        ctx.save_for_backward(h, w_local, G)
-        ctx.group = group
-        return loss
+def vocab_parallel_cross_entropy(h, w_local, target, group, chunk_cols=None):
+    """mean CE(h @ W^T, target) with W sharded by rows (vocab) over the TP group.
 
-    @staticmethod
-    def backward(ctx, g):
-        from ..utils.grad import commit
-        h, w, G = ctx.saved_tensors
-        G = G * g.to(G.dtype)
-        dh = _ar(torch.mm(G, w), ctx.group)                              # h is replicated: sum partials
-
-        def _w(out, acc):
-            if out is None:
-                return torch.mm(G.t(), h)
-            if acc:
-                out.addmm_(G.t(), h)
-            else:
-                torch.mm(G.t(), h, out=out)
-        return dh, commit(w, _w), None, None
-
-
-def vocab_parallel_cross_entropy(h, w_local, target, group):
-    """mean CE(h @ W^T, target) with W sharded by rows (vocab) over the TP group."""
+    Runs the vocab-chunked fused head (ops/xent.py ``_ChunkedLinearXent``, HIP kernels
+    ``xent_chunk_stats`` / ``xent_chunk_grad_``): per rank only a [N, Vc] chunk of its local
+    logits is ever live, and the ranks exchange [N]-float statistics (row max, then
+    sum-exp / target logit / logit sum in one packed all-reduce) -- never logits. Backward
+    recomputes the chunks, writes dlogits in place into the dW / dh GEMMs and all-reduces the
+    [N, D] dh partials (h is replicated over TP)."""
     if tp_rank_size(group)[1] == 1:
         return linear_cross_entropy(h, w_local, target)
-    return _VocabParallelXent.apply(h, w_local, target, group)
+    return chunked_linear_cross_entropy(h, w_local, target, group=group, chunk_cols=chunk_cols)
 
 
 def gather_vocab_logits(logits_local, group):

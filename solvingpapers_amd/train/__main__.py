@@ -6,6 +6,8 @@
     python -m solvingpapers_amd.train dsv3    --preset dsv3_ref --ckpt-dir ck/
     python -m solvingpapers_amd.train vit | ae | vae | kd
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m solvingpapers_amd.train llama3 --preset llama3_8b ...
+    torchrun --nproc-per-node 8 ... -m solvingpapers_amd.train gemma --preset gemma_7b_mqa --tp 8 --sp
+    torchrun --nproc-per-node 8 ... -m solvingpapers_amd.train dsv3 --preset dsv3_style --ep 8
 
 Model hyper-parameters can be overridden with ``--set key=value`` (config dataclass
 fields). Language models train through train/trainer.py (data parallel over RCCL when
@@ -57,8 +59,16 @@ def _lm(args, info):
     from ..data.loader import NativeTokenLoader
     from ..data.text import synthetic_corpus
     from ..models import deepseekv3, gemma, gpt, llama3
+    from ..parallel.groups import build_groups
     from .trainer import TrainConfig, Trainer
     dev = info.device if args.device is None else torch.device(args.device)
+    # world = tp x data, data = ep x expert-dp (parallel/groups.py); the data loader shards by the
+    # DATA coordinate: TP peers read the same batch, DP/EP ranks different ones
+    pg = build_groups(args.tp, args.ep)
+    if args.tp > 1 and args.model != "gemma":
+        raise SystemExit("--tp is implemented for gemma (Megatron column/row-parallel + vocab-parallel CE)")
+    if args.ep > 1 and args.model != "dsv3":
+        raise SystemExit("--ep is implemented for dsv3 (MoE all-to-all dispatch)")
     dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.dtype or ("bf16" if dev.type == "cuda" else "fp32")]
     sets = _parse_sets(args.set)
     char = args.preset in ("gpt_ref", "gpt_tiny_cpu", "gemma_ref")
@@ -84,14 +94,17 @@ def _lm(args, info):
         pre = args.preset or "gemma_ref"
         c = gemma.config(pre, **sets)
         if pre == "gemma_ref":
+            if args.tp > 1:
+                raise SystemExit("gemma_ref (reference-parity model) runs unsharded; use gemma_tiny / gemma_7b_mqa")
             model = gemma.GemmaRef(c).to(device=dev, dtype=dtype)
             V, T, B = c.vocab_size, c.block_size, c.batch_size
         else:
-            model = gemma.Gemma(c, device=dev, dtype=dtype, seed=args.seed)
+            model = gemma.Gemma(c, device=dev, dtype=dtype, seed=args.seed, tp_group=pg.tp_group,
+                                sequence_parallel=args.sp)
             V, T, B = c.vocab_size, args.seq or c.max_seq_len, c.batch_size
     elif fam == "dsv3":
         c = deepseekv3.config(args.preset or "dsv3_ref", **sets)
-        model = deepseekv3.DeepSeekV3(c, device=dev, dtype=dtype, seed=args.seed)
+        model = deepseekv3.DeepSeekV3(c, device=dev, dtype=dtype, seed=args.seed, ep_group=pg.ep_group)
         V, T, B = c.vocab_size, c.block_size, c.batch_size
     else:
         raise SystemExit(f"unknown model {fam}")
@@ -102,28 +115,27 @@ def _lm(args, info):
         # second file the eval batches are drawn from the training file with another seed
         from ..data.bpe import token_file_dtype
         fd = [torch.int32 if token_file_dtype(f) == "int32" else torch.uint16 for f in files]
-        tr = NativeTokenLoader(files[0], B, T, seed=args.seed, rank=info.rank, world=info.world_size, device=dev,
+        tr = NativeTokenLoader(files[0], B, T, seed=args.seed, rank=pg.dp_rank, world=pg.dp, device=dev,
                                file_dtype=fd[0])
-        ev = NativeTokenLoader(files[-1], B, T, seed=args.seed + 1, rank=info.rank, world=info.world_size,
+        ev = NativeTokenLoader(files[-1], B, T, seed=args.seed + 1, rank=pg.dp_rank, world=pg.dp,
                                device=dev, file_dtype=fd[-1])
     else:
         if not char:
             stream = torch.randint(0, V, (max(200_000, 4 * B * (T + 1)),),
                                    generator=torch.Generator().manual_seed(args.seed), dtype=torch.int32)
         n = int(stream.numel() * 0.9)
-        tr = NativeTokenLoader(stream[:n], B, T, seed=args.seed, rank=info.rank, world=info.world_size, device=dev)
-        ev = NativeTokenLoader(stream[n:], B, T, seed=args.seed + 1, rank=info.rank, world=info.world_size,
-                               device=dev)
+        tr = NativeTokenLoader(stream[:n], B, T, seed=args.seed, rank=pg.dp_rank, world=pg.dp, device=dev)
+        ev = NativeTokenLoader(stream[n:], B, T, seed=args.seed + 1, rank=pg.dp_rank, world=pg.dp, device=dev)
     tc = TrainConfig(steps=args.steps, lr=args.lr, min_lr=args.min_lr, warmup=args.warmup,
                      weight_decay=args.weight_decay, clip=args.clip, eval_every=args.eval_every,
                      eval_iters=args.eval_iters, ckpt_dir=args.ckpt_dir, ckpt_every=args.ckpt_every,
                      log_path=args.log, grad_accum=args.accum, zero1=args.zero1, optimizer=args.optimizer,
-                     grad_dtype=dtype)
+                     grad_dtype=dtype, log_every=args.log_every)
     hooks = [lambda r: print(json.dumps(r), flush=True)] if info.rank == 0 else []
     if info.rank == 0 and args.wandb:
         from .metrics import WandbHook
-        hooks.append(WandbHook(args.wandb, config=vars(args), tokens_per_step=B * T * args.accum * info.world_size))
-    trainer = Trainer(model, tc, tr, ev.batch_at, hooks=hooks)
+        hooks.append(WandbHook(args.wandb, config=vars(args), tokens_per_step=B * T * args.accum * pg.dp))
+    trainer = Trainer(model, tc, tr, ev.batch_at, hooks=hooks, groups=pg)
     trainer.fit()
     return trainer
 
@@ -170,6 +182,10 @@ def main(argv=None):
     ap.add_argument("--ckpt-every", type=int, default=0)
     ap.add_argument("--log", default=None)
     ap.add_argument("--zero1", action="store_true")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (gemma)")
+    ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism with --tp")
+    ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree (dsv3)")
+    ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--device", default=None)
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"])
     ap.add_argument("--mnist-root", default=None)

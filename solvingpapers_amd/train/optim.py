@@ -251,8 +251,8 @@ def FlatAdam(flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_
 
 class FlatSGD(FlatOptimizer):
     def __init__(self, flat, lr=1e-3, momentum=0.0, weight_decay=0.0, max_grad_norm=None, shard=None,
-                 graph_safe=False):
-        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, graph_safe=graph_safe)
+                 graph_safe=False, ep_group=None, tp_group=None):
+        super().__init__(flat, lr, weight_decay, max_grad_norm, shard, ep_group, tp_group, graph_safe=graph_safe)
         self.momentum = momentum
         self.buf = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device) if momentum else None
 

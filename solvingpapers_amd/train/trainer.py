@@ -71,11 +71,20 @@ class NonFiniteLoss(RuntimeError):
 class Trainer:
     def __init__(self, model, cfg: TrainConfig, train_batch: Callable[[int], tuple],
                  eval_batch: Optional[Callable[[int], tuple]] = None, dp_group=None, ep_group=None,
-                 expert_dp_group=None, hooks: Iterable[Callable] = ()):
+                 expert_dp_group=None, hooks: Iterable[Callable] = (), tp_group=None, groups=None):
+        """``groups`` (parallel/groups.py ProcessGroups) sets dp/tp/ep/expert-dp groups at once:
+        dense gradients are averaged over ``dp_group``, expert gradients summed over
+        ``expert_dp_group`` (then / dp), the grad norm reduced over TP and EP as needed."""
         self.model, self.cfg = model, cfg
         self.train_batch, self.eval_batch = train_batch, eval_batch
+        self.groups = groups
+        if groups is not None:
+            dp_group, tp_group = groups.dp_group, groups.tp_group
+            ep_group, expert_dp_group = groups.ep_group, groups.expert_dp_group
         self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.dp_size = (dist.get_world_size(dp_group) if dp_group is not None else self.world) \
+            if self.world > 1 else 1
         groups = model.param_groups() if hasattr(model, "param_groups") else None
         self.flat = FlatParams(model, groups=groups, align=64 * max(1, self.world),
                                grad_dtype=cfg.grad_dtype, param_dtype=cfg.param_dtype)
@@ -89,10 +98,10 @@ class Trainer:
         if cfg.optimizer in ("adamw", "adam"):
             self.opt = FlatAdamW(self.flat, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
                                  max_grad_norm=cfg.clip, adam_l2=cfg.optimizer == "adam", shard=shard,
-                                 ep_group=ep_group)
+                                 ep_group=ep_group, tp_group=tp_group)
         elif cfg.optimizer == "sgd":
             self.opt = FlatSGD(self.flat, lr=cfg.lr, weight_decay=cfg.weight_decay, max_grad_norm=cfg.clip,
-                               shard=shard)
+                               shard=shard, ep_group=ep_group, tp_group=tp_group)
         else:
             raise ValueError(cfg.optimizer)
         for m in getattr(model, "moe_layers", lambda: [])():
@@ -131,8 +140,10 @@ class Trainer:
             return None
         self.flat.wait_all()
         # saved step = index of the last completed step; resume continues at step + 1
-        return ckpt.save(self.cfg.ckpt_dir, self.step - 1, self.flat, self.opt, self.buffers(),
-                         extra={"loss": loss, "config": {k: str(v) for k, v in asdict(self.cfg).items()}},
+        extra = {"loss": loss, "config": {k: str(v) for k, v in asdict(self.cfg).items()}}
+        if self.groups is not None:
+            extra["layout"] = self.groups.layout()
+        return ckpt.save(self.cfg.ckpt_dir, self.step - 1, self.flat, self.opt, self.buffers(), extra=extra,
                          keep=self.cfg.keep)
 
     def maybe_resume(self):
@@ -143,6 +154,9 @@ class Trainer:
         if not path:
             return False
         info = ckpt.load(path, self.flat, self.opt, self.buffers())
+        saved = info["extra"].get("layout") if isinstance(info.get("extra"), dict) else None
+        if self.groups is not None and saved is not None and saved != self.groups.layout():
+            raise RuntimeError(f"checkpoint layout {saved} != running layout {self.groups.layout()}")
         self.step = info["step"] + 1
         return True
 
@@ -225,7 +239,7 @@ class Trainer:
                     dt = r["dt"]
                 gn = r["gn"]
                 rec = {"step": r["step"], "loss": float(r["loss"]) if ok else float("nan"), "lr": r["lr"],
-                       "ok": ok, "dt": dt, "tok_per_s": r["ntok"] * self.world / max(dt, 1e-9),
+                       "ok": ok, "dt": dt, "tok_per_s": r["ntok"] * self.dp_size / max(dt, 1e-9),
                        "grad_norm": float(gn) if gn is not None else None}
                 self.log(rec)
             if self.bad_steps >= self.cfg.max_bad_steps:

@@ -163,3 +163,28 @@ def test_gradcheck_fp64(name):
         fn = lambda a, w, b: misc.patch_embed(a, w, b, 4)  # noqa: E731
         args = (_req(2, 3, 8, 8), _req(5, 3, 4, 4), _req(5))
     assert gradcheck(fn, args, eps=1e-6, atol=1e-5)
+
+
+def test_chunked_linear_cross_entropy_matches_torch():
+    """ops/xent.py vocab-chunked fused head: loss and dh / dW / db equal
+    F.cross_entropy on materialised logits, across chunk sizes (one chunk, ragged last
+    chunk), label smoothing and ignored rows."""
+    import torch.nn.functional as F
+    from solvingpapers_amd.ops.xent import chunked_linear_cross_entropy
+    g = torch.Generator().manual_seed(0)
+    N, D, V = 24, 16, 1000
+    h0 = torch.randn(N, D, generator=g, dtype=torch.float64)
+    w0 = torch.randn(V, D, generator=g, dtype=torch.float64) * 0.3
+    b0 = torch.randn(V, generator=g, dtype=torch.float64) * 0.1
+    t = torch.randint(0, V, (N,), generator=g)
+    t[3] = -100
+    for chunk, sm in ((256, 0.0), (384, 0.1), (1000, 0.0)):
+        ref_args = [x.clone().requires_grad_() for x in (h0, w0, b0)]
+        ref = F.cross_entropy(F.linear(*ref_args), t, ignore_index=-100, label_smoothing=sm)
+        ref.backward()
+        args = [x.clone().requires_grad_() for x in (h0, w0, b0)]
+        loss = chunked_linear_cross_entropy(args[0], args[1], t, bias=args[2], label_smoothing=sm, chunk_cols=chunk)
+        (loss * 2.0).backward()
+        assert torch.allclose(loss, ref, atol=1e-10), (chunk, loss, ref)
+        for a, r in zip(args, ref_args):
+            assert torch.allclose(a.grad, 2.0 * r.grad, atol=1e-10), chunk
