@@ -1,0 +1,172 @@
+// Device helpers shared by the flash-attention kernels (attention.hip) and the wide-head
+// kernels (attention_wide.hip): MFMA 32x32x16 bf16 wrappers, the accumulator -> operand
+// packing, the swizzled LDS images with row (ds_read_b128) and transposed
+// (ds_read_b64_tr_b16) reads, and the register-staged tile loader.
+#pragma once
+#include "spa_common.h"
+#include <type_traits>
+
+namespace spa {
+
+// LDS image row width for a head dim: 192-wide rows are staged in 256-wide image rows
+template <int HD> constexpr int img_w() { return HD == 192 ? 256 : HD; }
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// deferred-rescale threshold in log2 units (T13): P = 2^(s*c - m) <= 2^8
+constexpr float kRescaleThr = 8.f;
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// max of x over lanes l and l^32 (one v_permlane32_swap, no LDS)
+__device__ __forceinline__ float halfmax(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halfsum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+  return z;
+}
+__device__ __forceinline__ f32x16 splat16(float v) {
+  f32x16 a;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a[r] = v;
+  return a;
+}
+// accumulator registers 8s..8s+7 -> bf16 operand fragment (permuted k order)
+__device__ __forceinline__ bf16x8 pack_acc(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+// ---- swizzled row-major [rows][HD] bf16 LDS images -------------------------
+template <int HD>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (HD >= 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+}
+template <int HD>
+__device__ __forceinline__ int img_off(int r, int ch) {  // element offset of 16B chunk ch of row r
+  return r * HD + 8 * (ch ^ swz<HD>(r));
+}
+// A/B operand "X^T" for one 16-deep k-step, where X is the row-major image with
+// rows = k index, columns = output index. Lane l gets X[r0 + 16s + perm(j)][c0 + (l&31)].
+template <int HD>
+__device__ __forceinline__ bf16x8 rd_tr(const bf16* img, int rbase, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3, hh = lane >> 5;
+  const int c = c0 + 16 * (g & 1) + 4 * pp;  // column (element) this lane addresses
+  const int ch = c >> 3, within = c & 7;
+  const int ra = rbase + 4 * hh + q, rb = ra + 8;
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4*)(img + ra * HD + 8 * (ch ^ swz<HD>(ra)) + within));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4*)(img + rb * HD + 8 * (ch ^ swz<HD>(rb)) + within));
+  // whole-vector bit casts: element-wise short->bf16 inserts miscompile (duplicated dwords)
+  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
+  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Per-lane LDS element offsets, computed once per kernel (the swizzle term is
+// invariant under the +32-row / +16-row steps of the loops, which become
+// immediate offsets): row reads (row = lane&31, chunk = 2ks + half) and the
+// two halves of each transposed read (k-step rows 0..15, d-tile dt).
+template <int HD>
+struct LdsOff {
+  int row[HD / 16];
+  int tra[HD / 32], trb[HD / 32];
+  __device__ __forceinline__ void init(int lane) {
+    const int l32 = lane & 31, hh = lane >> 5, g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int ks = 0; ks < HD / 16; ++ks) row[ks] = l32 * HD + 8 * ((2 * ks + hh) ^ swz<HD>(l32));
+    const int ra = 4 * hh + q, rb = ra + 8;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt) {
+      const int c = 32 * dt + 16 * (g & 1) + 4 * pp;
+      const int ch = c >> 3, within = c & 7;
+      tra[dt] = ra * HD + 8 * (ch ^ swz<HD>(ra)) + within;
+      trb[dt] = rb * HD + 8 * (ch ^ swz<HD>(rb)) + within;
+    }
+  }
+};
+__device__ __forceinline__ bf16x8 ld_row(const bf16* img, int off) {
+  return *reinterpret_cast<const bf16x8*>(img + off);
+}
+__device__ __forceinline__ bf16x8 ld_tr(const bf16* img, int offa, int offb) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + offa));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + offb));
+  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
+  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <int V> using IC = std::integral_constant<int, V>;
+
+// Register-staged tile loader: ROWS x HDC bf16 tile of a strided tensor -> regs -> LDS image
+// with IW-element rows (IW = img_w<HDC>, >= HDC).
+// Global side: one buffer descriptor per tile (scalar work), its range ending at the
+// tensor's last valid row, so rows >= nrows load as zeros without a branch. The per-lane
+// byte offsets and LDS offsets are loop invariant (computed once).
+// Thread -> chunk map: W = min(IW/8, 16) lanes share a row, a lane takes the chunk
+// columns ch, ch+16, ... of its row (IW = 256: two; chunks >= HDC/8 of a 192-wide row are
+// never loaded) and rows rr, rr+R, ... (R = NT/W, a multiple of 16). The XOR swizzle only
+// touches the low 4 chunk bits and repeats every 16 rows, so all of a lane's LDS offsets are
+// one register + immediates; on the global side each row pass gets its own scalar descriptor
+// and the column step is the instruction offset.
+template <int HDC, int ROWS, int NT>
+struct TileLoader {
+  static constexpr int IW = img_w<HDC>();
+  static constexpr int CPR = IW / 8;                   // 16B chunks per image row
+  static constexpr int W = CPR < 16 ? CPR : 16;        // lanes per row
+  static constexpr int NC = CPR / W;                   // column chunks per lane (16 apart)
+  static constexpr int R = NT / W;                     // rows between a lane's row passes
+  static constexpr int NP = ROWS / R;                  // row passes
+  static constexpr int CH = NP * NC;
+  static_assert(R % 16 == 0 && ROWS % R == 0 && NP >= 1, "tile/threads mismatch");
+  bf16x8 r[CH];
+  int voff;  // byte offset of this lane's first chunk within its row pass
+  int loff;  // element offset of this lane's first chunk in the LDS image
+  int ch;    // this lane's first chunk column
+  __device__ __forceinline__ void init(long stride, int tid) {
+    const int rr = tid / W;
+    ch = tid % W;
+    voff = (int)(((long)rr * stride + ch * 8) * 2);
+    loff = img_off<IW>(rr, ch);
+  }
+  __device__ __forceinline__ bool valid(int j) const { return HDC == IW || ch + 16 * j < HDC / 8; }
+  __device__ __forceinline__ void load(const bf16* base, long stride, int row0, int nrows) {
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps) {
+      const int r0 = row0 + ps * R;
+      const int left = nrows - r0;
+      const int bytes = left > 0 ? (int)(((long)(left - 1) * stride + HDC) * 2) : 0;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)r0 * stride), 0, bytes, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (valid(j))
+          r[ps * NC + j] =
+              __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 256 * j, 0, 0));
+    }
+  }
+  __device__ __forceinline__ void store(bf16* img) const {
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (valid(j)) *reinterpret_cast<bf16x8*>(img + loff + ps * R * IW + 128 * j) = r[ps * NC + j];
+  }
+};
+
+
+}  // namespace spa

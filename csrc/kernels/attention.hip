@@ -35,10 +35,20 @@
 //    also produces delta = rowsum(dO*O)) then dkdv (key-parallel, loops the GQA
 //    group's q-heads so dK/dV of a kv-head are summed in registers). An optional
 //    fused variant (dkdv<..., FUSEDQ>) adds dQ += dS K with fp32 atomics.
+//  * q/k and v may have different head dims (HDK, HDV): DeepSeek-V3 MLA trains with
+//    q/k = 128 nope + 64 rope = 192 and v = 128, run here with no zero padding (KS = HDK/16
+//    k-steps for S, HDV/32 output tiles for O; a 192-wide row is staged in a 256-wide LDS
+//    row so one swizzle serves every image).
+//  * Attention-probability dropout (gpt/gpt-jax.ipynb:351, gemma/gemma.ipynb:248,
+//    deepseekv3/deepseekv3.ipynb:1186) is fused: the keep mask of element (b, h, q, key) is a
+//    32-bit counter hash of (seed, b, h, q, key), regenerated bit-identically by the forward
+//    (query on the lane) and by both backward kernels (key on the lane) -- no (T, T) mask is
+//    ever stored. P's row sum (the softmax normaliser, the lse) is taken BEFORE the mask;
+//    O = (P * M / (1-p)) V, and the backward uses dS = P * (M * dP / (1-p) - delta) with
+//    delta = rowsum(dO * O) unchanged.
 // q/k/v/o and grads are addressed with (batch, seq, head) strides so the kernels
 // read/write a fused [B, T, H + 2*Hkv, hd] qkv buffer in place.
-#include "spa_common.h"
-#include <type_traits>
+#include "attn_common.h"
 
 namespace spa {
 
@@ -57,167 +67,36 @@ struct AttnParams {
   // each summing G/hsplit q-heads into fp32 partials dkacc/dvacc [hsplit, B, Tk, Hkv, HD]
   int hsplit;
   float* dkacc; float* dvacc;
+  // fused dropout on P (DROP kernels): keep iff hash(seed, b, h, q, key) >> 8 >= drop_thr
+  unsigned seed_lo, seed_hi, drop_thr;
+  float drop_scale;  // 1 / (1 - p)
 };
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-// deferred-rescale threshold in log2 units (T13): P = 2^(s*c - m) <= 2^8
-constexpr float kRescaleThr = 8.f;
-
-__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+// ---- dropout counter hash (bit-identical in ops/attention.py dropout_keep_mask) ------
+__device__ __forceinline__ unsigned mix32(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
 }
-__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
-// max of x over lanes l and l^32 (one v_permlane32_swap, no LDS)
-__device__ __forceinline__ float halfmax(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+// per (b, h) stream
+__device__ __forceinline__ unsigned drop_base(const AttnParams& p, int b, int h) {
+  return mix32(p.seed_lo ^ mix32(p.seed_hi + (unsigned)(b * p.H + h) * 0x9E3779B9U));
 }
-__device__ __forceinline__ float halfsum(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ bf16x8 zero8() {
-  bf16x8 z;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
-  return z;
-}
-__device__ __forceinline__ f32x16 splat16(float v) {
-  f32x16 a;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) a[r] = v;
-  return a;
-}
-// accumulator registers 8s..8s+7 -> bf16 operand fragment (permuted k order)
-__device__ __forceinline__ bf16x8 pack_acc(const f32x16& a, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
-  return r;
+__device__ __forceinline__ bool drop_keep(unsigned base, int q, int key, unsigned thr) {
+  return (mix32(base + (unsigned)q * 0x85EBCA6BU + (unsigned)key * 0xC2B2AE35U) >> 8) >= thr;
 }
 
-// ---- swizzled row-major [rows][HD] bf16 LDS images -------------------------
-template <int HD>
-__device__ __forceinline__ int swz(int r) {
-  if constexpr (HD >= 128) return ((r & 3) << 2) | ((r >> 2) & 3);
-  else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
-}
-template <int HD>
-__device__ __forceinline__ int img_off(int r, int ch) {  // element offset of 16B chunk ch of row r
-  return r * HD + 8 * (ch ^ swz<HD>(r));
-}
-// A/B operand "X^T" for one 16-deep k-step, where X is the row-major image with
-// rows = k index, columns = output index. Lane l gets X[r0 + 16s + perm(j)][c0 + (l&31)].
-template <int HD>
-__device__ __forceinline__ bf16x8 rd_tr(const bf16* img, int rbase, int c0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3, hh = lane >> 5;
-  const int c = c0 + 16 * (g & 1) + 4 * pp;  // column (element) this lane addresses
-  const int ch = c >> 3, within = c & 7;
-  const int ra = rbase + 4 * hh + q, rb = ra + 8;
-  typedef __attribute__((address_space(3))) s16x4 lds_s4;
-  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s4*)(img + ra * HD + 8 * (ch ^ swz<HD>(ra)) + within));
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s4*)(img + rb * HD + 8 * (ch ^ swz<HD>(rb)) + within));
-  // whole-vector bit casts: element-wise short->bf16 inserts miscompile (duplicated dwords)
-  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
-  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-// Per-lane LDS element offsets, computed once per kernel (the swizzle term is
-// invariant under the +32-row / +16-row steps of the loops, which become
-// immediate offsets): row reads (row = lane&31, chunk = 2ks + half) and the
-// two halves of each transposed read (k-step rows 0..15, d-tile dt).
-template <int HD>
-struct LdsOff {
-  int row[HD / 16];
-  int tra[HD / 32], trb[HD / 32];
-  __device__ __forceinline__ void init(int lane) {
-    const int l32 = lane & 31, hh = lane >> 5, g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
-#pragma unroll
-    for (int ks = 0; ks < HD / 16; ++ks) row[ks] = l32 * HD + 8 * ((2 * ks + hh) ^ swz<HD>(l32));
-    const int ra = 4 * hh + q, rb = ra + 8;
-#pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt) {
-      const int c = 32 * dt + 16 * (g & 1) + 4 * pp;
-      const int ch = c >> 3, within = c & 7;
-      tra[dt] = ra * HD + 8 * (ch ^ swz<HD>(ra)) + within;
-      trb[dt] = rb * HD + 8 * (ch ^ swz<HD>(rb)) + within;
-    }
-  }
-};
-__device__ __forceinline__ bf16x8 ld_row(const bf16* img, int off) {
-  return *reinterpret_cast<const bf16x8*>(img + off);
-}
-__device__ __forceinline__ bf16x8 ld_tr(const bf16* img, int offa, int offb) {
-  typedef __attribute__((address_space(3))) s16x4 lds_s4;
-  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + offa));
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + offb));
-  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
-  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-template <int V> using IC = std::integral_constant<int, V>;
-
-// Register-staged tile loader: ROWS x HD bf16 tile of a strided tensor -> regs -> LDS image.
-// Global side: one buffer descriptor per tile (scalar work), its range ending at the
-// tensor's last valid row, so rows >= nrows load as zeros without a branch. The per-lane
-// byte offsets and LDS offsets are loop invariant (computed once).
-// Thread -> chunk map: W = min(HD/8, 16) lanes share a row, a lane takes the chunk
-// columns ch, ch+16, ... of its row (HD = 256: two) and rows rr, rr+R, ... (R = NT/W,
-// a multiple of 16). The XOR swizzle only touches the low 4 chunk bits and repeats
-// every 16 rows, so all of a lane's LDS offsets are one register + immediates; on the
-// global side each row pass gets its own scalar descriptor and the column step is the
-// instruction offset.
-template <int HD, int ROWS, int NT>
-struct TileLoader {
-  static constexpr int CPR = HD / 8;                   // 16B chunks per row
-  static constexpr int W = CPR < 16 ? CPR : 16;        // lanes per row
-  static constexpr int NC = CPR / W;                   // column chunks per lane (16 apart)
-  static constexpr int R = NT / W;                     // rows between a lane's row passes
-  static constexpr int NP = ROWS / R;                  // row passes
-  static constexpr int CH = NP * NC;
-  static_assert(R % 16 == 0 && ROWS % R == 0 && NP >= 1, "tile/threads mismatch");
-  bf16x8 r[CH];
-  int voff;  // byte offset of this lane's first chunk within its row pass
-  int loff;  // element offset of this lane's first chunk in the LDS image
-  __device__ __forceinline__ void init(long stride, int tid) {
-    const int rr = tid / W, ch = tid % W;
-    voff = (int)(((long)rr * stride + ch * 8) * 2);
-    loff = img_off<HD>(rr, ch);
-  }
-  __device__ __forceinline__ void load(const bf16* base, long stride, int row0, int nrows) {
-#pragma unroll
-    for (int ps = 0; ps < NP; ++ps) {
-      const int r0 = row0 + ps * R;
-      const int left = nrows - r0;
-      const int bytes = left > 0 ? (int)(((long)(left - 1) * stride + HD) * 2) : 0;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)r0 * stride), 0, bytes, 0x00020000);
-#pragma unroll
-      for (int j = 0; j < NC; ++j)
-        r[ps * NC + j] =
-            __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 256 * j, 0, 0));
-    }
-  }
-  __device__ __forceinline__ void store(bf16* img) const {
-#pragma unroll
-    for (int ps = 0; ps < NP; ++ps)
-#pragma unroll
-      for (int j = 0; j < NC; ++j)
-        *reinterpret_cast<bf16x8*>(img + loff + ps * R * HD + 128 * j) = r[ps * NC + j];
-  }
-};
 
 // ---------------------------------------------------------------------------
-// Forward: block = NW waves x 32 query rows; K/V tiles of 64 keys.
+// Forward: block = NW waves x 32 query rows; K/V tiles of BN keys.
 // ---------------------------------------------------------------------------
-template <int HD, int NW, bool CAUSAL>
+template <int HDK, int HDV> constexpr int attn_bn() { return (HDK >= 256 || HDV >= 256) ? 32 : 64; }
+
+template <int HDK, int HDV, int NW, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
-  constexpr int BN = HD >= 256 ? 32 : 64, NSUB = BN / 32, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
-  constexpr int TILE = BN * HD;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][K|V]
+  constexpr int BN = attn_bn<HDK, HDV>(), NSUB = BN / 32, BM = 32 * NW, KS = HDK / 16, DT = HDV / 32;
+  constexpr int NT = NW * 64, IK = img_w<HDK>(), IV = img_w<HDV>();
+  constexpr int TK = BN * IK, TV = BN * IV, TB = TK + TV;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TB];  // [buf][K|V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lq = lane & 31, hh = lane >> 5;
   const int nqb = cdiv(p.Tq, BM);
@@ -230,6 +109,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
   const float c = p.scale_log2;
+  unsigned dbase = 0;
+  if constexpr (DROP) dbase = drop_base(p, b, h);
 
   bf16x8 qf[KS];
   {
@@ -249,19 +130,22 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
 
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
   const bf16* vbase = p.v + b * p.svb + hk * p.svh;
-  TileLoader<HD, BN, NT> lk, lv;
+  TileLoader<HDK, BN, NT> lk;
+  TileLoader<HDV, BN, NT> lv;
   lk.init(p.skt, tid);
   lv.init(p.svt, tid);
   if (ntiles > 0) {
     lk.load(kbase, p.skt, 0, p.Tk);
     lv.load(vbase, p.svt, 0, p.Tk);
     lk.store(smem);
-    lv.store(smem + TILE);
+    lv.store(smem + TK);
     if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk); lv.load(vbase, p.svt, BN, p.Tk); }
   }
   __syncthreads();
-  LdsOff<HD> off;
-  off.init(lane);
+  LdsOff<IK> offk;
+  LdsOff<IV> offv;
+  offk.init(lane);
+  offv.init(lane);
   // causal / tail mask of one 32-key sub-tile (keys k0..k0+31): only on diagonal / tail
   // tiles, and kept apart from the softmax so the O-rescale code exists once (two merged
   // copies made hipcc re-home all of O with 64 v_mov per sub-tile)
@@ -299,34 +183,43 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     }
     l += ls;
   };
+  // P -> P * M / (1-p): after the row sum, so the normaliser (and the lse) is the undropped one
+  auto dropout = [&](f32x16& s, const int k0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      s[r] = drop_keep(dbase, q, key, p.drop_thr) ? s[r] * p.drop_scale : 0.f;
+    }
+  };
   // body(j, buffer) with the buffer a compile-time constant (loop unrolled x2) so
   // every LDS address is a precomputed lane offset + an immediate
   auto body = [&](const int j, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     const int k0 = j * BN;
-    const bf16* Ks = smem + BUF * 2 * TILE;
-    const bf16* Vs = Ks + TILE;
+    const bf16* Ks = smem + BUF * TB;
+    const bf16* Vs = Ks + TK;
     if (j + 1 < ntiles) {
-      bf16* Kn = smem + (1 - BUF) * 2 * TILE;
+      bf16* Kn = smem + (1 - BUF) * TB;
       lk.store(Kn);
-      lv.store(Kn + TILE);
+      lv.store(Kn + TK);
       if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk); }
     }
 #pragma unroll
     for (int t = 0; t < NSUB; ++t) {
       const int ks0 = k0 + 32 * t;
       if (ks0 < wave_kend) {
-        f32x16 s = mfma32(ld_row(Ks + 32 * t * HD, off.row[0]), qf[0], splat16(0.f));
+        f32x16 s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[0]), qf[0], splat16(0.f));
 #pragma unroll
-        for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s);
+        for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[ks]), qf[ks], s);
         const bool need_mask = (ks0 + 32 > p.Tk) || (CAUSAL && ks0 + 31 > q0 + p.causal_off);
         if (need_mask) mask(s, ks0);
         softmax(s);
+        if constexpr (DROP) dropout(s, ks0);
         const bf16x8 pa = pack_acc(s, 0), pb = pack_acc(s, 1);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          o[dt] = mfma32(ld_tr(Vs + 32 * t * HD, off.tra[dt], off.trb[dt]), pa, o[dt]);
-          o[dt] = mfma32(ld_tr(Vs + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), pb, o[dt]);
+          o[dt] = mfma32(ld_tr(Vs + 32 * t * IV, offv.tra[dt], offv.trb[dt]), pa, o[dt]);
+          o[dt] = mfma32(ld_tr(Vs + (32 * t + 16) * IV, offv.tra[dt], offv.trb[dt]), pb, o[dt]);
         }
       }
     }
@@ -358,12 +251,14 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
 // Backward dQ (query-parallel; also writes delta = rowsum(dO*O)).
 //   S^T = K Q^T ; P^T = exp2(S^T*c - lse2) ; dP^T = V dO^T - delta ; dS^T = P^T dP^T
 //   dQ^T += K^T dS^T   (K^T via tr reads of the K image)
+// DROP: dP^T = M * (V dO^T) / (1-p) - delta  (the accumulator starts at 0, not -delta)
 // ---------------------------------------------------------------------------
-template <int HD, int NW, bool CAUSAL>
+template <int HDK, int HDV, int NW, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
-  constexpr int BN = HD >= 256 ? 32 : 64, NSUB = BN / 32, BM = 32 * NW, KS = HD / 16, DT = HD / 32, NT = NW * 64;
-  constexpr int TILE = BN * HD;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];
+  constexpr int BN = attn_bn<HDK, HDV>(), NSUB = BN / 32, BM = 32 * NW, KSK = HDK / 16, KSV = HDV / 16;
+  constexpr int DT = HDK / 32, NT = NW * 64, IK = img_w<HDK>(), IV = img_w<HDV>();
+  constexpr int TK = BN * IK, TV = BN * IV, TB = TK + TV;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lq = lane & 31, hh = lane >> 5;
   const int nqb = cdiv(p.Tq, BM);
@@ -377,16 +272,19 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const int q = q0 + lq;
   const bool qvalid = q < p.Tq;
   const float c = p.scale_log2;
+  unsigned dbase = 0;
+  if constexpr (DROP) dbase = drop_base(p, b, h);
 
-  bf16x8 qf[KS], df[KS];
+  bf16x8 qf[KSK], df[KSV];
   float dlt = 0.f;
   {
     const bf16* qp = p.q + b * p.sqb + (long)q * p.sqt + h * p.sqh + 8 * hh;
     const bf16* dp = p.dout + b * p.sdob + (long)q * p.sdot + h * p.sdoh + 8 * hh;
     const bf16* op = p.o + b * p.sob + (long)q * p.sot + h * p.soh + 8 * hh;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      qf[s] = qvalid ? *reinterpret_cast<const bf16x8*>(qp + 16 * s) : zero8();
+    for (int s = 0; s < KSK; ++s) qf[s] = qvalid ? *reinterpret_cast<const bf16x8*>(qp + 16 * s) : zero8();
+#pragma unroll
+    for (int s = 0; s < KSV; ++s) {
       df[s] = qvalid ? *reinterpret_cast<const bf16x8*>(dp + 16 * s) : zero8();
       const bf16x8 ov = qvalid ? *reinterpret_cast<const bf16x8*>(op + 16 * s) : zero8();
 #pragma unroll
@@ -407,19 +305,22 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const int ntiles = kend > 0 ? cdiv(kend, BN) : 0;
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
   const bf16* vbase = p.v + b * p.svb + hk * p.svh;
-  TileLoader<HD, BN, NT> lk, lv;
+  TileLoader<HDK, BN, NT> lk;
+  TileLoader<HDV, BN, NT> lv;
   lk.init(p.skt, tid);
   lv.init(p.svt, tid);
   if (ntiles > 0) {
     lk.load(kbase, p.skt, 0, p.Tk);
     lv.load(vbase, p.svt, 0, p.Tk);
     lk.store(smem);
-    lv.store(smem + TILE);
+    lv.store(smem + TK);
     if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk); lv.load(vbase, p.svt, BN, p.Tk); }
   }
   __syncthreads();
-  LdsOff<HD> off;
-  off.init(lane);
+  LdsOff<IK> offk;
+  LdsOff<IV> offv;
+  offk.init(lane);
+  offv.init(lane);
   auto mask = [&](f32x16& s, const int k0) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -435,24 +336,30 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   auto body = [&](const int j, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     const int k0 = j * BN;
-    const bf16* Ks = smem + BUF * 2 * TILE;
-    const bf16* Vs = Ks + TILE;
+    const bf16* Ks = smem + BUF * TB;
+    const bf16* Vs = Ks + TK;
     if (j + 1 < ntiles) {
-      bf16* Kn = smem + (1 - BUF) * 2 * TILE;
+      bf16* Kn = smem + (1 - BUF) * TB;
       lk.store(Kn);
-      lv.store(Kn + TILE);
+      lv.store(Kn + TK);
       if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk); }
     }
 #pragma unroll
     for (int t = 0; t < NSUB; ++t) {
       const int ks0 = k0 + 32 * t;
       if (ks0 < wave_kend) {
-        f32x16 s = mfma32(ld_row(Ks + 32 * t * HD, off.row[0]), qf[0], splat16(0.f));
-        f32x16 dp = mfma32(ld_row(Vs + 32 * t * HD, off.row[0]), df[0], splat16(-dlt));
+        f32x16 s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[0]), qf[0], splat16(0.f));
 #pragma unroll
-        for (int ks = 1; ks < KS; ++ks) {
-          s = mfma32(ld_row(Ks + 32 * t * HD, off.row[ks]), qf[ks], s);
-          dp = mfma32(ld_row(Vs + 32 * t * HD, off.row[ks]), df[ks], dp);
+        for (int ks = 1; ks < KSK; ++ks) s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[ks]), qf[ks], s);
+        f32x16 dp = mfma32(ld_row(Vs + 32 * t * IV, offv.row[0]), df[0], splat16(DROP ? 0.f : -dlt));
+#pragma unroll
+        for (int ks = 1; ks < KSV; ++ks) dp = mfma32(ld_row(Vs + 32 * t * IV, offv.row[ks]), df[ks], dp);
+        if constexpr (DROP) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = ks0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            dp[r] = (drop_keep(dbase, q, key, p.drop_thr) ? dp[r] * p.drop_scale : 0.f) - dlt;
+          }
         }
         const bool need_mask = (ks0 + 32 > p.Tk) || (CAUSAL && ks0 + 31 > q0 + p.causal_off);
         if (need_mask) mask(s, ks0);
@@ -460,8 +367,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
         const bf16x8 sa = pack_acc(s, 0), sb = pack_acc(s, 1);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          acc[dt] = mfma32(ld_tr(Ks + 32 * t * HD, off.tra[dt], off.trb[dt]), sa, acc[dt]);
-          acc[dt] = mfma32(ld_tr(Ks + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), sb, acc[dt]);
+          acc[dt] = mfma32(ld_tr(Ks + 32 * t * IK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
+          acc[dt] = mfma32(ld_tr(Ks + (32 * t + 16) * IK, offk.tra[dt], offk.trb[dt]), sb, acc[dt]);
         }
       }
     }
@@ -526,18 +433,21 @@ __device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 
 //                                     the dP accumulator starts at -delta of its row)
 //   dV^T += dO^T P, dK^T += Q^T dS   (A = tr reads of the Q / dO images, B = accumulators)
 // Loops over the q-heads sharing this kv-head (GQA) so the group sum stays in regs.
+// DROP: dV^T += dO^T (P M / (1-p)); dS = P (M dP / (1-p) - delta), M regenerated by hash.
 // ---------------------------------------------------------------------------
-template <int HD, bool CAUSAL, int MT, bool FUSEDQ>
+template <int HDK, int HDV, bool CAUSAL, int MT, bool FUSEDQ, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   // MT 32-row q sub-tiles per iteration (more MFMA work per barrier / LDS fill)
-  constexpr int BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 256;
-  constexpr int TILE = BMQ * HD;
+  constexpr int BMQ = 32 * MT, BNK = 128, KSK = HDK / 16, KSV = HDV / 16, DTK = HDK / 32, DTV = HDV / 32;
+  constexpr int NT = 256, IK = img_w<HDK>(), IV = img_w<HDV>();
+  constexpr int TQ = BMQ * IK, TD = BMQ * IV, TB = TQ + TD;
+  static_assert(!FUSEDQ || HDK == HDV, "fused dQ path: equal head dims only");
   // FUSEDQ: dQ computed here too (dQ += dS K over this block's 128 keys, fp32 atomics into
   // p.dqacc) -> 5 MFMA products per tile instead of 7 for the split dq + dkdv kernels.
   // dS crosses LDS once ([key][q] image, transposed reads), K sits in a [key][d] image.
-  constexpr int KIMG = FUSEDQ ? BNK * HD : 8, DSIMG = FUSEDQ ? BNK * 64 : 8;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE + KIMG + DSIMG];  // [buf][Q|dO] | K | dS
-  bf16* kimg = smem + 4 * TILE;
+  constexpr int KIMG = FUSEDQ ? BNK * IK : 8, DSIMG = FUSEDQ ? BNK * 64 : 8;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TB + KIMG + DSIMG];  // [buf][Q|dO] | K | dS
+  bf16* kimg = smem + 2 * TB;
   bf16* dsimg = kimg + KIMG;
   __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];  // [buf][-lse2 | -delta]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -554,21 +464,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const bool kvalid = key < p.Tk;
   const float c = p.scale_log2;
 
-  bf16x8 kf[KS], vf[KS];
+  bf16x8 kf[KSK], vf[KSV];
   {
     const bf16* kp = p.k + b * p.skb + (long)key * p.skt + hk * p.skh + 8 * hh;
     const bf16* vp = p.v + b * p.svb + (long)key * p.svt + hk * p.svh + 8 * hh;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+    for (int s = 0; s < KSK; ++s) {
       kf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(kp + 16 * s) : zero8();
-      vf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(vp + 16 * s) : zero8();
       if constexpr (FUSEDQ)   // row = this lane's key; chunk 2s+hh holds d = 16s + 8hh .. +8
-        *reinterpret_cast<bf16x8*>(kimg + img_off<HD>(wave * 32 + lk, 2 * s + hh)) = kf[s];
+        *reinterpret_cast<bf16x8*>(kimg + img_off<IK>(wave * 32 + lk, 2 * s + hh)) = kf[s];
     }
-  }
-  f32x16 dkt[DT], dvt[DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) { dkt[i] = splat16(0.f); dvt[i] = splat16(0.f); }
+    for (int s = 0; s < KSV; ++s) vf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(vp + 16 * s) : zero8();
+  }
+  f32x16 dkt[DTK], dvt[DTV];
+#pragma unroll
+  for (int i = 0; i < DTK; ++i) dkt[i] = splat16(0.f);
+#pragma unroll
+  for (int i = 0; i < DTV; ++i) dvt[i] = splat16(0.f);
 
   int qstart = 0, wave_qstart = 0;
   if (CAUSAL) {
@@ -579,7 +492,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
   const int nper = ntq - t0 > 0 ? ntq - t0 : 0;  // q-tiles per head
   const int total = nper * G;                      // (head, q-tile) iterations
-  TileLoader<HD, BMQ, NT> lq_, ld_;
+  TileLoader<HDK, BMQ, NT> lq_;
+  TileLoader<HDV, BMQ, NT> ld_;
   lq_.init(p.sqt, tid);
   ld_.init(p.sdot, tid);
   float rl = 0.f, rd = 0.f;  // per-thread row constants for the prefetched tile (tid < BMQ)
@@ -597,8 +511,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     }
   };
   auto commit_tile = [&](int buf) {
-    lq_.store(smem + buf * 2 * TILE);
-    ld_.store(smem + buf * 2 * TILE + TILE);
+    lq_.store(smem + buf * TB);
+    ld_.store(smem + buf * TB + TQ);
     if (tid < BMQ) { rowc[buf][tid] = rl; rowc[buf][BMQ + tid] = rd; }
   };
   if (total > 0) {
@@ -607,8 +521,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     if (total > 1) fetch(1);
   }
   __syncthreads();
-  LdsOff<HD> off;
-  off.init(lane);
+  LdsOff<IK> offk;
+  LdsOff<IV> offv;
+  offk.init(lane);
+  offv.init(lane);
   // rows of s/dp[t] are queries qq0 + 32t + 8g + 4hh + i (r = 4g + i); column = key (lane)
   // one 32-query sub-tile (rows qt0 + 8g + 4hh + i): s <- P, dp <- dS = P (dP - delta)
   auto mask = [&](f32x16& s, const int qt0) {
@@ -635,8 +551,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     constexpr int BUF = decltype(bufc)::value;
     const int tq = t0 + it % nper;
     const int qq0 = tq * BMQ;
-    const bf16* Qs = smem + BUF * 2 * TILE;
-    const bf16* Ds = Qs + TILE;
+    const bf16* Qs = smem + BUF * TB;
+    const bf16* Ds = Qs + TQ;
     const float* rc = rowc[BUF];
     if (it + 1 < total) {
       commit_tile(1 - BUF);
@@ -644,27 +560,47 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     }
     const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
     if (active) {
+      unsigned dbase = 0;
+      if constexpr (DROP) dbase = drop_base(p, b, h0 + it / nper);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
-        // dP accumulator starts at -delta of each row (register r <-> query row 8g+4hh+i)
+        // dP accumulator starts at -delta of each row (register r <-> query row 8g+4hh+i);
+        // with dropout at 0 (delta is subtracted after the mask)
         f32x16 dp;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) dp[4 * g + i] = dv[i];
+          for (int i = 0; i < 4; ++i) dp[4 * g + i] = DROP ? 0.f : dv[i];
         }
-        f32x16 s = mfma32(ld_row(Qs + 32 * t * HD, off.row[0]), kf[0], splat16(0.f));
-        dp = mfma32(ld_row(Ds + 32 * t * HD, off.row[0]), vf[0], dp);
+        f32x16 s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[0]), kf[0], splat16(0.f));
 #pragma unroll
-        for (int ks = 1; ks < KS; ++ks) {
-          s = mfma32(ld_row(Qs + 32 * t * HD, off.row[ks]), kf[ks], s);
-          dp = mfma32(ld_row(Ds + 32 * t * HD, off.row[ks]), vf[ks], dp);
-        }
+        for (int ks = 1; ks < KSK; ++ks) s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[ks]), kf[ks], s);
+#pragma unroll
+        for (int ks = 0; ks < KSV; ++ks) dp = mfma32(ld_row(Ds + 32 * t * IV, offv.row[ks]), vf[ks], dp);
         const int qt0 = qq0 + 32 * t;
+        unsigned keep = 0xffffu;  // bit r: element r kept by dropout
+        if constexpr (DROP) {
+          keep = 0;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = 4 * g + i;
+              const bool kp = drop_keep(dbase, qt0 + 8 * g + 4 * hh + i, key, p.drop_thr);
+              keep |= (unsigned)kp << r;
+              dp[r] = (kp ? dp[r] * p.drop_scale : 0.f) + dv[i];
+            }
+          }
+        }
         const bool need_mask = CAUSAL && qt0 + p.causal_off < kw0 + 31;
         if (need_mask) mask(s, qt0);
         dsoft(s, dp, rc + 32 * t);
+        if constexpr (DROP) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[r] = ((keep >> r) & 1) ? s[r] * p.drop_scale : 0.f;
+        }
         const bf16x8 pa = pack_acc(s, 0), pb = pack_acc(s, 1), sa = pack_acc(dp, 0), sb = pack_acc(dp, 1);
         if constexpr (FUSEDQ) {
           // dS rows of this wave's 32 keys -> [key][q] image (registers 4g..4g+3 = 4 consecutive q)
@@ -677,11 +613,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
           }
         }
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dvt[dt] = mfma32(ld_tr(Ds + 32 * t * HD, off.tra[dt], off.trb[dt]), pa, dvt[dt]);
-          dkt[dt] = mfma32(ld_tr(Qs + 32 * t * HD, off.tra[dt], off.trb[dt]), sa, dkt[dt]);
-          dvt[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), pb, dvt[dt]);
-          dkt[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), sb, dkt[dt]);
+        for (int dt = 0; dt < DTV; ++dt) {
+          dvt[dt] = mfma32(ld_tr(Ds + 32 * t * IV, offv.tra[dt], offv.trb[dt]), pa, dvt[dt]);
+          dvt[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * IV, offv.tra[dt], offv.trb[dt]), pb, dvt[dt]);
+        }
+#pragma unroll
+        for (int dt = 0; dt < DTK; ++dt) {
+          dkt[dt] = mfma32(ld_tr(Qs + 32 * t * IK, offk.tra[dt], offk.trb[dt]), sa, dkt[dt]);
+          dkt[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * IK, offk.tra[dt], offk.trb[dt]), sb, dkt[dt]);
         }
       }
     } else if constexpr (FUSEDQ) {
@@ -699,20 +638,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
       __syncthreads();  // dS image complete
       const int h = h0 + it / nper;
 #pragma unroll
-      for (int tile = wave; tile < MT * DT; tile += 4) {
-        const int tq = tile / DT, td = tile % DT;
+      for (int tile = wave; tile < MT * DTK; tile += 4) {
+        const int tq = tile / DTK, td = tile % DTK;
         const int q0 = qq0 + 32 * tq;
         if (CAUSAL && q0 + 31 + p.causal_off < kb * BNK) continue;   // every key of the block is masked
         if (q0 >= p.Tq) continue;
         f32x16 acc = splat16(0.f);
 #pragma unroll
         for (int kk = 0; kk < BNK / 16; ++kk)
-          acc = mfma32(rd_tr<64>(dsimg, 16 * kk, 32 * tq, lane), rd_tr<HD>(kimg, 16 * kk, 32 * td, lane), acc);
-        float* dst = p.dqacc + ((long)b * p.Tq * p.H + h) * HD + 32 * td + lk;
+          acc = mfma32(rd_tr<64>(dsimg, 16 * kk, 32 * tq, lane), rd_tr<IK>(kimg, 16 * kk, 32 * td, lane), acc);
+        float* dst = p.dqacc + ((long)b * p.Tq * p.H + h) * HDK + 32 * td + lk;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qq = q0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (qq < p.Tq) atomicAdd(dst + (long)qq * p.H * HD, acc[r]);
+          if (qq < p.Tq) atomicAdd(dst + (long)qq * p.H * HDK, acc[r]);
         }
       }
     }
@@ -722,8 +661,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     body(it, IC<0>{});
     if (it + 1 < total) body(it + 1, IC<1>{});
   }
-  store_kv_grad<HD>(p, dkt, true, b, hk, key, split, hh);
-  store_kv_grad<HD>(p, dvt, false, b, hk, key, split, hh);
+  store_kv_grad<HDK>(p, dkt, true, b, hk, key, split, hh);
+  store_kv_grad<HDV>(p, dvt, false, b, hk, key, split, hh);
 }
 
 // ---------------------------------------------------------------------------
@@ -738,11 +677,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 // pair's P crosses LDS once per 32x32 sub-tile ([pair][t][j][lane][4] fp32 image,
 // conflict-free 16-byte rows). Q / dO tiles of 64 rows are double-buffered as before.
 // ---------------------------------------------------------------------------
-template <int HD, bool CAUSAL>
+template <int HDK, int HDV, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
-  constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 512;
-  constexpr int TILE = BMQ * HD;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];               // [buf][Q|dO]
+  constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KSK = HDK / 16, KSV = HDV / 16, DTK = HDK / 32;
+  constexpr int DTV = HDV / 32, NT = 512, IK = img_w<HDK>(), IV = img_w<HDV>();
+  constexpr int TQ = BMQ * IK, TD = BMQ * IV, TB = TQ + TD;
+  constexpr int KSX = KSK > KSV ? KSK : KSV, DTX = DTK > DTV ? DTK : DTV;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TB];                 // [buf][Q|dO]
   __shared__ __attribute__((aligned(16))) float pimg[4 * MT * 4 * 64 * 4];  // [pair][t][j][lane][4]
   __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];           // [buf][-lse2 | -delta]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -761,16 +702,18 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
   const bool kvalid = key < p.Tk;
   const float c = p.scale_log2;
 
-  bf16x8 xf[KS];  // A: K fragments, B: V fragments of this lane's key
+  bf16x8 xf[KSX];  // A: K fragments (KSK), B: V fragments (KSV) of this lane's key
   {
     const bf16* xp = role == 0 ? p.k + b * p.skb + (long)key * p.skt + hk * p.skh + 8 * hh
                                : p.v + b * p.svb + (long)key * p.svt + hk * p.svh + 8 * hh;
+    const int ks_n = role == 0 ? KSK : KSV;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) xf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
+    for (int s = 0; s < KSX; ++s)
+      xf[s] = (kvalid && s < ks_n) ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
   }
-  f32x16 acc[DT];  // A: dV^T, B: dK^T
+  f32x16 acc[DTX];  // A: dV^T (DTV tiles), B: dK^T (DTK tiles)
 #pragma unroll
-  for (int i = 0; i < DT; ++i) acc[i] = splat16(0.f);
+  for (int i = 0; i < DTX; ++i) acc[i] = splat16(0.f);
 
   int qstart = 0, wave_qstart = 0;
   if (CAUSAL) {
@@ -781,7 +724,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
   const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
   const int nper = ntq - t0 > 0 ? ntq - t0 : 0;
   const int total = nper * Gs;
-  TileLoader<HD, BMQ, NT> lq_, ld_;
+  TileLoader<HDK, BMQ, NT> lq_;
+  TileLoader<HDV, BMQ, NT> ld_;
   lq_.init(p.sqt, tid);
   ld_.init(p.sdot, tid);
   float rl = 0.f, rd = 0.f;
@@ -798,8 +742,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
     }
   };
   auto commit_tile = [&](int buf) {
-    lq_.store(smem + buf * 2 * TILE);
-    ld_.store(smem + buf * 2 * TILE + TILE);
+    lq_.store(smem + buf * TB);
+    ld_.store(smem + buf * TB + TQ);
     if (tid < BMQ) { rowc[buf][tid] = rl; rowc[buf][BMQ + tid] = rd; }
   };
   if (total > 0) {
@@ -808,30 +752,34 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
     if (total > 1) fetch(1);
   }
   __syncthreads();
-  LdsOff<HD> off;
-  off.init(lane);
+  LdsOff<IK> offk;
+  LdsOff<IV> offv;
+  offk.init(lane);
+  offv.init(lane);
   float* pme = pimg + pair * (MT * 4 * 64 * 4) + lane * 4;  // + (t*4 + j) * 256
   auto body = [&](const int it, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     const int qq0 = (t0 + it % nper) * BMQ;
-    const bf16* Qs = smem + BUF * 2 * TILE;
-    const bf16* Ds = Qs + TILE;
+    const bf16* Qs = smem + BUF * TB;
+    const bf16* Ds = Qs + TQ;
     const float* rc = rowc[BUF];
     if (it + 1 < total) {
       commit_tile(1 - BUF);
       if (it + 2 < total) fetch(it + 2);
     }
     const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
-    bf16x8 pk[2 * MT];  // A: packed P of both sub-tiles (kept over the barrier)
+    unsigned dbase = 0;
+    if constexpr (DROP) dbase = drop_base(p, b, h0 + it / nper);
+    bf16x8 pk[2 * MT];  // A: packed P (dropped) of both sub-tiles (kept over the barrier)
     f32x16 dp[MT];      // B: dP - delta of both sub-tiles (kept over the barrier)
     // ---- phase 1
     if (active) {
       if (role == 0) {
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
-          f32x16 s = mfma32(ld_row(Qs + 32 * t * HD, off.row[0]), xf[0], splat16(0.f));
+          f32x16 s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[0]), xf[0], splat16(0.f));
 #pragma unroll
-          for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Qs + 32 * t * HD, off.row[ks]), xf[ks], s);
+          for (int ks = 1; ks < KSK; ++ks) s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[ks]), xf[ks], s);
           const int qt0 = qq0 + 32 * t;
           if (CAUSAL && qt0 + p.causal_off < kw0 + 31) {
 #pragma unroll
@@ -846,8 +794,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
             for (int i = 0; i < 4; ++i) {
               pv[i] = fexp2(fmaf(s[4 * g + i], c, lv[i]));  // rows >= Tq: -lse2 = -inf -> 0
               s[4 * g + i] = pv[i];
+              if constexpr (DROP)
+                s[4 * g + i] = drop_keep(dbase, qt0 + 8 * g + 4 * hh + i, key, p.drop_thr) ? pv[i] * p.drop_scale
+                                                                                            : 0.f;
             }
-            *reinterpret_cast<f32x4*>(pme + (t * 4 + g) * 256) = pv;
+            *reinterpret_cast<f32x4*>(pme + (t * 4 + g) * 256) = pv;   // undropped P for role B
           }
           pk[2 * t] = pack_acc(s, 0);
           pk[2 * t + 1] = pack_acc(s, 1);
@@ -859,10 +810,23 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
           for (int g = 0; g < 4; ++g) {
             const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) dp[t][4 * g + i] = dv[i];
+            for (int i = 0; i < 4; ++i) dp[t][4 * g + i] = DROP ? 0.f : dv[i];
           }
 #pragma unroll
-          for (int ks = 0; ks < KS; ++ks) dp[t] = mfma32(ld_row(Ds + 32 * t * HD, off.row[ks]), xf[ks], dp[t]);
+          for (int ks = 0; ks < KSV; ++ks) dp[t] = mfma32(ld_row(Ds + 32 * t * IV, offv.row[ks]), xf[ks], dp[t]);
+          if constexpr (DROP) {
+            const int qt0 = qq0 + 32 * t;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int r = 4 * g + i;
+                dp[t][r] = (drop_keep(dbase, qt0 + 8 * g + 4 * hh + i, key, p.drop_thr) ? dp[t][r] * p.drop_scale
+                                                                                         : 0.f) + dv[i];
+              }
+            }
+          }
         }
       }
     }
@@ -873,9 +837,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
 #pragma unroll
         for (int t = 0; t < MT; ++t)
 #pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            acc[dt] = mfma32(ld_tr(Ds + 32 * t * HD, off.tra[dt], off.trb[dt]), pk[2 * t], acc[dt]);
-            acc[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), pk[2 * t + 1], acc[dt]);
+          for (int dt = 0; dt < DTV; ++dt) {
+            acc[dt] = mfma32(ld_tr(Ds + 32 * t * IV, offv.tra[dt], offv.trb[dt]), pk[2 * t], acc[dt]);
+            acc[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * IV, offv.tra[dt], offv.trb[dt]), pk[2 * t + 1], acc[dt]);
           }
       } else {
 #pragma unroll
@@ -889,9 +853,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
           }
           const bf16x8 sa = pack_acc(ds, 0), sb = pack_acc(ds, 1);
 #pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            acc[dt] = mfma32(ld_tr(Qs + 32 * t * HD, off.tra[dt], off.trb[dt]), sa, acc[dt]);
-            acc[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * HD, off.tra[dt], off.trb[dt]), sb, acc[dt]);
+          for (int dt = 0; dt < DTK; ++dt) {
+            acc[dt] = mfma32(ld_tr(Qs + 32 * t * IK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
+            acc[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * IK, offk.tra[dt], offk.trb[dt]), sb, acc[dt]);
           }
         }
       }
@@ -902,21 +866,34 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
     body(it, IC<0>{});
     if (it + 1 < total) body(it + 1, IC<1>{});
   }
-  store_kv_grad<HD>(p, acc, role == 1, b, hk, key, split, hh);
+  if constexpr (HDK == HDV) {
+    store_kv_grad<HDK>(p, acc, role == 1, b, hk, key, split, hh);
+  } else {
+    if (role == 1) {
+      f32x16 ak[DTK];
+#pragma unroll
+      for (int i = 0; i < DTK; ++i) ak[i] = acc[i];
+      store_kv_grad<HDK>(p, ak, true, b, hk, key, split, hh);
+    } else {
+      f32x16 av[DTV];
+#pragma unroll
+      for (int i = 0; i < DTV; ++i) av[i] = acc[i];
+      store_kv_grad<HDV>(p, av, false, b, hk, key, split, hh);
+    }
+  }
 }
 
-// sum the q-head-split fp32 partials -> bf16 dK (scaled) / dV
+// sum the q-head-split fp32 partials of ONE tensor (dK with HD = HDK, or dV with HD = HDV)
+// -> bf16 dK (scaled) / dV
 template <int HD>
-__global__ __launch_bounds__(256) void attn_kv_reduce_kernel(AttnParams p) {
+__global__ __launch_bounds__(256) void attn_kv_reduce_kernel(AttnParams p, int is_k) {
   constexpr int TPR = HD / 8;
   const long rows = (long)p.B * p.Tk * p.Hkv;
-  const long n = rows * TPR * 2;
+  const long n = rows * TPR;
   const long slab = rows * HD;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const bool is_k = i < rows * TPR;
-    const long j = is_k ? i : i - rows * TPR;
-    const int t = j % TPR;
-    const long row = j / TPR;  // (b, key, hk)
+    const int t = i % TPR;
+    const long row = i / TPR;  // (b, key, hk)
     const long hk = row % p.Hkv, key = (row / p.Hkv) % p.Tk, b = row / ((long)p.Hkv * p.Tk);
     const float* src = (is_k ? p.dkacc : p.dvacc) + row * HD + 8 * t;
     float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -987,14 +964,19 @@ static void check_qkv(const at::Tensor& t, const char* n) {
               n, ": rows must be 16-byte aligned");
 }
 
-// forward / dq use 8 waves (2 per SIMD) for hd <= 128, 4 waves for hd = 256
-template <int HD> constexpr int fwd_waves() { return HD <= 128 ? 8 : 4; }
+// forward uses 8 waves (2 per SIMD) for head dims <= 192, 4 waves for 256; dq keeps q, dO and
+// the dQ accumulator in registers and needs one wave per SIMD (the AGPR half of the register
+// file) beyond square 128
+template <int HDK, int HDV> constexpr int fwd_waves() { return (HDK <= 192 && HDV <= 192) ? 8 : 4; }
+template <int HDK, int HDV> constexpr int dq_waves() { return (HDK <= 128 && HDV <= 128) ? 8 : 4; }
 
-#define HD_SWITCH(HDV, ...)                                                        \
-  if (HDV == 64) { constexpr int HD_ = 64; __VA_ARGS__; }                          \
-  else if (HDV == 128) { constexpr int HD_ = 128; __VA_ARGS__; }                   \
-  else if (HDV == 256) { constexpr int HD_ = 256; __VA_ARGS__; }                   \
-  else TORCH_CHECK(false, "flash attention: head dim must be 64, 128 or 256");
+// (q/k head dim, v head dim) instantiations: the square 64/128/256 and MLA's 192/128
+#define HDKV_SWITCH(HK, HV, ...)                                                                   \
+  if (HK == 64 && HV == 64) { constexpr int HDK_ = 64, HDV_ = 64; __VA_ARGS__; }                  \
+  else if (HK == 128 && HV == 128) { constexpr int HDK_ = 128, HDV_ = 128; __VA_ARGS__; }         \
+  else if (HK == 256 && HV == 256) { constexpr int HDK_ = 256, HDV_ = 256; __VA_ARGS__; }         \
+  else if (HK == 192 && HV == 128) { constexpr int HDK_ = 192, HDV_ = 128; __VA_ARGS__; }         \
+  else TORCH_CHECK(false, "flash attention: (qk, v) head dims must be (64,64), (128,128), (256,256) or (192,128)");
 
 static void fill_strides(AttnParams& p, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   p.sqb = q.stride(0); p.sqt = q.stride(1); p.sqh = q.stride(2);
@@ -1002,50 +984,113 @@ static void fill_strides(AttnParams& p, const at::Tensor& q, const at::Tensor& k
   p.svb = v.stride(0); p.svt = v.stride(1); p.svh = v.stride(2);
 }
 
-// q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd] (strided views allowed). Returns (out [B,Tq,H,hd], lse [B,H,Tq]).
+static void fill_dropout(AttnParams& p, double dropout_p, int64_t seed) {
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "attention dropout p must be in [0, 1)");
+  p.seed_lo = (unsigned)(seed & 0xffffffffu);
+  p.seed_hi = (unsigned)(((uint64_t)seed >> 32) & 0xffffffffu);
+  p.drop_thr = (unsigned)std::llround(dropout_p * 16777216.0);  // 24-bit uniform
+  p.drop_scale = (float)(1.0 / (1.0 - dropout_p));
+}
+
+// q [B,Tq,H,dk], k [B,Tk,Hkv,dk], v [B,Tk,Hkv,dv] (strided views allowed).
+// Returns (out [B,Tq,H,dv], lse [B,H,Tq]). dropout_p > 0: fused dropout on P (seeded hash).
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
-                                 bool causal) {
+                                 bool causal, double dropout_p, int64_t seed) {
   check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v");
-  const int B = q.size(0), Tq = q.size(1), H = q.size(2), HD = q.size(3);
+  const int B = q.size(0), Tq = q.size(1), H = q.size(2), HDK = q.size(3), HDV = v.size(3);
   const int Tk = k.size(1), Hkv = k.size(2);
-  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Tk && v.size(2) == Hkv && k.size(3) == HD &&
-              v.size(3) == HD, "attn: shape mismatch");
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Tk && v.size(2) == Hkv && k.size(3) == HDK,
+              "attn: shape mismatch");
   TORCH_CHECK(H % Hkv == 0, "attn: H must be a multiple of Hkv");
+  const bool drop = dropout_p > 0.0;
+  TORCH_CHECK(!drop || HDK == HDV, "attn: dropout needs equal q/k and v head dims");
   DeviceGuard g(q.device());
-  auto out = at::empty({B, Tq, H, HD}, q.options());
+  auto out = at::empty({B, Tq, H, HDV}, q.options());
   auto lse = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
   AttnParams p{};
   p.q = (const bf16*)q.data_ptr(); p.k = (const bf16*)k.data_ptr(); p.v = (const bf16*)v.data_ptr();
   p.out = (bf16*)out.data_ptr(); p.lse = lse.data_ptr<float>();
   p.B = B; p.H = H; p.Hkv = Hkv; p.Tq = Tq; p.Tk = Tk;
   fill_strides(p, q, k, v);
+  fill_dropout(p, dropout_p, seed);
   p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
   p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal_off = Tk - Tq;
   p.hsplit = 1;
   if (B * Tq * H == 0) return {out, lse};
   auto st = stream();
-  HD_SWITCH(HD, {
-    constexpr int NW = fwd_waves<HD_>();
+  HDKV_SWITCH(HDK, HDV, {
+    constexpr int NW = fwd_waves<HDK_, HDV_>();
+    constexpr bool SQ = HDK_ == HDV_;
     const int grid = cdiv(Tq, 32 * NW) * H * B;
-    if (causal) attn_fwd_kernel<HD_, NW, true><<<grid, NW * 64, 0, st>>>(p);
-    else attn_fwd_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
+    if (drop) {
+      if constexpr (SQ) {
+        if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, true><<<grid, NW * 64, 0, st>>>(p);
+        else attn_fwd_kernel<HDK_, HDV_, NW, false, true><<<grid, NW * 64, 0, st>>>(p);
+      }
+    } else {
+      if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, false><<<grid, NW * 64, 0, st>>>(p);
+      else attn_fwd_kernel<HDK_, HDV_, NW, false, false><<<grid, NW * 64, 0, st>>>(p);
+    }
   });
   SPA_LAUNCH_CHECK();
   return {out, lse};
 }
 
+template <int HDK, int HDV, bool DROP>
+static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, int nkv, hipStream_t st) {
+  constexpr int NW = dq_waves<HDK, HDV>();
+  constexpr int MT = (HDK <= 128 && HDV <= 128) ? 2 : 1;
+  // paired-wave dK/dV keeps half the state per wave at 2 waves/SIMD: spill-free for square
+  // head dims <= 128 without dropout (the hash keys of the dropout variant tip the 128 one
+  // over; at 256 one role needs > 256 registers, which 2 waves/SIMD cannot hold)
+  constexpr bool PAIRED_OK = HDK == HDV && HDK <= 128 && !DROP;
+  const int g2 = nkv * p.hsplit;
+  if constexpr (HDK == HDV && HDK <= 128 && !DROP) {
+    if (fused) {   // hd 256: the fused body exceeds the register file (spills)
+      const long rows = (long)p.B * p.Tq * p.H;
+      attn_delta_kernel<HDK><<<(int)cdiv(rows, 256 / (HDK / 8)), 256, 0, st>>>(p);
+      if (causal) attn_bwd_dkdv_kernel<HDK, HDV, true, MT, true, false><<<g2, 256, 0, st>>>(p);
+      else attn_bwd_dkdv_kernel<HDK, HDV, false, MT, true, false><<<g2, 256, 0, st>>>(p);
+      const long n = rows * (HDK / 8);
+      attn_dq_store_kernel<HDK><<<(int)std::min<long>((n + 255) / 256, 65536), 256, 0, st>>>(p);
+      return;
+    }
+  }
+  const int grid = cdiv(p.Tq, 32 * NW) * p.H * p.B;
+  if (causal) attn_bwd_dq_kernel<HDK, HDV, NW, true, DROP><<<grid, NW * 64, 0, st>>>(p);
+  else attn_bwd_dq_kernel<HDK, HDV, NW, false, DROP><<<grid, NW * 64, 0, st>>>(p);
+  if (p.Tk == 0) return;
+  const bool paired = PAIRED_OK && (dkdv_mode == 2 || (dkdv_mode == 0 && HDV == 128));
+  if (paired) {
+    if constexpr (PAIRED_OK) {
+      if (causal) attn_bwd_dkdv2_kernel<HDK, HDV, true, DROP><<<g2, 512, 0, st>>>(p);
+      else attn_bwd_dkdv2_kernel<HDK, HDV, false, DROP><<<g2, 512, 0, st>>>(p);
+    }
+  } else {
+    if (causal) attn_bwd_dkdv_kernel<HDK, HDV, true, MT, false, DROP><<<g2, 256, 0, st>>>(p);
+    else attn_bwd_dkdv_kernel<HDK, HDV, false, MT, false, DROP><<<g2, 256, 0, st>>>(p);
+  }
+  if (p.hsplit > 1) {
+    const long rows = (long)p.B * p.Tk * p.Hkv;
+    attn_kv_reduce_kernel<HDK><<<(int)std::min<long>((rows * (HDK / 8) + 255) / 256, 65536), 256, 0, st>>>(p, 1);
+    attn_kv_reduce_kernel<HDV><<<(int)std::min<long>((rows * (HDV / 8) + 255) / 256, 65536), 256, 0, st>>>(p, 0);
+  }
+}
+
 // Gradients written into dq/dk/dv (strided views allowed, e.g. slices of one dqkv buffer).
 void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
               const at::Tensor& out, const at::Tensor& lse, const at::Tensor& dq, const at::Tensor& dk,
-              const at::Tensor& dv, double scale, bool causal) {
+              const at::Tensor& dv, double scale, bool causal, double dropout_p, int64_t seed) {
   check_qkv(dout, "dout"); check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(out, "out");
   check_qkv(dq, "dq"); check_qkv(dk, "dk"); check_qkv(dv, "dv");
-  const int B = q.size(0), Tq = q.size(1), H = q.size(2), HD = q.size(3);
+  const int B = q.size(0), Tq = q.size(1), H = q.size(2), HDK = q.size(3), HDV = v.size(3);
   const int Tk = k.size(1), Hkv = k.size(2);
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)B * H * Tq);
   TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes());
-  TORCH_CHECK(dout.sizes() == q.sizes() && out.sizes() == q.sizes());
+  TORCH_CHECK(dout.sizes() == out.sizes() && out.size(3) == HDV && out.size(2) == H && out.size(1) == Tq);
+  const bool drop = dropout_p > 0.0;
+  TORCH_CHECK(!drop || HDK == HDV, "attn: dropout needs equal q/k and v head dims");
   DeviceGuard g(q.device());
   auto delta = at::empty({B, H, Tq}, q.options().dtype(at::kFloat));
   AttnParams p{};
@@ -1055,6 +1100,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   p.lse_in = lse.data_ptr<float>(); p.delta = delta.data_ptr<float>();
   p.B = B; p.H = H; p.Hkv = Hkv; p.Tq = Tq; p.Tk = Tk;
   fill_strides(p, q, k, v);
+  fill_dropout(p, dropout_p, seed);
   p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
   p.sdob = dout.stride(0); p.sdot = dout.stride(1); p.sdoh = dout.stride(2);
   p.sdqb = dq.stride(0); p.sdqt = dq.stride(1); p.sdqh = dq.stride(2);
@@ -1071,19 +1117,19 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   // fused 3.87 ms vs split 2.74 ms -- with 128-key blocks each dQ row receives T/128 atomic
   // adds (~4 GB of adds per call), past the chip-wide atomic rate; kept as an option.
   static const bool want_fused = getenv("SPA_ATTN_BWD_FUSED") && atoi(getenv("SPA_ATTN_BWD_FUSED")) != 0;
-  const bool fused = want_fused && Tk > 0 && HD <= 128;
+  const bool fused = want_fused && Tk > 0 && HDK <= 128 && HDK == HDV && !drop;
   at::Tensor dqacc;
   if (fused) {
-    dqacc = at::zeros({B, Tq, H, HD}, q.options().dtype(at::kFloat));
+    dqacc = at::zeros({B, Tq, H, HDK}, q.options().dtype(at::kFloat));
     p.dqacc = dqacc.data_ptr<float>();
   }
   // dK/dV grid: key blocks x kv-heads x batch, times a q-head split when that grid cannot
   // fill the chip (MQA: Hkv = 1 launched 32 blocks at T = 4096); partials are summed by
-  // attn_kv_reduce_kernel. dK/dV kernel: paired-wave (2) for hd 128, single-wave (1) else;
-  // SPA_ATTN_DKDV overrides (read per call, so one process can A/B them). Measured in one
-  // process on MI355X: LLaMA3-8B shape bwd 2.22 ms paired vs 2.45 ms single-wave; ViT-B
+  // attn_kv_reduce_kernel. dK/dV kernel: paired-wave (2) for v head dim 128, single-wave (1)
+  // else; SPA_ATTN_DKDV overrides (read per call, so one process can A/B them). Measured in
+  // one process on MI355X: LLaMA3-8B shape bwd 2.22 ms paired vs 2.45 ms single-wave; ViT-B
   // hd 64 (T 197, B 64) 0.121 ms paired vs 0.097 ms single-wave.
-  const int dkdv_mode = getenv("SPA_ATTN_DKDV") ? atoi(getenv("SPA_ATTN_DKDV")) : (HD == 128 ? 2 : 1);
+  const int dkdv_mode = getenv("SPA_ATTN_DKDV") ? atoi(getenv("SPA_ATTN_DKDV")) : 0;
   const int G = H / Hkv;
   const int nkv = cdiv(Tk, 128) * Hkv * B;
   int hsplit = 1;
@@ -1096,38 +1142,15 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   p.hsplit = hsplit;
   at::Tensor kvacc;
   if (hsplit > 1) {
-    kvacc = at::empty({2, hsplit, B, Tk, Hkv, HD}, q.options().dtype(at::kFloat));
+    kvacc = at::empty({(long)hsplit * B * Tk * Hkv * (HDK + HDV)}, q.options().dtype(at::kFloat));
     p.dkacc = kvacc.data_ptr<float>();
-    p.dvacc = p.dkacc + (long)hsplit * B * Tk * Hkv * HD;
+    p.dvacc = p.dkacc + (long)hsplit * B * Tk * Hkv * HDK;
   }
-  HD_SWITCH(HD, {
-    constexpr int NW = fwd_waves<HD_>();
-    constexpr int MT = HD_ == 128 ? 2 : 1;
-    const int g2 = nkv * hsplit;
-    if (fused && HD_ <= 128) {   // hd 256: the fused body exceeds the register file (spills)
-      const long rows = (long)B * Tq * H;
-      attn_delta_kernel<HD_><<<(int)cdiv(rows, 256 / (HD_ / 8)), 256, 0, st>>>(p);
-      if (causal) attn_bwd_dkdv_kernel<HD_, true, MT, true><<<g2, 256, 0, st>>>(p);
-      else attn_bwd_dkdv_kernel<HD_, false, MT, true><<<g2, 256, 0, st>>>(p);
-      const long n = rows * (HD_ / 8);
-      attn_dq_store_kernel<HD_><<<(int)std::min<long>((n + 255) / 256, 65536), 256, 0, st>>>(p);
+  HDKV_SWITCH(HDK, HDV, {
+    if (drop) {
+      if constexpr (HDK_ == HDV_) launch_bwd<HDK_, HDV_, true>(p, causal, false, dkdv_mode, nkv, st);
     } else {
-      const int grid = cdiv(Tq, 32 * NW) * H * B;
-      if (causal) attn_bwd_dq_kernel<HD_, NW, true><<<grid, NW * 64, 0, st>>>(p);
-      else attn_bwd_dq_kernel<HD_, NW, false><<<grid, NW * 64, 0, st>>>(p);
-      if (Tk > 0) {
-        if (HD_ <= 128 && dkdv_mode != 1) {
-          if (causal) attn_bwd_dkdv2_kernel<(HD_ <= 128 ? HD_ : 128), true><<<g2, 512, 0, st>>>(p);
-          else attn_bwd_dkdv2_kernel<(HD_ <= 128 ? HD_ : 128), false><<<g2, 512, 0, st>>>(p);
-        } else {
-          if (causal) attn_bwd_dkdv_kernel<HD_, true, MT, false><<<g2, 256, 0, st>>>(p);
-          else attn_bwd_dkdv_kernel<HD_, false, MT, false><<<g2, 256, 0, st>>>(p);
-        }
-        if (hsplit > 1) {
-          const long n = (long)B * Tk * Hkv * (HD_ / 8) * 2;
-          attn_kv_reduce_kernel<HD_><<<(int)std::min<long>((n + 255) / 256, 65536), 256, 0, st>>>(p);
-        }
-      }
+      launch_bwd<HDK_, HDV_, false>(p, causal, fused, dkdv_mode, nkv, st);
     }
   });
   SPA_LAUNCH_CHECK();
@@ -1136,9 +1159,10 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal) -> Tensor[]");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, float dropout_p=0.0, int seed=0) "
+        "-> Tensor[]");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
-        "Tensor(c!) dv, float scale, bool causal) -> ()");
+        "Tensor(c!) dv, float scale, bool causal, float dropout_p=0.0, int seed=0) -> ()");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("attn_fwd", &spa::attn_fwd);

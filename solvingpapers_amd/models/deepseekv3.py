@@ -242,8 +242,9 @@ class MLA(tnn.Module):
         qf = torch.cat([q[..., :dn], qr], dim=-1)
         k = torch.cat([kv[..., :dn], kr.expand(B, T, H, dr)], dim=-1)
         v = kv[..., dn:]
-        # dv == dn + dr runs the flash kernel directly; V3's 192/128 heads are zero-padded onto it
-        o = flash_attention(qf, k, v.contiguous() if dv == dn + dr else v, causal=True, scale=scale)
+        # the flash kernels take (q/k, v) head dims (64,64) / (128,128) / (192,128) -- V3's MLA
+        # heads -- directly, reading v as a strided view of the up-projection output
+        o = flash_attention(qf, k, v, causal=True, scale=scale)
         return linear(o.reshape(B, T, H * dv), self.wo)
 
     def _decode(self, qn, qr, ckv, kr, cache, pos, scale):

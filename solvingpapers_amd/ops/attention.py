@@ -3,10 +3,15 @@
 Tensors are [B, T, H, hd] views (hd contiguous); the kernels take (b, t, h)
 strides, so q/k/v may be slices of one packed qkv projection output and the
 gradients can be written into slices of one dqkv buffer (``attention_packed``).
-Head dims 64/128/256 run the MFMA flash kernel; other q/k and v head dims up to
-256 (DeepSeek-V3 MLA's 192/128) are zero-padded onto it; wider heads fall back to
-a materialised GEMM + softmax path (used only by reference-parity presets such
-as Gemma-ref's 768-wide heads).
+
+Kernel head dims (q/k, v): (64, 64), (128, 128), (256, 256) and DeepSeek-V3 MLA's
+(192, 128), all without padding. Other dims up to 256 are zero-padded onto the
+smallest kernel pair that holds them; wider heads (Gemma-ref's 768) take the wide-head
+kernels (csrc/kernels/attention_wide.hip).
+
+Attention-probability dropout is fused into the kernels (counter-hash mask regenerated
+from a per-call seed in the forward and both backward kernels; nothing (T, T) is stored).
+``dropout_keep_mask`` reproduces the exact mask on the host for oracles.
 """
 from __future__ import annotations
 
@@ -16,19 +21,58 @@ import torch
 
 from . import _ext, reference
 
+FLASH_PAIRS = ((64, 64), (128, 128), (256, 256), (192, 128))
 FLASH_HD = (64, 128, 256)
+
+
+def _pair_for(dqk, dv):
+    """Smallest kernel (q/k, v) head-dim pair holding (dqk, dv) (None: none does)."""
+    best = None
+    for a, b in FLASH_PAIRS:
+        if a >= dqk and b >= dv and (best is None or a + b < best[0] + best[1]):
+            best = (a, b)
+    return best
 
 
 def _flash_ok(q):
     return q.is_cuda and q.dtype == torch.bfloat16 and (q.dim() == 3 or q.shape[-1] in FLASH_HD)
 
 
+# ------------------------------------------------------------------ dropout mask (host)
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x):
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def dropout_keep_mask(seed: int, B: int, H: int, Tq: int, Tk: int, p: float, device="cpu"):
+    """Bool [B, H, Tq, Tk]: the keep mask the fused kernels apply for ``seed`` (same 32-bit
+    counter hash as csrc/kernels/attention.hip drop_keep)."""
+    thr = int(round(p * 16777216.0))
+    lo, hi = seed & _M32, (seed >> 32) & _M32
+    bh = torch.arange(B * H, device=device, dtype=torch.int64)
+    base = _mix32(lo ^ _mix32((hi + bh * 0x9E3779B9) & _M32))             # [B*H]
+    q = torch.arange(Tq, device=device, dtype=torch.int64)
+    k = torch.arange(Tk, device=device, dtype=torch.int64)
+    x = (base[:, None, None] + (q * 0x85EBCA6B)[None, :, None] + (k * 0xC2B2AE35)[None, None, :]) & _M32
+    return ((_mix32(x) >> 8) >= thr).view(B, H, Tq, Tk)
+
+
+def _new_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,)).item())   # host generator: no device sync
+
+
 class _FlashFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale):
-        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal)
+    def forward(ctx, q, k, v, causal, scale, dropout_p, seed):
+        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal, dropout_p, seed)
         ctx.save_for_backward(q, k, v, out, lse)
-        ctx.causal, ctx.scale = causal, scale
+        ctx.causal, ctx.scale, ctx.dropout_p, ctx.seed = causal, scale, dropout_p, seed
         return out
 
     @staticmethod
@@ -37,8 +81,9 @@ class _FlashFn(torch.autograd.Function):
         dq = torch.empty_like(q, memory_format=torch.contiguous_format)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format)
-        _ext.ops().attn_bwd(dout.contiguous(), q, k, v, out, lse, dq, dk, dv, ctx.scale, ctx.causal)
-        return dq, dk, dv, None, None
+        _ext.ops().attn_bwd(dout.contiguous(), q, k, v, out, lse, dq, dk, dv, ctx.scale, ctx.causal,
+                            ctx.dropout_p, ctx.seed)
+        return dq, dk, dv, None, None, None, None
 
 
 class _PackedFn(torch.autograd.Function):
@@ -47,13 +92,14 @@ class _PackedFn(torch.autograd.Function):
     Output is [B, T, H*hd] (a fresh tensor, ready for the output projection)."""
 
     @staticmethod
-    def forward(ctx, qkv, H, Hkv, hd, causal, scale):
+    def forward(ctx, qkv, H, Hkv, hd, causal, scale, dropout_p=0.0, seed=0):
         B, T = qkv.shape[0], qkv.shape[1]
         x4 = qkv.view(B, T, H + 2 * Hkv, hd)
         q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
-        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal)
+        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal, dropout_p, seed)
         ctx.save_for_backward(qkv, out, lse)
         ctx.H, ctx.Hkv, ctx.hd, ctx.causal, ctx.scale = H, Hkv, hd, causal, scale
+        ctx.dropout_p, ctx.seed = dropout_p, seed
         return torch.ops.aten._unsafe_view(out, (B, T, H * hd))
 
     @staticmethod
@@ -66,82 +112,15 @@ class _PackedFn(torch.autograd.Function):
         d4 = dqkv.view(B, T, H + 2 * Hkv, hd)
         _ext.ops().attn_bwd(dout.contiguous().view(B, T, H, hd), x4[:, :, :H], x4[:, :, H:H + Hkv],
                             x4[:, :, H + Hkv:], out, lse, d4[:, :, :H], d4[:, :, H:H + Hkv], d4[:, :, H + Hkv:],
-                            ctx.scale, ctx.causal)
-        return dqkv, None, None, None, None, None
+                            ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed)
+        return dqkv, None, None, None, None, None, None, None
 
 
-def _materialised(q, k, v, causal, scale):
-    """GEMM + softmax path for unsupported head dims (autograd through torch ops)."""
+def _materialised(q, k, v, causal, scale, dropout_p=0.0, seed=0, neg=float("-inf")):
+    """GEMM + softmax path (CPU autograd, and the oracle of the fused kernels): with
+    ``dropout_p`` it applies exactly the kernels' hash mask for ``seed``."""
     B, Tq, H, hd = q.shape
     Tk, Hkv = k.shape[1], k.shape[2]
-    rep = H // Hkv
-    qh = q.transpose(1, 2)
-    kh = k.transpose(1, 2).repeat_interleave(rep, dim=1)
-    vh = v.transpose(1, 2).repeat_interleave(rep, dim=1)
-    s = torch.matmul(qh, kh.transpose(-1, -2)).float() * scale
-    if causal:
-        i = torch.arange(Tq, device=q.device)[:, None]
-        j = torch.arange(Tk, device=q.device)[None, :]
-        s = s.masked_fill(j > i + (Tk - Tq), float("-inf"))
-    p = torch.softmax(s, dim=-1).to(q.dtype)
-    return torch.matmul(p, vh).transpose(1, 2)
-
-
-def _flash_pad_dim(dqk, dv):
-    """Smallest flash head dim that holds both the q/k and the v head dim (None: none does)."""
-    return next((h for h in FLASH_HD if h >= max(dqk, dv)), None)
-
-
-def _pad_last(x, n):
-    return x if x.shape[-1] == n else torch.nn.functional.pad(x, (0, n - x.shape[-1]))
-
-
-def flash_attention(q, k, v, causal=True, scale=None):
-    """softmax(q k^T * scale [+causal]) v.  q/k [B,T,H(kv),dqk], v [B,Tk,Hkv,dv].
-
-    dqk == dv in FLASH_HD runs the MFMA kernel directly. Other head dims up to 256
-    (DeepSeek-V3 MLA: dqk = 128 nope + 64 rope = 192, dv = 128) are zero-padded to
-    the next kernel head dim: zero q/k columns leave every score unchanged, zero v
-    columns give zero output columns that are sliced off, and the pad's backward
-    slices the gradients. O(T) memory instead of the materialised O(T^2) path."""
-    scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    if _flash_ok(q) and v.shape[-1] == q.shape[-1]:
-        return _FlashFn.apply(q, k, v, causal, scale)
-    if q.is_cuda and q.dtype == torch.bfloat16 and q.dim() == 4:
-        P = _flash_pad_dim(q.shape[-1], v.shape[-1])
-        if P is not None:
-            o = _FlashFn.apply(_pad_last(q, P), _pad_last(k, P), _pad_last(v, P), causal, scale)
-            return o[..., :v.shape[-1]]
-    if q.is_cuda:
-        return _materialised(q, k, v, causal, scale)
-    if torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad):
-        return _materialised(q, k, v, causal, scale)
-    return reference.attention(q, k, v, causal, scale)[0]
-
-
-def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None):
-    """qkv [B, T, H+2Hkv, hd] (or [B, T, (H+2Hkv)*hd] with head_dim) -> out [B, T, H*hd]."""
-    hd = head_dim if head_dim is not None else qkv.shape[-1]
-    B, T = qkv.shape[0], qkv.shape[1]
-    scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
-    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and hd in FLASH_HD:
-        return _PackedFn.apply(qkv, H, Hkv, hd, causal, scale)
-    x4 = qkv.view(B, T, H + 2 * Hkv, hd)
-    q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
-    return flash_attention(q, k, v, causal, scale).reshape(B, T, H * hd)
-
-
-def attention_dropout(q, k, v, causal=True, scale=None, p=0.0, training=True, neg=float("-inf")):
-    """Materialised attention with dropout on the probability matrix (GPT-ref
-    gpt/gpt-jax.ipynb:351 / DeepSeek-ref attention dropout). Used only when a
-    reference preset trains with attention-weight dropout; inference and p=0 take
-    the flash kernels. q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd]."""
-    from .misc import dropout
-    if not training or p == 0.0:
-        return flash_attention(q, k, v, causal, scale)
-    B, Tq, H, hd = q.shape
-    Tk, Hkv = k.shape[1], k.shape[2]
-    scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
     rep = H // Hkv
     qh = q.transpose(1, 2)
     kh = k.transpose(1, 2).repeat_interleave(rep, dim=1)
@@ -151,8 +130,80 @@ def attention_dropout(q, k, v, causal=True, scale=None, p=0.0, training=True, ne
         i = torch.arange(Tq, device=q.device)[:, None]
         j = torch.arange(Tk, device=q.device)[None, :]
         s = s.masked_fill(j > i + (Tk - Tq), neg)
-    pr = dropout(torch.softmax(s, dim=-1).to(q.dtype), p, training)
-    return torch.matmul(pr, vh).transpose(1, 2)
+    p = torch.softmax(s, dim=-1)
+    if dropout_p > 0.0:
+        keep = dropout_keep_mask(seed, B, H, Tq, Tk, dropout_p, device=q.device)
+        p = p * keep / (1.0 - dropout_p)
+    return torch.matmul(p.to(q.dtype), vh).transpose(1, 2)
+
+
+def _pad_last(x, n):
+    return x if x.shape[-1] == n else torch.nn.functional.pad(x, (0, n - x.shape[-1]))
+
+
+def _wide_ok(q, k, v):
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.dim() == 4 and q.shape[-1] == v.shape[-1]
+            and q.shape[-1] in (512, 768))
+
+
+def flash_attention(q, k, v, causal=True, scale=None, dropout_p=0.0, seed=None):
+    """softmax(q k^T * scale [+causal]) [dropout] v.  q/k [B,T,H(kv),dqk], v [B,Tk,Hkv,dv].
+
+    (dqk, dv) in FLASH_PAIRS runs the MFMA kernel directly (MLA's 192/128 included). Other
+    head dims up to 256 are zero-padded to the smallest kernel pair: zero q/k columns leave
+    every score unchanged, zero v columns give zero output columns that are sliced off, and
+    the pad's backward slices the gradients. ``dropout_p`` > 0 fuses dropout on P into the
+    kernels (``seed`` drawn from torch's host generator when None)."""
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    dropout_p = float(dropout_p)
+    if dropout_p > 0.0 and seed is None:
+        seed = _new_seed()
+    seed = int(seed or 0)
+    dqk, dv = q.shape[-1], v.shape[-1]
+    if q.is_cuda and q.dtype == torch.bfloat16 and q.dim() == 4:
+        if (dqk, dv) in FLASH_PAIRS and (dropout_p == 0.0 or dqk == dv):
+            return _FlashFn.apply(q, k, v, causal, scale, dropout_p, seed)
+        pair = _pair_for(dqk, dv) if dropout_p == 0.0 else _pair_for(max(dqk, dv), max(dqk, dv))
+        if pair is not None:
+            o = _FlashFn.apply(_pad_last(q, pair[0]), _pad_last(k, pair[0]), _pad_last(v, pair[1]), causal, scale,
+                               dropout_p, seed)
+            return o[..., :dv]
+        if _wide_ok(q, k, v) and dropout_p == 0.0:
+            from .attention_wide import wide_attention
+            return wide_attention(q, k, v, causal, scale)
+    if q.is_cuda:
+        raise NotImplementedError(f"no HIP attention kernel for head dims ({dqk}, {dv}) / dtype {q.dtype}")
+    if dropout_p > 0.0 or (torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)):
+        return _materialised(q, k, v, causal, scale, dropout_p, seed)
+    return reference.attention(q, k, v, causal, scale)[0]
+
+
+def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None, dropout_p=0.0, seed=None):
+    """qkv [B, T, H+2Hkv, hd] (or [B, T, (H+2Hkv)*hd] with head_dim) -> out [B, T, H*hd]."""
+    hd = head_dim if head_dim is not None else qkv.shape[-1]
+    B, T = qkv.shape[0], qkv.shape[1]
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
+    if dropout_p > 0.0 and seed is None:
+        seed = _new_seed()
+    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and hd in FLASH_HD:
+        return _PackedFn.apply(qkv, H, Hkv, hd, causal, scale, float(dropout_p), int(seed or 0))
+    x4 = qkv.view(B, T, H + 2 * Hkv, hd)
+    q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
+    return flash_attention(q, k, v, causal, scale, dropout_p, seed).reshape(B, T, H * hd)
+
+
+def attention_dropout(q, k, v, causal=True, scale=None, p=0.0, training=True, neg=float("-inf")):
+    """Attention with dropout on the probability matrix (GPT-ref gpt/gpt-jax.ipynb:351,
+    Gemma-ref gemma/gemma.ipynb:248, DeepSeek-ref deepseekv3/deepseekv3.ipynb:1186): the fused
+    HIP kernels on the GPU. ``neg`` (GPT-ref masks with -1e4 instead of -inf) only changes
+    scores of fully masked rows, which causal attention never has; the kernels mask with -inf.
+    q [B,Tq,H,hd], k/v [B,Tk,Hkv,hd]."""
+    if not training or p == 0.0:
+        return flash_attention(q, k, v, causal, scale)
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if q.is_cuda:
+        return flash_attention(q, k, v, causal, scale, dropout_p=p)
+    return _materialised(q, k, v, causal, scale, p, _new_seed(), neg)
 
 
 DECODE_MAX_ROWS = 16

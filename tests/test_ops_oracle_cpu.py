@@ -188,3 +188,22 @@ def test_chunked_linear_cross_entropy_matches_torch():
         assert torch.allclose(loss, ref, atol=1e-10), (chunk, loss, ref)
         for a, r in zip(args, ref_args):
             assert torch.allclose(a.grad, 2.0 * r.grad, atol=1e-10), chunk
+
+
+def test_attention_dropout_cpu_mask_is_seeded_and_calibrated():
+    """CPU path of attention_dropout: the same counter-hash mask the HIP kernels apply
+    (ops/attention.py dropout_keep_mask) -- deterministic per seed, keep rate 1 - p."""
+    from solvingpapers_amd.ops.attention import _materialised, dropout_keep_mask
+    m1 = dropout_keep_mask(42, 2, 3, 64, 64, 0.25)
+    m2 = dropout_keep_mask(42, 2, 3, 64, 64, 0.25)
+    m3 = dropout_keep_mask(43, 2, 3, 64, 64, 0.25)
+    assert torch.equal(m1, m2) and not torch.equal(m1, m3)
+    assert abs(m1.float().mean().item() - 0.75) < 0.02
+    g = torch.Generator().manual_seed(0)
+    q, k, v = (torch.randn(2, 64, 3, 16, generator=g) for _ in range(3))
+    o = _materialised(q, k, v, True, 0.25, 0.25, 42)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * 0.25
+    s = s.masked_fill(torch.triu(torch.ones(64, 64, dtype=torch.bool), 1), float("-inf"))
+    pr = torch.softmax(s, -1) * m1 / 0.75
+    want = torch.einsum("bhqk,bkhd->bqhd", pr, v)
+    assert torch.allclose(o, want, atol=1e-5)

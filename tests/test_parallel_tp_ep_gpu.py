@@ -99,7 +99,7 @@ def test_gemma_tp2_on_one_gpu_matches_unsharded(sp):
     loss = full(ids[:, :-2], ids[:, 1:-1])
     loss.backward()
     fg = {n: p.main_grad.float().cpu() for n, p in full.named_parameters()}
-    ref_loss = float(loss)
+    ref_loss = float(loss.detach())
     del full
     torch.cuda.synchronize()
     world = 2
@@ -151,7 +151,7 @@ def _ep_worker(rank, world, port, q, fp8):
     y = m(xr)
     (y.float() * gy[rank].cuda()).sum().backward()
     torch.cuda.synchronize()
-    q.put((rank, y.float().cpu().numpy(), xr.grad.float().cpu().numpy(), m.w13.grad.float().cpu().numpy(),
+    q.put((rank, y.detach().float().cpu().numpy(), xr.grad.float().cpu().numpy(), m.w13.grad.float().cpu().numpy(),
            m.w2.grad.float().cpu().numpy()))
     sdist.cleanup()
 

@@ -12,17 +12,22 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=1); ap.add_argument("--T", type=int, default=8192)
 ap.add_argument("--H", type=int, default=32); ap.add_argument("--Hkv", type=int, default=8)
 ap.add_argument("--hd", type=int, default=128); ap.add_argument("--noncausal", action="store_true")
+ap.add_argument("--hdv", type=int, default=0, help="v head dim (default = hd); 128 with --hd 192 = MLA")
+ap.add_argument("--pad", type=int, default=0, help="also time the same problem zero-padded to this head dim")
+ap.add_argument("--dropout", type=float, default=0.0)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--ab", default="")
 a = ap.parse_args()
 ops = _ext.ops()
 B, T, H, Hkv, hd = a.B, a.T, a.H, a.Hkv, a.hd
+hdv = a.hdv or hd
 causal = not a.noncausal
 q = torch.randn(B, T, H, hd, device="cuda", dtype=torch.bfloat16)
 k = torch.randn(B, T, Hkv, hd, device="cuda", dtype=torch.bfloat16)
-v = torch.randn(B, T, Hkv, hd, device="cuda", dtype=torch.bfloat16)
+v = torch.randn(B, T, Hkv, hdv, device="cuda", dtype=torch.bfloat16)
 sc = 1 / math.sqrt(hd)
-out, lse = ops.attn_fwd(q, k, v, sc, causal)
+P, SEED = a.dropout, 1234
+out, lse = ops.attn_fwd(q, k, v, sc, causal, P, SEED)
 do = torch.randn_like(out)
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
 def t(fn):
@@ -30,16 +35,29 @@ def t(fn):
     torch.cuda.synchronize(); s = time.perf_counter()
     for _ in range(a.iters): fn()
     torch.cuda.synchronize(); return (time.perf_counter() - s) / a.iters
-fl = 4 * B * H * T * T * hd * (0.5 if causal else 1.0)
-tf = t(lambda: ops.attn_fwd(q, k, v, sc, causal))
-tb = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal))
-print(f"attn B{B} T{T} H{H}/{Hkv} hd{hd} causal={causal}: fwd {tf*1e3:.3f} ms {fl/tf/1e12:.0f} TF | bwd {tb*1e3:.3f} ms {2.5*fl/tb/1e12:.0f} TF(2.5x)", flush=True)
+cf = 0.5 if causal else 1.0
+fl = 2 * B * H * T * T * (hd + hdv) * cf                 # useful fwd FLOPs (QK^T + PV)
+flb = 2 * B * H * T * T * (3 * hd + 2 * hdv) * cf        # useful bwd FLOPs (S, dP, dV, dK, dQ)
+tf = t(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
+tb = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
+print(f"attn B{B} T{T} H{H}/{Hkv} hd{hd}/{hdv} causal={causal} p={P}: fwd {tf*1e3:.3f} ms {fl/tf/1e12:.0f} TF | "
+      f"bwd {tb*1e3:.3f} ms {flb/tb/1e12:.0f} TF", flush=True)
+if a.pad:
+    pad = lambda x: torch.nn.functional.pad(x, (0, a.pad - x.shape[-1]))
+    qp, kp, vp = pad(q), pad(k), pad(v)
+    op_, lp = ops.attn_fwd(qp, kp, vp, sc, causal)
+    dop = torch.randn_like(op_)
+    dqp, dkp, dvp = torch.empty_like(qp), torch.empty_like(kp), torch.empty_like(vp)
+    tfp = t(lambda: ops.attn_fwd(qp, kp, vp, sc, causal))
+    tbp = t(lambda: ops.attn_bwd(dop, qp, kp, vp, op_, lp, dqp, dkp, dvp, sc, causal))
+    print(f"   same problem zero-padded to hd {a.pad}: fwd {tfp*1e3:.3f} ms ({fl/tfp/1e12:.0f} useful TF) | "
+          f"bwd {tbp*1e3:.3f} ms ({flb/tbp/1e12:.0f} useful TF)", flush=True)
 for setting in filter(None, a.ab.split(",")):
     key, val = setting.split("=")
     old = os.environ.get(key)
     os.environ[key] = val
-    tb2 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal))
+    tb2 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
     if old is None: os.environ.pop(key)
     else: os.environ[key] = old
-    tb3 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal))
-    print(f"   bwd with {key}={val}: {tb2*1e3:.3f} ms ({2.5*fl/tb2/1e12:.0f} TF) vs default again {tb3*1e3:.3f} ms", flush=True)
+    tb3 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
+    print(f"   bwd with {key}={val}: {tb2*1e3:.3f} ms ({flb/tb2/1e12:.0f} TF) vs default again {tb3*1e3:.3f} ms", flush=True)
