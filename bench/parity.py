@@ -6,6 +6,8 @@ the numbers the reference published on Tesla T4s.
   B1  LLaMA-tiny training tok/s    (llama3_ref: 2L d256 4h/2kv T128 B16, SGD 3e-4)  ref 29.0K tok/s (1xT4 fp32)
   B5  GPT-tiny training tok/s      (gpt_ref: 8L d256 1 head T256 B128, AdamW)        ref 16.2K tok/s (1xT4 fp32)
   B9  DeepSeek-V3-tiny tok/s       (dsv3_ref: 6L d512 T256 B16, AdamW, dropout .1)   ref 5.3K tok/s (2xT4 fp16)
+  B13 Gemma-tiny tok/s             (gemma_ref: 12L d768, 2 q-heads x 768 over 1 K/V head, T128 B64,
+                                    AdamW 2.5e-4, dropout .1; the reference recorded no throughput)
   B14 ViT-MNIST test accuracy, B15 AE MSE, B16 VAE loss, B17 KD student accuracy: trained
       with the reference epochs on synthetic MNIST-like digits (no dataset access) —
       quality parity unpinned, reported for completeness with wall-clock.
@@ -24,7 +26,7 @@ import torch
 
 from common import sdist
 
-REF = {"B1": 29.0e3, "B5": 16.2e3, "B9": 5.3e3, "B14": 97.25, "B15": 0.012954, "B16": 13881.32, "B17": 97.50}
+REF = {"B1": 29.0e3, "B5": 16.2e3, "B9": 5.3e3, "B13": None, "B14": 97.25, "B15": 0.012954, "B16": 13881.32, "B17": 97.50}
 
 
 def _lm_throughput(tag, model, flat, opt, V, B, T, steps, warmup, dtype_name, graph):
@@ -54,7 +56,8 @@ def _lm_throughput(tag, model, flat, opt, V, B, T, steps, warmup, dtype_name, gr
     el = time.perf_counter() - t0
     tok_s = B * T * steps / el
     print(json.dumps({"run": tag, "metric": "training tokens/sec", "value": round(tok_s, 1), "unit": "tokens/s",
-                      "reference": REF[tag], "vs_reference": round(tok_s / REF[tag], 2), "dtype": dtype_name,
+                      "reference": REF[tag], "vs_reference": round(tok_s / REF[tag], 2) if REF[tag] else None,
+                      "dtype": dtype_name,
                       "ms_per_step": round(el / steps * 1e3, 3), "hip_graph": graph,
                       "loss": round(float(out["loss"].detach()), 4), "n_gpus": 1}), flush=True)
 
@@ -91,6 +94,17 @@ def run_b9(a, dev, dt, name):
     opt = FlatAdamW(flat, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
                     graph_safe=a.graph)
     _lm_throughput("B9", m, flat, opt, c.vocab_size, 16, 256, a.steps, a.warmup, name, a.graph)
+
+
+def run_b13(a, dev, dt, name):
+    from solvingpapers_amd.models import gemma
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = gemma.config("gemma_ref")
+    m = gemma.GemmaRef(c).to(device=dev, dtype=dt)
+    flat = FlatParams(m)
+    opt = FlatAdamW(flat, lr=2.5e-4, weight_decay=0.01, graph_safe=a.graph)
+    _lm_throughput("B13", m, flat, opt, c.vocab_size, c.batch_size, c.block_size, a.steps, a.warmup, name, a.graph)
 
 
 def run_quality(tag, dev):
@@ -131,6 +145,8 @@ def main():
             run_b5(a, info.device, dt, a.dtype)
         elif tag == "B9":
             run_b9(a, info.device, dt, a.dtype)
+        elif tag == "B13":
+            run_b13(a, info.device, dt, a.dtype)
         else:
             run_quality(tag, str(info.device))
 

@@ -70,6 +70,7 @@ struct AttnParams {
   // fused dropout on P (DROP kernels): keep iff hash(seed, b, h, q, key) >> 8 >= drop_thr
   unsigned seed_lo, seed_hi, drop_thr;
   float drop_scale;  // 1 / (1 - p)
+  const int64_t* seed_ptr;  // device seed (graph-safe: a fresh mask per HIP-graph replay) or null
 };
 
 // ---- dropout counter hash (bit-identical in ops/attention.py dropout_keep_mask) ------
@@ -79,7 +80,13 @@ __device__ __forceinline__ unsigned mix32(unsigned x) {
 }
 // per (b, h) stream
 __device__ __forceinline__ unsigned drop_base(const AttnParams& p, int b, int h) {
-  return mix32(p.seed_lo ^ mix32(p.seed_hi + (unsigned)(b * p.H + h) * 0x9E3779B9U));
+  unsigned lo = p.seed_lo, hi = p.seed_hi;
+  if (p.seed_ptr) {
+    const uint64_t sd = (uint64_t)*p.seed_ptr;
+    lo = (unsigned)(sd & 0xffffffffu);
+    hi = (unsigned)(sd >> 32);
+  }
+  return mix32(lo ^ mix32(hi + (unsigned)(b * p.H + h) * 0x9E3779B9U));
 }
 __device__ __forceinline__ bool drop_keep(unsigned base, int q, int key, unsigned thr) {
   return (mix32(base + (unsigned)q * 0x85EBCA6BU + (unsigned)key * 0xC2B2AE35U) >> 8) >= thr;
@@ -984,7 +991,12 @@ static void fill_strides(AttnParams& p, const at::Tensor& q, const at::Tensor& k
   p.svb = v.stride(0); p.svt = v.stride(1); p.svh = v.stride(2);
 }
 
-static void fill_dropout(AttnParams& p, double dropout_p, int64_t seed) {
+static void fill_dropout(AttnParams& p, double dropout_p, int64_t seed, const c10::optional<at::Tensor>& seed_t) {
+  if (seed_t) {
+    TORCH_CHECK(seed_t->is_cuda() && seed_t->scalar_type() == at::kLong && seed_t->numel() >= 1,
+                "attention seed_t: int64 device tensor");
+    p.seed_ptr = seed_t->data_ptr<int64_t>();
+  }
   TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "attention dropout p must be in [0, 1)");
   p.seed_lo = (unsigned)(seed & 0xffffffffu);
   p.seed_hi = (unsigned)(((uint64_t)seed >> 32) & 0xffffffffu);
@@ -995,7 +1007,8 @@ static void fill_dropout(AttnParams& p, double dropout_p, int64_t seed) {
 // q [B,Tq,H,dk], k [B,Tk,Hkv,dk], v [B,Tk,Hkv,dv] (strided views allowed).
 // Returns (out [B,Tq,H,dv], lse [B,H,Tq]). dropout_p > 0: fused dropout on P (seeded hash).
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
-                                 bool causal, double dropout_p, int64_t seed) {
+                                 bool causal, double dropout_p, int64_t seed,
+                                 const c10::optional<at::Tensor>& seed_t) {
   check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v");
   const int B = q.size(0), Tq = q.size(1), H = q.size(2), HDK = q.size(3), HDV = v.size(3);
   const int Tk = k.size(1), Hkv = k.size(2);
@@ -1012,7 +1025,7 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   p.out = (bf16*)out.data_ptr(); p.lse = lse.data_ptr<float>();
   p.B = B; p.H = H; p.Hkv = Hkv; p.Tq = Tq; p.Tk = Tk;
   fill_strides(p, q, k, v);
-  fill_dropout(p, dropout_p, seed);
+  fill_dropout(p, dropout_p, seed, seed_t);
   p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
   p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal_off = Tk - Tq;
@@ -1081,7 +1094,8 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
 // Gradients written into dq/dk/dv (strided views allowed, e.g. slices of one dqkv buffer).
 void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
               const at::Tensor& out, const at::Tensor& lse, const at::Tensor& dq, const at::Tensor& dk,
-              const at::Tensor& dv, double scale, bool causal, double dropout_p, int64_t seed) {
+              const at::Tensor& dv, double scale, bool causal, double dropout_p, int64_t seed,
+              const c10::optional<at::Tensor>& seed_t) {
   check_qkv(dout, "dout"); check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(out, "out");
   check_qkv(dq, "dq"); check_qkv(dk, "dk"); check_qkv(dv, "dv");
   const int B = q.size(0), Tq = q.size(1), H = q.size(2), HDK = q.size(3), HDV = v.size(3);
@@ -1100,7 +1114,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   p.lse_in = lse.data_ptr<float>(); p.delta = delta.data_ptr<float>();
   p.B = B; p.H = H; p.Hkv = Hkv; p.Tq = Tq; p.Tk = Tk;
   fill_strides(p, q, k, v);
-  fill_dropout(p, dropout_p, seed);
+  fill_dropout(p, dropout_p, seed, seed_t);
   p.sob = out.stride(0); p.sot = out.stride(1); p.soh = out.stride(2);
   p.sdob = dout.stride(0); p.sdot = dout.stride(1); p.sdoh = dout.stride(2);
   p.sdqb = dq.stride(0); p.sdqt = dq.stride(1); p.sdqh = dq.stride(2);
@@ -1159,10 +1173,10 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, float dropout_p=0.0, int seed=0) "
-        "-> Tensor[]");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, float dropout_p=0.0, int seed=0, "
+        "Tensor? seed_t=None) -> Tensor[]");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
-        "Tensor(c!) dv, float scale, bool causal, float dropout_p=0.0, int seed=0) -> ()");
+        "Tensor(c!) dv, float scale, bool causal, float dropout_p=0.0, int seed=0, Tensor? seed_t=None) -> ()");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("attn_fwd", &spa::attn_fwd);

@@ -220,12 +220,19 @@ class MLA(tnn.Module):
             return linear(rms_norm(linear(xn, self.wdq), self.q_norm, c.norm_eps), self.wuq)
         return linear(xn, self.wq)
 
+    def _rope(self, x, pos):
+        from ..infer.graph import DecodeState
+        if isinstance(pos, DecodeState):   # device positions: graph-capture safe
+            return apply_rope(x, self.c.rope_theta, positions=pos.positions.expand(x.shape[0], x.shape[1]),
+                              max_len=pos.max_len)
+        return apply_rope(x, self.c.rope_theta, pos)
+
     def _latent(self, xn, pos):
         c = self.c
         B, T, _ = xn.shape
         ckr = linear(xn, self.wdkv)
         ckv = rms_norm(ckr[..., :c.kv_lora_rank].contiguous(), self.kv_norm, c.norm_eps)
-        kr = apply_rope(ckr[..., c.kv_lora_rank:].reshape(B, T, 1, c.qk_rope_dim), c.rope_theta, pos)
+        kr = self._rope(ckr[..., c.kv_lora_rank:].reshape(B, T, 1, c.qk_rope_dim), pos)
         return ckv, kr
 
     def forward(self, xn, L0=None, cache=None, pos=0):
@@ -234,7 +241,7 @@ class MLA(tnn.Module):
         H, dn, dr, dv = c.n_heads, c.qk_nope_dim, c.qk_rope_dim, c.v_head_dim
         scale = 1.0 / math.sqrt(dn + dr)
         q = self._q(xn).view(B, T, H, dn + dr)
-        qr = apply_rope(q[..., dn:], c.rope_theta, pos)
+        qr = self._rope(q[..., dn:], pos)
         ckv, kr = self._latent(xn, pos)
         if cache is not None:
             return self._decode(q[..., :dn], qr, ckv, kr, cache, pos, scale)
@@ -249,23 +256,31 @@ class MLA(tnn.Module):
 
     def _decode(self, qn, qr, ckv, kr, cache, pos, scale):
         """Latent-space attention over the compressed cache (W_uk absorbed into q, W_uv applied
-        after): per token the cache holds kv_lora + rope values instead of 2*H*hd."""
+        after): per token the cache holds kv_lora + rope values instead of 2*H*hd. The scores
+        and the latent output come from one HIP launch (csrc/kernels/mla_decode.hip: 576-wide
+        single-head MQA, split-K flash-decoding); the absorptions are two batched GEMMs.
+        ``pos`` is an int (eager) or a DecodeState (HIP-graph decode: write row and valid
+        length on the device)."""
+        from ..infer.graph import DecodeState
+        from ..ops.attention import mla_decode_attention
         c = self.c
         B, T, H, dn = qn.shape
+        C, dv = c.kv_lora_rank, c.v_head_dim
         cc, cr = cache
-        cc[:, pos:pos + T] = ckv.to(cc.dtype)
-        cr[:, pos:pos + T] = kr.reshape(B, T, -1).to(cr.dtype)
-        S = pos + T
-        w = self.wukv.view(H, dn + c.v_head_dim, c.kv_lora_rank)
-        q_abs = torch.einsum("bthn,hnc->bthc", qn.float(), w[:, :dn].float())
-        s = (torch.einsum("bthc,bsc->bhts", q_abs, cc[:, :S].float())
-             + torch.einsum("bthr,bsr->bhts", qr.float(), cr[:, :S].float())) * scale
-        i = torch.arange(T, device=s.device)[:, None] + pos
-        j = torch.arange(S, device=s.device)[None, :]
-        s = s.masked_fill(j > i, float("-inf"))
-        o_lat = torch.einsum("bhts,bsc->bthc", torch.softmax(s, -1), cc[:, :S].float())
-        o = torch.einsum("bthc,hvc->bthv", o_lat, w[:, dn:].float()).to(qn.dtype)
-        return linear(o.reshape(B, T, H * c.v_head_dim), self.wo)
+        if isinstance(pos, DecodeState):
+            cc.index_copy_(1, pos.index, ckv.to(cc.dtype))
+            cr.index_copy_(1, pos.index, kr.reshape(B, T, -1).to(cr.dtype))
+            kv_len, kv_len_t = 0, pos.kv_len
+        else:
+            cc[:, pos:pos + T] = ckv.to(cc.dtype)
+            cr[:, pos:pos + T] = kr.reshape(B, T, -1).to(cr.dtype)
+            kv_len, kv_len_t = pos + T, None
+        w = self.wukv.view(H, dn + dv, C)
+        # q_abs[b, t, h] = q_nope[b, t, h] @ W_uk[h]  (one batched GEMM over heads)
+        q_abs = torch.bmm(qn.permute(2, 0, 1, 3).reshape(H, B * T, dn), w[:, :dn]).view(H, B, T, C)
+        o_lat = mla_decode_attention(q_abs.permute(1, 2, 0, 3), qr, cc, cr, scale, kv_len, kv_len_t)
+        o = torch.bmm(o_lat.permute(2, 0, 1, 3).reshape(H, B * T, C), w[:, dn:].transpose(1, 2))
+        return linear(o.view(H, B, T, dv).permute(1, 2, 0, 3).reshape(B, T, H * dv), self.wo)
 
 
 # =============================================================================== FFN / MoE
@@ -542,6 +557,16 @@ class DeepSeekV3(tnn.Module):
         """Write ids' latents at cache rows [pos, pos+T), return the last position's logits [B, V]."""
         n, _ = self.hidden(ids, cache, pos)
         return self.logits(n[:, -1:]).float()[:, -1]
+
+    def step_graph(self, ids, cache, state):
+        """One-token decode step with every position on the device (HIP-graph capturable,
+        infer/graph.py GraphDecoder): RoPE at ``state.positions``, latent cache rows written at
+        ``state.index``, the MLA decode kernel reads the valid length from ``state.kv_len``; the
+        MoE routing / permutation / grouped GEMMs never read device values on the host."""
+        if self.c.attention == "ref":
+            raise NotImplementedError("graph decode needs the paper MLA (the ref preset adds sinusoidal PE by position)")
+        n, _ = self.hidden(ids, cache, state)
+        return self.logits(n).float()[:, -1]
 
     @torch.no_grad()
     def generate(self, ids, max_new_tokens, temperature=1.0, top_k=None, greedy=False, generator=None,

@@ -67,10 +67,19 @@ def _new_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,)).item())   # host generator: no device sync
 
 
+def _seed_args(seed):
+    """(int seed, device seed tensor or None): a tensor seed is read by the kernels on the
+    device, so a captured HIP graph draws a fresh mask at every replay."""
+    if isinstance(seed, torch.Tensor):
+        return 0, seed
+    return int(seed or 0), None
+
+
 class _FlashFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, scale, dropout_p, seed):
-        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal, dropout_p, seed)
+        si, st = _seed_args(seed)
+        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal, dropout_p, si, st)
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.causal, ctx.scale, ctx.dropout_p, ctx.seed = causal, scale, dropout_p, seed
         return out
@@ -81,8 +90,9 @@ class _FlashFn(torch.autograd.Function):
         dq = torch.empty_like(q, memory_format=torch.contiguous_format)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format)
+        si, st = _seed_args(ctx.seed)
         _ext.ops().attn_bwd(dout.contiguous(), q, k, v, out, lse, dq, dk, dv, ctx.scale, ctx.causal,
-                            ctx.dropout_p, ctx.seed)
+                            ctx.dropout_p, si, st)
         return dq, dk, dv, None, None, None, None
 
 
@@ -96,7 +106,8 @@ class _PackedFn(torch.autograd.Function):
         B, T = qkv.shape[0], qkv.shape[1]
         x4 = qkv.view(B, T, H + 2 * Hkv, hd)
         q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
-        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal, dropout_p, seed)
+        si, st = _seed_args(seed)
+        out, lse = _ext.ops().attn_fwd(q, k, v, scale, causal, dropout_p, si, st)
         ctx.save_for_backward(qkv, out, lse)
         ctx.H, ctx.Hkv, ctx.hd, ctx.causal, ctx.scale = H, Hkv, hd, causal, scale
         ctx.dropout_p, ctx.seed = dropout_p, seed
@@ -112,7 +123,7 @@ class _PackedFn(torch.autograd.Function):
         d4 = dqkv.view(B, T, H + 2 * Hkv, hd)
         _ext.ops().attn_bwd(dout.contiguous().view(B, T, H, hd), x4[:, :, :H], x4[:, :, H:H + Hkv],
                             x4[:, :, H + Hkv:], out, lse, d4[:, :, :H], d4[:, :, H:H + Hkv], d4[:, :, H + Hkv:],
-                            ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed)
+                            ctx.scale, ctx.causal, ctx.dropout_p, *_seed_args(ctx.seed))
         return dqkv, None, None, None, None, None, None, None
 
 
@@ -157,8 +168,10 @@ def flash_attention(q, k, v, causal=True, scale=None, dropout_p=0.0, seed=None):
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     dropout_p = float(dropout_p)
     if dropout_p > 0.0 and seed is None:
-        seed = _new_seed()
-    seed = int(seed or 0)
+        # on the GPU a device seed (torch's graph-capture-safe generator): fresh mask per replay
+        seed = torch.randint(0, 2 ** 62, (1,), device=q.device, dtype=torch.int64) if q.is_cuda else _new_seed()
+    if not isinstance(seed, torch.Tensor):
+        seed = int(seed or 0)
     dqk, dv = q.shape[-1], v.shape[-1]
     if q.is_cuda and q.dtype == torch.bfloat16 and q.dim() == 4:
         if (dqk, dv) in FLASH_PAIRS and (dropout_p == 0.0 or dqk == dv):
@@ -184,9 +197,10 @@ def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None, dropou
     B, T = qkv.shape[0], qkv.shape[1]
     scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
     if dropout_p > 0.0 and seed is None:
-        seed = _new_seed()
+        seed = torch.randint(0, 2 ** 62, (1,), device=qkv.device, dtype=torch.int64) if qkv.is_cuda else _new_seed()
     if qkv.is_cuda and qkv.dtype == torch.bfloat16 and hd in FLASH_HD:
-        return _PackedFn.apply(qkv, H, Hkv, hd, causal, scale, float(dropout_p), int(seed or 0))
+        return _PackedFn.apply(qkv, H, Hkv, hd, causal, scale, float(dropout_p),
+                               seed if isinstance(seed, torch.Tensor) else int(seed or 0))
     x4 = qkv.view(B, T, H + 2 * Hkv, hd)
     q, k, v = x4[:, :, :H], x4[:, :, H:H + Hkv], x4[:, :, H + Hkv:]
     return flash_attention(q, k, v, causal, scale, dropout_p, seed).reshape(B, T, H * hd)
@@ -233,3 +247,20 @@ def decode_attention(q, k, v, causal=True, scale=None, nsplit=0, kv_len=None):
     if kv_len is not None:
         raise ValueError("decode_attention: kv_len needs the decode kernel (Tq * H / Hkv <= 16, bf16 on the GPU)")
     return flash_attention(q.contiguous(), k, v, causal, scale)
+
+
+def mla_decode_attention(q_abs, q_rope, cc, cr, scale, kv_len=0, kv_len_t=None, nsplit=0):
+    """DeepSeek MLA decode in latent space (csrc/kernels/mla_decode.hip): q_abs [B,T,H,C]
+    (q_nope with W_uk absorbed), q_rope [B,T,H,R]; caches cc [B,Smax,C], cr [B,Smax,R] with
+    rows [0, kv_len) valid (``kv_len_t``: device int32 [1], graph mode); query token t sits at
+    cache row kv_len - T + t. Returns the latent output [B,T,H,C] (W_uv applied by the caller)."""
+    if q_abs.is_cuda:
+        return _ext.ops().mla_decode(q_abs, q_rope, cc, cr, float(scale), int(kv_len), kv_len_t, int(nsplit))
+    B, T, H, C = q_abs.shape
+    S = int(kv_len_t.item()) if kv_len_t is not None else int(kv_len)
+    s = (torch.einsum("bthc,bsc->bhts", q_abs.float(), cc[:, :S].float())
+         + torch.einsum("bthr,bsr->bhts", q_rope.float(), cr[:, :S].float())) * scale
+    i = torch.arange(T, device=s.device)[:, None] + (S - T)
+    j = torch.arange(S, device=s.device)[None, :]
+    s = s.masked_fill(j > i, float("-inf"))
+    return torch.einsum("bhts,bsc->bthc", torch.softmax(s, -1), cc[:, :S].float()).to(q_abs.dtype)

@@ -74,10 +74,14 @@ def rope_packed_(x, nrot, theta=10000.0, pos_off=0, interleaved=True, head_dim=N
     return torch.cat([rot, x4[:, :, nrot:]], dim=2).view(x.shape)
 
 
-def apply_rope(x, theta=10000.0, pos_off=0, interleaved=True, positions=None, ref_freqs=False):
-    """Out-of-place rotation of every head of x [B, T, H, hd]."""
+def apply_rope(x, theta=10000.0, pos_off=0, interleaved=True, positions=None, ref_freqs=False, max_len=None):
+    """Out-of-place rotation of every head of x [B, T, H, hd]. ``positions`` (int [B, T] on
+    the device) with ``max_len`` (table size) is graph-capture safe: no host read."""
     B, T, H, hd = x.shape
-    n = (int(positions.max()) + 1) if positions is not None else pos_off + T
+    if positions is not None:
+        n = max_len if max_len is not None else int(positions.max()) + 1
+    else:
+        n = pos_off + T
     cos, sin = RopeCache.get(n, hd, theta, x.device, ref_freqs)
     if x.is_cuda and positions is None:
         return _RopeFn.apply(x.clone(), H, cos, sin, pos_off, interleaved, False, hd)
