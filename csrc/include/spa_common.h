@@ -108,6 +108,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// Elementwise kernels walk storage order: any dense (non-overlapping, gap-free) tensor -- e.g. a
+// channels-last conv activation -- is used as is and its output keeps the same strides.
+inline at::Tensor dense(const at::Tensor& t) { return t.is_non_overlapping_and_dense() ? t : t.contiguous(); }
+// `t` laid out exactly like `like` (a no-op when the strides already match)
+inline at::Tensor dense_like(const at::Tensor& t, const at::Tensor& like) {
+  if (t.strides() == like.strides() && t.is_non_overlapping_and_dense()) return t;
+  return at::empty_like(like, t.options()).copy_(t);
+}
+
 }  // namespace spa
 
 #define SPA_CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a HIP tensor")

@@ -159,7 +159,7 @@ static int ew_grid(long n) { return (int)std::max<long>(1, std::min<long>((n + 2
 
 at::Tensor act_fwd(const at::Tensor& x_, int64_t kind, double alpha) {
   SPA_CHECK_CUDA(x_);
-  auto x = x_.contiguous();
+  auto x = dense(x_);
   auto y = at::empty_like(x);
   const long n = x.numel();
   if (n == 0) return y;
@@ -171,8 +171,8 @@ at::Tensor act_fwd(const at::Tensor& x_, int64_t kind, double alpha) {
   return y;
 }
 at::Tensor act_bwd(const at::Tensor& dy_, const at::Tensor& x_, int64_t kind, double alpha) {
-  auto x = x_.contiguous();
-  auto dy = dy_.contiguous();
+  auto x = dense(x_);
+  auto dy = dense_like(dy_, x);
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.numel() == x.numel());
   auto dx = at::empty_like(x);
   const long n = x.numel();

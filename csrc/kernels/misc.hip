@@ -29,38 +29,124 @@ __device__ __forceinline__ float u01(uint64_t seed, uint64_t i) {  // (0, 1]
 }
 
 // --------------------------------------------------------------------------- dropout
+// 8 elements per thread per step (16-byte bf16 / 2 x 16-byte fp32 vectors); the keep bit of
+// element i is a 32-bit counter hash of (seed, i) -- ~10 integer ops, so the kernel stays on the
+// HBM roof (a 64-bit mix per element made it VALU-bound at 3.2 TB/s).
+__device__ __forceinline__ unsigned hash32(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ bool drop_keep_elem(unsigned base, unsigned hi_mix, long i, unsigned thr) {
+  return (hash32(base + (unsigned)i * 0x9E3779B1U + hi_mix) >> 8) >= thr;
+}
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, float p,
-                                                      uint64_t seed, const int64_t* __restrict__ seed_ptr) {
+                                                      uint64_t seed, const int64_t* __restrict__ seed_ptr, bool vec) {
   if (seed_ptr) seed = (uint64_t)*seed_ptr;   // device seed: fresh mask per HIP-graph replay
+  const unsigned base = hash32((unsigned)seed ^ 0x5bd1e995U), shi = (unsigned)(seed >> 32);
+  const unsigned thr = (unsigned)(p * 16777216.f);
   const float scale = 1.f / (1.f - p);
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const bool keep = u01(seed, i) > p;
-    y[i] = (T)(keep ? (float)x[i] * scale : 0.f);
+  const long nv = vec ? n / 8 : 0;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
+    const long i0 = v * 8;
+    const unsigned hm = hash32(shi + (unsigned)(i0 >> 32) * 0x85EBCA6BU);
+    float f[8];
+    load8(x + i0, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = drop_keep_elem(base, hm, i0 + k, thr) ? f[k] * scale : 0.f;
+    store8(y + i0, f);
+  }
+  for (long i = nv * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned hm = hash32(shi + (unsigned)(i >> 32) * 0x85EBCA6BU);
+    y[i] = (T)(drop_keep_elem(base, hm, i, thr) ? (float)x[i] * scale : 0.f);
   }
 }
 at::Tensor dropout_apply(const at::Tensor& x_, double p, int64_t seed, const c10::optional<at::Tensor>& seed_t) {
   SPA_CHECK_CUDA(x_);
   if (seed_t) TORCH_CHECK(seed_t->scalar_type() == at::kLong && seed_t->is_cuda() && seed_t->numel() >= 1);
   const int64_t* sp = seed_t ? seed_t->data_ptr<int64_t>() : nullptr;
-  auto x = x_.contiguous();
+  auto x = dense(x_);
   auto y = at::empty_like(x);
   const long n = x.numel();
   if (n == 0) return y;
+  const bool vec = (uintptr_t)x.data_ptr() % 32 == 0;   // y is fresh (allocator-aligned); views may not be
   DeviceGuard g(x.device());
-  const int grid = (int)std::min<long>((n + 255) / 256, 8192);
+  const int grid = (int)std::max<long>(1, std::min<long>((n / 8 + 255) / 256, 4096));
   if (x.scalar_type() == at::kBFloat16)
-    dropout_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), n, (float)p, seed, sp);
+    dropout_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), n, (float)p, seed, sp, vec);
   else if (x.scalar_type() == at::kFloat)
-    dropout_kernel<float><<<grid, 256, 0, stream()>>>(x.data_ptr<float>(), y.data_ptr<float>(), n, (float)p, seed, sp);
+    dropout_kernel<float><<<grid, 256, 0, stream()>>>(x.data_ptr<float>(), y.data_ptr<float>(), n, (float)p, seed, sp, vec);
   else TORCH_CHECK(false, "dropout: bf16/fp32 only");
   SPA_LAUNCH_CHECK();
   return y;
 }
 
+
 // --------------------------------------------------------------------------- kd loss
 // per row: hard = lse(s) - s[y]; soft = sum_c p_c (log p_c - log q_c), p = softmax(t/T), q = softmax(s/T)
 // grad (in place into gs): alpha/B (softmax(s) - onehot) + (1-alpha) T / B (q - p)
+// One WAVE per row with the row held in registers (VPL values of s and of t per lane, C <= 64 VPL):
+// one HBM read of each input, three online (max, sum-exp) pairs, wave reductions only -- the
+// reference shape (C = 10) leaves no 256-thread block idle, and C = 1000 reads each row once.
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void kd_wave_kernel(const T* __restrict__ s, const T* __restrict__ t,
+                                                      const int64_t* __restrict__ y, float* __restrict__ hard,
+                                                      float* __restrict__ soft, T* __restrict__ gs, int B, int C,
+                                                      float invT, float alpha, float invB) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  const T* sr = s + (long)row * C;
+  const T* tr = t + (long)row * C;
+  float a[VPL], b[VPL];
+  float m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = lane + 64 * v;
+    a[v] = c < C ? (float)sr[c] : -INFINITY;
+    b[v] = c < C ? (float)tr[c] : -INFINITY;
+    m1 = fmaxf(m1, a[v]);
+    m3 = fmaxf(m3, b[v]);
+  }
+  m1 = wave_max(m1);
+  m3 = wave_max(m3) * invT;
+  m2 = m1 * invT;  // T > 0: max(s/T) = max(s)/T
+  float z1 = 0.f, z2 = 0.f, z3 = 0.f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    if (lane + 64 * v < C) {
+      z1 += __expf(a[v] - m1);
+      z2 += __expf(a[v] * invT - m2);
+      z3 += __expf(b[v] * invT - m3);
+    }
+  }
+  z1 = wave_sum(z1); z2 = wave_sum(z2); z3 = wave_sum(z3);
+  const float l1 = m1 + __logf(z1), l2 = m2 + __logf(z2), l3 = m3 + __logf(z3);
+  const int64_t yy = y[row];
+  float kl = 0.f, sy = 0.f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = lane + 64 * v;
+    if (c < C) {
+      const float lp = b[v] * invT - l3, lq = a[v] * invT - l2;
+      const float pc = __expf(lp);
+      kl += pc * (lp - lq);
+      if (c == yy) sy = a[v];
+      if (gs) {
+        const float g = alpha * invB * (__expf(a[v] - l1) - (c == yy ? 1.f : 0.f)) +
+                        (1.f - alpha) * invB / invT * (__expf(lq) - pc);
+        gs[(long)row * C + c] = (T)g;
+      }
+    }
+  }
+  kl = wave_sum(kl);
+  sy = wave_sum(sy);
+  if (lane == 0) {
+    hard[row] = l1 - sy;
+    soft[row] = kl;
+  }
+}
+
+// rows wider than 64 x 32 values: one block per row, three passes (the general fallback)
 template <typename T>
 __global__ __launch_bounds__(256) void kd_kernel(const T* __restrict__ s, const T* __restrict__ t,
                                                  const int64_t* __restrict__ y, float* __restrict__ hard,
@@ -119,13 +205,24 @@ std::vector<at::Tensor> kd_loss_fwd(const at::Tensor& s_, const at::Tensor& t_, 
   auto gs = want_grad ? at::empty_like(s) : at::Tensor();
   if (B == 0) return {hard, soft, gs};
   auto yc = y.contiguous();
+  TORCH_CHECK(T > 0, "kd_loss: temperature must be positive");
+#define KDW(TT, V)                                                                                            \
+  (kd_wave_kernel<TT, V>)<<<cdiv(B, 4), 256, 0, stream()>>>(                                                     \
+      (const TT*)s.data_ptr(), (const TT*)t.data_ptr(), yc.data_ptr<int64_t>(), hard.data_ptr<float>(),       \
+      soft.data_ptr<float>(), want_grad ? (TT*)gs.data_ptr() : nullptr, B, C, (float)(1.0 / T), (float)alpha, \
+      1.f / B)
 #define KDL(TT)                                                                                              \
-  kd_kernel<TT><<<B, 256, 0, stream()>>>((const TT*)s.data_ptr(), (const TT*)t.data_ptr(),                   \
-                                         yc.data_ptr<int64_t>(), hard.data_ptr<float>(), soft.data_ptr<float>(), \
-                                         want_grad ? (TT*)gs.data_ptr() : nullptr, C, (float)(1.0 / T),       \
-                                         (float)alpha, 1.f / B)
-  if (s.scalar_type() == at::kBFloat16) KDL(bf16); else KDL(float);
+  if (C <= 64) KDW(TT, 1);                                                                                   \
+  else if (C <= 256) KDW(TT, 4);                                                                             \
+  else if (C <= 1024) KDW(TT, 16);                                                                           \
+  else if (C <= 2048) KDW(TT, 32);                                                                           \
+  else (kd_kernel<TT>)<<<B, 256, 0, stream()>>>((const TT*)s.data_ptr(), (const TT*)t.data_ptr(),              \
+                                              yc.data_ptr<int64_t>(), hard.data_ptr<float>(),                 \
+                                              soft.data_ptr<float>(), want_grad ? (TT*)gs.data_ptr() : nullptr, \
+                                              C, (float)(1.0 / T), (float)alpha, 1.f / B)
+  if (s.scalar_type() == at::kBFloat16) { KDL(bf16); } else { KDL(float); }
 #undef KDL
+#undef KDW
   SPA_LAUNCH_CHECK();
   return {hard, soft, gs};
 }
@@ -247,20 +344,19 @@ std::vector<at::Tensor> mse_fwd(const at::Tensor& a_, const at::Tensor& b_, bool
   return {part.sum().reshape({1}), ga};
 }
 
-// --------------------------------------------------------------------------- LRN (NCHW)
+// --------------------------------------------------------------------------- LRN (NCHW or channels-last)
 // b_c = a_c * s_c^-beta, s_c = k + alpha/n * sum_{c' in [c-(n-1)/2, c+n/2]} a_c'^2   (torch convention)
+// i walks the storage; cs is the channel stride (H*W for NCHW, 1 for NHWC): c = (i / cs) % C and
+// channel j of the same pixel sits at i + (j - c) * cs.
 template <typename T>
 __global__ __launch_bounds__(256) void lrn_fwd_kernel(const T* __restrict__ a, T* __restrict__ b,
-                                                      float* __restrict__ sc, int N, int C, long HW, int size,
+                                                      float* __restrict__ sc, long total, int C, long cs, int size,
                                                       float alpha, float beta, float k) {
-  const long total = (long)N * C * HW;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long hw = i % HW;
-    const int c = (i / HW) % C;
-    const long n = i / (HW * C);
+    const int c = (i / cs) % C;
     const int lo = max(0, c - size / 2), hi = min(C - 1, c + (size - 1) / 2);
     float ss = 0.f;
-    for (int j = lo; j <= hi; ++j) { const float v = (float)a[(n * C + j) * HW + hw]; ss += v * v; }
+    for (int j = lo; j <= hi; ++j) { const float v = (float)a[i + (j - c) * cs]; ss += v * v; }
     const float s = k + alpha / size * ss;
     sc[i] = s;
     b[i] = (T)((float)a[i] * __powf(s, -beta));
@@ -269,35 +365,37 @@ __global__ __launch_bounds__(256) void lrn_fwd_kernel(const T* __restrict__ a, T
 // da_c = dy_c s_c^-beta - 2 alpha beta / n * a_c * sum_{c': c in window(c')} dy_c' a_c' s_c'^(-beta-1)
 template <typename T>
 __global__ __launch_bounds__(256) void lrn_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ a,
-                                                      const float* __restrict__ sc, T* __restrict__ da, int N, int C,
-                                                      long HW, int size, float alpha, float beta) {
-  const long total = (long)N * C * HW;
+                                                      const float* __restrict__ sc, T* __restrict__ da, long total,
+                                                      int C, long cs, int size, float alpha, float beta) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long hw = i % HW;
-    const int c = (i / HW) % C;
-    const long n = i / (HW * C);
+    const int c = (i / cs) % C;
     // c' whose window contains c: c' - size/2 <= c <= c' + (size-1)/2
     const int lo = max(0, c - (size - 1) / 2), hi = min(C - 1, c + size / 2);
     float acc = 0.f;
     for (int j = lo; j <= hi; ++j) {
-      const long o = (n * C + j) * HW + hw;
+      const long o = i + (j - c) * cs;
       acc += (float)dy[o] * (float)a[o] * __powf(sc[o], -beta - 1.f);
     }
     da[i] = (T)((float)dy[i] * __powf(sc[i], -beta) - 2.f * alpha * beta / size * (float)a[i] * acc);
   }
 }
+static bool channels_last(const at::Tensor& t) {
+  return t.dim() == 4 && !t.is_contiguous() && t.is_contiguous(at::MemoryFormat::ChannelsLast);
+}
 std::vector<at::Tensor> lrn_fwd(const at::Tensor& a_, int64_t size, double alpha, double beta, double k) {
-  auto a = a_.contiguous();
-  TORCH_CHECK(a.dim() == 4, "lrn: NCHW input");
+  TORCH_CHECK(a_.dim() == 4, "lrn: 4-D input");
+  const bool cl = channels_last(a_);
+  auto a = cl ? a_ : a_.contiguous();
   DeviceGuard g(a.device());
   auto b = at::empty_like(a);
-  auto sc = at::empty(a.sizes(), a.options().dtype(at::kFloat));
+  auto sc = at::empty_like(a, a.options().dtype(at::kFloat));
   const long total = a.numel();
   if (total == 0) return {b, sc};
+  const long cs = cl ? 1 : a.size(2) * a.size(3);
   const int grid = (int)std::min<long>((total + 255) / 256, 8192);
 #define LF(TT)                                                                                                \
   lrn_fwd_kernel<TT><<<grid, 256, 0, stream()>>>((const TT*)a.data_ptr(), (TT*)b.data_ptr(), sc.data_ptr<float>(), \
-                                                 a.size(0), a.size(1), a.size(2) * a.size(3), size, alpha, beta, k)
+                                                 total, a.size(1), cs, size, alpha, beta, k)
   if (a.scalar_type() == at::kBFloat16) LF(bf16); else LF(float);
 #undef LF
   SPA_LAUNCH_CHECK();
@@ -305,96 +403,116 @@ std::vector<at::Tensor> lrn_fwd(const at::Tensor& a_, int64_t size, double alpha
 }
 at::Tensor lrn_bwd(const at::Tensor& dy_, const at::Tensor& a_, const at::Tensor& sc, int64_t size, double alpha,
                    double beta) {
-  auto dy = dy_.contiguous(), a = a_.contiguous();
+  const bool cl = channels_last(a_);
+  const auto fmt = cl ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
+  auto a = a_.contiguous(fmt), dy = dy_.contiguous(fmt);
+  TORCH_CHECK(sc.is_contiguous(fmt), "lrn_bwd: scale layout");
   DeviceGuard g(a.device());
   auto da = at::empty_like(a);
   const long total = a.numel();
   if (total == 0) return da;
+  const long cs = cl ? 1 : a.size(2) * a.size(3);
   const int grid = (int)std::min<long>((total + 255) / 256, 8192);
 #define LB(TT)                                                                                                  \
   lrn_bwd_kernel<TT><<<grid, 256, 0, stream()>>>((const TT*)dy.data_ptr(), (const TT*)a.data_ptr(),              \
-                                                 sc.data_ptr<float>(), (TT*)da.data_ptr(), a.size(0), a.size(1), \
-                                                 a.size(2) * a.size(3), size, alpha, beta)
+                                                 sc.data_ptr<float>(), (TT*)da.data_ptr(), total, a.size(1), cs, \
+                                                 size, alpha, beta)
   if (a.scalar_type() == at::kBFloat16) LB(bf16); else LB(float);
 #undef LB
   SPA_LAUNCH_CHECK();
   return da;
 }
 
-// --------------------------------------------------------------------------- maxpool2d (NCHW, no padding)
-template <typename T>
+// --------------------------------------------------------------------------- maxpool2d (NCHW or NHWC, no padding)
+// i walks the output storage; arg holds h * W + w of the window max (first max, NaN wins)
+template <typename T, bool NHWC>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                          int* __restrict__ arg, int NC, int H, int W, int OH, int OW,
-                                                          int ks, int st) {
-  const long total = (long)NC * OH * OW;
+                                                          int* __restrict__ arg, int N, int C, int H, int W, int OH,
+                                                          int OW, int ks, int st) {
+  const long total = (long)N * C * OH * OW;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int ow = i % OW, oh = (i / OW) % OH;
-    const long nc = i / ((long)OH * OW);
-    const T* xp = x + nc * H * W;
+    int c, ow, oh;
+    long n;
+    if (NHWC) { c = i % C; ow = (i / C) % OW; oh = (i / ((long)C * OW)) % OH; n = i / ((long)C * OW * OH); }
+    else { ow = i % OW; oh = (i / OW) % OH; c = (i / ((long)OW * OH)) % C; n = i / ((long)OW * OH * C); }
+    // element (h, w) of this (n, c) plane: x[pb + (h * W + w) * ps]
+    const long pb = NHWC ? n * H * W * C + c : (n * C + c) * H * W;
+    const int ps = NHWC ? C : 1;
     float best = -INFINITY;
     int bi = 0;
     for (int r = 0; r < ks; ++r)
-      for (int c = 0; c < ks; ++c) {
-        const int hh = oh * st + r, ww = ow * st + c;
-        const float v = (float)xp[hh * W + ww];
-        if (v > best || (v != v)) { best = v; bi = hh * W + ww; }
+      for (int q = 0; q < ks; ++q) {
+        const int hw = (oh * st + r) * W + ow * st + q;
+        const float v = (float)x[pb + (long)hw * ps];
+        if (v > best || (v != v)) { best = v; bi = hw; }
       }
     y[i] = (T)best;
     arg[i] = bi;
   }
 }
 // gather-form backward: each input pixel sums the gradients of the windows whose argmax it is
-template <typename T>
+template <typename T, bool NHWC>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy, const int* __restrict__ arg,
-                                                          T* __restrict__ dx, int NC, int H, int W, int OH, int OW,
-                                                          int ks, int st) {
-  const long total = (long)NC * H * W;
+                                                          T* __restrict__ dx, int N, int C, int H, int W, int OH,
+                                                          int OW, int ks, int st) {
+  const long total = (long)N * C * H * W;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int w = i % W, h = (i / W) % H;
-    const long nc = i / ((long)H * W);
+    int c, w, h;
+    long n;
+    if (NHWC) { c = i % C; w = (i / C) % W; h = (i / ((long)C * W)) % H; n = i / ((long)C * W * H); }
+    else { w = i % W; h = (i / W) % H; c = (i / ((long)W * H)) % C; n = i / ((long)W * H * C); }
+    const long ob = NHWC ? n * OH * OW * C + c : (n * C + c) * OH * OW;
+    const int os = NHWC ? C : 1;
     const int oh0 = max(0, (h - ks + st) / st), oh1 = min(OH - 1, h / st);
     const int ow0 = max(0, (w - ks + st) / st), ow1 = min(OW - 1, w / st);
     float acc = 0.f;
     for (int oh = oh0; oh <= oh1; ++oh)
       for (int ow = ow0; ow <= ow1; ++ow) {
-        const long o = nc * OH * OW + oh * OW + ow;
+        const long o = ob + (long)(oh * OW + ow) * os;
         if (arg[o] == h * W + w) acc += (float)dy[o];
       }
     dx[i] = (T)acc;
   }
 }
 std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x_, int64_t ks, int64_t st) {
-  auto x = x_.contiguous();
-  TORCH_CHECK(x.dim() == 4, "maxpool2d: NCHW input");
+  TORCH_CHECK(x_.dim() == 4, "maxpool2d: 4-D input");
+  const bool cl = channels_last(x_);
+  const auto fmt = cl ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
+  auto x = x_.contiguous(fmt);
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int OH = (H - ks) / st + 1, OW = (W - ks) / st + 1;
   DeviceGuard g(x.device());
-  auto y = at::empty({N, C, OH, OW}, x.options());
-  auto arg = at::empty({N, C, OH, OW}, x.options().dtype(at::kInt));
+  auto y = at::empty({N, C, OH, OW}, x.options().memory_format(fmt));
+  auto arg = at::empty({N, C, OH, OW}, x.options().dtype(at::kInt).memory_format(fmt));
   const long total = (long)N * C * OH * OW;
   if (total == 0) return {y, arg};
   const int grid = (int)std::min<long>((total + 255) / 256, 8192);
-#define MP(TT)                                                                                          \
-  maxpool_fwd_kernel<TT><<<grid, 256, 0, stream()>>>((const TT*)x.data_ptr(), (TT*)y.data_ptr(),        \
-                                                     arg.data_ptr<int>(), N * C, H, W, OH, OW, ks, st)
-  if (x.scalar_type() == at::kBFloat16) MP(bf16); else MP(float);
+#define MP(TT, L)                                                                                   \
+  maxpool_fwd_kernel<TT, L><<<grid, 256, 0, stream()>>>((const TT*)x.data_ptr(), (TT*)y.data_ptr(), \
+                                                        arg.data_ptr<int>(), N, C, H, W, OH, OW, ks, st)
+  if (x.scalar_type() == at::kBFloat16) { if (cl) MP(bf16, true); else MP(bf16, false); }
+  else { if (cl) MP(float, true); else MP(float, false); }
 #undef MP
   SPA_LAUNCH_CHECK();
   return {y, arg};
 }
 at::Tensor maxpool2d_bwd(const at::Tensor& dy_, const at::Tensor& arg, int64_t H, int64_t W, int64_t ks,
                          int64_t st) {
-  auto dy = dy_.contiguous();
+  const bool cl = channels_last(arg);
+  const auto fmt = cl ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
+  TORCH_CHECK(arg.is_contiguous(fmt), "maxpool2d_bwd: argmax layout");
+  auto dy = dy_.contiguous(fmt);
   const int N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
   DeviceGuard g(dy.device());
-  auto dx = at::empty({N, C, H, W}, dy.options());
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(fmt));
   const long total = (long)N * C * H * W;
   if (total == 0) return dx;
   const int grid = (int)std::min<long>((total + 255) / 256, 8192);
-#define MB(TT)                                                                                        \
-  maxpool_bwd_kernel<TT><<<grid, 256, 0, stream()>>>((const TT*)dy.data_ptr(), arg.data_ptr<int>(),   \
-                                                     (TT*)dx.data_ptr(), N * C, H, W, OH, OW, ks, st)
-  if (dy.scalar_type() == at::kBFloat16) MB(bf16); else MB(float);
+#define MB(TT, L)                                                                                   \
+  maxpool_bwd_kernel<TT, L><<<grid, 256, 0, stream()>>>((const TT*)dy.data_ptr(), arg.data_ptr<int>(), \
+                                                        (TT*)dx.data_ptr(), N, C, H, W, OH, OW, ks, st)
+  if (dy.scalar_type() == at::kBFloat16) { if (cl) MB(bf16, true); else MB(bf16, false); }
+  else { if (cl) MB(float, true); else MB(float, false); }
 #undef MB
   SPA_LAUNCH_CHECK();
   return dx;

@@ -13,6 +13,7 @@
 //   grouped_gemm   Y_e = X_e W_e^T  and its two backward products, one launch each;
 //   combine        y[n] = sum_j w[n,j] * y_perm[inv[n,j]]  (gather form: deterministic).
 #include "spa_common.h"
+#include "gemm_common.h"
 
 namespace spa {
 
@@ -204,37 +205,6 @@ __global__ __launch_bounds__(256) void scatter_grad_kernel(const T* __restrict__
 // Tile -> expert: per-block scan of the per-expert tile counts (E <= threads), so launch
 // count and grid are independent of the routing (no host sync); logical tile ids are
 // XCD-remapped so tiles sharing an A panel run on one XCD's L2.
-typedef short s16x4_t __attribute__((ext_vector_type(4)));
-
-template <int BK>
-__device__ __forceinline__ int kc_off(int r, int u) {
-  constexpr int P = 128 / BK;              // rows per 256-byte (64-bank) span
-  constexpr int NU = BK / 4;               // 8-byte units per row
-  return r * BK + 4 * (u ^ ((r / P) & (NU - 1)));
-}
-template <int L>
-__device__ __forceinline__ int ks_off(int r, int ch) {   // 16B chunk ch of k-row r, row length L
-  return r * L + 8 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
-}
-// MFMA operand with permuted k order: k = 16s + 4hh + {0..3}, 16s + 8 + 4hh + {0..3}
-template <int BK>
-__device__ __forceinline__ bf16x8 ld_kc(const bf16* t, int row, int s, int hh) {
-  const bf16x4 a = *reinterpret_cast<const bf16x4*>(t + kc_off<BK>(row, 4 * s + hh));
-  const bf16x4 b = *reinterpret_cast<const bf16x4*>(t + kc_off<BK>(row, 4 * s + 2 + hh));
-  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-template <int L>
-__device__ __forceinline__ bf16x8 ld_ks(const bf16* t, int col0, int s, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3, hh = lane >> 5;
-  const int c = col0 + 16 * (g & 1) + 4 * pp;
-  const int ra = 16 * s + 4 * hh + q, rb = ra + 8;
-  typedef __attribute__((address_space(3))) s16x4_t LT;
-  const s16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LT*)(t + ks_off<L>(ra, c >> 3) + (c & 7)));
-  const s16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LT*)(t + ks_off<L>(rb, c >> 3) + (c & 7)));
-  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
-  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
 template <int BM, int BN, int BK, int WGM, int WGN, bool A_KC, bool B_KC, bool GROUP_K>
 __global__ __launch_bounds__(64 * WGM * WGN, (BM * BN / (WGM * WGN) <= 8192 && WGM * WGN == 4) ? 2 : 1)
 void grouped_gemm_kernel(

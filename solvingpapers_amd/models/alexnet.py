@@ -1,8 +1,10 @@
 """AlexNet (Krizhevsky et al. 2012).
 
-Reference: alexnet/alexnet.py:5-44 (model class only). Convs run as HIP im2col +
-hipBLASLt GEMM (col2im gather backward), LRN and MaxPool are HIP kernels, dropout
-is the HIP counter-hash kernel. Input must be 193-224 px (Q15: Linear(256*5*5)).
+Reference: alexnet/alexnet.py:5-44 (model class only). bf16 convs run on the
+implicit-GEMM MFMA kernels (csrc/kernels/conv.hip: fwd / data grad / weight grad, no
+column buffer) and the feature stack stays channels-last end to end: LRN, MaxPool,
+ReLU and dropout have NHWC-native HIP kernels. fp32 (parity) convs use HIP im2col +
+fp32 GEMM. Input must be 193-224 px (Q15: Linear(256*5*5)).
 State-dict keys match: features.{0,4,8,10,12}.*, classifier.{1,4,6}.*.
 """
 from __future__ import annotations

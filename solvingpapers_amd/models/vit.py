@@ -7,7 +7,9 @@ State-dict keys match the reference (patch_embedding.patch_embed.*, cls_token,
 pos_embedding, transformer_blocks.{i}.{layer_norm1,layer_norm2,multihead_attention.
 {in_proj_weight,in_proj_bias,out_proj.*},mlp.{0,2}.*}, mlp_head.{layer_norm1,mlp_head}.*).
 
-Hot path: HIP patchify (im2col with k = stride) + GEMM, fused LayerNorm(+residual),
+Hot path: implicit-GEMM MFMA patch embedding (bf16: patches gathered straight from the
+NCHW image when patch and width are multiples of 8 -- ViT-B/16 -- else from an NHWC copy;
+the NHWC output is the token matrix), fused LayerNorm(+residual),
 non-causal flash attention (hd 64 for ViT-B/16; T = 197 ragged tile), GELU kernel.
 Presets: ``vit_mnist_ref`` and ``vit_b16`` (224^2, patch 16, D768, L12, H12, MLP 3072).
 """

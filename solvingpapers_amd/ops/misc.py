@@ -28,16 +28,23 @@ def _device_seed(device):
     return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
 
 
+def _fmt(x):
+    """Storage order the HIP elementwise kernels walk: channels-last conv activations keep it."""
+    if x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last):
+        return torch.channels_last
+    return torch.contiguous_format
+
+
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p, seed_t):
-        ctx.p, ctx.seed_t = p, seed_t
-        return _ext.ops().dropout_apply(x, p, 0, seed_t)
+        ctx.p, ctx.seed_t, ctx.fmt = p, seed_t, _fmt(x)
+        return _ext.ops().dropout_apply(x.contiguous(memory_format=ctx.fmt), p, 0, seed_t)
 
     @staticmethod
     def backward(ctx, g):
-        # same mask (regenerated from the seed), same 1/(1-p) scale
-        return _ext.ops().dropout_apply(g.contiguous(), ctx.p, 0, ctx.seed_t), None, None
+        # same mask (regenerated from the seed over the same storage order), same 1/(1-p) scale
+        return _ext.ops().dropout_apply(g.contiguous(memory_format=ctx.fmt), ctx.p, 0, ctx.seed_t), None, None
 
 
 def dropout(x, p=0.1, training=True):
@@ -185,7 +192,7 @@ def max_pool2d(x, kernel_size=3, stride=2):
     return F.max_pool2d(x, kernel_size, stride)
 
 
-# ------------------------------------------------------------------------------- conv as im2col + GEMM
+# ------------------------------------------------------------------------------- conv2d / patch embed
 class _Im2ColFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kh, kw, sh, sw, ph, pw):
@@ -198,28 +205,44 @@ class _Im2ColFn(torch.autograd.Function):
         return _ext.ops().col2im(g, N, C, H, W, kh, kw, sh, sw, ph, pw), None, None, None, None, None, None
 
 
+def _conv2d_fp32(x, weight, bias, sh, sw, ph, pw):
+    """fp32 convs (reference-parity runs) stay exact: HIP im2col + fp32 GEMM. bf16 -- every training
+    and benchmark config -- runs the implicit-GEMM MFMA kernels (ops/conv.py)."""
+    N, C, H, W = x.shape
+    OC, _, KH, KW = weight.shape
+    OH, OW = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    cols = _Im2ColFn.apply(x.contiguous(), KH, KW, sh, sw, ph, pw)   # [N*OH*OW, C*KH*KW]
+    y = linear(cols, weight.reshape(OC, -1), bias)                  # [N*OH*OW, OC]
+    return y.view(N, OH, OW, OC).permute(0, 3, 1, 2)                 # channels-last view
+
+
 def conv2d(x, weight, bias=None, stride=1, padding=0):
-    """NCHW conv as im2col (HIP) + GEMM, output NCHW. K20 (AlexNet convs, ViT patch embed)."""
+    """2-D convolution, K20 (alexnet/alexnet.py:11-25). bf16 on the GPU: implicit-GEMM MFMA
+    kernels, output channels-last (logically NCHW). CPU: torch."""
     sh, sw = (stride, stride) if isinstance(stride, int) else stride
     ph, pw = (padding, padding) if isinstance(padding, int) else padding
     if not _hip(x):
         return F.conv2d(x, weight, bias, (sh, sw), (ph, pw))
-    N, C, H, W = x.shape
-    OC, _, KH, KW = weight.shape
-    OH, OW = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
-    cols = _Im2ColFn.apply(x, KH, KW, sh, sw, ph, pw)              # [N*OH*OW, C*KH*KW]
-    y = linear(cols, weight.reshape(OC, -1), bias)                  # [N*OH*OW, OC]
-    return y.view(N, OH, OW, OC).permute(0, 3, 1, 2).contiguous()
+    if x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16:
+        from .conv import conv2d_igemm
+        return conv2d_igemm(x, weight, bias, (sh, sw), (ph, pw))
+    return _conv2d_fp32(x, weight, bias, sh, sw, ph, pw)
 
 
 def patch_embed(x, weight, bias, patch):
     """Non-overlapping patchify (kernel == stride) + projection -> [N, P, D] tokens
-    (vision transformer/ViT.ipynb:182-192: Conv2d(k=s=patch) -> flatten(2).transpose(1,2))."""
+    (vision transformer/ViT.ipynb:182-192: Conv2d(k=s=patch) -> flatten(2).transpose(1,2)).
+    bf16: the implicit-GEMM kernel gathers patches straight from the NCHW image (no column
+    buffer); its NHWC output IS the [N, P, D] token matrix."""
     if not _hip(x):
         return F.conv2d(x, weight, bias, patch).flatten(2).transpose(1, 2)
     N, C, H, W = x.shape
     OC = weight.shape[0]
-    cols = _Im2ColFn.apply(x, patch, patch, patch, patch, 0, 0)     # a pure permutation
+    if x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16:
+        from .conv import conv2d_igemm
+        y = conv2d_igemm(x, weight, bias, (patch, patch), (0, 0))     # [N, OC, OH, OW] channels-last
+        return y.permute(0, 2, 3, 1).reshape(N, -1, OC)
+    cols = _Im2ColFn.apply(x.contiguous(), patch, patch, patch, patch, 0, 0)
     y = linear(cols, weight.reshape(OC, -1), bias)
     return y.view(N, (H // patch) * (W // patch), OC)
 

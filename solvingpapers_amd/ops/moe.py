@@ -216,10 +216,19 @@ class _GroupedLinearFn(torch.autograd.Function):
         return dx, gw, None
 
 
+# decode: at most this many expert-sorted rows go to the weight-streaming grouped GEMV
+GEMV_MAX_ROWS = 64
+
+
 def grouped_linear(xp, W, plan: MoEPlan, fp8: bool = False):
     """Per-expert ``xp[rows_e] @ W[e]^T`` for expert-ordered rows; W [E, out, in].
     ``fp8``: forward and dX products in OCP e4m3 on the block-scaled MFMA (per-row scales,
-    csrc/kernels/moe_fp8.hip); dW stays bf16."""
+    csrc/kernels/moe_fp8.hip); dW stays bf16. Inference with few rows (decode) streams each
+    active expert's weights once (``grouped_gemv``, csrc/kernels/gemv.hip) instead of paying a
+    256-row MFMA tile per expert for one or two tokens."""
+    if (xp.is_cuda and not torch.is_grad_enabled() and xp.shape[0] <= GEMV_MAX_ROWS
+            and xp.dtype == torch.bfloat16 and W.dtype == torch.bfloat16):
+        return ops().grouped_gemv(xp.contiguous(), W.contiguous(), plan.offsets)
     if fp8:
         return _GroupedLinearFP8Fn.apply(xp, W, plan)
     return _GroupedLinearFn.apply(xp, W, plan)

@@ -20,8 +20,11 @@ def _ext_loaded():
     assert _ext.load()
 
 
-def test_dropout_mask_consistency():
-    x = torch.randn(1000, 257, device=DEV, requires_grad=True)
+@pytest.mark.parametrize("shape,off", [((1000, 257), 0), ((1001, 259), 0), ((999, 64), 3)])
+def test_dropout_mask_consistency(shape, off):
+    """8-wide vector body, scalar tail (numel % 8 != 0) and an unaligned view (scalar path)."""
+    base = torch.randn(shape[0] * shape[1] + off, device=DEV)
+    x = base[off:].view(shape).detach().requires_grad_(True)
     y = misc.dropout(x, 0.3)
     keep = (y != 0)
     frac = keep.float().mean().item()
@@ -31,11 +34,13 @@ def test_dropout_mask_consistency():
     assert torch.equal(x.grad != 0, keep)  # same mask regenerated in backward
 
 
+@pytest.mark.parametrize("C", [10, 100, 1000, 2048, 3000])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_kd_loss(dtype):
-    s = torch.randn(128, 10, device=DEV, dtype=dtype, requires_grad=True)
-    t = torch.randn(128, 10, device=DEV, dtype=dtype)
-    y = torch.randint(0, 10, (128,), device=DEV)
+def test_kd_loss(dtype, C):
+    """wave-per-row register-resident kernel (C <= 2048, every VPL bucket) and block fallback."""
+    s = torch.randn(130, C, device=DEV, dtype=dtype, requires_grad=True)
+    t = torch.randn(130, C, device=DEV, dtype=dtype)
+    y = torch.randint(0, C, (130,), device=DEV)
     tot, hard, soft = misc.distillation_loss(s, t, y, 7.0, 0.3)
     tot.backward()
     sf = s.detach().float().requires_grad_()

@@ -202,3 +202,19 @@ def test_moe_ffn_fp8_close_to_bf16():
         outs.append([y.float()] + [t.float() for t in g])
     for a, b in zip(outs[1], outs[0]):
         assert _rel(a, b) < 0.1
+
+
+@pytest.mark.parametrize("A,E,N,K", [(6, 64, 2816, 2048), (96, 64, 512, 2048), (40, 8, 200, 264), (3, 4, 1024, 512)])
+def test_grouped_gemv_matches_reference(A, E, N, K):
+    """Decode-size grouped GEMV (csrc/kernels/gemv.hip grouped_gemv): rows skewed onto few
+    experts (one expert with > 4 rows exercises the 4-row groups), empty experts."""
+    from solvingpapers_amd.ops import _ext
+    torch.manual_seed(0)
+    x = torch.randn(A, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(E, N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    ids = torch.cat([torch.zeros(A // 3, dtype=torch.long), torch.randint(0, E, (A - A // 3,))]).sort().values
+    counts = torch.bincount(ids, minlength=E)
+    off = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)]).int().cuda()
+    y = _ext.ops().grouped_gemv(x, w, off)
+    ref = torch.einsum("ak,ank->an", x.float(), w[ids.cuda()].float())
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2

@@ -46,6 +46,9 @@ def cases():
     dy = rn(N, D)
     out["rmsnorm_bwd_8192x4096"] = (lambda: torch.autograd.grad(yr, (xr, wr), dy, retain_graph=True),
                                     3 * N * D * 2)
+    _, hn, rstd, _ = _ext.ops().norm_fwd(x, None, w, None, 1e-5)
+    out["rmsnorm_bwd_kernel_8192x4096"] = (lambda: _ext.ops().norm_bwd(dy, x, w, rstd, None, None, None, None),
+                                           3 * N * D * 2)
     Nv, Dv = 256 * 197, 768                                 # ViT-B/16 batch 256
     xl, wl, bl = rn(Nv, Dv), torch.ones(Dv, device=DEV, dtype=BF), torch.zeros(Dv, device=DEV, dtype=BF)
     out["layernorm_fwd_50432x768"] = (lambda: O.layer_norm(xl, wl, bl), 2 * Nv * Dv * 2)
@@ -72,6 +75,10 @@ def cases():
     s, t = rn(16384, 1000, dtype=torch.float32), rn(16384, 1000, dtype=torch.float32)
     y = torch.randint(0, 1000, (16384,), device=DEV, generator=g)
     out["kd_loss_16384x1000"] = (lambda: misc.distillation_loss(s, t, y, 7.0, 0.3), 2 * 16384 * 1000 * 4)
+    sb, tb = rn(65536, 10), rn(65536, 10)                   # reference shape: CIFAR-10 logits, big batch
+    yb = torch.randint(0, 10, (65536,), device=DEV, generator=g)
+    out["kd_loss_grad_65536x10_bf16"] = (lambda: _ext.ops().kd_loss_fwd(sb, tb, yb, 7.0, 0.3, True), 3 * 65536 * 10 * 2)
+    out["kd_loss_grad_16384x1000"] = (lambda: _ext.ops().kd_loss_fwd(s, t, y, 7.0, 0.3, True), 3 * 16384 * 1000 * 4)
     xd = rn(N, D)
     out["dropout_8192x4096"] = (lambda: misc.dropout(xd, 0.1, True), 2 * N * D * 2)
     return out

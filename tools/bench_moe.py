@@ -62,7 +62,7 @@ wq = wq.view(E, 2 * F, D)
 ms = tm(lambda: ops.grouped_gemm_fp8(xq, sx, wq, sw.view(E, 2 * F), plan.offsets))
 print(f"fp8 fwd W13 grouped GEMM: {2 * A * 2 * F * D / ms / 1e9:.0f} TF (e4m3, block-scaled MFMA)")
 msq = tm(lambda: M.quant_rows_fp8(x))
-print(f"quant_rows_fp8 [{A}x{D}]: {msq*1e3:.3f} ms = {A * D * 3 / msq / 1e9:.0f} GB/s")
+print(f"quant_rows_fp8 [{A}x{D}]: {msq:.3f} ms = {A * D * 3 / msq / 1e6:.0f} GB/s")
 a = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
 b = torch.randn(2 * F, D, device=dev, dtype=torch.bfloat16)
 ms = tm(lambda: torch.mm(a, b.t()))
