@@ -511,7 +511,11 @@ std::vector<at::Tensor> conv_wgrad(const at::Tensor& dy, const at::Tensor& x, co
   auto db = want_bias ? at::empty({G.OC}, opts.dtype(w_dtype)) : at::Tensor();
   const long rows = G.rows();
   const int tiles = cdiv(G.OC, CBM) * cdiv(K, CBN);
-  int S = splits > 0 ? (int)splits : std::max(1, std::min<int>(cdiv(2048, tiles), cdiv(rows, 512)));
+  // ~2048 blocks, >= 512 rows per split, and the fp32 partial slab kept to <= 64 MiB
+  const long slab = (long)G.OC * K * 4;
+  int S = splits > 0 ? (int)splits
+                     : std::max(1, std::min<int>(std::min<int>(cdiv(2048, tiles), cdiv(rows, 512)),
+                                                 (int)std::max<long>(1, (64L << 20) / slab)));
   const int kchunk = cdiv(cdiv(rows, S), CBK) * CBK;
   S = std::max(1, cdiv(rows, kchunk));
   auto part = at::empty({S, G.OC, K}, opts.dtype(at::kFloat));

@@ -1,0 +1,468 @@
+// Grouped MoE GEMM, second generation: 256 x 256 x 64 tiles, 8 waves, operands DMA'd straight
+// from HBM into LDS (buffer_load ... lds, 16 B per lane), four phases per K-tile with counted
+// vmcnt waits so four half-tiles stay in flight across the raw barriers.
+//
+// Modes (same contract as grouped_gemm in moe.hip):
+//   0 fwd   Y[M, N]  = X[M, K] W_e[N, K]^T        rows grouped by offsets
+//   1 dX    dX[M, N] = dY[M, K] W_e[K, N]          rows grouped (W_e stored [K=Nw][N=Kw])
+//   2 dW    dW_e[N, K] = dY_e[T, N]^T X_e[T, K]   reduction rows grouped (token segments)
+//
+// Block 512 threads = 8 waves as 2 (M) x 4 (N). The 256 x 256 C tile is split into two
+// 128-row A halves and two 128-col B halves; wave (wm, wn) owns rows {h*128 + wm*64 + [0,64)} and
+// cols {h*128 + wn*32 + [0,32)} of both halves, so each of its four quadrants (mh, nh) reads one
+// A half and one B half. Per K-tile the wave computes its quadrants in the order
+// (0,0) (0,1) (1,1) (1,0) -- 16 v_mfma_f32_16x16x32_bf16 each -- while the block stages one half
+// (2 DMA per thread) per phase, up to two K-tiles ahead (schedule at the main loop):
+//
+//   phase: ds_read this quadrant's new fragments | DMA one half | [vmcnt] | s_barrier |
+//          lgkmcnt(0) | 16 MFMA | s_barrier
+//
+// Waves 4-7 run one barrier behind waves 0-3 (an extra s_barrier before the loop), so on every
+// SIMD -- which holds wave w and wave w+4 -- one wave reads LDS / issues DMA while the other runs
+// its MFMA cluster. A wait in phase p still precedes every reader of phase p+1 by a barrier in
+// both groups, and every restage is >= 2 phases after the last read (one barrier of slack for
+// the stagger).
+//
+// The counted waits (vmcnt 8 after phases 1, 2 and 4) retire exactly the half the next phase
+// reads (B1, A1, then A0 + B0 of the next tile); every half is restaged >= 2 phases after
+// its last read. All LDS is one array and every barrier is a bare s_barrier, so no implicit
+// vmcnt(0) drains the DMA queue inside the loop.
+//
+// LDS images (lane-linear DMA destinations; the swizzle lives in the per-lane SOURCE address
+// and the matching read address, an involution):
+//   K-contiguous half [128 rows][64 k]: 16-B chunk c of row r at r*128 + 16*(c ^ ((r >> 1) & 7))
+//     -- ds_read_b128 row reads of 16 consecutive rows hit 16 distinct bank slots;
+//   K-strided half [64 k][128 cols]: chunk c of k-row r at r*256 + 16*(c ^ f(r)),
+//     f(r) = ((r & 3) << 2) | ((r >> 2) & 3) -- read with ds_read_b64_tr_b16 (conflict-free).
+// Out-of-range rows / columns / tokens read as zero through the buffer descriptor range check
+// (dW descriptors start at the expert's first token and end at its last).
+#include "spa_common.h"
+#include "gemm_common.h"
+
+namespace spa {
+
+namespace g8 {
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int HALF = 128 * 64 * 2;            // bytes per half-tile image (16 KiB)
+constexpr int STAGE = 4 * HALF;               // A0 A1 B0 B1 of one K-tile (64 KiB)
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
+  const long nb = bytes < 0 ? 0 : (bytes > 0xFFFFFFFFL ? 0xFFFFFFFFL : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)(unsigned)nb, 0x00020000);
+}
+
+// Per-thread byte offset of the j-th (0, 1) 16-B DMA piece of a half image, relative to the
+// half's origin in global memory. Fixed for the whole kernel: the tile-dependent part of every
+// address lives in the (scalar) buffer descriptor base, so the K loop does no VALU address math.
+//   K-contiguous half [128 rows][64 k]: slot q -> row q >> 3, chunk (q & 7) ^ ((row >> 1) & 7)
+//   K-strided half    [64 k][128 cols]: slot q -> k-row q >> 4, chunk (q & 15) ^ f(row)
+__device__ __forceinline__ unsigned dma_off(bool kc, int tid, int j, long ld) {
+  const int q = j * NT + tid;
+  if (kc) {
+    const int r = q >> 3, c = (q & 7) ^ ((r >> 1) & 7);
+    return (unsigned)((r * ld + 8 * c) * 2);
+  }
+  const int r = q >> 4, c = (q & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+  return (unsigned)((r * ld + 8 * c) * 2);
+}
+// DMA one half image: origin = element offset of its first (row, k) in `base`, limit = elements
+// readable before the range check zero-fills. lds_wave = this wave's 1 KiB slice of the half.
+__device__ __forceinline__ void stage_half(const bf16* base, long origin, long limit, char* lds_wave,
+                                           const unsigned (&vo)[2]) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc(base + origin, (limit - origin) * 2);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_wave + j * (NT * 16)), 16, vo[j], 0, 0, 0);
+}
+
+// 16x16x32 operand (16 rows of the half starting at row0, k-slice s of the 64-k tile) from a
+// K-contiguous image: lane l -> row row0 + (l & 15), k 32 s + 8 (l >> 4) .. +7
+__device__ __forceinline__ bf16x8 rd_kc(const char* half, int row0, int s, int lane) {
+  const int r = row0 + (lane & 15), c = 4 * s + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(half + r * 128 + 16 * (c ^ ((r >> 1) & 7)));
+}
+// same operand from a K-strided image (rows of the operand = image columns col0 .. col0+15)
+__device__ __forceinline__ bf16x8 rd_ks(const char* half, int col0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ch = (col0 >> 3) + (p >> 1);
+  const int ra = 32 * s + 8 * g + q, rb = ra + 4;
+  const int fa = ((ra & 3) << 2) | ((ra >> 2) & 3), fb = ((rb & 3) << 2) | ((rb >> 2) & 3);
+  const s16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(half + ra * 256 + 16 * (ch ^ fa) + 8 * (p & 1)));
+  const s16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(half + rb * 256 + 16 * (ch ^ fb) + 8 * (p & 1)));
+  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
+  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+}  // namespace g8
+
+#define G8_WAIT_VM(N) \
+  do {                \
+    if (ABL != 3) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+  } while (0)
+#define G8_WAIT_LGKM0()                                \
+  do {                                                 \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    __builtin_amdgcn_sched_barrier(0);                 \
+  } while (0)
+
+// ABL: ablation switch for profiling only (tools/bench_moe.py --ablate): 0 normal, 1 no DMA
+// (compute on whatever LDS holds), 2 no LDS fragment reads, 3 no vmcnt waits; env value 4
+// selects the ILV schedule (DMA pieces issued between the MFMAs of each cluster). Measured at
+// 8192^3 (tools/bench_moe.py, profiles/r2_gemm8_ablation.txt): ILV 764 TF vs 1113 TF for the
+// shipped schedule -- a DMA piece's issue stalls the issuing wave's own MFMA stream. 1-3 give wrong
+// results by construction and are never selected by the op unless SPA_GG8_ABLATE is set.
+template <int MODE, int ABL = 0, bool ILV = false>
+__global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                               bf16* __restrict__ C, const int* __restrict__ offsets,
+                                                               int E, int M, int N, int K, long lda, long ldb, long ldc,
+                                                               long strideB, long strideC, int accumulate, long a_rows,
+                                                               long b_rows) {
+  using namespace g8;
+  constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
+  // ONE LDS array (a second __shared__ object can make hipcc drain the DMA queue before ds_reads);
+  // the tile -> expert scan scratch sits past the two stages, where no DMA lands
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 64];
+  int* scratch = reinterpret_cast<int*>(smem + 2 * STAGE);   // [0] expert, [1] tile, [8..15] wave sums
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nnt = (N + BN - 1) / BN;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = lid % nnt;
+  int mt = lid / nnt;
+  int e = 0;
+  long m0 = 0, mend = M, k0 = 0, kend = K;
+  const bf16* Bp = B;
+  bf16* Cp = C;
+  if (MODE != 2) {
+    int* wsum = scratch + 8;
+    const int cnt = tid < E ? offsets[tid + 1] - offsets[tid] : 0;
+    const int tiles = (cnt + BM - 1) / BM;
+    int inc = tiles;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    if (tid == 0) scratch[0] = -1;
+    __syncthreads();
+    int pre = inc - tiles;
+    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) { scratch[0] = tid; scratch[1] = mt - pre; }
+    __syncthreads();
+    e = __builtin_amdgcn_readfirstlane(scratch[0]);
+    if (e < 0) return;
+    mt = __builtin_amdgcn_readfirstlane(scratch[1]);
+    m0 = __builtin_amdgcn_readfirstlane(offsets[e]) + (long)mt * BM;
+    mend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
+    Bp = B + e * strideB;
+  } else {
+    const int nmt = (M + BM - 1) / BM;
+    e = mt / nmt;
+    mt = mt % nmt;
+    if (e >= E) return;
+    m0 = (long)mt * BM;
+    k0 = __builtin_amdgcn_readfirstlane(offsets[e]);
+    kend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
+    Cp = C + e * strideC;
+  }
+  const int n0 = nt * BN;
+  const int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  unsigned voA[2], voB[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    voA[j] = dma_off(A_KC, tid, j, lda);
+    voB[j] = dma_off(B_KC, tid, j, ldb);
+  }
+  // readable extents (elements): whole operands, or up to the expert's last token (dW)
+  const long limA = MODE == 2 ? kend * lda : a_rows * lda;
+  const long limB = MODE == 2 ? kend * ldb : b_rows * ldb;
+
+  // half images of stage s: A0 A1 B0 B1
+  auto half = [&](int s, int which) -> char* { return smem + s * STAGE + which * HALF; };
+  auto stage = [&](int t, int which) {       // which: 0 A0, 1 A1, 2 B0, 3 B1
+    if (ABL == 1) return;
+    char* dst = half(t & 1, which) + wave_u * 1024;
+    const long kk = k0 + (long)t * BK;       // absolute reduction index of the tile
+    if (which < 2) {
+      const long r = m0 + 128 * which;
+      stage_half(A, A_KC ? r * lda + kk : kk * lda + r, limA, dst, voA);
+    } else {
+      const long c = n0 + 128 * (which - 2);
+      stage_half(Bp, B_KC ? c * ldb + kk : kk * ldb + c, limB, dst, voB);
+    }
+  };
+  auto stage_piece = [&](int t, int which, int j) {   // one of the two DMA pieces of a half
+    if (ABL == 1) return;
+    char* dst = half(t & 1, which) + wave_u * 1024 + j * (NT * 16);
+    const long kk = k0 + (long)t * BK;
+    const bf16* base;
+    long origin, limit;
+    unsigned vo;
+    if (which < 2) {
+      const long r = m0 + 128 * which;
+      base = A; origin = A_KC ? r * lda + kk : kk * lda + r; limit = limA; vo = voA[j];
+    } else {
+      const long c = n0 + 128 * (which - 2);
+      base = Bp; origin = B_KC ? c * ldb + kk : kk * ldb + c; limit = limB; vo = voB[j];
+    }
+    const __amdgpu_buffer_rsrc_t rs = rsrc(base + origin, (limit - origin) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, vo, 0, 0, 0);
+  };
+
+  f32x4 acc[8][4];   // [m frag: mh*4 + i][n frag: nh*2 + j], C^T tiles (rows n, cols m)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], b0f[2][2], b1f[2][2];     // one A half, BOTH B halves in registers
+  bool do_reads = true;                      // ablation 2: fragments read in the first K-tile only
+
+  auto read_a = [&](const char* h) {
+    if (!do_reads) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        af[i][s] = A_KC ? rd_kc(h, wm * 64 + 16 * i, s, lane) : rd_ks(h, wm * 64 + 16 * i, s, lane);
+  };
+  auto read_b = [&](const char* h, bf16x8 (&bf)[2][2]) {
+    if (!do_reads) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        bf[j][s] = B_KC ? rd_kc(h, wn * 32 + 16 * j, s, lane) : rd_ks(h, wn * 32 + 16 * j, s, lane);
+  };
+  // MFMA cluster with the phase's two DMA pieces issued between MFMAs 4|5 and 10|11, so their
+  // (long) address-processing issue overlaps this wave's own MFMAs (st_t < 0: nothing to stage)
+  auto mfma_qs = [&](int mh, int nh, const bf16x8 (&bf)[2][2], int st_t, int st_w) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[mh * 4 + i][nh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][s], af[i][s], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+          const int idx = s * 8 + i * 2 + j;
+          if ((idx == 4 || idx == 10) && st_t >= 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            stage_piece(st_t, st_w, idx == 4 ? 0 : 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mfma_q = [&](int mh, int nh, const bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh * 4 + i][nh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][s], af[i][s], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // Schedule (K-tile t lives in stage t & 1). Reads: P1 A0 + B0, P2 B1, P3 A1, P4 none (B0
+  // still in registers). A half is free 2 phases after its last read, so tile t+2 refills the
+  // stage of tile t while t is still being computed:
+  //   P1 stages B1(t+1)   P2 A1(t+1)   P3 A0(t+2)   P4 B0(t+2)
+  // => 4 halves (8 DMA per thread) stay in flight across every wait; each half has 5-6 phases
+  // between issue and first read. Waits (end of P1, P2, P4) retire exactly the next reader's half.
+  const bool late = __builtin_amdgcn_readfirstlane(wave) >= 4;   // scalar branch, not an EXEC mask
+  if (ILV) {
+    // (measured slower; kept for the A/B) DMA issue inside the MFMA clusters (after the phase's first barrier): with the stagger a
+    // half waited for at the end of phase q may be read from phase q+2 on, so the waits run one
+    // phase earlier than the reads need: end of P1 -> A1(t) (read P3), end of P3 -> A0, B0(t+1)
+    // (read P1 next), end of P4 -> B1(t+1) (read P2 next); 3 halves stay in flight.
+    if (ktiles > 0) {
+      stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+      if (ktiles > 1) { stage(1, 0); stage(1, 2); G8_WAIT_VM(6); } else { G8_WAIT_VM(2); }  // A0 B0 B1 (0)
+      __builtin_amdgcn_s_barrier();
+      if (late) __builtin_amdgcn_s_barrier();
+    }
+    for (int t = 0; t < ktiles; ++t) {
+      const int s = t & 1;
+      const bool n1 = t + 1 < ktiles, n2 = t + 2 < ktiles;
+      do_reads = ABL != 2 || t == 0;
+      // ---- phase 1: quadrant (0,0); stages B1(t+1)
+      read_a(half(s, 0));
+      read_b(half(s, 2), b0f);
+      __builtin_amdgcn_s_barrier();
+      G8_WAIT_LGKM0();
+      mfma_qs(0, 0, b0f, n1 ? t + 1 : -1, 3);
+      if (n1) { G8_WAIT_VM(6); } else { G8_WAIT_VM(0); }                    // retire A1(t)
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 2: quadrant (0,1); stages A1(t+1)
+      read_b(half(s, 3), b1f);
+      __builtin_amdgcn_s_barrier();
+      G8_WAIT_LGKM0();
+      mfma_qs(0, 1, b1f, n1 ? t + 1 : -1, 1);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 3: quadrant (1,1); stages A0(t+2)
+      read_a(half(s, 1));
+      __builtin_amdgcn_s_barrier();
+      G8_WAIT_LGKM0();
+      mfma_qs(1, 1, b1f, n2 ? t + 2 : -1, 0);
+      if (n1) { if (n2) { G8_WAIT_VM(6); } else { G8_WAIT_VM(4); } }        // retire A0, B0(t+1)
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 4: quadrant (1,0), no LDS reads; stages B0(t+2)
+      __builtin_amdgcn_s_barrier();
+      mfma_qs(1, 0, b0f, n2 ? t + 2 : -1, 2);
+      if (n1) { if (n2) { G8_WAIT_VM(6); } else { G8_WAIT_VM(2); } }        // retire B1(t+1)
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+  if (ktiles > 0) {
+    stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+    if (ktiles > 1) { stage(1, 0); stage(1, 2); G8_WAIT_VM(8); } else { G8_WAIT_VM(4); }   // A0, B0 (0)
+    __builtin_amdgcn_s_barrier();
+    if (late) __builtin_amdgcn_s_barrier();
+  }
+  for (int t = 0; t < ktiles; ++t) {
+    const int s = t & 1;
+    const bool n1 = t + 1 < ktiles, n2 = t + 2 < ktiles;
+    do_reads = ABL != 2 || t == 0;
+    // ---- phase 1: quadrant (0,0)
+    read_a(half(s, 0));
+    read_b(half(s, 2), b0f);
+    if (n1) { stage(t + 1, 3); G8_WAIT_VM(8); } else { G8_WAIT_VM(2); }      // retire B1(t)
+    __builtin_amdgcn_s_barrier();
+    G8_WAIT_LGKM0();
+    mfma_q(0, 0, b0f);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 2: quadrant (0,1)
+    read_b(half(s, 3), b1f);
+    if (n1) { stage(t + 1, 1); G8_WAIT_VM(8); } else { G8_WAIT_VM(0); }      // retire A1(t)
+    __builtin_amdgcn_s_barrier();
+    G8_WAIT_LGKM0();
+    mfma_q(0, 1, b1f);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 3: quadrant (1,1)
+    read_a(half(s, 1));
+    if (n2) stage(t + 2, 0);
+    __builtin_amdgcn_s_barrier();
+    G8_WAIT_LGKM0();
+    mfma_q(1, 1, b1f);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 4: quadrant (1,0) -- no LDS reads
+    if (n2) { stage(t + 2, 2); G8_WAIT_VM(8); }                              // retire A0, B0(t+1)
+    else if (n1) { G8_WAIT_VM(0); }
+    __builtin_amdgcn_s_barrier();
+    mfma_q(1, 0, b0f);
+    __builtin_amdgcn_s_barrier();
+  }
+  }
+  if (ktiles > 0 && !late) __builtin_amdgcn_s_barrier();   // equal barrier counts on exit
+  // ---- epilogue: C^T fragment (n = 4 (l >> 4) + q, m = l & 15) -> 8-byte row stores
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long gm = m0 + mh * 128 + wm * 64 + 16 * i + (lane & 15);
+      if (MODE == 2 ? gm >= M : gm >= mend) continue;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
+          if (gn >= N) continue;
+          bf16* cp = Cp + gm * ldc + gn;
+          const f32x4 v = acc[mh * 4 + i][nh * 2 + j];
+          float o[4] = {v[0], v[1], v[2], v[3]};
+          if (accumulate) {
+            const bf16x4 old = *reinterpret_cast<const bf16x4*>(cp);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] += (float)old[q];
+          }
+          bf16x4 w4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w4[q] = (bf16)o[q];
+          *reinterpret_cast<bf16x4*>(cp) = w4;
+        }
+    }
+}
+
+static int ablation() {
+  const char* e = getenv("SPA_GG8_ABLATE");
+  return e ? atoi(e) : 0;
+}
+
+// same contract as grouped_gemm (moe.hip); requires the reduction dim % 64 == 0 in modes 0/1
+// and N, K % 8 == 0
+at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t mode,
+                         const c10::optional<at::Tensor>& out_, bool accumulate) {
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "grouped_gemm8: bf16");
+  TORCH_CHECK(a.is_contiguous() && w.is_contiguous() && offsets.scalar_type() == at::kInt);
+  const int E = offsets.numel() - 1;
+  TORCH_CHECK(E >= 1 && E <= 512, "grouped_gemm8: 1..512 experts");
+  TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)w.data_ptr() % 16 == 0, "grouped_gemm8: 16-B aligned");
+  DeviceGuard g(a.device());
+  auto st = stream();
+  if (mode == 0 || mode == 1) {
+    TORCH_CHECK(w.dim() == 3 && w.size(0) == E);
+    const int M = a.size(0), Nw = w.size(1), Kw = w.size(2);
+    const int N = mode == 0 ? Nw : Kw, K = mode == 0 ? Kw : Nw;
+    TORCH_CHECK(a.size(1) == K, "grouped_gemm8: A/W shape mismatch");
+    TORCH_CHECK(K % 64 == 0 && N % 8 == 0, "grouped_gemm8: reduction % 64, output cols % 8");
+    TORCH_CHECK((long)(M + 256) * K * 2 < (1L << 32) && (long)(Nw + 256) * Kw * 2 < (1L << 32),
+                "grouped_gemm8: operands < 4 GiB");
+    auto out = out_ ? *out_ : at::empty({M, N}, a.options());
+    if (M == 0) return out;
+    TORCH_CHECK(out.is_contiguous() && out.size(0) == M && out.size(1) == N);
+    const int grid = (cdiv(M, 256) + E) * cdiv(N, 256);
+#define G8_L(MD, AB)                                                                                          \
+  if (abl == 4) grouped_gemm8_kernel<MD, 0, true><<<grid, 512, 0, st>>>(                                     \
+      (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,  \
+      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw);                                           \
+  else grouped_gemm8_kernel<MD, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),     \
+                                                     (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
+                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw)
+    const int abl = ablation();
+    if (mode == 0) {
+      if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else { G8_L(0, 0); }
+    } else {
+      if (abl == 1) { G8_L(1, 1); } else if (abl == 2) { G8_L(1, 2); } else if (abl == 3) { G8_L(1, 3); } else { G8_L(1, 0); }
+    }
+#undef G8_L
+    SPA_LAUNCH_CHECK();
+    return out;
+  }
+  TORCH_CHECK(mode == 2, "grouped_gemm8: mode 0/1/2");
+  const int N = a.size(1), K = w.size(1), T = a.size(0);
+  TORCH_CHECK(w.size(0) == T && N % 8 == 0 && K % 8 == 0);
+  TORCH_CHECK((long)(T + 64) * (N + 256) * 2 < (1L << 32) && (long)(T + 64) * (K + 256) * 2 < (1L << 32),
+              "grouped_gemm8: operands < 4 GiB");
+  auto out = out_ ? *out_ : at::empty({E, N, K}, a.options());
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * N * K);
+  const int grid = E * cdiv(N, 256) * cdiv(K, 256);
+#define G8_L2(AB)                                                                                             \
+  if (abl == 4) grouped_gemm8_kernel<2, 0, true><<<grid, 512, 0, st>>>(                                      \
+      (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N,  \
+      K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, T, T);                                              \
+  else grouped_gemm8_kernel<2, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),      \
+                                                    (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, \
+                                                    K, 0, (long)N * K, accumulate ? 1 : 0, T, T)
+  const int abl = ablation();
+  if (abl == 1) { G8_L2(1); } else if (abl == 2) { G8_L2(2); } else if (abl == 3) { G8_L2(3); } else { G8_L2(0); }
+#undef G8_L2
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("grouped_gemm8(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("grouped_gemm8", &spa::grouped_gemm8); }

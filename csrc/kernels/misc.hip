@@ -146,6 +146,55 @@ __global__ __launch_bounds__(256) void kd_wave_kernel(const T* __restrict__ s, c
   }
 }
 
+// tiny rows (C <= 16, the reference's 10-class heads): one LANE per row, the row in registers,
+// no cross-lane reductions at all -- a wave per row would idle 54 of 64 lanes and spend its time
+// in shuffles.
+template <typename T, int CM>
+__global__ __launch_bounds__(256) void kd_lane_kernel(const T* __restrict__ s, const T* __restrict__ t,
+                                                      const int64_t* __restrict__ y, float* __restrict__ hard,
+                                                      float* __restrict__ soft, T* __restrict__ gs, int B, int C,
+                                                      float invT, float alpha, float invB) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= B) return;
+  const T* sr = s + (long)row * C;
+  const T* tr = t + (long)row * C;
+  float a[CM], b[CM];
+  float m1 = -INFINITY, m3 = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    a[c] = c < C ? (float)sr[c] : -INFINITY;
+    b[c] = c < C ? (float)tr[c] : -INFINITY;
+    m1 = fmaxf(m1, a[c]);
+    m3 = fmaxf(m3, b[c]);
+  }
+  const float m2 = m1 * invT;
+  m3 *= invT;
+  float z1 = 0.f, z2 = 0.f, z3 = 0.f;
+#pragma unroll
+  for (int c = 0; c < CM; ++c)
+    if (c < C) {
+      z1 += __expf(a[c] - m1);
+      z2 += __expf(a[c] * invT - m2);
+      z3 += __expf(b[c] * invT - m3);
+    }
+  const float l1 = m1 + __logf(z1), l2 = m2 + __logf(z2), l3 = m3 + __logf(z3);
+  const int64_t yy = y[row];
+  float kl = 0.f, sy = 0.f;
+#pragma unroll
+  for (int c = 0; c < CM; ++c)
+    if (c < C) {
+      const float lp = b[c] * invT - l3, lq = a[c] * invT - l2;
+      const float pc = __expf(lp);
+      kl += pc * (lp - lq);
+      if (c == yy) sy = a[c];
+      if (gs)
+        gs[(long)row * C + c] = (T)(alpha * invB * (__expf(a[c] - l1) - (c == yy ? 1.f : 0.f)) +
+                                    (1.f - alpha) * invB / invT * (__expf(lq) - pc));
+    }
+  hard[row] = l1 - sy;
+  soft[row] = kl;
+}
+
 // rows wider than 64 x 32 values: one block per row, three passes (the general fallback)
 template <typename T>
 __global__ __launch_bounds__(256) void kd_kernel(const T* __restrict__ s, const T* __restrict__ t,
@@ -212,7 +261,11 @@ std::vector<at::Tensor> kd_loss_fwd(const at::Tensor& s_, const at::Tensor& t_, 
       soft.data_ptr<float>(), want_grad ? (TT*)gs.data_ptr() : nullptr, B, C, (float)(1.0 / T), (float)alpha, \
       1.f / B)
 #define KDL(TT)                                                                                              \
-  if (C <= 64) KDW(TT, 1);                                                                                   \
+  if (C <= 16) (kd_lane_kernel<TT, 16>)<<<cdiv(B, 256), 256, 0, stream()>>>(                                   \
+      (const TT*)s.data_ptr(), (const TT*)t.data_ptr(), yc.data_ptr<int64_t>(), hard.data_ptr<float>(),       \
+      soft.data_ptr<float>(), want_grad ? (TT*)gs.data_ptr() : nullptr, B, C, (float)(1.0 / T), (float)alpha, \
+      1.f / B);                                                                                               \
+  else if (C <= 64) KDW(TT, 1);                                                                                   \
   else if (C <= 256) KDW(TT, 4);                                                                             \
   else if (C <= 1024) KDW(TT, 16);                                                                           \
   else if (C <= 2048) KDW(TT, 32);                                                                           \

@@ -271,7 +271,9 @@ at::Tensor mla_decode(const at::Tensor& q, const at::Tensor& qr, const at::Tenso
   const int ntiles = cdiv(Sbound, kMlaKT);
   const int nrb = cdiv(p.rows, kMlaRB);
   // splits: enough workgroups to cover the chip at small batch, >= 2 tiles per split
-  int nsplit = nsplit_req > 0 ? (int)nsplit_req : std::max(1, std::min(ntiles / 2, 256 / std::max(1, B * nrb)));
+  // splits: at small batch a block streams few tiles serially and the tile load latency is the
+  // cost, so spread the key range up to one tile per split until the grid covers the chip
+  int nsplit = nsplit_req > 0 ? (int)nsplit_req : std::max(1, std::min(ntiles, 256 / std::max(1, B * nrb)));
   nsplit = std::max(1, std::min(nsplit, ntiles));
   p.tiles_per_split = cdiv(ntiles, nsplit);
   nsplit = cdiv(ntiles, p.tiles_per_split);
@@ -290,11 +292,22 @@ at::Tensor mla_decode(const at::Tensor& q, const at::Tensor& qr, const at::Tenso
     mla_decode_kernel<CV, RV><<<grid, 256, 0, st>>>(p);                            \
     if (nsplit > 1) mla_merge_kernel<CV><<<B * p.rows, 256, 0, st>>>(p);           \
   } while (0)
-  if (C == 512 && R == 64) MLA_L(512, 64);
-  else if (C == 256 && R == 64) MLA_L(256, 64);
-  else if (C == 64 && R == 32) MLA_L(64, 32);
-  else if (C == 128 && R == 64) MLA_L(128, 64);
-  else TORCH_CHECK(false, "mla_decode: (kv_lora, rope) must be (512,64), (256,64), (128,64) or (64,32)");
+  // kv_lora in {64, 128, 256, 512} x rope in {32, 64}: every preset (tiny, V2-Lite, V3)
+  if (R == 64) {
+    if (C == 512) MLA_L(512, 64);
+    else if (C == 256) MLA_L(256, 64);
+    else if (C == 128) MLA_L(128, 64);
+    else if (C == 64) MLA_L(64, 64);
+    else TORCH_CHECK(false, "mla_decode: kv_lora must be 64, 128, 256 or 512");
+  } else if (R == 32) {
+    if (C == 512) MLA_L(512, 32);
+    else if (C == 256) MLA_L(256, 32);
+    else if (C == 128) MLA_L(128, 32);
+    else if (C == 64) MLA_L(64, 32);
+    else TORCH_CHECK(false, "mla_decode: kv_lora must be 64, 128, 256 or 512");
+  } else {
+    TORCH_CHECK(false, "mla_decode: rope dim must be 32 or 64");
+  }
 #undef MLA_L
   SPA_LAUNCH_CHECK();
   return out;

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import os
+
 import torch
 
 from ..utils.grad import commit
@@ -172,10 +174,29 @@ def _cpu_grouped(a, w, offsets, mode):
     return out
 
 
+GG8 = os.environ.get("SPA_GG8", "1") != "0"
+GG8_DW = os.environ.get("SPA_GG8", "1") == "2"
+
+
+def _gg8_ok(a, w, mode):
+    """the 8-phase LDS-DMA kernel (csrc/kernels/gemm8.hip) needs a reduction dim % 64 in modes 0/1
+    and output dims % 8. It wins fwd (+45 %) and dX (+12 %) at DeepSeek widths; the dW form
+    (short per-expert token loops) measures no faster than the register-staged 256x256 kernel
+    (profiles/r2_grouped_gemm_sweep.txt), so mode 2 stays on moe.hip unless SPA_GG8=2."""
+    if mode == 0:
+        return w.shape[2] % 64 == 0 and w.shape[1] % 8 == 0
+    if mode == 1:
+        return w.shape[1] % 64 == 0 and w.shape[2] % 8 == 0
+    return GG8_DW and a.shape[1] % 8 == 0 and w.shape[1] % 8 == 0
+
+
 def grouped_gemm(a, w, offsets, mode, out=None, accumulate=False):
     """mode 0: a_e @ w_e^T ; mode 1: a_e @ w_e ; mode 2: per-expert a_e^T @ w_e (w = X rows)."""
     if _gpu(a):
-        return ops().grouped_gemm(a.contiguous(), w.contiguous(), offsets, mode, out, accumulate)
+        a, w = a.contiguous(), w.contiguous()
+        if GG8 and _gg8_ok(a, w, mode):
+            return ops().grouped_gemm8(a, w, offsets, mode, out, accumulate)
+        return ops().grouped_gemm(a, w, offsets, mode, out, accumulate)
     r = _cpu_grouped(a, w, offsets, mode)
     if out is None:
         return r

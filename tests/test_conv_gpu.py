@@ -70,7 +70,7 @@ def test_channels_last_pool_lrn_act_dropout():
     a = torch.randn(2, 24, 13, 11, device=DEV, generator=g).bfloat16()
     outs = {}
     for fmt in (torch.contiguous_format, torch.channels_last):
-        x = a.contiguous(memory_format=fmt).requires_grad_()
+        x = a.clone(memory_format=fmt).detach().requires_grad_()
         y = misc.max_pool2d(misc.local_response_norm(x, 5), 3, 2)
         assert y.is_contiguous(memory_format=fmt)
         gy = torch.linspace(-1, 1, y.numel(), device=DEV).view(y.shape).bfloat16()
@@ -79,7 +79,7 @@ def test_channels_last_pool_lrn_act_dropout():
     (y0, g0), (y1, g1) = outs.values()
     assert torch.equal(y0, y1) and rel(g1, g0) < 1e-3
     from solvingpapers_amd.ops import activation
-    x = a.contiguous(memory_format=torch.channels_last).requires_grad_()
+    x = a.clone(memory_format=torch.channels_last).detach().requires_grad_()
     r = activation.relu(x)
     assert r.is_contiguous(memory_format=torch.channels_last) and torch.equal(r, torch.relu(a))
     d = misc.dropout(x, 0.5)

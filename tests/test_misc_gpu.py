@@ -34,10 +34,11 @@ def test_dropout_mask_consistency(shape, off):
     assert torch.equal(x.grad != 0, keep)  # same mask regenerated in backward
 
 
-@pytest.mark.parametrize("C", [10, 100, 1000, 2048, 3000])
+@pytest.mark.parametrize("C", [10, 16, 33, 100, 1000, 2048, 3000])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_kd_loss(dtype, C):
-    """wave-per-row register-resident kernel (C <= 2048, every VPL bucket) and block fallback."""
+    """lane-per-row (C <= 16), wave-per-row register-resident (C <= 2048, every VPL bucket) and
+    block fallback kernels."""
     s = torch.randn(130, C, device=DEV, dtype=dtype, requires_grad=True)
     t = torch.randn(130, C, device=DEV, dtype=dtype)
     y = torch.randint(0, C, (130,), device=DEV)

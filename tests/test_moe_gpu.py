@@ -218,3 +218,38 @@ def test_grouped_gemv_matches_reference(A, E, N, K):
     y = _ext.ops().grouped_gemv(x, w, off)
     ref = torch.einsum("ak,ank->an", x.float(), w[ids.cuda()].float())
     assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("counts,N,K", [
+    ([300, 0, 129, 1, 64, 700, 0, 33], 320, 192),       # ragged tiles, N % 256 != 0
+    ([0] * 7 + [513], 256, 512),
+    ([257, 255], 1408, 2048),                           # DeepSeek-V2-Lite expert widths
+    (None, 576, 256),                                   # 64 experts, skewed routing
+])
+def test_grouped_gemm8_elementwise(counts, N, K):
+    """csrc/kernels/gemm8.hip (LDS-DMA 8-phase kernel) per element against the fp32 oracle in all
+    three modes: a wrong fragment map or a mis-counted vmcnt shows up as a wrong 16x16 block,
+    which a relative-norm check over the whole tensor could hide."""
+    g = torch.Generator().manual_seed(5)
+    if counts is None:
+        counts = (torch.rand(64, generator=g) ** 3 * 1500).long().tolist()
+    E, M_ = len(counts), sum(counts)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    x = torch.randn(M_, K, generator=g).to(dev, torch.bfloat16)
+    W = (torch.randn(E, N, K, generator=g) / K ** 0.5).to(dev, torch.bfloat16)
+    dy = torch.randn(M_, N, generator=g).to(dev, torch.bfloat16)
+    ops = M.ops()
+
+    def check(got, ref, tol=2e-2):
+        err = (got.float().cpu() - ref).abs()
+        scale = ref.abs().amax(dim=-1, keepdim=True).clamp_min(1e-3)
+        assert (err / scale).max() < tol, float((err / scale).max())
+
+    check(ops.grouped_gemm8(x, W, off, 0, None, False), _oracle(x, W, off, 0))
+    check(ops.grouped_gemm8(dy, W, off, 1, None, False), _oracle(dy, W, off, 1))
+    ref = _oracle(dy, x, off, 2)
+    dw = ops.grouped_gemm8(dy, x, off, 2, None, False)
+    check(dw.reshape(E * N, K), ref.reshape(E * N, K))
+    dw2 = dw.clone()
+    ops.grouped_gemm8(dy, x, off, 2, dw2, True)
+    check(dw2.reshape(E * N, K), 2 * ref.reshape(E * N, K))
