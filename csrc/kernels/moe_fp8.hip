@@ -56,14 +56,140 @@ __global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16* __restr
   }
 }
 
+// --------------------------------------------------------------------------- block-scaled quantize
+// DeepSeek-V3 fp8 recipe (arXiv 2412.19437 sec. 3.3) on CDNA4's MX scale operands: activations in
+// 1 x 128 tiles, weights in 128 x 128 blocks, each with a power-of-two (E8M0) scale 2^e chosen as
+// the smallest with amax / 2^e <= 448. The GEMM hands the E8M0 bytes straight to
+// v_mfma_scale_f32_32x32x64_f8f6f4, so the accumulation over differently scaled k-blocks happens
+// inside the MFMA in fp32 -- no per-block promotion pass.
+__device__ __forceinline__ int e8m0_exp(float amax) {       // e with amax / 2^e <= 448, minimal
+  if (!(amax > 0.f)) return 0;
+  const unsigned b = __float_as_uint(amax * (1.f / 448.f));
+  int e = (int)((b >> 23) & 0xff) - 127;
+  if (b & 0x7fffff) ++e;                                     // round the power up
+  return max(-126, min(127, e));
+}
+__device__ __forceinline__ float e8m0_inv(int e) { return __uint_as_float((unsigned)(127 - e) << 23); }
+__device__ __forceinline__ int2 q8(const float (&v)[8], float inv) {
+  float w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = fminf(fmaxf(v[i] * inv, -448.f), 448.f);
+  int lo = 0, hi = 0;
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(w[0], w[1], lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(w[2], w[3], lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(w[4], w[5], hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(w[6], w[7], hi, true);
+  return make_int2(lo, hi);
+}
+
+// x [R, K] bf16 -> q [R, K] e4m3, s [R, K/128] E8M0; 16 lanes per 128-wide tile, one read of x
+__global__ __launch_bounds__(256) void quant_act_blk_kernel(const bf16* __restrict__ x, uint8_t* __restrict__ q,
+                                                            uint8_t* __restrict__ s, long units, int KB) {
+  const long u = ((long)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int l = threadIdx.x & 15;
+  if (u >= units) return;                                    // whole 16-lane groups exit together
+  const long off = u * 128 + l * 8;                          // [R][K] with K = 128 KB: tile u is contiguous
+  float v[8];
+  load8(x + off, v);
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 16));
+  const int e = e8m0_exp(amax);
+  *reinterpret_cast<int2*>(q + off) = q8(v, e8m0_inv(e));
+  if (l == 0) s[u] = (uint8_t)(e + 127);
+}
+
+// W [E, N, K] bf16 -> wq [E, N, K] e4m3, wtq [E, K, N] e4m3 (the same bytes transposed: a 128 x 128
+// block scale is transpose-invariant), s [E, N/128, K/128], st [E, K/128, N/128] E8M0.
+// One workgroup per block: one read of W, two writes of the fp8 bytes.
+__global__ __launch_bounds__(256) void quant_weight_blk_kernel(const bf16* __restrict__ w, uint8_t* __restrict__ wq,
+                                                               uint8_t* __restrict__ wtq, uint8_t* __restrict__ s,
+                                                               uint8_t* __restrict__ st, int N, int K) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[128 * 132];
+  __shared__ float red[4];
+  const int NB = N / 128, KB = K / 128;
+  const int kb = blockIdx.x % KB, nb = (blockIdx.x / KB) % NB, e = blockIdx.x / (KB * NB);
+  const int tid = threadIdx.x, c8 = (tid & 15) * 8, r0 = tid >> 4;
+  const bf16* wb = w + ((long)e * N + nb * 128) * K + kb * 128;
+  float v[8][8], amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    load8(wb + (long)(r0 + 16 * i) * K + c8, v[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[i][j]));
+  }
+  amax = block_max<256>(amax, red);
+  const int ex = e8m0_exp(amax);
+  const float inv = e8m0_inv(ex);
+  uint8_t* qb = wq + ((long)e * N + nb * 128) * K + kb * 128;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int2 p = q8(v[i], inv);
+    *reinterpret_cast<int2*>(qb + (long)(r0 + 16 * i) * K + c8) = p;
+    *reinterpret_cast<int2*>(tile + (r0 + 16 * i) * 132 + c8) = p;
+  }
+  if (tid == 0) {
+    s[((long)e * NB + nb) * KB + kb] = (uint8_t)(ex + 127);
+    st[((long)e * KB + kb) * NB + nb] = (uint8_t)(ex + 127);
+  }
+  __syncthreads();
+  // transposed write: 4 x 4 byte blocks, lanes along n for coalesced 4-byte stores
+  const int bn = tid & 31;
+  uint8_t* tb = wtq + ((long)e * K + kb * 128) * N + nb * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int bk = (tid >> 5) + 8 * i;
+    unsigned r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const unsigned*>(tile + (4 * bn + j) * 132 + 4 * bk);
+    // r[j] byte c = (n = 4bn + j, k = 4bk + c); output row c gathers byte c of r[0..3]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const unsigned o = ((r[0] >> (8 * c)) & 0xff) | (((r[1] >> (8 * c)) & 0xff) << 8) |
+                         (((r[2] >> (8 * c)) & 0xff) << 16) | (((r[3] >> (8 * c)) & 0xff) << 24);
+      *reinterpret_cast<unsigned*>(tb + (long)(4 * bk + c) * N + 4 * bn) = o;
+    }
+  }
+}
+
+// q [R, K] e4m3 + s [R, ldS] E8M0 (first K/128 used) -> bf16 [R, K]; 8 elements per lane
+__global__ __launch_bounds__(256) void dequant_act_blk_kernel(const uint8_t* __restrict__ q,
+                                                              const uint8_t* __restrict__ s, bf16* __restrict__ y,
+                                                              long n8, int K, int ldS) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const long off = i * 8;
+    const long row = off / K;
+    const int col = off % K;
+    const float sc = __uint_as_float((unsigned)s[row * ldS + col / 128] << 23);
+    const int2 p = *reinterpret_cast<const int2*>(q + off);
+    float f[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int w = h ? p.y : p.x;
+      const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(w, false), b = __builtin_amdgcn_cvt_pk_f32_fp8(w, true);
+      f[4 * h + 0] = a[0] * sc; f[4 * h + 1] = a[1] * sc; f[4 * h + 2] = b[0] * sc; f[4 * h + 3] = b[1] * sc;
+    }
+    store8(y + off, f);
+  }
+}
+
 // --------------------------------------------------------------------------- GEMM
 __device__ __forceinline__ int f8_off(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
 
-template <int BM, int BN, int WGM, int WGN>
+// BLK = false: per-row fp32 scales sa [M], sb [E, N] applied in the epilogue (unit MFMA scales).
+// BLK = true: E8M0 block scales sa [M, K/128] (1 x 128 activation tiles), sb [E, N/128, K/128]
+// (128 x 128 weight blocks) fed to the MFMA scale operands per k-step; no epilogue scaling.
+template <int BM, int BN, int WGM, int WGN, bool BLK>
 __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
-    const uint8_t* __restrict__ A, const float* __restrict__ sa, const uint8_t* __restrict__ B,
-    const float* __restrict__ sb, bf16* __restrict__ C, const int* __restrict__ offsets, int E, int N, int K,
+    const uint8_t* __restrict__ A, const void* __restrict__ sa_, const uint8_t* __restrict__ B,
+    const void* __restrict__ sb_, bf16* __restrict__ C, const int* __restrict__ offsets, int E, int N, int K,
     long strideB) {
+  const float* sa = static_cast<const float*>(sa_);
+  const float* sb = static_cast<const float*>(sb_);
+  const uint8_t* sa8 = static_cast<const uint8_t*>(sa_);
+  const uint8_t* sb8 = static_cast<const uint8_t*>(sb_);
   constexpr int BK = 128;                                  // bytes (= fp8 elements) per k-step
   constexpr int NT = 64 * WGM * WGN;
   constexpr int TM = BM / WGM, TN = BN / WGN, IM = TM / 32, IN = TN / 32;
@@ -71,6 +197,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
   constexpr int CA = AB / 16 / NT, CB = BB / 16 / NT;
   static_assert(CA * 16 * NT == AB && CB * 16 * NT == BB, "tile/threads mismatch");
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (AB + BB)];
+  __shared__ uint8_t scl[2][BM + BN / 128];                 // BLK: E8M0 scales of the staged k-tile
   __shared__ int s_e, s_mt;
   __shared__ int wsum[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -103,7 +230,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
   const int n0 = nt * BN;
   const uint8_t* Bp = B + e * strideB;
   uint4 ra[CA], rb[CB];
+  int rs = 127;                                             // BLK: this thread's staged scale byte
+  const int KB = K / 128, NB = (N + 127) / 128;
   auto load_tiles = [&](int kk) {
+    if (BLK) {
+      const int kb = kk / 128;
+      if (tid < BM) rs = (m0 + tid < mend) ? sa8[(long)(m0 + tid) * KB + kb] : 127;
+      else if (tid < BM + BN / 128) {
+        const int nb = n0 / 128 + (tid - BM);
+        rs = nb < NB ? sb8[((long)e * NB + nb) * KB + kb] : 127;
+      }
+    }
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT, r = idx >> 3, ch = idx & 7;
@@ -118,6 +255,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
     }
   };
   auto store_tiles = [&](int buf) {
+    if (BLK && tid < BM + BN / 128) scl[buf][tid] = (uint8_t)rs;
     uint8_t* At = smem + buf * (AB + BB);
     uint8_t* Bt = At + AB;
 #pragma unroll
@@ -166,11 +304,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
       for (int j = 0; j < IM; ++j) af[j] = frag(At, wm * TM + j * 32 + l32, s, hh);
 #pragma unroll
       for (int i = 0; i < IN; ++i) bfr[i] = frag(Bt, wn * TN + i * 32 + l32, s, hh);
+      int sca[IM], scb = 127;
+#pragma unroll
+      for (int j = 0; j < IM; ++j) sca[j] = BLK ? (int)scl[buf][wm * TM + j * 32 + l32] : 127;
+      if (BLK) scb = scl[buf][BM + (wn * TN) / 128];
 #pragma unroll
       for (int i = 0; i < IN; ++i)
 #pragma unroll
-        for (int j = 0; j < IM; ++j)   // fp8 e4m3 x fp8 e4m3, unit block scales (E8M0 127 = 1.0)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[i], af[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+        for (int j = 0; j < IM; ++j)   // e4m3 x e4m3; MX scales: weight block (A), token tile (B)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[i], af[j], acc[i][j], 0, 0, 0, scb, 0,
+                                                                      sca[j]);
     }
     __syncthreads();
   }
@@ -179,14 +322,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
   for (int j = 0; j < IM; ++j) {
     const int gm = m0 + wm * TM + j * 32 + l32;
     if (gm >= mend) continue;
-    const float sm = sa[gm];
+    const float sm = BLK ? 1.f : sa[gm];
 #pragma unroll
     for (int i = 0; i < IN; ++i)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int gn = n0 + wn * TN + i * 32 + 8 * g + 4 * hh;
         if (gn >= N) continue;
-        const f32x4 sw = *reinterpret_cast<const f32x4*>(sb + (long)e * N + gn);
+        const f32x4 sw = BLK ? f32x4{1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sb + (long)e * N + gn);
         bf16x4 w4;
 #pragma unroll
         for (int q = 0; q < 4; ++q) w4[q] = (bf16)(acc[i][j][4 * g + q] * sm * sw[q]);
@@ -229,8 +372,89 @@ at::Tensor grouped_gemm_fp8(const at::Tensor& xq, const at::Tensor& sx, const at
   if (M == 0) return out;
   constexpr int BM = 256, BN = 256;
   const int grid = (cdiv(M, BM) + E) * cdiv(N, BN);
-  grouped_gemm_fp8_kernel<BM, BN, 2, 4><<<grid, 512, 0, stream()>>>(
+  grouped_gemm_fp8_kernel<BM, BN, 2, 4, false><<<grid, 512, 0, stream()>>>(
       (const uint8_t*)xq.data_ptr(), sx.data_ptr<float>(), (const uint8_t*)wq.data_ptr(), sw.data_ptr<float>(),
+      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, (long)N * K);
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+// block-scaled: xq [M, K] e4m3 + sx [M, K/128] E8M0 (uint8); wq [E, N, K] e4m3 + sw [E, N/128, K/128]
+std::vector<at::Tensor> quant_act_fp8_blk(const at::Tensor& x_) {
+  SPA_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "quant_act_fp8_blk: bf16 input");
+  const int K = x.size(-1);
+  TORCH_CHECK(K % 128 == 0, "quant_act_fp8_blk: K % 128 == 0");
+  const long R = x.numel() / K;
+  DeviceGuard g(x.device());
+  auto q = at::empty(x.sizes(), x.options().dtype(at::kFloat8_e4m3fn));
+  auto s = at::empty({R, K / 128}, x.options().dtype(at::kByte));
+  const long units = R * (K / 128);
+  if (units == 0) return {q, s};
+  quant_act_blk_kernel<<<(int)((units * 16 + 255) / 256), 256, 0, stream()>>>(
+      (const bf16*)x.data_ptr(), (uint8_t*)q.data_ptr(), s.data_ptr<uint8_t>(), units, K / 128);
+  SPA_LAUNCH_CHECK();
+  return {q, s};
+}
+
+// returns (wq [E,N,K], wtq [E,K,N], s [E,N/128,K/128], st [E,K/128,N/128])
+std::vector<at::Tensor> quant_weight_fp8_blk(const at::Tensor& w_) {
+  SPA_CHECK_CUDA(w_);
+  auto w = w_.contiguous();
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 3, "quant_weight_fp8_blk: bf16 [E, N, K]");
+  const int E = w.size(0), N = w.size(1), K = w.size(2);
+  TORCH_CHECK(N % 128 == 0 && K % 128 == 0, "quant_weight_fp8_blk: N, K % 128 == 0");
+  DeviceGuard g(w.device());
+  auto o8 = w.options().dtype(at::kFloat8_e4m3fn);
+  auto wq = at::empty({E, N, K}, o8), wtq = at::empty({E, K, N}, o8);
+  auto s = at::empty({E, N / 128, K / 128}, w.options().dtype(at::kByte));
+  auto st = at::empty({E, K / 128, N / 128}, w.options().dtype(at::kByte));
+  const long blocks = (long)E * (N / 128) * (K / 128);
+  if (blocks == 0) return {wq, wtq, s, st};
+  quant_weight_blk_kernel<<<(int)blocks, 256, 0, stream()>>>((const bf16*)w.data_ptr(), (uint8_t*)wq.data_ptr(),
+                                                             (uint8_t*)wtq.data_ptr(), s.data_ptr<uint8_t>(),
+                                                             st.data_ptr<uint8_t>(), N, K);
+  SPA_LAUNCH_CHECK();
+  return {wq, wtq, s, st};
+}
+
+// (q [R, K] e4m3, s [R, >= K/128] E8M0 rows) -> bf16 [R, K]
+at::Tensor dequant_act_fp8_blk(const at::Tensor& q, const at::Tensor& s) {
+  SPA_CHECK_CUDA(q);
+  TORCH_CHECK(q.is_contiguous() && s.is_contiguous() && s.scalar_type() == at::kByte && q.dim() == 2 && s.dim() == 2);
+  const long R = q.size(0);
+  const int K = q.size(1), ldS = s.size(1);
+  TORCH_CHECK(K % 128 == 0 && s.size(0) == R && ldS >= K / 128, "dequant_act_fp8_blk: shapes");
+  DeviceGuard g(q.device());
+  auto y = at::empty({R, K}, q.options().dtype(at::kBFloat16));
+  const long n8 = R * K / 8;
+  if (n8 == 0) return y;
+  dequant_act_blk_kernel<<<(int)std::min<long>((n8 + 255) / 256, 16384), 256, 0, stream()>>>(
+      (const uint8_t*)q.data_ptr(), s.data_ptr<uint8_t>(), (bf16*)y.data_ptr(), n8, K, ldS);
+  SPA_LAUNCH_CHECK();
+  return y;
+}
+
+at::Tensor grouped_gemm_fp8_blk(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& wq, const at::Tensor& sw,
+                                const at::Tensor& offsets) {
+  TORCH_CHECK(xq.scalar_type() == at::kFloat8_e4m3fn && wq.scalar_type() == at::kFloat8_e4m3fn, "e4m3 operands");
+  TORCH_CHECK(sx.scalar_type() == at::kByte && sw.scalar_type() == at::kByte, "E8M0 (uint8) scales");
+  TORCH_CHECK(xq.is_contiguous() && wq.is_contiguous() && sx.is_contiguous() && sw.is_contiguous());
+  TORCH_CHECK(offsets.scalar_type() == at::kInt);
+  const int E = offsets.numel() - 1;
+  TORCH_CHECK(E >= 1 && E <= 256 && wq.dim() == 3 && wq.size(0) == E);
+  const int M = xq.size(0), K = xq.size(1), N = wq.size(1);
+  TORCH_CHECK(wq.size(2) == K && K % 128 == 0 && N % 8 == 0, "grouped_gemm_fp8_blk: K % 128, N % 8");
+  TORCH_CHECK(sx.numel() == (long)M * (K / 128) && sw.numel() == (long)E * ((N + 127) / 128) * (K / 128),
+              "grouped_gemm_fp8_blk: scale shapes");
+  DeviceGuard g(xq.device());
+  auto out = at::empty({M, N}, xq.options().dtype(at::kBFloat16));
+  if (M == 0) return out;
+  constexpr int BM = 256, BN = 256;
+  const int grid = (cdiv(M, BM) + E) * cdiv(N, BN);
+  grouped_gemm_fp8_kernel<BM, BN, 2, 4, true><<<grid, 512, 0, stream()>>>(
+      (const uint8_t*)xq.data_ptr(), sx.data_ptr<uint8_t>(), (const uint8_t*)wq.data_ptr(), sw.data_ptr<uint8_t>(),
       (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, (long)N * K);
   SPA_LAUNCH_CHECK();
   return out;
@@ -241,8 +465,16 @@ at::Tensor grouped_gemm_fp8(const at::Tensor& xq, const at::Tensor& sx, const at
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("quant_rows_fp8(Tensor x) -> Tensor[]");
   m.def("grouped_gemm_fp8(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor offsets) -> Tensor");
+  m.def("quant_act_fp8_blk(Tensor x) -> Tensor[]");
+  m.def("dequant_act_fp8_blk(Tensor q, Tensor s) -> Tensor");
+  m.def("quant_weight_fp8_blk(Tensor w) -> Tensor[]");
+  m.def("grouped_gemm_fp8_blk(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor offsets) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("quant_rows_fp8", &spa::quant_rows_fp8);
   m.impl("grouped_gemm_fp8", &spa::grouped_gemm_fp8);
+  m.impl("quant_act_fp8_blk", &spa::quant_act_fp8_blk);
+  m.impl("dequant_act_fp8_blk", &spa::dequant_act_fp8_blk);
+  m.impl("quant_weight_fp8_blk", &spa::quant_weight_fp8_blk);
+  m.impl("grouped_gemm_fp8_blk", &spa::grouped_gemm_fp8_blk);
 }

@@ -282,11 +282,115 @@ def _quant_weight(W):
     return q.view(E, N, K), s.view(E, N)
 
 
+# ---- DeepSeek-V3-style block scaling (1 x 128 activation tiles, 128 x 128 weight blocks, E8M0
+# scales consumed by the MFMA scale operands: csrc/kernels/moe_fp8.hip)
+_WEIGHT_EPOCH = [0]
+_WQ_CACHE: dict = {}
+
+
+def bump_weight_epoch():
+    """Called by the optimizers after every parameter update: cached fp8 weight images are
+    rebuilt once per step instead of once per forward/backward use."""
+    _WEIGHT_EPOCH[0] += 1
+
+
+def _blk_ok(W):
+    return W.shape[1] % 128 == 0 and W.shape[2] % 128 == 0
+
+
+def quant_act_fp8_blk(x):
+    """x [R, K] -> (q e4m3, s uint8 E8M0 [R, K/128]); x ~= q * 2^(s - 127) per 128-wide tile."""
+    if x.is_cuda:
+        return tuple(ops().quant_act_fp8_blk(x.contiguous()))
+    x2 = x.reshape(-1, x.shape[-1]).float()
+    t = x2.view(x2.shape[0], -1, 128)
+    e = _e8m0(t.abs().amax(-1))
+    q = (t * torch.exp2(-e.float())[..., None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    return q.view(x.shape), (e + 127).to(torch.uint8)
+
+
+def _e8m0(amax):
+    """smallest e with amax / 2^e <= 448 (0 for all-zero blocks) -- matches e8m0_exp on the GPU."""
+    v = (amax / 448.0).float()
+    e = torch.ceil(torch.log2(torch.where(v > 0, v, torch.ones_like(v))))
+    e = torch.where(torch.exp2(e - 1) >= v, e - 1, e)          # guard log2 rounding up
+    e = torch.where(torch.exp2(e) < v, e + 1, e)
+    return torch.where(v > 0, e, torch.zeros_like(e)).clamp(-126, 127).to(torch.int32)
+
+
+def quant_weight_fp8_blk(W):
+    """W [E, N, K] -> (wq [E,N,K], wtq [E,K,N], s [E,N/128,K/128], st [E,K/128,N/128]); cached per
+    weight version and optimizer step (never while a HIP graph is being captured)."""
+    capturing = W.is_cuda and torch.cuda.is_current_stream_capturing()
+    key = (W.data_ptr(), tuple(W.shape), W._version, _WEIGHT_EPOCH[0])
+    hit = None if capturing else _WQ_CACHE.get(key)
+    if hit is not None:
+        return hit
+    if W.is_cuda:
+        out = tuple(ops().quant_weight_fp8_blk(W.detach().contiguous()))
+    else:
+        E, N, K = W.shape
+        t = W.detach().float().view(E, N // 128, 128, K // 128, 128)
+        e = _e8m0(t.abs().amax(dim=(2, 4)))                       # [E, NB, KB]
+        q = (t * torch.exp2(-e.float())[:, :, None, :, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+        q = q.view(E, N, K)
+        out = (q, q.transpose(1, 2).contiguous(), (e + 127).to(torch.uint8),
+               (e + 127).to(torch.uint8).transpose(1, 2).contiguous())
+    if not capturing:
+        stale = [k for k in _WQ_CACHE if k[0] == key[0] and k[1] == key[1]]
+        for k in stale:
+            del _WQ_CACHE[k]
+        _WQ_CACHE[key] = out
+    return out
+
+
+def dequant_act_fp8_blk(q, s, dtype=torch.bfloat16):
+    """inverse of quant_act_fp8_blk (scale rows may be padded past K/128)."""
+    if q.is_cuda:
+        return ops().dequant_act_fp8_blk(q.contiguous(), s.contiguous()).to(dtype)
+    R, K = q.shape
+    return (q.float().view(R, -1, 128) * torch.exp2(s[:, :K // 128].float() - 127)[..., None]).view(R, K).to(dtype)
+
+
+def commit_weight_grad(W, dy, xp, plan):
+    """bf16 dW_e = dy_e^T xp_e (grouped), committed into W's gradient storage."""
+    def _w(out, acc):
+        if out is None:
+            return grouped_gemm(dy, xp, plan.offsets, 2)
+        if out.dtype == dy.dtype and out.is_contiguous():
+            grouped_gemm(dy, xp, plan.offsets, 2, out=out.view(W.shape), accumulate=acc)
+        else:
+            g = grouped_gemm(dy, xp, plan.offsets, 2)
+            if acc:
+                out.add_(g.view_as(out))
+            else:
+                out.copy_(g.view_as(out))
+    return commit(W, _w)
+
+
+def grouped_gemm_fp8_blk(xq, sx, wq, sw, offsets):
+    if xq.is_cuda:
+        return ops().grouped_gemm_fp8_blk(xq, sx, wq, sw, offsets)
+    x = xq.float().view(xq.shape[0], -1, 128) * torch.exp2(sx.float() - 127)[..., None]
+    E, N, K = wq.shape
+    w = wq.float().view(E, N // 128, 128, K // 128, 128) * torch.exp2(sw.float() - 127)[:, :, None, :, None]
+    return _cpu_grouped(x.view(xq.shape), w.view(E, N, K), offsets, 0).to(torch.bfloat16)
+
+
 class _GroupedLinearFP8Fn(torch.autograd.Function):
+    """fp8 expert projection. Block-scaled path (N, K % 128): X in 1 x 128 tiles, W in 128 x 128
+    blocks, W^T for dX from the same quantized bytes; weights quantized once per optimizer step.
+    Otherwise per-row scales. dW is a bf16 grouped GEMM."""
+
     @staticmethod
     def forward(ctx, xp, W, plan):
         ctx.plan, ctx.W = plan, W
         ctx.save_for_backward(xp)
+        ctx.blk = _blk_ok(W)
+        if ctx.blk:
+            xq, sx = quant_act_fp8_blk(xp)
+            wq, _, sw, _ = quant_weight_fp8_blk(W)
+            return grouped_gemm_fp8_blk(xq, sx, wq, sw, plan.offsets).to(xp.dtype)
         xq, sx = quant_rows_fp8(xp)
         wq, sw = _quant_weight(W)
         return grouped_gemm_fp8(xq, sx, wq, sw, plan.offsets).to(xp.dtype)
@@ -299,9 +403,14 @@ class _GroupedLinearFP8Fn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            dq, sd = quant_rows_fp8(dy)
-            wtq, swt = _quant_weight(transpose2d(W))          # [E, in, out]
-            dx = grouped_gemm_fp8(dq, sd, wtq, swt, plan.offsets).to(xp.dtype)
+            if ctx.blk:
+                dq, sd = quant_act_fp8_blk(dy)
+                _, wtq, _, swt = quant_weight_fp8_blk(W)              # [E, in, out], cached
+                dx = grouped_gemm_fp8_blk(dq, sd, wtq, swt, plan.offsets).to(xp.dtype)
+            else:
+                dq, sd = quant_rows_fp8(dy)
+                wtq, swt = _quant_weight(transpose2d(W))          # [E, in, out]
+                dx = grouped_gemm_fp8(dq, sd, wtq, swt, plan.offsets).to(xp.dtype)
         gw = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):

@@ -10,7 +10,9 @@ The reference keeps all 8 experts on every replica and runs them in a Python loo
    host sync (one D2H copy of 2*E ints per MoE layer);
 3. token rows exchanged (``all_to_all_single`` with uneven splits) — they arrive
    ordered by (source rank, local expert) and are regrouped to (local expert, source)
-   by one device kernel (``regroup_rows``, csrc/kernels/ep.hip; no host loop);
+   by one device kernel (``regroup_rows``, csrc/kernels/ep.hip; no host loop). With fp8
+   experts the payload is e4m3 rows + 1 x 128 E8M0 scales (``_Fp8DispatchW13``);
+   the combine stays bf16;
 4. the local experts run as ONE grouped GEMM per projection (csrc/kernels/moe.hip);
 5. the inverse regroup + all-to-all return the rows; ``combine`` applies the gate
    weights in the original token order.
@@ -28,7 +30,8 @@ import torch.distributed as dist
 
 from ..ops._ext import ops
 from ..ops.activation import glu
-from ..ops.moe import combine, gather, grouped_linear, permute
+from ..ops.moe import (combine, commit_weight_grad, dequant_act_fp8_blk, gather, grouped_gemm_fp8_blk, grouped_linear,
+                       permute, quant_act_fp8_blk, quant_weight_fp8_blk)
 
 
 def ep_rank_size(group):
@@ -97,6 +100,51 @@ class _Regroup(torch.autograd.Function):
         return regroup_rows(g.contiguous(), ctx.rc, not ctx.to_em), None, None
 
 
+class _Fp8DispatchW13(torch.autograd.Function):
+    """fp8 dispatch fused with the first expert projection (DeepSeek-V3 sec. 3.3: dispatch in fp8,
+    combine in bf16). The sender quantizes its expert-sorted rows once (1 x 128 E8M0 tiles); the
+    all-to-all carries e4m3 bytes + scales (~0.52x the bf16 payload); the receiver regroups the
+    packed rows and feeds them straight to the block-scaled grouped GEMM. Backward: dX in fp8 on
+    the cached W^T bytes, returned in bf16 through the inverse regroup + all-to-all; dW in bf16
+    on the dequantized received rows (the same values the forward consumed)."""
+
+    @staticmethod
+    def forward(ctx, xp, W13, rc, send_splits, recv_splits, offsets, group):
+        D = xp.shape[1]
+        KB = D // 128
+        q, sx = quant_act_fp8_blk(xp)
+        pad = (-KB) % 16
+        pay = torch.cat([q.view(torch.uint8), torch.nn.functional.pad(sx, (0, pad))], 1).contiguous()
+        pr = pay.new_empty((sum(recv_splits), pay.shape[1]))
+        dist.all_to_all_single(pr, pay, recv_splits, send_splits, group=group)
+        pl = regroup_rows(pr, rc, True)
+        xq_l = pl[:, :D].contiguous().view(torch.float8_e4m3fn)
+        sx_l = pl[:, D:D + KB].contiguous()
+        wq, _, sw, _ = quant_weight_fp8_blk(W13)
+        ctx.save_for_backward(xq_l, sx_l, rc, offsets)
+        ctx.W, ctx.splits, ctx.group = W13, (send_splits, recv_splits), group
+        return grouped_gemm_fp8_blk(xq_l, sx_l, wq, sw, offsets).to(xp.dtype)
+
+    @staticmethod
+    def backward(ctx, dh):
+        xq_l, sx_l, rc, offsets = ctx.saved_tensors
+        W, (send_splits, recv_splits) = ctx.W, ctx.splits
+        dh = dh.contiguous()
+        lplan = SimpleNamespace(offsets=offsets)
+        dxp = None
+        if ctx.needs_input_grad[0]:
+            dq, sd = quant_act_fp8_blk(dh)
+            _, wtq, _, swt = quant_weight_fp8_blk(W)
+            dxl = grouped_gemm_fp8_blk(dq, sd, wtq, swt, offsets).to(dh.dtype)
+            dxr = regroup_rows(dxl, rc, False)
+            dxp = dxr.new_empty((sum(send_splits), dxr.shape[1]))
+            dist.all_to_all_single(dxp, dxr, send_splits, recv_splits, group=ctx.group)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gw = commit_weight_grad(W, dh, dequant_act_fp8_blk(xq_l, sx_l, dh.dtype), lplan)
+        return dxp, gw, None, None, None, None, None
+
+
 def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
     [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
@@ -117,14 +165,20 @@ def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     rc = both[1].view(P, El)
     recv_splits = rc.sum(1).tolist()
     xp = gather(x, plan)                                      # [A, D] sorted by global expert
-    xr = all_to_all(xp, recv_splits, send_splits, group)     # [R, D] (src, e_local) order
     per_e = rc.sum(0)
     loff = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
     dev = x.device
     rc_dev = recv.view(P, El)                                # device copy of the counts
     lplan = SimpleNamespace(offsets=loff.to(device=dev, dtype=torch.int32))
-    xl = _Regroup.apply(xr, rc_dev, True)                    # (src, e) -> (e, src) rows
-    h = glu(grouped_linear(xl, W13, lplan, fp8), act)
+    D = x.shape[-1]
+    if fp8 and D % 128 == 0 and W13.shape[1] % 128 == 0:
+        # fp8 dispatch payload (e4m3 rows + E8M0 tile scales), fused with the W13 projection
+        h13 = _Fp8DispatchW13.apply(xp, W13, rc_dev, send_splits, recv_splits, lplan.offsets, group)
+    else:
+        xr = all_to_all(xp, recv_splits, send_splits, group)  # [R, D] (src, e_local) order
+        xl = _Regroup.apply(xr, rc_dev, True)                 # (src, e) -> (e, src) rows
+        h13 = grouped_linear(xl, W13, lplan, fp8)
+    h = glu(h13, act)
     yl = grouped_linear(h, W2, lplan, fp8)
     yr = _Regroup.apply(yl, rc_dev, False)
     yp = all_to_all(yr, send_splits, recv_splits, group)

@@ -84,6 +84,8 @@ class FlatOptimizer:
         memory-bound optimizer overlaps the compute-bound forward of the next
         step (see FlatParams.wait_bucket)."""
         self.step_count += 1
+        from ..ops.moe import bump_weight_epoch
+        bump_weight_epoch()                  # cached fp8 expert-weight images go stale now
         if self.hyper is not None:
             if not torch.cuda.is_current_stream_capturing():
                 self.hyper[0].fill_(lr)

@@ -253,3 +253,56 @@ def test_grouped_gemm8_elementwise(counts, N, K):
     dw2 = dw.clone()
     ops.grouped_gemm8(dy, x, off, 2, dw2, True)
     check(dw2.reshape(E * N, K), 2 * ref.reshape(E * N, K))
+
+
+def test_fp8_block_quant_matches_reference():
+    """quant_act_fp8_blk / quant_weight_fp8_blk (E8M0 block scales) == the torch reference bit for
+    bit; W^T bytes are the transpose of W's; scales are powers of two with amax / 2^e <= 448."""
+    g = torch.Generator().manual_seed(1)
+    x = (torch.randn(333, 512, generator=g) * torch.logspace(-3, 2, 512)).to(torch.bfloat16)
+    q, s = M.quant_act_fp8_blk(x.to(dev))
+    qr, sr = M.quant_act_fp8_blk(x)
+    assert torch.equal(s.cpu(), sr)
+    assert torch.equal(q.cpu().view(torch.uint8), qr.view(torch.uint8))
+    W = (torch.randn(3, 256, 384, generator=g) * 0.02).to(torch.bfloat16)
+    got = M.quant_weight_fp8_blk(W.to(dev))
+    ref = M.quant_weight_fp8_blk(W)
+    for a, b in zip(got, ref):
+        assert torch.equal(a.cpu().view(torch.uint8), b.view(torch.uint8))
+
+
+@pytest.mark.parametrize("counts", [[300, 0, 129, 1, 64, 700, 0, 33], [256] * 4])
+def test_grouped_gemm_fp8_blk_exact_on_dequantized(counts):
+    """block-scaled MFMA (scale operands) == fp32 GEMM of the dequantized operands."""
+    g = torch.Generator().manual_seed(2)
+    E, N, K = len(counts), 384, 512
+    M_ = sum(counts)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    x = (torch.randn(M_, K, generator=g) * torch.logspace(-2, 1, K)).to(dev, torch.bfloat16)
+    W = (torch.randn(E, N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    xq, sx = M.quant_act_fp8_blk(x)
+    wq, wtq, sw, swt = M.quant_weight_fp8_blk(W)
+    y = M.grouped_gemm_fp8_blk(xq, sx, wq, sw, off)
+    xd = (xq.float().view(M_, -1, 128) * torch.exp2(sx.float() - 127)[..., None]).view(M_, K)
+    wd = (wq.float().view(E, N // 128, 128, K // 128, 128)
+          * torch.exp2(sw.float() - 127)[:, :, None, :, None]).view(E, N, K)
+    ref = _oracle(xd, wd, off, 0)
+    assert _rel(y.cpu(), ref) < 5e-3
+    # dX form on the transposed bytes: dy [M, N] @ W -> [M, K]
+    dy = torch.randn(M_, N, generator=g).to(dev, torch.bfloat16)
+    dq, sd = M.quant_act_fp8_blk(dy)
+    dx = M.grouped_gemm_fp8_blk(dq, sd, wtq, swt, off)
+    dyd = (dq.float().view(M_, -1, 128) * torch.exp2(sd.float() - 127)[..., None]).view(M_, N)
+    assert _rel(dx.cpu(), _oracle(dyd, wd, off, 1)) < 5e-3
+
+
+def test_fp8_weight_cache_follows_optimizer_steps():
+    W = torch.randn(2, 256, 256, device=dev, dtype=torch.bfloat16) * 0.02
+    a = M.quant_weight_fp8_blk(W)
+    assert M.quant_weight_fp8_blk(W)[0] is a[0]               # cached within a step
+    with torch.no_grad():
+        W.mul_(2)                                            # in-place update bumps W._version
+    b = M.quant_weight_fp8_blk(W)
+    assert b[0] is not a[0] and not torch.equal(b[2], a[2])
+    M.bump_weight_epoch()                                    # optimizer step
+    assert M.quant_weight_fp8_blk(W)[0] is not b[0]

@@ -309,3 +309,48 @@ def test_nan_on_one_rank_skips_update_on_every_rank(zero1):
         assert (s0[s] == s1[s]).all(), s                  # replicas never diverge
     assert (s0[1] == s0[0]).all()                          # step 1 applied no update
     assert not (s0[2] == s0[1]).all()                      # later steps do
+
+
+def _ep_fp8_inputs():
+    g = torch.Generator().manual_seed(11)
+    E, D, F, N, k = 4, 128, 128, 24, 2
+    x = torch.randn(2, N, D, generator=g)
+    idx = torch.stack([torch.randperm(E, generator=g)[:k] for _ in range(2 * N)]).view(2, N, k).int()
+    w = torch.rand(2, N, k, generator=g)
+    W13 = torch.randn(E, 2 * F, D, generator=g) * 0.05
+    W2 = torch.randn(E, D, F, generator=g) * 0.05
+    gy = torch.randn(2, N, D, generator=g)
+    return x, idx, w, W13, W2, gy
+
+
+def _ep_fp8_worker(rank, world, port, q):
+    _init(rank, world, port)
+    from solvingpapers_amd.parallel.expert_parallel import ep_moe_ffn, shard_experts
+    x, idx, w, W13, W2, gy = _ep_fp8_inputs()
+    grp = dist.new_group([0, 1])
+    w13 = shard_experts(W13, rank, world).clone().requires_grad_(True)
+    w2 = shard_experts(W2, rank, world).clone().requires_grad_(True)
+    xr = x[rank].clone().requires_grad_(True)
+    y, _ = ep_moe_ffn(xr, idx[rank], w[rank], w13, w2, 4, grp, fp8=True)
+    (y * gy[rank]).sum().backward()
+    q.put((rank, y.detach().numpy(), xr.grad.numpy(), w13.grad.numpy(), w2.grad.numpy()))
+    dist.destroy_process_group()
+
+
+def test_expert_parallel_fp8_dispatch_matches_local_fp8():
+    """fp8 dispatch (e4m3 rows + E8M0 1x128 scales over the all-to-all, fused with the
+    block-scaled W13 GEMM) == the single-process block-scaled fp8 MoE: outputs and input grads
+    to fp32 rounding; expert grads to the fp8 rounding of the dW operand (the EP path forms dW13
+    from the dequantized received rows, as DeepSeek-V3 does)."""
+    from solvingpapers_amd.ops.moe import moe_ffn
+    x, idx, w, W13, W2, gy = _ep_fp8_inputs()
+    W13r, W2r = W13.clone().requires_grad_(True), W2.clone().requires_grad_(True)
+    xs = x.clone().requires_grad_(True)
+    ys = [moe_ffn(xs[r], idx[r], w[r], W13r, W2r, fp8=True)[0] for r in range(2)]
+    sum((y * gy[r]).sum() for r, y in enumerate(ys)).backward()
+    for rank, y, gx, g13, g2 in _run(_ep_fp8_worker, 2):
+        assert torch.allclose(torch.from_numpy(y), ys[rank].detach(), atol=1e-4)
+        assert torch.allclose(torch.from_numpy(gx), xs.grad[rank], atol=1e-4)
+        ref13 = W13r.grad[rank * 2:(rank + 1) * 2]
+        assert ((torch.from_numpy(g13) - ref13).norm() / ref13.norm()) < 5e-2
+        assert torch.allclose(torch.from_numpy(g2), W2r.grad[rank * 2:(rank + 1) * 2], atol=1e-4)

@@ -70,6 +70,19 @@ wq, sw = M.quant_rows_fp8(W13.view(E * 2 * F, D))
 wq = wq.view(E, 2 * F, D)
 ms = tm(lambda: ops.grouped_gemm_fp8(xq, sx, wq, sw.view(E, 2 * F), plan.offsets))
 print(f"fp8 fwd W13 grouped GEMM: {2 * A * 2 * F * D / ms / 1e9:.0f} TF (e4m3, per-row scales applied in the epilogue)")
+xb, sxb = M.quant_act_fp8_blk(x)
+wqb, wtqb, swb, swtb = M.quant_weight_fp8_blk(W13)
+ms = tm(lambda: ops.grouped_gemm_fp8_blk(xb, sxb, wqb, swb, plan.offsets))
+print(f"fp8 fwd W13 grouped GEMM, 1x128 / 128x128 E8M0 block scales on the MFMA: {2 * A * 2 * F * D / ms / 1e9:.0f} TF")
+dq, sdq = M.quant_act_fp8_blk(dy13)
+ms = tm(lambda: ops.grouped_gemm_fp8_blk(dq, sdq, wtqb, swtb, plan.offsets))
+print(f"fp8 dX W13 grouped GEMM (block scales, W^T bytes): {2 * A * 2 * F * D / ms / 1e9:.0f} TF")
+ms = tm(lambda: M.quant_act_fp8_blk(x))
+print(f"quant_act_fp8_blk [{A}x{D}]: {ms:.3f} ms = {A * D * 3.06 / ms / 1e6:.0f} GB/s")
+M.bump_weight_epoch()
+ms = tm(lambda: (M.bump_weight_epoch(), M.quant_weight_fp8_blk(W13)))
+print(f"quant_weight_fp8_blk W13 [{E}x{2 * F}x{D}] (+ transposed bytes): {ms:.3f} ms = "
+      f"{E * 2 * F * D * 4 / ms / 1e6:.0f} GB/s")
 msq = tm(lambda: M.quant_rows_fp8(x))
 print(f"quant_rows_fp8 [{A}x{D}]: {msq:.3f} ms = {A * D * 3 / msq / 1e6:.0f} GB/s")
 a = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
