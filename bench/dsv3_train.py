@@ -28,7 +28,9 @@ def main():
     ap.add_argument("--experts", type=int, default=None, help="routed experts (whole job; EP splits them)")
     ap.add_argument("--dense-layers", type=int, default=None)
     ap.add_argument("--accum", type=int, default=1, help="micro-batches accumulated per optimizer step")
-    ap.add_argument("--fp8", action="store_true", help="fp8 (OCP e4m3) routed-expert GEMMs")
+    ap.add_argument("--fp8", action="store_true",
+                    help="DeepSeek-V3 fp8 recipe: routed experts + dense projections in block-scaled e4m3")
+    ap.add_argument("--fp8-experts-only", action="store_true", help="with --fp8: dense projections stay bf16")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
@@ -41,6 +43,7 @@ def main():
         kw["n_dense_layers"] = a.dense_layers
     if a.fp8:
         kw["moe_fp8"] = True
+        kw["fp8_linears"] = not a.fp8_experts_only
     c = ds.config(a.preset, **kw)
     ep = torch.distributed.group.WORLD if world > 1 else None
     m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep)
@@ -69,7 +72,8 @@ def main():
     el = timed(step, a.steps, a.warmup)
     tok_s = world * B * T * a.accum * a.steps / el
     tf = tok_s * m.flops_per_token(T) / world / 1e12
-    report("training tokens/sec, DeepSeek-V3-style MLA+MoE bf16", tok_s, "tokens/s", a.steps, a.warmup, el,
+    report("training tokens/sec, DeepSeek-V3-style MLA+MoE " + ("fp8 (e4m3 block-scaled GEMMs)" if a.fp8 else "bf16"),
+           tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
             + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum,
             "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu", "params": m.num_params(),

@@ -72,6 +72,7 @@ class DSV3Config:
     n_dense_layers: int = 0         # leading layers with a dense SwiGLU FFN
     dense_hidden: int = 0
     moe_fp8: bool = False           # routed-expert fwd/dX GEMMs in OCP e4m3 (BASELINE config #5)
+    fp8_linears: bool = False       # dense projections too (MLA, shared / dense FFN): the V3 recipe
     aux_free: bool = True
     bias_update_rate: float = 1e-3
     bias_in_weights: bool = True    # ref: softmax over (logits + bias); paper: bias steers selection only
@@ -217,8 +218,9 @@ class MLA(tnn.Module):
     def _q(self, xn):
         c = self.c
         if c.q_lora_rank:
-            return linear(rms_norm(linear(xn, self.wdq), self.q_norm, c.norm_eps), self.wuq)
-        return linear(xn, self.wq)
+            return linear(rms_norm(linear(xn, self.wdq, fp8=c.fp8_linears), self.q_norm, c.norm_eps), self.wuq,
+                          fp8=c.fp8_linears)
+        return linear(xn, self.wq, fp8=c.fp8_linears)
 
     def _rope(self, x, pos):
         from ..infer.graph import DecodeState
@@ -230,7 +232,7 @@ class MLA(tnn.Module):
     def _latent(self, xn, pos):
         c = self.c
         B, T, _ = xn.shape
-        ckr = linear(xn, self.wdkv)
+        ckr = linear(xn, self.wdkv, fp8=c.fp8_linears)
         ckv = rms_norm(ckr[..., :c.kv_lora_rank].contiguous(), self.kv_norm, c.norm_eps)
         kr = self._rope(ckr[..., c.kv_lora_rank:].reshape(B, T, 1, c.qk_rope_dim), pos)
         return ckv, kr
@@ -245,14 +247,14 @@ class MLA(tnn.Module):
         ckv, kr = self._latent(xn, pos)
         if cache is not None:
             return self._decode(q[..., :dn], qr, ckv, kr, cache, pos, scale)
-        kv = linear(ckv, self.wukv).view(B, T, H, dn + dv)
+        kv = linear(ckv, self.wukv, fp8=c.fp8_linears).view(B, T, H, dn + dv)
         qf = torch.cat([q[..., :dn], qr], dim=-1)
         k = torch.cat([kv[..., :dn], kr.expand(B, T, H, dr)], dim=-1)
         v = kv[..., dn:]
         # the flash kernels take (q/k, v) head dims (64,64) / (128,128) / (192,128) -- V3's MLA
         # heads -- directly, reading v as a strided view of the up-projection output
         o = flash_attention(qf, k, v, causal=True, scale=scale)
-        return linear(o.reshape(B, T, H * dv), self.wo)
+        return linear(o.reshape(B, T, H * dv), self.wo, fp8=c.fp8_linears)
 
     def _decode(self, qn, qr, ckv, kr, cache, pos, scale):
         """Latent-space attention over the compressed cache (W_uk absorbed into q, W_uv applied
@@ -285,9 +287,9 @@ class MLA(tnn.Module):
 
 # =============================================================================== FFN / MoE
 class DenseFFN(tnn.Module):
-    def __init__(self, D, F, **fk):
+    def __init__(self, D, F, fp8=False, **fk):
         super().__init__()
-        self.F, self.Fp = F, _pad8(F)
+        self.F, self.Fp, self.fp8 = F, _pad8(F), fp8
         self.w13 = tnn.Parameter(torch.zeros(2 * self.Fp, D, **fk))    # [gate ; up], padded rows zero
         self.w2 = tnn.Parameter(torch.zeros(D, self.Fp, **fk))
 
@@ -301,7 +303,7 @@ class DenseFFN(tnn.Module):
         self.w2[:, :F].normal_(0, std, generator=g)
 
     def forward(self, x):
-        return linear(glu(linear(x, self.w13), "silu"), self.w2)
+        return linear(glu(linear(x, self.w13, fp8=self.fp8), "silu"), self.w2, fp8=self.fp8)
 
 
 class MoE(tnn.Module):
@@ -323,7 +325,7 @@ class MoE(tnn.Module):
         self.w2 = tnn.Parameter(torch.zeros(El, D, self.Fp, **fk))
         self.w13.expert_parallel = self.ep > 1
         self.w2.expert_parallel = self.ep > 1
-        self.shared = DenseFFN(D, F * c.n_shared, **fk) if c.n_shared else None
+        self.shared = DenseFFN(D, F * c.n_shared, fp8=c.fp8_linears, **fk) if c.n_shared else None
         self.register_buffer("routing_bias", torch.zeros(c.n_experts, device=fk.get("device")))
         self.balance_group = None      # DP group for the counts all-reduce (set by the trainer)
         self.last_counts = None
@@ -392,7 +394,7 @@ class DSV3Layer(tnn.Module):
         self.ffn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
         self.attn = RefLatentAttention(c, **fk) if c.attention == "ref" else MLA(c, **fk)
         if dense:
-            self.ffn = DenseFFN(c.dim, c.dense_hidden or c.ffn_hidden, **fk)
+            self.ffn = DenseFFN(c.dim, c.dense_hidden or c.ffn_hidden, fp8=c.fp8_linears, **fk)
         else:
             self.ffn = MoE(c, ep_group, **fk)
 

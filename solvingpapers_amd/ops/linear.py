@@ -80,7 +80,89 @@ def _gemv_ok(x, w, b) -> bool:
             and x.data_ptr() % 16 == 0)
 
 
-def linear(x, w, b=None):
+class _LinearFP8Fn(torch.autograd.Function):
+    """fp8 Linear for the dense projections of the DeepSeek-V3 recipe (arXiv 2412.19437 sec. 3.3):
+    forward and dX are e4m3 GEMMs on hipBLASLt (torch._scaled_mm, row-wise fp32 scales: one per
+    token row of X / dY, one per output channel of W for the forward and per input channel for
+    dX), dW stays bf16 through the fused-accumulation path. Weight images (W and W^T, e4m3 +
+    scales) are quantized once per optimizer step (ops/moe.py weight cache). Measured on MI355X
+    (tools/probe_scaled_mm.py): 1.7-2.7 PF vs 0.9-1.5 PF bf16 at V3 projection shapes. The
+    routed experts use the 1 x 128 / 128 x 128 block-scaled grouped kernel instead."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        from .moe import quant_rows_fp8, quant_weight_fp8_rows
+        ctx.w, ctx.b = w, b
+        ctx.save_for_backward(x)
+        x2 = x.reshape(-1, x.shape[-1])
+        xq, sx = quant_rows_fp8(x2)
+        wq, sw, _, _ = quant_weight_fp8_rows(w)
+        y = torch._scaled_mm(xq, wq.t(), sx[:, None], sw[None, :], bias=b, out_dtype=x.dtype)
+        return torch.ops.aten._unsafe_view(y, (*x.shape[:-1], w.shape[0]))
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .moe import quant_rows_fp8, quant_weight_fp8_rows
+        (x,) = ctx.saved_tensors
+        w, b = ctx.w, ctx.b
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dq, sd = quant_rows_fp8(dy2)
+            _, _, wtq, swt = quant_weight_fp8_rows(w)
+            dx = torch._scaled_mm(dq, wtq.t(), sd[:, None], swt[None, :], out_dtype=dy.dtype).view(x.shape)
+        gw = gb = None
+        if ctx.needs_input_grad[1]:
+            def _w(out, acc):
+                if out is not None and out.dtype != dy2.dtype:
+                    g = wgrad(dy2, x2)
+                    if acc:
+                        out.add_(g)
+                    else:
+                        out.copy_(g)
+                    return None
+                return wgrad(dy2, x2, out, acc)
+            gw = commit(w, _w)
+        if b is not None and ctx.needs_input_grad[2]:
+            def _b(out, acc):
+                s = dy2.sum(0, dtype=torch.float32)
+                if out is None:
+                    return s.to(b.dtype)
+                if acc:
+                    out.add_(s.to(out.dtype))
+                else:
+                    out.copy_(s)
+            gb = commit(b, _b)
+        return dx, gw, gb
+
+
+_GROUP1: dict = {}
+
+
+def _one_group(rows, device):
+    """device offsets [0, rows] for the grouped kernels, cached (no per-call H2D copy)."""
+    key = (rows, str(device))
+    t = _GROUP1.get(key)
+    if t is None:
+        t = torch.tensor([0, rows], dtype=torch.int32, device=device)
+        if len(_GROUP1) > 512:
+            _GROUP1.clear()
+        _GROUP1[key] = t
+    return t
+
+
+def _fp8_ok(x, w) -> bool:
+    K = x.shape[-1]
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2
+            and w.shape[0] % 16 == 0 and K % 16 == 0 and x.numel() > 0 and (x.numel() // K) % 16 == 0)
+
+
+def linear(x, w, b=None, fp8=False):
+    """y = x w^T (+ b). ``fp8``: e4m3 forward / dX on hipBLASLt with row-wise scales (dims
+    multiples of 16; else bf16)."""
+    if fp8 and _fp8_ok(x, w) and not _gemv_ok(x, w, b):
+        return _LinearFP8Fn.apply(x, w, b)
     if _gemv_ok(x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
         if x2.stride(0) % 8:

@@ -322,7 +322,7 @@ def quant_weight_fp8_blk(W):
     """W [E, N, K] -> (wq [E,N,K], wtq [E,K,N], s [E,N/128,K/128], st [E,K/128,N/128]); cached per
     weight version and optimizer step (never while a HIP graph is being captured)."""
     capturing = W.is_cuda and torch.cuda.is_current_stream_capturing()
-    key = (W.data_ptr(), tuple(W.shape), W._version, _WEIGHT_EPOCH[0])
+    key = ("blk", W.data_ptr(), tuple(W.shape), W._version, _WEIGHT_EPOCH[0])
     hit = None if capturing else _WQ_CACHE.get(key)
     if hit is not None:
         return hit
@@ -337,8 +337,7 @@ def quant_weight_fp8_blk(W):
         out = (q, q.transpose(1, 2).contiguous(), (e + 127).to(torch.uint8),
                (e + 127).to(torch.uint8).transpose(1, 2).contiguous())
     if not capturing:
-        stale = [k for k in _WQ_CACHE if k[0] == key[0] and k[1] == key[1]]
-        for k in stale:
+        for k in [k for k in _WQ_CACHE if k[:3] == key[:3]]:
             del _WQ_CACHE[k]
         _WQ_CACHE[key] = out
     return out
@@ -366,6 +365,26 @@ def commit_weight_grad(W, dy, xp, plan):
             else:
                 out.copy_(g.view_as(out))
     return commit(W, _w)
+
+
+def quant_weight_fp8_rows(W):
+    """2-D W [N, K] -> (wq [N,K] e4m3, sw [N], wtq [K,N] e4m3, swt [K]) with one fp32 scale per
+    output channel (forward) / per input channel (dX); cached like the block images."""
+    capturing = W.is_cuda and torch.cuda.is_current_stream_capturing()
+    key = ("rows", W.data_ptr(), tuple(W.shape), W._version, _WEIGHT_EPOCH[0])
+    hit = None if capturing else _WQ_CACHE.get(key)
+    if hit is not None:
+        return hit
+    from .layout import transpose2d
+    Wd = W.detach().contiguous()
+    wq, sw = quant_rows_fp8(Wd)
+    wtq, swt = quant_rows_fp8(transpose2d(Wd) if Wd.is_cuda else Wd.t().contiguous())
+    out = (wq, sw, wtq, swt)
+    if not capturing:
+        for k in [k for k in _WQ_CACHE if k[:3] == key[:3]]:
+            del _WQ_CACHE[k]
+        _WQ_CACHE[key] = out
+    return out
 
 
 def grouped_gemm_fp8_blk(xq, sx, wq, sw, offsets):

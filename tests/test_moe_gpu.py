@@ -306,3 +306,22 @@ def test_fp8_weight_cache_follows_optimizer_steps():
     assert b[0] is not a[0] and not torch.equal(b[2], a[2])
     M.bump_weight_epoch()                                    # optimizer step
     assert M.quant_weight_fp8_blk(W)[0] is not b[0]
+
+
+def test_fp8_linear_close_to_bf16():
+    """ops.linear(fp8=True): e4m3 fwd / dX on hipBLASLt (row-wise scales, cached weight images), bf16 dW."""
+    from solvingpapers_amd.ops.linear import linear
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 96, 512, generator=g).to(dev, torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(384, 512, generator=g) * 0.04).to(dev, torch.bfloat16).requires_grad_(True)
+    b = torch.randn(384, generator=g).to(dev, torch.bfloat16).requires_grad_(True)
+    gy = torch.randn(3, 96, 384, generator=g).to(dev, torch.bfloat16)
+    y = linear(x, w, b, fp8=True)
+    y.backward(gy)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = xr @ wr.t() + br
+    yr.backward(gy.float())
+    assert _rel(y, yr) < 4e-2
+    assert _rel(x.grad, xr.grad) < 4e-2
+    assert _rel(w.grad, wr.grad) < 1e-2            # dW stays bf16 (hipBLASLt)
+    assert _rel(b.grad, br.grad) < 1e-2
