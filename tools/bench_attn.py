@@ -56,8 +56,14 @@ for setting in filter(None, a.ab.split(",")):
     key, val = setting.split("=")
     old = os.environ.get(key)
     os.environ[key] = val
+    tf2 = t(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
+    o2, _ = ops.attn_fwd(q, k, v, sc, causal, P, SEED)
+    err = ((o2.float() - out.float()).norm() / out.float().norm()).item()
     tb2 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
     if old is None: os.environ.pop(key)
     else: os.environ[key] = old
+    tf3 = t(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
     tb3 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
-    print(f"   bwd with {key}={val}: {tb2*1e3:.3f} ms ({flb/tb2/1e12:.0f} TF) vs default again {tb3*1e3:.3f} ms", flush=True)
+    print(f"   with {key}={val}: fwd {tf2*1e3:.3f} ms ({fl/tf2/1e12:.0f} TF, out rel diff {err:.1e}) vs default "
+          f"{tf3*1e3:.3f} ms ({fl/tf3/1e12:.0f} TF) | bwd {tb2*1e3:.3f} ms ({flb/tb2/1e12:.0f} TF) vs "
+          f"{tb3*1e3:.3f} ms", flush=True)
