@@ -364,33 +364,47 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   }
   }
   if (ktiles > 0 && !late) __builtin_amdgcn_s_barrier();   // equal barrier counts on exit
-  // ---- epilogue: C^T fragment (n = 4 (l >> 4) + q, m = l & 15) -> 8-byte row stores
+  // ---- epilogue through LDS, one 128-row half at a time: C^T fragments (n = 4 (l >> 4) + q,
+  // m = l & 15) -> padded row image (528-B rows: the 16 rows of a fragment store land on 16
+  // distinct bank pairs) -> whole-row 16-byte global stores (a per-lane 8-byte store at a row
+  // stride would touch 16 cache lines per instruction)
+  constexpr int RS = 256 * 2 + 16;
+  __syncthreads();
 #pragma unroll
-  for (int mh = 0; mh < 2; ++mh)
+  for (int mh = 0; mh < 2; ++mh) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long gm = m0 + mh * 128 + wm * 64 + 16 * i + (lane & 15);
-      if (MODE == 2 ? gm >= M : gm >= mend) continue;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
-          if (gn >= N) continue;
-          bf16* cp = Cp + gm * ldc + gn;
           const f32x4 v = acc[mh * 4 + i][nh * 2 + j];
-          float o[4] = {v[0], v[1], v[2], v[3]};
-          if (accumulate) {
-            const bf16x4 old = *reinterpret_cast<const bf16x4*>(cp);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] += (float)old[q];
-          }
           bf16x4 w4;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) w4[q] = (bf16)o[q];
-          *reinterpret_cast<bf16x4*>(cp) = w4;
+          for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+          const int r = wm * 64 + 16 * i + (lane & 15);
+          const int cn = nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
+          *reinterpret_cast<bf16x4*>(smem + r * RS + cn * 2) = w4;
         }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
+      const long gm = m0 + mh * 128 + r;
+      const int gn = n0 + ch * 8;
+      if ((MODE == 2 ? gm < M : gm < mend) && gn < N) {
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * RS + ch * 16);
+        bf16* cp = Cp + gm * ldc + gn;
+        if (accumulate) {
+          const bf16x8 old = *reinterpret_cast<const bf16x8*>(cp);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)old[q]);
+        }
+        *reinterpret_cast<bf16x8*>(cp) = v;
+      }
     }
+    __syncthreads();
+  }
 }
 
 static int ablation() {

@@ -175,14 +175,14 @@ def _cpu_grouped(a, w, offsets, mode):
 
 
 GG8 = os.environ.get("SPA_GG8", "1") != "0"
-GG8_DW = os.environ.get("SPA_GG8", "1") == "2"
+GG8_DW = os.environ.get("SPA_GG8", "1") != "0"
 
 
 def _gg8_ok(a, w, mode):
     """the 8-phase LDS-DMA kernel (csrc/kernels/gemm8.hip) needs a reduction dim % 64 in modes 0/1
-    and output dims % 8. It wins fwd (+45 %) and dX (+12 %) at DeepSeek widths; the dW form
-    (short per-expert token loops) measures no faster than the register-staged 256x256 kernel
-    (profiles/r2_grouped_gemm_sweep.txt), so mode 2 stays on moe.hip unless SPA_GG8=2."""
+    and output dims % 8. Measured at DeepSeek widths (profiles/r2_grouped_gemm_sweep.txt): fwd
+    907 / 870 TF vs 560 / 530, dX 787 / 708 vs 653 / 623, dW 718 / 697 vs 687 / 690 for the
+    register-staged moe.hip kernel, which SPA_GG8=0 selects."""
     if mode == 0:
         return w.shape[2] % 64 == 0 and w.shape[1] % 8 == 0
     if mode == 1:
