@@ -317,24 +317,44 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
     }
     __syncthreads();
   }
-  // epilogue: C^T tiles, lane = token column m, rows n = 8g + 4hh + {0..3}
+  // epilogue through LDS, one 128-token half (= the waves with wm == half) at a time: C^T
+  // fragments (lane = token m, rows n = 8g + 4hh + {0..3}) -> padded [m][n] bf16 image ->
+  // whole-row 16-byte global stores
+  static_assert(BM == 256 && BN == 256 && WGM == 2, "fp8 epilogue: 256 x 256 tile, 2 wave rows");
+  constexpr int RS = BN * 2 + 16;
+  __syncthreads();
 #pragma unroll
-  for (int j = 0; j < IM; ++j) {
-    const int gm = m0 + wm * TM + j * 32 + l32;
-    if (gm >= mend) continue;
-    const float sm = BLK ? 1.f : sa[gm];
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
 #pragma unroll
-    for (int i = 0; i < IN; ++i)
+      for (int j = 0; j < IM; ++j) {
+        const int rm = j * 32 + l32;
+        const int gm = m0 + wm * TM + rm;
+        const float sm = (BLK || gm >= mend) ? 1.f : sa[gm];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int gn = n0 + wn * TN + i * 32 + 8 * g + 4 * hh;
-        if (gn >= N) continue;
-        const f32x4 sw = BLK ? f32x4{1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sb + (long)e * N + gn);
-        bf16x4 w4;
+        for (int i = 0; i < IN; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) w4[q] = (bf16)(acc[i][j][4 * g + q] * sm * sw[q]);
-        *reinterpret_cast<bf16x4*>(C + (long)gm * N + gn) = w4;
+          for (int g = 0; g < 4; ++g) {
+            const int cn = wn * TN + i * 32 + 8 * g + 4 * hh;
+            const int gn = n0 + cn;
+            const f32x4 sw = (BLK || gn >= N) ? f32x4{1.f, 1.f, 1.f, 1.f}
+                                               : *reinterpret_cast<const f32x4*>(sb + (long)e * N + gn);
+            bf16x4 w4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w4[q] = (bf16)(acc[i][j][4 * g + q] * sm * sw[q]);
+            *reinterpret_cast<bf16x4*>(smem + rm * RS + cn * 2) = w4;
+          }
       }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 128 * (BN / 8) / NT; ++c) {
+      const int idx = tid + c * NT, r = idx / (BN / 8), ch = idx % (BN / 8);
+      const int gm = m0 + half * 128 + r, gn = n0 + ch * 8;
+      if (gm < mend && gn < N)
+        *reinterpret_cast<uint4*>(C + (long)gm * N + gn) = *reinterpret_cast<const uint4*>(smem + r * RS + ch * 16);
+    }
+    __syncthreads();
   }
 }
 
