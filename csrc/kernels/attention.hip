@@ -71,6 +71,8 @@ struct AttnParams {
   unsigned seed_lo, seed_hi, drop_thr;
   float drop_scale;  // 1 / (1 - p)
   const int64_t* seed_ptr;  // device seed (graph-safe: a fresh mask per HIP-graph replay) or null
+  // profiling only (SPA_ATTN_STAMP): per-wave s_memtime segment sums of the dK/dV loop, or null
+  long long* stamp;
 };
 
 // ---- dropout counter hash (bit-identical in ops/attention.py dropout_keep_mask) ------
@@ -503,7 +505,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   TileLoader<HDV, BMQ, NT> ld_;
   lq_.init(p.sqt, tid);
   ld_.init(p.sdot, tid);
-  float rl = 0.f, rd = 0.f;  // per-thread row constants for the prefetched tile (tid < BMQ)
+  // per-thread row constants of the prefetched tile (tid < BMQ): raw loads, transformed only at
+  // commit time so the loads stay in flight (an immediate use would wait vmcnt(0) on the whole
+  // Q / dO tile prefetch issued just before)
+  float rl = 0.f, rd = 0.f;
+  bool rv = false;
   auto fetch = [&](int it) {
     const int hg = it / nper, tq = t0 + it % nper;
     const int h = h0 + hg;
@@ -513,14 +519,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     if (tid < BMQ) {
       const int qq = qq0 + tid;
       const long rbase = ((long)b * p.H + h) * p.Tq;
-      rl = qq < p.Tq ? -p.lse_in[rbase + qq] * 1.4426950408889634f : -INFINITY;
-      rd = qq < p.Tq ? -p.delta[rbase + qq] : 0.f;
+      rv = qq < p.Tq;
+      const long r = rbase + min(qq, p.Tq - 1);
+      rl = p.lse_in[r];
+      rd = p.delta[r];
     }
   };
   auto commit_tile = [&](int buf) {
     lq_.store(smem + buf * TB);
     ld_.store(smem + buf * TB + TQ);
-    if (tid < BMQ) { rowc[buf][tid] = rl; rowc[buf][BMQ + tid] = rd; }
+    if (tid < BMQ) {
+      rowc[buf][tid] = rv ? -rl * 1.4426950408889634f : -INFINITY;
+      rowc[buf][BMQ + tid] = rv ? -rd : 0.f;
+    }
   };
   if (total > 0) {
     fetch(0);
@@ -735,7 +746,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
   TileLoader<HDV, BMQ, NT> ld_;
   lq_.init(p.sqt, tid);
   ld_.init(p.sdot, tid);
-  float rl = 0.f, rd = 0.f;
+  float rl = 0.f, rd = 0.f;   // raw row constants, transformed at commit (see the kernel above)
+  bool rv = false;
   auto fetch = [&](int it) {
     const int h = h0 + it / nper;
     const int qq0 = (t0 + it % nper) * BMQ;
@@ -744,14 +756,19 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
     if (tid < BMQ) {
       const int qq = qq0 + tid;
       const long rbase = ((long)b * p.H + h) * p.Tq;
-      rl = qq < p.Tq ? -p.lse_in[rbase + qq] * 1.4426950408889634f : -INFINITY;
-      rd = qq < p.Tq ? -p.delta[rbase + qq] : 0.f;
+      rv = qq < p.Tq;
+      const long r = rbase + min(qq, p.Tq - 1);
+      rl = p.lse_in[r];
+      rd = p.delta[r];
     }
   };
   auto commit_tile = [&](int buf) {
     lq_.store(smem + buf * TB);
     ld_.store(smem + buf * TB + TQ);
-    if (tid < BMQ) { rowc[buf][tid] = rl; rowc[buf][BMQ + tid] = rd; }
+    if (tid < BMQ) {
+      rowc[buf][tid] = rv ? -rl * 1.4426950408889634f : -INFINITY;
+      rowc[buf][BMQ + tid] = rv ? -rd : 0.f;
+    }
   };
   if (total > 0) {
     fetch(0);
@@ -764,16 +781,21 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
   offk.init(lane);
   offv.init(lane);
   float* pme = pimg + pair * (MT * 4 * 64 * 4) + lane * 4;  // + (t*4 + j) * 256
+  long long seg[5] = {0, 0, 0, 0, 0};
+  const bool stamp = p.stamp != nullptr;
+  auto tick = [&]() -> long long { return stamp ? (long long)__builtin_amdgcn_s_memtime() : 0LL; };
   auto body = [&](const int it, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     const int qq0 = (t0 + it % nper) * BMQ;
     const bf16* Qs = smem + BUF * TB;
     const bf16* Ds = Qs + TQ;
     const float* rc = rowc[BUF];
+    long long ts = tick();
     if (it + 1 < total) {
       commit_tile(1 - BUF);
       if (it + 2 < total) fetch(it + 2);
     }
+    if (stamp) { const long long tn = tick(); seg[0] += tn - ts; ts = tn; }
     const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
     unsigned dbase = 0;
     if constexpr (DROP) dbase = drop_base(p, b, h0 + it / nper);
@@ -837,7 +859,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
         }
       }
     }
+    if (stamp) { const long long tn = tick(); seg[1] += tn - ts; ts = tn; }
     __syncthreads();  // P images complete
+    if (stamp) { const long long tn = tick(); seg[2] += tn - ts; ts = tn; }
     // ---- phase 2
     if (active) {
       if (role == 0) {
@@ -867,11 +891,18 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
         }
       }
     }
+    if (stamp) { const long long tn = tick(); seg[3] += tn - ts; ts = tn; }
     __syncthreads();
+    if (stamp) { const long long tn = tick(); seg[4] += tn - ts; }
   };
   for (int it = 0; it < total; it += 2) {
     body(it, IC<0>{});
     if (it + 1 < total) body(it + 1, IC<1>{});
+  }
+  if (stamp && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) p.stamp[((long)blockIdx.x * 8 + wave) * 8 + i] = seg[i];
+    p.stamp[((long)blockIdx.x * 8 + wave) * 8 + 5] = total;
   }
   if constexpr (HDK == HDV) {
     store_kv_grad<HDK>(p, acc, role == 1, b, hk, key, split, hh);
@@ -888,6 +919,198 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
       store_kv_grad<HDV>(p, av, false, b, hk, key, split, hh);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Backward dK/dV, paired waves, software-pipelined (HD <= 128, no dropout). Same pairing as
+// dkdv2 (role A holds K and dV^T, role B holds V and dK^T of the pair's 32 keys), but role A
+// produces P one interval ahead of its consumers, so every interval has ONE block barrier and
+// the same MFMA count per role:
+//   interval k, role A:  dV^T += dO(k-1)^T P(k-1)          |  S(k) = Q(k) K^T -> P(k) -> LDS
+//   interval k, role B:  dP(k-1) = dO(k-1) V^T - delta;  dS = P(k-1) dP(k-1);  dK^T += Q(k-1)^T dS
+// (dkdv2 runs both roles in two phases with a barrier each; s_memtime stamps showed each role
+// idle about a third of the time at those barriers: profiles/r2_attn_dkdv_stamps.txt). Nothing
+// but the accumulators is carried across intervals: P travels through a 2-deep bf16 LDS ring
+// in MFMA-operand order (role A re-reads its own P for dV). Q / dO tiles live in a 3-deep LDS
+// ring (tiles k-1 and k are read while k+1 is committed); lse / delta travel with their tile.
+// ---------------------------------------------------------------------------
+template <int HD, bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
+  constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 512, IW = img_w<HD>();
+  constexpr int TQ = BMQ * IW, TB = 2 * TQ, PSLOT = 4 * MT * 2 * 64 * 8;
+  __shared__ __attribute__((aligned(16))) bf16 smem[3 * TB];     // [ring][Q | dO]
+  __shared__ __attribute__((aligned(16))) bf16 pimg[2 * PSLOT];  // [slot][pair][t][half][lane][8]
+  __shared__ __attribute__((aligned(16))) float rowc[3][2 * BMQ]; // [ring][-lse2 | -delta]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pair = wave & 3, role = wave >> 2;
+  const int hh = lane >> 5;
+  const int nbh = p.Hkv * p.B;
+  const int bh = blockIdx.x % nbh;
+  const int rest = blockIdx.x / nbh;
+  const int split = rest % p.hsplit, kb = rest / p.hsplit;
+  const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  const int Gs = p.H / p.Hkv / p.hsplit;
+  const int h0 = hk * (p.H / p.Hkv) + split * Gs;
+  const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + pair * 32);
+  const int key = kw0 + (lane & 31);
+  const bool kvalid = key < p.Tk;
+  const float c = p.scale_log2;
+
+  bf16x8 xf[KS];  // A: K fragments, B: V fragments of this lane's key
+  {
+    const bf16* xp = role == 0 ? p.k + b * p.skb + (long)key * p.skt + hk * p.skh + 8 * hh
+                               : p.v + b * p.svb + (long)key * p.svt + hk * p.svh + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) xf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
+  }
+  f32x16 acc[DT];  // A: dV^T, B: dK^T
+#pragma unroll
+  for (int i = 0; i < DT; ++i) acc[i] = splat16(0.f);
+
+  int qstart = 0, wave_qstart = 0;
+  if (CAUSAL) {
+    qstart = max(0, kb * BNK - p.causal_off);
+    wave_qstart = max(0, kw0 - p.causal_off);
+  }
+  const int t0 = qstart / BMQ;
+  const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
+  const int nper = ntq - t0 > 0 ? ntq - t0 : 0;
+  const int total = nper * Gs;
+  TileLoader<HD, BMQ, NT> lq_;
+  TileLoader<HD, BMQ, NT> ld_;
+  lq_.init(p.sqt, tid);
+  ld_.init(p.sdot, tid);
+  float rl = 0.f, rd = 0.f;   // raw row constants of the prefetched tile (transformed at commit)
+  bool rv = false;
+  auto fetch = [&](int it) {
+    const int h = h0 + it / nper;
+    const int qq0 = (t0 + it % nper) * BMQ;
+    lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq);
+    ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq);
+    if (tid < BMQ) {
+      const int qq = qq0 + tid;
+      const long r = ((long)b * p.H + h) * p.Tq + min(qq, p.Tq - 1);
+      rv = qq < p.Tq;
+      rl = p.lse_in[r];
+      rd = p.delta[r];
+    }
+  };
+  auto commit_tile = [&](int slot) {
+    lq_.store(smem + slot * TB);
+    ld_.store(smem + slot * TB + TQ);
+    if (tid < BMQ) {
+      rowc[slot][tid] = rv ? -rl * 1.4426950408889634f : -INFINITY;
+      rowc[slot][BMQ + tid] = rv ? -rd : 0.f;
+    }
+  };
+  auto tile_active = [&](int it) {
+    const int qq0 = (t0 + it % nper) * BMQ;
+    return kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
+  };
+  if (total > 0) {
+    fetch(0);
+    commit_tile(0);
+    if (total > 1) fetch(1);
+  }
+  __syncthreads();
+  LdsOff<IW> off;
+  off.init(lane);
+  bf16* pme = pimg + pair * (MT * 2 * 64 * 8) + lane * 8;   // + slot * PSLOT + (t * 2 + half) * 512
+  bool prev_act = false;
+  // interval k (slot SC = k % 3): tiles k-1 (slot (SC+2)%3) and k (slot SC) resident; commits k+1
+  auto interval = [&](const int k, auto slotc) {
+    constexpr int SC = decltype(slotc)::value, SP = (SC + 2) % 3;
+    if (k + 1 < total) {
+      commit_tile((SC + 1) % 3);
+      if (k + 2 < total) fetch(k + 2);
+    }
+    const bool cur = k < total && tile_active(k);
+    const bf16* Qc = smem + SC * TB;
+    const bf16* Qp = smem + SP * TB;
+    const bf16* Dp = Qp + TQ;
+    const bf16* pr = pme + ((k + 1) & 1) * PSLOT;        // P(k-1)
+    if (role == 0) {
+      if (prev_act) {                                    // dV^T += dO(k-1)^T P(k-1)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 0) * 512);
+          const bf16x8 pb = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 1) * 512);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            acc[dt] = mfma32(ld_tr(Dp + 32 * t * IW, off.tra[dt], off.trb[dt]), pa, acc[dt]);
+            acc[dt] = mfma32(ld_tr(Dp + (32 * t + 16) * IW, off.tra[dt], off.trb[dt]), pb, acc[dt]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (cur) {                                         // S(k) -> P(k) -> LDS slot k & 1
+        const int qq0 = (t0 + k % nper) * BMQ;
+        const float* rc = rowc[SC];
+        bf16* pw = pme + (k & 1) * PSLOT;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          f32x16 s = mfma32(ld_row(Qc + 32 * t * IW, off.row[0]), xf[0], splat16(0.f));
+#pragma unroll
+          for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Qc + 32 * t * IW, off.row[ks]), xf[ks], s);
+          const int qt0 = qq0 + 32 * t;
+          if (CAUSAL && qt0 + p.causal_off < kw0 + 31) {
+            const int d = key - qt0 - 4 * hh - p.causal_off;   // row offsets below d are masked
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if ((r & 3) + 8 * (r >> 2) < d) s[r] = -INFINITY;
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 32 * t + 8 * g + 4 * hh);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s[4 * g + i] = fexp2(fmaf(s[4 * g + i], c, lv[i]));
+          }
+          *reinterpret_cast<bf16x8*>(pw + (t * 2 + 0) * 512) = pack_acc(s, 0);
+          *reinterpret_cast<bf16x8*>(pw + (t * 2 + 1) * 512) = pack_acc(s, 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else if (prev_act) {                               // tile k-1: dP, dS, dK^T
+      const bf16* Dpr = Dp;
+      const float* rc = rowc[SP];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        f32x16 dp;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dp[4 * g + i] = dv[i];
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) dp = mfma32(ld_row(Dpr + 32 * t * IW, off.row[ks]), xf[ks], dp);
+        const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 0) * 512);
+        const bf16x8 pb = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 1) * 512);
+        f32x16 ds;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          ds[r] = (float)pa[r] * dp[r];
+          ds[8 + r] = (float)pb[r] * dp[8 + r];
+        }
+        const bf16x8 sa = pack_acc(ds, 0), sb = pack_acc(ds, 1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          acc[dt] = mfma32(ld_tr(Qp + 32 * t * IW, off.tra[dt], off.trb[dt]), sa, acc[dt]);
+          acc[dt] = mfma32(ld_tr(Qp + (32 * t + 16) * IW, off.tra[dt], off.trb[dt]), sb, acc[dt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    prev_act = cur;
+    __syncthreads();
+  };
+  for (int k = 0; k <= total; k += 3) {
+    interval(k, IC<0>{});
+    if (k + 1 <= total) interval(k + 1, IC<1>{});
+    if (k + 2 <= total) interval(k + 2, IC<2>{});
+  }
+  store_kv_grad<HD>(p, acc, role == 1, b, hk, key, split, hh);
 }
 
 // sum the q-head-split fp32 partials of ONE tensor (dK with HD = HDK, or dV with HD = HDV)
@@ -1075,7 +1298,13 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
   else attn_bwd_dq_kernel<HDK, HDV, NW, false, DROP><<<grid, NW * 64, 0, st>>>(p);
   if (p.Tk == 0) return;
   const bool paired = PAIRED_OK && (dkdv_mode == 2 || (dkdv_mode == 0 && HDV == 128));
-  if (paired) {
+  const bool piped = PAIRED_OK && dkdv_mode == 3;
+  if (piped) {
+    if constexpr (PAIRED_OK) {
+      if (causal) attn_bwd_dkdv3_kernel<HDK, true><<<g2, 512, 0, st>>>(p);
+      else attn_bwd_dkdv3_kernel<HDK, false><<<g2, 512, 0, st>>>(p);
+    }
+  } else if (paired) {
     if constexpr (PAIRED_OK) {
       if (causal) attn_bwd_dkdv2_kernel<HDK, HDV, true, DROP><<<g2, 512, 0, st>>>(p);
       else attn_bwd_dkdv2_kernel<HDK, HDV, false, DROP><<<g2, 512, 0, st>>>(p);
@@ -1090,6 +1319,14 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
     attn_kv_reduce_kernel<HDV><<<(int)std::min<long>((rows * (HDV / 8) + 255) / 256, 65536), 256, 0, st>>>(p, 0);
   }
 }
+
+static at::Tensor& last_stamps() {
+  static at::Tensor t;
+  return t;
+}
+// profiling: the segment sums of the last SPA_ATTN_STAMP backward ([blocks * 8 waves, 8] int64:
+// staging, phase-1 issue, barrier-1 wait, phase-2 issue, barrier-2 wait, iterations)
+at::Tensor attn_bwd_stamps() { return last_stamps().defined() ? last_stamps().view({-1, 8}).clone() : at::Tensor(); }
 
 // Gradients written into dq/dk/dv (strided views allowed, e.g. slices of one dqkv buffer).
 void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
@@ -1154,6 +1391,17 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
       hsplit = d;
     }
   p.hsplit = hsplit;
+  // SPA_ATTN_STAMP=1: per-wave s_memtime segment sums of the paired dK/dV loop, kept in a
+  // process-global buffer the profiling tool reads back (attn_bwd_stamps)
+  static at::Tensor stamps;
+  const char* se = getenv("SPA_ATTN_STAMP");
+  if (se && atoi(se) != 0) {
+    const long need = (long)nkv * hsplit * 8 * 8;
+    if (!stamps.defined() || stamps.numel() < need || stamps.device() != q.device())
+      stamps = at::zeros({need}, q.options().dtype(at::kLong));
+    p.stamp = (long long*)stamps.data_ptr<int64_t>();
+    last_stamps() = stamps.narrow(0, 0, need);
+  }
   at::Tensor kvacc;
   if (hsplit > 1) {
     kvacc = at::empty({(long)hsplit * B * Tk * Hkv * (HDK + HDV)}, q.options().dtype(at::kFloat));
@@ -1177,6 +1425,7 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
         "Tensor? seed_t=None) -> Tensor[]");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
         "Tensor(c!) dv, float scale, bool causal, float dropout_p=0.0, int seed=0, Tensor? seed_t=None) -> ()");
+  m.def("attn_bwd_stamps() -> Tensor", &spa::attn_bwd_stamps);   // no tensor args: catch-all impl
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("attn_fwd", &spa::attn_fwd);

@@ -271,7 +271,8 @@ def test_packed_attention_matches_split():
     assert rel(qkv.grad, q2.grad.reshape(B, T, -1)) < 1e-3
 
 
-@pytest.mark.parametrize("env", [{"SPA_ATTN_BWD_FUSED": "1"}, {"SPA_ATTN_DKDV": "1"}, {"SPA_ATTN_DKDV": "2"}])
+@pytest.mark.parametrize("env", [{"SPA_ATTN_BWD_FUSED": "1"}, {"SPA_ATTN_DKDV": "1"}, {"SPA_ATTN_DKDV": "2"},
+                                 {"SPA_ATTN_DKDV": "3"}])
 def test_attention_bwd_variants_match_default(env):
     """The optional backward variants -- fused (dQ via fp32 atomics inside the dK/dV kernel)
     and the paired-wave dK/dV kernel -- against the default kernels, each run in a subprocess

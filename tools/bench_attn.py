@@ -67,3 +67,14 @@ for setting in filter(None, a.ab.split(",")):
     print(f"   with {key}={val}: fwd {tf2*1e3:.3f} ms ({fl/tf2/1e12:.0f} TF, out rel diff {err:.1e}) vs default "
           f"{tf3*1e3:.3f} ms ({fl/tf3/1e12:.0f} TF) | bwd {tb2*1e3:.3f} ms ({flb/tb2/1e12:.0f} TF) vs "
           f"{tb3*1e3:.3f} ms", flush=True)
+
+if os.environ.get("SPA_ATTN_STAMP"):
+    st = ops.attn_bwd_stamps().double()
+    live = st[st[:, 5] > 0]
+    seg = live[:, :5].sum(0) / live[:, 5].sum()
+    names = ["staging", "phase-1 issue", "barrier-1 wait", "phase-2 issue", "barrier-2 wait"]
+    for role, sel in (("A (S/P, dV)", (torch.arange(live.shape[0]) % 8) < 4), ("B (dP, dK)", (torch.arange(live.shape[0]) % 8) >= 4)):
+        r = live[sel]
+        per = r[:, :5].sum(0) / r[:, 5].sum()
+        print(f"   dK/dV loop, role {role}: cycles per iteration " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist()))
+              + f" | total {per.sum().item():.0f}", flush=True)
