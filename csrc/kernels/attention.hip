@@ -1297,8 +1297,8 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
   if (causal) attn_bwd_dq_kernel<HDK, HDV, NW, true, DROP><<<grid, NW * 64, 0, st>>>(p);
   else attn_bwd_dq_kernel<HDK, HDV, NW, false, DROP><<<grid, NW * 64, 0, st>>>(p);
   if (p.Tk == 0) return;
-  const bool paired = PAIRED_OK && (dkdv_mode == 2 || (dkdv_mode == 0 && HDV == 128));
-  const bool piped = PAIRED_OK && dkdv_mode == 3;
+  const bool paired = PAIRED_OK && dkdv_mode == 2;
+  const bool piped = PAIRED_OK && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
   if (piped) {
     if constexpr (PAIRED_OK) {
       if (causal) attn_bwd_dkdv3_kernel<HDK, true><<<g2, 512, 0, st>>>(p);
@@ -1376,10 +1376,13 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   }
   // dK/dV grid: key blocks x kv-heads x batch, times a q-head split when that grid cannot
   // fill the chip (MQA: Hkv = 1 launched 32 blocks at T = 4096); partials are summed by
-  // attn_kv_reduce_kernel. dK/dV kernel: paired-wave (2) for v head dim 128, single-wave (1)
-  // else; SPA_ATTN_DKDV overrides (read per call, so one process can A/B them). Measured in
-  // one process on MI355X: LLaMA3-8B shape bwd 2.22 ms paired vs 2.45 ms single-wave; ViT-B
-  // hd 64 (T 197, B 64) 0.121 ms paired vs 0.097 ms single-wave.
+  // attn_kv_reduce_kernel. dK/dV kernel: software-pipelined paired-wave (3) for v head dim
+  // 128, single-wave (1) else; the two-phase paired kernel (2) stays selectable.
+  // SPA_ATTN_DKDV overrides (read per call, so one process can A/B them). Measured on
+  // MI355X (rocprofv3, LLaMA3-8B shape B1 T8192 H32/8 hd128 causal): dK/dV kernel 1.31 ms
+  // pipelined vs 1.46 ms two-phase (whole bwd 2.22 ms two-phase vs 2.45 ms single-wave);
+  // ViT-B hd 64 (T 197, B 64) whole bwd 0.113 pipelined / 0.121 two-phase / 0.097-0.103
+  // single-wave.
   const int dkdv_mode = getenv("SPA_ATTN_DKDV") ? atoi(getenv("SPA_ATTN_DKDV")) : 0;
   const int G = H / Hkv;
   const int nkv = cdiv(Tk, 128) * Hkv * B;
