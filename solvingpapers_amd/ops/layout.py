@@ -7,10 +7,16 @@ import torch
 
 from . import _ext
 
-# dW = dY^T X through K-contiguous transposed operands + the NT GEMM (see layout.hip);
-# SPA_WGRAD_NT=0 restores the direct TN product
+# dW = dY^T X: hipBLASLt's direct TN form is slow on gfx950 for wide operands, so for those one
+# operand is first transposed to token-contiguous rows (layout.hip). Measured with
+# tools/bench_wgrad_layouts.py (profiles/r2_wgrad_layouts_vit_llama.txt): at LLaMA3-8B shapes
+# (T 8192) transposing only the narrower operand wins (w13 1.450 ms vs 1.517 both-transposed /
+# 1.638 direct, w2 0.807 vs 0.811 / 0.899); at ViT-B/16 shapes
+# (T 50432, 768-3072 wide) the transposes cost more than they save (fc1 0.392 direct vs 0.514
+# both). SPA_WGRAD_NT=0 forces the direct product everywhere.
 WGRAD_NT = os.environ.get("SPA_WGRAD_NT", "1") != "0"
 WGRAD_NT_MIN_TOKENS = 2048
+WGRAD_NT_MIN_WIDTH = 2048
 
 
 def transpose2d(x: torch.Tensor) -> torch.Tensor:
@@ -29,10 +35,23 @@ def wgrad_nt_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0)
 
 
-def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False):
-    """dW = dy2^T @ x2 ([N, K] from [T, N] and [T, K]); NT formulation for large T."""
-    if wgrad_nt_ok(dy2, x2):
-        a, b = transpose2d(dy2), transpose2d(x2).t()
+def wgrad_operand(dy2: torch.Tensor, x2: torch.Tensor):
+    """x2 transposed to token-contiguous rows when wgrad(dy2, x2) would transpose it, else None
+    (lets a caller issuing several dW products against one x2 transpose it once)."""
+    if wgrad_nt_ok(dy2, x2) and min(dy2.shape[1], x2.shape[1]) >= WGRAD_NT_MIN_WIDTH and x2.shape[1] <= dy2.shape[1]:
+        return transpose2d(x2)
+    return None
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False, x2t=None):
+    """dW = dy2^T @ x2 ([N, K] from [T, N] and [T, K]); the narrower operand is transposed to
+    token-contiguous rows first when both are wide and T is large (x2t: x2 already transposed)."""
+    N, K = dy2.shape[1], x2.shape[1]
+    if wgrad_nt_ok(dy2, x2) and min(N, K) >= WGRAD_NT_MIN_WIDTH:
+        if K <= N:
+            a, b = dy2.t(), (x2t if x2t is not None else transpose2d(x2)).t()
+        else:
+            a, b = transpose2d(dy2), x2
     else:
         a, b = dy2.t(), x2
     if out is None:

@@ -14,7 +14,7 @@ import torch.distributed as dist
 
 from . import _ext
 from . import reference
-from .layout import wgrad
+from .layout import wgrad, wgrad_operand
 from ..utils.grad import commit, commit_tensor
 
 
@@ -200,6 +200,7 @@ class _ChunkedLinearXent(torch.autograd.Function):
         acc_dt = lse.dtype
         dh = torch.zeros(h2.shape, device=h2.device, dtype=acc_dt) if need_h else None
         gb = torch.zeros(Vl, device=h2.device, dtype=acc_dt) if need_b else None
+        gw = h2t = None
         for v0 in range(0, Vl, Vc):
             v1 = min(Vl, v0 + Vc)
             wc = w[v0:v1]
@@ -208,25 +209,24 @@ class _ChunkedLinearXent(torch.autograd.Function):
             if need_h:
                 _addmm_f32_(dh, G, wc)
             if need_w:
-                def _w(out, acc, G=G, v0=v0, v1=v1):
-                    if out is None:
-                        return wgrad(G, h2)
-                    o = out[v0:v1]
-                    if o.dtype != G.dtype:
-                        gg = wgrad(G, h2)
-                        o.add_(gg) if acc else o.copy_(gg)
-                    else:
-                        wgrad(G, h2, o, acc)
-                    return None
-                if v0 == 0:
-                    gw_parts = []
-                r = _commit_rows(w, _w, v0 == 0)
-                if r is not None:
-                    gw_parts.append(r)
+                if h2t is None:
+                    h2t = wgrad_operand(G, h2)      # h2 transposed once for every chunk (or None)
+                if getattr(w, "main_grad", None) is None:
+                    if gw is None:                  # written chunk by chunk, no per-chunk parts + cat
+                        gw = torch.empty(w.shape, device=w.device, dtype=G.dtype)
+                    wgrad(G, h2, gw[v0:v1], x2t=h2t)
+                else:
+                    def _w(out, acc, G=G, v0=v0, v1=v1):
+                        o = out[v0:v1]
+                        if o.dtype != G.dtype:
+                            gg = wgrad(G, h2, x2t=h2t)
+                            o.add_(gg) if acc else o.copy_(gg)
+                        else:
+                            wgrad(G, h2, o, acc, x2t=h2t)
+                    _commit_rows(w, _w, v0 == 0)
             if need_b:
                 gb[v0:v1] = G.to(acc_dt).sum(0)
             del lc, G
-        gw = torch.cat(gw_parts, 0) if (need_w and gw_parts) else None
         if need_h:
             if group is not None and dist.get_world_size(group) > 1:
                 dist.all_reduce(dh, group=group)      # h is replicated over TP: sum the vocab partials
@@ -256,14 +256,12 @@ def _addmm_f32_(acc32, a, b):
     acc32.add_(torch.mm(a, b))
 
 
-def _commit_rows(w, compute, first_chunk):
+def _commit_rows(w, compute, first_chunk):  # w has main_grad
     """commit() for a row slice of w's gradient: the generation bookkeeping happens on the first
     chunk only, so every chunk of one backward overwrites (or, when this backward accumulates,
     adds to) its own rows."""
     from ..utils.grad import _Gen
-    mg = getattr(w, "main_grad", None)
-    if mg is None:
-        return compute(None, False)
+    mg = w.main_grad
     if first_chunk:
         w._spa_chunk_acc = getattr(w, "_spa_gen", -1) == _Gen.value
         w._spa_gen = _Gen.value

@@ -315,13 +315,17 @@ def test_attention_bwd_variants_match_default(env):
             assert (x.float() - y.float()).norm() / x.float().norm() < 2e-2
 
 
-@pytest.mark.parametrize("R,C,dt", [(8192, 4096, torch.bfloat16), (200, 136, torch.bfloat16), (64, 4100, torch.float32)])
+@pytest.mark.parametrize("R,C,dt", [(8192, 4096, torch.bfloat16), (200, 136, torch.bfloat16), (64, 4100, torch.float32),
+                                    (50432, 768, torch.bfloat16), (8, 8, torch.bfloat16), (136, 200, torch.float32)])
 def test_transpose2d(R, C, dt):
     from solvingpapers_amd.ops.layout import transpose2d
     x = torch.randn(R, C, device="cuda", dtype=dt)
     assert torch.equal(transpose2d(x), x.t().contiguous())
     xs = torch.randn(R, C + 16, device="cuda", dtype=dt)[:, 8:C + 8]
     assert torch.equal(transpose2d(xs), xs.t().contiguous())
+    xb = torch.randn(3, R, C, device="cuda", dtype=dt) if R * C <= 1 << 22 else None
+    if xb is not None:
+        assert torch.equal(transpose2d(xb), xb.transpose(1, 2).contiguous())
 
 
 def test_wgrad_nt_matches_tn():

@@ -42,8 +42,8 @@ def test_chunked_head_matches_fp32_oracle(V, chunk, sm, bias):
 
 
 def test_chunked_head_peak_memory_below_materialised():
-    """8192 x 128256 x 4096 bf16 (the LLaMA3-8B head): the chunked head (512 MiB chunks) must hold
-    at least 2 GB less than the materialised one (which keeps the 2.1 GB logits until backward)."""
+    """8192 x 128256 x 4096 bf16 (the LLaMA3-8B head): beyond the gradients themselves the chunked
+    head (512 MiB chunks) holds about one chunk, the materialised one the whole 2.1 GB of logits."""
     N, D, V = 8192, 4096, 128256
     g = torch.Generator(device="cuda").manual_seed(1)
     h = (torch.randn(N, D, device="cuda", generator=g) * 0.5).bfloat16().requires_grad_()
@@ -64,4 +64,8 @@ def test_chunked_head_peak_memory_below_materialised():
         peaks[name] = torch.cuda.max_memory_allocated() - base
         losses[name] = loss.item()
     assert abs(losses["chunked"] - losses["materialised"]) < 1e-3 * losses["materialised"]
-    assert peaks["materialised"] - peaks["chunked"] >= 2e9, peaks
+    grads = (N * D + V * D) * 2
+    chunk = 1 << 29
+    assert peaks["chunked"] - grads <= 2 * chunk, peaks
+    assert peaks["materialised"] - grads >= N * V * 2, peaks
+    assert peaks["materialised"] - peaks["chunked"] >= 1.2e9, peaks

@@ -6,7 +6,7 @@
   direct dW = dY^T @ X      no transpose (hipBLASLt's slow form on gfx950)
 
 Prints GEMM time, transpose time (csrc/kernels/layout.hip) and the sum per form.
-    python tools/bench_wgrad_layouts.py [--tune OUT.csv]
+    python tools/bench_wgrad_layouts.py [--tune OUT.csv] [--vit]
 --tune lets TunableOp search hipBLASLt + rocBLAS for every form's shape first (results to OUT.csv).
 """
 import os
@@ -21,6 +21,9 @@ from solvingpapers_amd.utils.tuning import load_gemm_tuning  # noqa: E402
 
 T = 8192
 shapes = {"wqkv": (6144, 4096), "wo": (4096, 4096), "w13": (28672, 4096), "w2": (4096, 14336)}
+if "--vit" in sys.argv:   # ViT-B/16 at batch 256: 256 x 197 tokens
+    T = 256 * 197
+    shapes = {"qkv": (2304, 768), "proj": (768, 768), "fc1": (3072, 768), "fc2": (768, 3072)}
 
 
 def tm(fn, it=20):
@@ -34,7 +37,7 @@ def tm(fn, it=20):
 
 
 def main():
-    tune = sys.argv[2] if len(sys.argv) > 2 and sys.argv[1] == "--tune" else None
+    tune = sys.argv[sys.argv.index("--tune") + 1] if "--tune" in sys.argv else None
     print("table loaded:", load_gemm_tuning(), flush=True)
     if tune:
         import torch.cuda.tunable as tunable
@@ -53,6 +56,7 @@ def main():
             "x": (lambda: torch.mm(dy.t(), xT.t(), out=out), lambda: transpose2d(x)),
             "direct": (lambda: torch.mm(dy.t(), x, out=out), None),
         }
+
         ref = torch.mm(dy.t(), x)
         for f, (g, tr) in forms.items():
             if tune:
