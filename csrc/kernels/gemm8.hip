@@ -39,6 +39,11 @@
 #include "spa_common.h"
 #include "gemm_common.h"
 
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
 namespace spa {
 
 namespace g8 {
@@ -115,7 +120,9 @@ __device__ __forceinline__ bf16x8 rd_ks(const char* half, int col0, int s, int l
 // 8192^3 (tools/bench_moe.py, profiles/r2_gemm8_ablation.txt): ILV 764 TF vs 1113 TF for the
 // shipped schedule -- a DMA piece's issue stalls the issuing wave's own MFMA stream. 1-3 give wrong
 // results by construction and are never selected by the op unless SPA_GG8_ABLATE is set.
-template <int MODE, int ABL = 0, bool ILV = false>
+// PART (mode 2 only): the "experts" are token slices of one dense dW product (split-K) and each
+// writes its fp32 partial [M, N] at C + e * strideC floats, summed by wgrad_reduce_kernel.
+template <int MODE, int ABL = 0, bool ILV = false, bool PART = false>
 __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                                bf16* __restrict__ C, const int* __restrict__ offsets,
                                                                int E, int M, int N, int K, long lda, long ldb, long ldc,
@@ -364,6 +371,23 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   }
   }
   if (ktiles > 0 && !late) __builtin_amdgcn_s_barrier();   // equal barrier counts on exit
+  if constexpr (PART) {
+    // fp32 partials straight from the fragments: 16 rows x 64 contiguous bytes per store
+    float* Cf = reinterpret_cast<float*>(C) + (long)e * strideC;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const long gm = m0 + mh * 128 + wm * 64 + 16 * i + (lane & 15);
+            const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
+            if (gm < M && gn < N) *reinterpret_cast<f32x4*>(Cf + gm * ldc + gn) = acc[mh * 4 + i][nh * 2 + j];
+          }
+    return;
+  }
   // ---- epilogue through LDS, one 128-row half at a time: C^T fragments (n = 4 (l >> 4) + q,
   // m = l & 15) -> padded row image (528-B rows: the 16 rows of a fragment store land on 16
   // distinct bank pairs) -> whole-row 16-byte global stores (a per-lane 8-byte store at a row
@@ -405,6 +429,97 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     }
     __syncthreads();
   }
+}
+
+// out[i] (+)= sum_s part[s, i] over n elements (n % 4 == 0), bf16 or fp32 out
+template <typename OT>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, OT* __restrict__ out, long n,
+                                                           int S, int accumulate) {
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (long)gridDim.x * 1024) {
+    f32x4 a = *reinterpret_cast<const f32x4*>(part + i);
+    for (int s = 1; s < S; ++s) a += *reinterpret_cast<const f32x4*>(part + (long)s * n + i);
+    if constexpr (sizeof(OT) == 4) {
+      if (accumulate) a += *reinterpret_cast<const f32x4*>(out + i);
+      *reinterpret_cast<f32x4*>(out + i) = a;
+    } else {
+      bf16x4 o;
+      if (accumulate) {
+        const bf16x4 old = *reinterpret_cast<const bf16x4*>(out + i);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] += (float)old[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (bf16)a[q];
+      *reinterpret_cast<bf16x4*>(out + i) = o;
+    }
+  }
+}
+
+// Dense weight gradient out[N, K] (+)= dy[T, N]^T x[T, K] on the 8-phase kernel's token-major
+// (mode 2) path, split over tokens into S slices so that S x tiles fills the chip; fp32
+// partials, deterministic reduce. For the T >> N, K products (ViT-B/16: T = 50432, N, K
+// 768..3072) where hipBLASLt's direct TN form runs 230-600 TF
+// (profiles/r2_wgrad_layouts_vit_llama.txt). out: bf16 or fp32 (a main_grad), contiguous.
+at::Tensor wgrad8(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out_, bool accumulate,
+                  int64_t splits) {
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "wgrad8: bf16 operands");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad8: dy [T, N], x [T, K]");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad8: unit column stride");
+  const long T = dy.size(0);
+  const int N = dy.size(1), K = x.size(1);
+  const long lda = dy.stride(0), ldb = x.stride(0);
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "wgrad8: dims and row strides % 8");
+  TORCH_CHECK((uintptr_t)dy.data_ptr() % 16 == 0 && (uintptr_t)x.data_ptr() % 16 == 0, "wgrad8: 16-B aligned");
+  TORCH_CHECK((T + 64) * (lda + 256) * 2 < (1L << 32) && (T + 64) * (ldb + 256) * 2 < (1L << 32),
+              "wgrad8: operands < 4 GiB");
+  DeviceGuard g(dy.device());
+  auto out = out_ ? *out_ : at::empty({N, K}, dy.options());
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)N * K &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "wgrad8: out [N, K] bf16/fp32 contiguous");
+  if (N == 0 || K == 0) return out;
+  auto st = stream();
+  const int tiles = cdiv(N, 256) * cdiv(K, 256);
+  int S = (int)splits;
+  if (S <= 0) S = std::max(1, 256 / tiles);              // one wave of blocks over 256 CUs
+  S = (int)std::max<long>(1, std::min<long>(S, T / 512));  // >= 8 k-iterations per slice
+  const long chunk = ((T + S - 1) / S + 63) / 64 * 64;
+  S = (int)((T + chunk - 1) / chunk);
+  if (S == 0) {
+    if (!accumulate) out.zero_();
+    return out;
+  }
+  // slice offsets live on the device, one tensor per (device, T, S): the upload (a synchronising
+  // pageable copy) happens on first use only, never per backward
+  static std::map<std::tuple<int, long, int>, at::Tensor> offs_cache;
+  static std::mutex offs_mu;
+  at::Tensor offsets;
+  {
+    std::lock_guard<std::mutex> lk(offs_mu);
+    auto key = std::make_tuple((int)dy.get_device(), T, S);
+    auto it = offs_cache.find(key);
+    if (it == offs_cache.end()) {
+      std::vector<int> off(S + 1);
+      for (int i = 0; i <= S; ++i) off[i] = (int)std::min<long>(T, (long)i * chunk);
+      it = offs_cache.emplace(key, at::from_blob(off.data(), {S + 1}, at::kInt).to(dy.device())).first;
+    }
+    offsets = it->second;
+  }
+  auto part = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
+  grouped_gemm8_kernel<2, 0, false, true><<<S * tiles, 512, 0, st>>>(
+      (const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(), reinterpret_cast<bf16*>(part.data_ptr<float>()),
+      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T);
+  SPA_LAUNCH_CHECK();
+  const long n = (long)N * K;
+  const int rb = (int)std::min<long>((n / 4 + 255) / 256, 4096);
+  if (out.scalar_type() == at::kFloat)
+    wgrad_reduce_kernel<float><<<rb, 256, 0, st>>>(part.data_ptr<float>(), out.data_ptr<float>(), n, S,
+                                                   accumulate ? 1 : 0);
+  else
+    wgrad_reduce_kernel<bf16><<<rb, 256, 0, st>>>(part.data_ptr<float>(), (bf16*)out.data_ptr(), n, S,
+                                                  accumulate ? 1 : 0);
+  SPA_LAUNCH_CHECK();
+  return out;
 }
 
 static int ablation() {
@@ -478,5 +593,9 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("grouped_gemm8(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
+  m.def("wgrad8(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate, int splits) -> Tensor");
 }
-TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("grouped_gemm8", &spa::grouped_gemm8); }
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("grouped_gemm8", &spa::grouped_gemm8);
+  m.impl("wgrad8", &spa::wgrad8);
+}

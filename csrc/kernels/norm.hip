@@ -220,6 +220,49 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
     part2[(size_t)blockIdx.y * D + c] = s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x];
 }
 
+// Bias gradient: fp32 column sums of a bf16 [R, N] matrix (row stride ld). Block (bx, by) sums
+// rows [by*rpb, (by+1)*rpb) of 256 columns: 32 lanes x 8 columns cover one 512-byte row segment,
+// 8 row groups stride the rows with 4 16-byte loads in flight each; the 8 group partials meet in
+// LDS and one fp32 row of part[by, :] is written (summed by colsum_kernel: deterministic).
+__global__ __launch_bounds__(256) void rowsum_part_kernel(const bf16* __restrict__ x, float* __restrict__ part,
+                                                          long R, int N, long ld, long rpb) {
+  __shared__ __attribute__((aligned(16))) float red[8][256];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c0 = blockIdx.x * 256 + cl * 8;
+  const long r0 = (long)blockIdx.y * rpb, r1 = min(R, r0 + rpb);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto add = [&](const uint4& v) {
+    const unsigned* u = reinterpret_cast<const unsigned*>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[2 * k] += __uint_as_float(u[k] << 16);
+      acc[2 * k + 1] += __uint_as_float(u[k] & 0xffff0000u);
+    }
+  };
+  if (c0 < N) {
+    const bf16* p = x + c0;
+    long r = r0 + rg;
+    for (; r + 24 < r1; r += 32) {
+      const uint4 a = *reinterpret_cast<const uint4*>(p + r * ld);
+      const uint4 b = *reinterpret_cast<const uint4*>(p + (r + 8) * ld);
+      const uint4 c = *reinterpret_cast<const uint4*>(p + (r + 16) * ld);
+      const uint4 d = *reinterpret_cast<const uint4*>(p + (r + 24) * ld);
+      add(a); add(b); add(c); add(d);
+    }
+    for (; r < r1; r += 8) add(*reinterpret_cast<const uint4*>(p + r * ld));
+  }
+  *reinterpret_cast<float4*>(&red[rg][cl * 8]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(&red[rg][cl * 8 + 4]) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][threadIdx.x];
+    part[(long)blockIdx.y * N + c] = t;
+  }
+}
+
 #define NORM_FWD_DISPATCH(NT, MAXV)                                                              \
   do {                                                                                           \
     dim3 grid(cdiv(M, 256 / NT));                                                                \
@@ -358,14 +401,53 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& h, cons
   return {dx, dw, db};
 }
 
+// x [R, N] bf16 (unit column stride, N and the row stride % 8) -> fp32 [N] column sums
+at::Tensor rowsum_bf16(const at::Tensor& x) {
+  SPA_CHECK_CUDA(x);
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kBFloat16 && x.stride(1) == 1, "rowsum_bf16: [R, N] bf16");
+  const long R = x.size(0);
+  const int N = x.size(1);
+  const long ld = x.stride(0);
+  TORCH_CHECK(N % 8 == 0 && ld % 8 == 0 && (uintptr_t)x.data_ptr() % 16 == 0, "rowsum_bf16: 16-byte rows");
+  DeviceGuard g(x.device());
+  auto opts = x.options().dtype(at::kFloat);
+  auto out = at::empty({N}, opts);
+  if (N == 0) return out;
+  if (R == 0) return out.zero_();
+  auto st = stream();
+  // enough row blocks for >= 1024 blocks, each at least 64 rows
+  const int nx = cdiv(N, 256);
+  const long want = std::max<long>(1, std::min<long>(cdiv(1024, nx), cdiv(R, 64)));
+  const long rpb = (R + want - 1) / want;
+  const int P = (int)cdiv(R, rpb);
+  auto part = at::empty({P, N}, opts);
+  rowsum_part_kernel<<<dim3(nx, P), 256, 0, st>>>((const bf16*)x.data_ptr(), part.data_ptr<float>(), R, N, ld, rpb);
+  const float* src = part.data_ptr<float>();
+  int PP = P;
+  at::Tensor p2;
+  if (PP > 64) {
+    const int Y = std::min(64, cdiv(PP, 16));
+    const int chunk = cdiv(PP, Y);
+    p2 = at::empty({Y, N}, opts);
+    colsum_partial_kernel<<<dim3(cdiv(N, 64), Y), 256, 0, st>>>(src, p2.data_ptr<float>(), PP, N, chunk);
+    src = p2.data_ptr<float>();
+    PP = Y;
+  }
+  colsum_kernel<float><<<cdiv(N, 64), 256, 0, st>>>(src, out.data_ptr<float>(), PP, N);
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("rowsum_bf16(Tensor x) -> Tensor");
   m.def("norm_fwd(Tensor x, Tensor? residual, Tensor w, Tensor? b, float eps) -> Tensor[]");
   m.def("norm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? mean, Tensor? dres, Tensor(a!)? dw_out, "
         "Tensor(b!)? db_out) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("rowsum_bf16", &spa::rowsum_bf16);
   m.impl("norm_fwd", &spa::norm_fwd);
   m.impl("norm_bwd", &spa::norm_bwd);
 }

@@ -17,6 +17,11 @@ from . import _ext
 WGRAD_NT = os.environ.get("SPA_WGRAD_NT", "1") != "0"
 WGRAD_NT_MIN_TOKENS = 2048
 WGRAD_NT_MIN_WIDTH = 2048
+# the narrow-operand / many-token products go to wgrad8 (csrc/kernels/gemm8.hip): token-major
+# operands read as they are, split over tokens to fill the chip, fp32 partials; SPA_WGRAD8=0
+# keeps them on hipBLASLt's direct form
+WGRAD8 = os.environ.get("SPA_WGRAD8", "1") != "0"
+WGRAD8_MIN_TOKENS = 4096
 
 
 def transpose2d(x: torch.Tensor) -> torch.Tensor:
@@ -43,9 +48,27 @@ def wgrad_operand(dy2: torch.Tensor, x2: torch.Tensor):
     return None
 
 
+def wgrad8_ok(dy2: torch.Tensor, x2: torch.Tensor, out=None) -> bool:
+    return (WGRAD8 and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            and dy2.dim() == 2 and x2.dim() == 2 and dy2.shape[0] >= WGRAD8_MIN_TOKENS
+            and min(dy2.shape[1], x2.shape[1]) < WGRAD_NT_MIN_WIDTH
+            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1
+            and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
+            and (out is None or (out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32))))
+
+
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False, x2t=None):
-    """dW = dy2^T @ x2 ([N, K] from [T, N] and [T, K]); the narrower operand is transposed to
-    token-contiguous rows first when both are wide and T is large (x2t: x2 already transposed)."""
+    """dW = dy2^T @ x2 ([N, K] from [T, N] and [T, K]) into a fresh tensor, or written into /
+    added to ``out`` (any float dtype, e.g. an fp32 main_grad). Many tokens with a narrow
+    operand: wgrad8; else the narrower operand is transposed to token-contiguous rows first
+    when both are wide and T is large (x2t: x2 already transposed)."""
+    if wgrad8_ok(dy2, x2, out):
+        return _ext.ops().wgrad8(dy2, x2, out, accumulate, 0)
+    if out is not None and out.dtype != dy2.dtype:
+        g = wgrad(dy2, x2, x2t=x2t)
+        out.add_(g) if accumulate else out.copy_(g)
+        return out
     N, K = dy2.shape[1], x2.shape[1]
     if wgrad_nt_ok(dy2, x2) and min(N, K) >= WGRAD_NT_MIN_WIDTH:
         if K <= N:
@@ -61,3 +84,12 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False, x2t=N
     else:
         torch.mm(a, b, out=out)
     return out
+
+
+def bias_grad(dy2: torch.Tensor) -> torch.Tensor:
+    """fp32 column sums of [T, N] (the bias gradient): csrc/kernels/norm.hip rowsum_bf16 for bf16
+    on the GPU (two-level deterministic sum filling the chip), else torch."""
+    if (dy2.is_cuda and dy2.dtype == torch.bfloat16 and dy2.dim() == 2 and dy2.stride(1) == 1
+            and dy2.shape[1] % 8 == 0 and dy2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0):
+        return _ext.ops().rowsum_bf16(dy2)
+    return dy2.sum(0, dtype=torch.float32)

@@ -13,7 +13,7 @@ import torch
 
 from ..utils.grad import commit
 from . import _ext
-from .layout import wgrad
+from .layout import bias_grad, wgrad
 
 # decode-time products with <= 4 token rows go to the GEMV kernel; SPA_GEMV=0 -> torch.mm
 GEMV = os.environ.get("SPA_GEMV", "1") != "0"
@@ -44,18 +44,11 @@ class _LinearFn(torch.autograd.Function):
         gw = gb = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):
-                if out is not None and out.dtype != dy2.dtype:
-                    g = wgrad(dy2, x2)
-                    if acc:
-                        out.add_(g)
-                    else:
-                        out.copy_(g)
-                    return None
                 return wgrad(dy2, x2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
             def _b(out, acc):
-                s = dy2.sum(0, dtype=torch.float32)
+                s = bias_grad(dy2)
                 if out is None:
                     return s.to(b.dtype)
                 if acc:
@@ -115,18 +108,11 @@ class _LinearFP8Fn(torch.autograd.Function):
         gw = gb = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):
-                if out is not None and out.dtype != dy2.dtype:
-                    g = wgrad(dy2, x2)
-                    if acc:
-                        out.add_(g)
-                    else:
-                        out.copy_(g)
-                    return None
                 return wgrad(dy2, x2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
             def _b(out, acc):
-                s = dy2.sum(0, dtype=torch.float32)
+                s = bias_grad(dy2)
                 if out is None:
                     return s.to(b.dtype)
                 if acc:

@@ -14,7 +14,7 @@ import torch.distributed as dist
 
 from . import _ext
 from . import reference
-from .layout import wgrad, wgrad_operand
+from .layout import bias_grad, wgrad, wgrad_operand
 from ..utils.grad import commit, commit_tensor
 
 
@@ -86,17 +86,10 @@ class _LinearXentFn(torch.autograd.Function):
         gw = gb = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):
-                if out is not None and out.dtype != G.dtype:
-                    g = wgrad(G, h2)
-                    if acc:
-                        out.add_(g)
-                    else:
-                        out.copy_(g)
-                    return None
                 return wgrad(G, h2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
-            gb = commit_tensor(b, G.float().sum(0).to(b.dtype))
+            gb = commit_tensor(b, bias_grad(G).to(b.dtype))
         return dh, gw, gb, None, None, None
 
 
@@ -217,12 +210,7 @@ class _ChunkedLinearXent(torch.autograd.Function):
                     wgrad(G, h2, gw[v0:v1], x2t=h2t)
                 else:
                     def _w(out, acc, G=G, v0=v0, v1=v1):
-                        o = out[v0:v1]
-                        if o.dtype != G.dtype:
-                            gg = wgrad(G, h2, x2t=h2t)
-                            o.add_(gg) if acc else o.copy_(gg)
-                        else:
-                            wgrad(G, h2, o, acc, x2t=h2t)
+                        wgrad(G, h2, out[v0:v1], acc, x2t=h2t)
                     _commit_rows(w, _w, v0 == 0)
             if need_b:
                 gb[v0:v1] = G.to(acc_dt).sum(0)

@@ -328,6 +328,41 @@ def test_transpose2d(R, C, dt):
         assert torch.equal(transpose2d(xb), xb.transpose(1, 2).contiguous())
 
 
+@pytest.mark.parametrize("R,N", [(50432, 768), (100, 24), (7, 3072), (0, 16), (8192, 2304), (300, 264)])
+def test_bias_grad_rowsum(R, N):
+    from solvingpapers_amd.ops import _ext
+    from solvingpapers_amd.ops.layout import bias_grad
+    x = torch.randn(R, N + 8, device="cuda", dtype=torch.bfloat16)
+    for t in (x[:, :N].contiguous(), x[:, 8:]):     # contiguous and a row-strided view
+        ref = t.float().sum(0)
+        out = _ext.ops().rowsum_bf16(t)
+        assert out.dtype == torch.float32 and out.shape == (N,)
+        assert torch.allclose(out, ref, rtol=1e-4, atol=1e-3)
+        assert torch.equal(bias_grad(t), out)
+
+
+@pytest.mark.parametrize("T,N,K", [(50432, 768, 3072), (50432, 2304, 768), (5000, 24, 40), (4096, 264, 520), (700, 64, 64)])
+def test_wgrad8_dense_dw(T, N, K):
+    from solvingpapers_amd.ops import _ext
+    ops = _ext.ops()
+    dyb = torch.randn(T, N + 8, device="cuda", dtype=torch.bfloat16)
+    xb = torch.randn(T, K + 16, device="cuda", dtype=torch.bfloat16)
+    for dy, x in ((dyb[:, :N].contiguous(), xb[:, :K].contiguous()), (dyb[:, 8:], xb[:, 16:])):
+        ref = dy.float().t() @ x.float()
+        tol = 2e-3 * ref.norm()
+        out = ops.wgrad8(dy, x, None, False, 0)
+        assert out.dtype == torch.bfloat16 and out.shape == (N, K)
+        assert (out.float() - ref).norm() < tol
+        acc = out.clone()
+        ops.wgrad8(dy, x, acc, True, 0)
+        assert (acc.float() - 2 * ref).norm() < 2 * tol
+        f32 = torch.full((N, K), 1.0, device="cuda")
+        ops.wgrad8(dy, x, f32, True, 3)
+        assert (f32 - 1.0 - ref).norm() < 1e-4 * ref.norm()
+        ops.wgrad8(dy, x, f32, False, 1)
+        assert (f32 - ref).norm() < 1e-4 * ref.norm()
+
+
 def test_wgrad_nt_matches_tn():
     from solvingpapers_amd.ops.layout import wgrad
     dy = torch.randn(4096, 1024, device="cuda", dtype=torch.bfloat16)

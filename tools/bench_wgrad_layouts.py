@@ -4,6 +4,7 @@
   dy     dW = dYt @ X       only dY transposed (the dgrad-like NN form)
   x      dW = dY^T @ Xt^T   only X transposed
   direct dW = dY^T @ X      no transpose (hipBLASLt's slow form on gfx950)
+  wgrad8 dW = dY^T @ X      csrc/kernels/gemm8.hip token-major path, split over tokens, fp32 partials
 
 Prints GEMM time, transpose time (csrc/kernels/layout.hip) and the sum per form.
     python tools/bench_wgrad_layouts.py [--tune OUT.csv] [--vit]
@@ -16,6 +17,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
+from solvingpapers_amd.ops import _ext  # noqa: E402
 from solvingpapers_amd.ops.layout import transpose2d  # noqa: E402
 from solvingpapers_amd.utils.tuning import load_gemm_tuning  # noqa: E402
 
@@ -55,6 +57,7 @@ def main():
             "dy": (lambda: torch.mm(dyT, x, out=out), lambda: transpose2d(dy)),
             "x": (lambda: torch.mm(dy.t(), xT.t(), out=out), lambda: transpose2d(x)),
             "direct": (lambda: torch.mm(dy.t(), x, out=out), None),
+            "wgrad8": (lambda: _ext.ops().wgrad8(dy, x, out, False, 0), None),
         }
 
         ref = torch.mm(dy.t(), x)
