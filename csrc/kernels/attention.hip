@@ -134,7 +134,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
 
   int kend = p.Tk;
   if (CAUSAL) kend = min(p.Tk, qb * BM + BM + p.causal_off);
-  const int wave_kend = CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
+  // a wave past the last query row (T = 197: rows 224..255 of a 256-row block) skips all MFMA
+  // work but keeps staging tiles and meeting the block's barriers
+  const int wave_kend = q0 >= p.Tq ? 0 : CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
   const int ntiles = kend > 0 ? cdiv(kend, BN) : 0;
 
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
@@ -310,7 +312,9 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 
   int kend = p.Tk;
   if (CAUSAL) kend = min(p.Tk, qb * BM + BM + p.causal_off);
-  const int wave_kend = CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
+  // a wave past the last query row (T = 197: rows 224..255 of a 256-row block) skips all MFMA
+  // work but keeps staging tiles and meeting the block's barriers
+  const int wave_kend = q0 >= p.Tq ? 0 : CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
   const int ntiles = kend > 0 ? cdiv(kend, BN) : 0;
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
   const bf16* vbase = p.v + b * p.svb + hk * p.svh;
