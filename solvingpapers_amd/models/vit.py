@@ -99,9 +99,20 @@ class TransformerEncoder(tnn.Module):
                                   snn.Linear(c.mlp_hidden, c.embedding_dim, **fk))
 
     def forward(self, x):
-        a = self.multihead_attention(self.layer_norm1(x))
-        n2, h = self.layer_norm2(a, residual=x)      # h = x + attn, n2 = LN2(h) (one fused pass)
-        return h + self.mlp(n2)
+        h, m = self.forward_pair(x, None)
+        return h + m
+
+    def forward_pair(self, h, m):
+        """Block on the unsummed residual pair (input x = h + m; m None: x = h) -> (h', m') with
+        output h' + m'. The sum happens inside the next LayerNorm (one fused pass that also
+        returns x), so the chain has no standalone residual add in either direction."""
+        if m is None:
+            x, n1 = h, self.layer_norm1(h)
+        else:
+            n1, x = self.layer_norm1(m, residual=h)
+        a = self.multihead_attention(n1)
+        n2, h2 = self.layer_norm2(a, residual=x)     # h2 = x + attn, n2 = LN2(h2)
+        return h2, self.mlp(n2)
 
 
 class MLPHead(tnn.Module):
@@ -133,11 +144,12 @@ class ViT(tnn.Module):
     def forward(self, x, targets=None):
         x = self.patch_embedding(x)
         x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1), x], dim=1) + self.pos_embedding
+        h, m = x, None
         for i, blk in enumerate(self.transformer_blocks):
-            x = mark_ready(x, self.grad_ready_cb, i + 1)
-            x = blk(x)
-        x = mark_ready(x, self.grad_ready_cb, len(self.transformer_blocks) + 1)
-        logits = self.mlp_head(x[:, 0])
+            h = mark_ready(h, self.grad_ready_cb, i + 1)
+            h, m = blk.forward_pair(h, m)
+        h = mark_ready(h, self.grad_ready_cb, len(self.transformer_blocks) + 1)
+        logits = self.mlp_head(h[:, 0] + m[:, 0] if m is not None else h[:, 0])
         if targets is None:
             return logits
         return cross_entropy(logits, targets)
