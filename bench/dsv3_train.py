@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--fp8", action="store_true",
                     help="DeepSeek-V3 fp8 recipe: routed experts + dense projections in block-scaled e4m3")
     ap.add_argument("--fp8-experts-only", action="store_true", help="with --fp8: dense projections stay bf16")
+    ap.add_argument("--bf16-moments", action="store_true",
+                    help="AdamW moments in bf16 (DeepSeek-V3 sec. 3.3.2; fp32 master weights kept)")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
@@ -49,7 +51,8 @@ def main():
     m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep)
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16, align=64 * world)
     dp = DataParallel(m, flat) if world > 1 else None
-    opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, ep_group=ep)
+    opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, ep_group=ep,
+                    moment_dtype=torch.bfloat16 if a.bf16_moments else torch.float32)
     for l in m.moe_layers():
         l.balance_group = None
     gen = torch.Generator(device=dev).manual_seed(7 + info.rank)
@@ -75,7 +78,7 @@ def main():
     report("training tokens/sec, DeepSeek-V3-style MLA+MoE " + ("fp8 (e4m3 block-scaled GEMMs)" if a.fp8 else "bf16"),
            tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
-            + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum,
+            + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum, "adam_moments": "bf16" if a.bf16_moments else "fp32",
             "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu", "params": m.num_params(),
             "active_params": m.num_params(active=True)},
            tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4))

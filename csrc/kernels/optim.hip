@@ -13,14 +13,16 @@
 // coefficient so clipping never syncs the host.
 //
 // Math matches torch.optim.AdamW: p *= 1 - lr*wd; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).
+// Moments fp32, or bf16 (MT): the DeepSeek-V3 recipe (arXiv 2412.19437 sec. 3.3.2: AdamW moments
+// tracked in BF16, master weights fp32) -- 20 instead of 28 bytes of HBM traffic per parameter.
 #include "spa_common.h"
 
 namespace spa {
 
-template <typename PT, typename GT, bool MASTER>
+template <typename PT, typename GT, bool MASTER, typename MT = float>
 __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* __restrict__ master,
-                                                    const GT* __restrict__ g, float* __restrict__ m,
-                                                    float* __restrict__ v, long n, float lr, float b1, float b2,
+                                                    const GT* __restrict__ g, MT* __restrict__ m,
+                                                    MT* __restrict__ v, long n, float lr, float b1, float b2,
                                                     float eps, float wd, float inv_bc1, float inv_sqrt_bc2,
                                                     const float* __restrict__ coef_ptr, int adam_l2,
                                                     const float* __restrict__ hyper) {
@@ -51,8 +53,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* _
         const long j = base + k;
         pv[k] = j < n ? (MASTER ? master[j] : (float)p[j]) : 0.f;
         gv[k] = j < n ? (float)g[j] : 0.f;
-        mv[k] = j < n ? m[j] : 0.f;
-        vv[k] = j < n ? v[j] : 0.f;
+        mv[k] = j < n ? (float)m[j] : 0.f;
+        vv[k] = j < n ? (float)v[j] : 0.f;
       }
     }
 #pragma unroll
@@ -78,8 +80,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* _
         if (j < n) {
           if constexpr (MASTER) master[j] = pv[k];
           p[j] = (PT)pv[k];
-          m[j] = mv[k];
-          v[j] = vv[k];
+          m[j] = (MT)mv[k];
+          v[j] = (MT)vv[k];
         }
       }
     }
@@ -141,7 +143,8 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   for (auto* t : {&p, &g, &m, &v}) TORCH_CHECK(t->is_contiguous(), "adamw: flat contiguous buffers required");
   const long n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n);
-  TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat);
+  const bool mb = m.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(m.scalar_type() == v.scalar_type() && (mb || m.scalar_type() == at::kFloat), "adamw: fp32 or bf16 moments");
   if (master) TORCH_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous());
   if (coef) TORCH_CHECK(coef->scalar_type() == at::kFloat && coef->numel() == 1);
   if (n == 0) return;
@@ -152,17 +155,25 @@ void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const 
   const float* cp = coef ? coef->data_ptr<float>() : nullptr;
   if (hyper) TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->numel() >= 2 && hyper->is_cuda());
   const float* hp = hyper ? hyper->data_ptr<float>() : nullptr;
-#define AL(PT, GT, MS)                                                                                           \
-  adamw_kernel<PT, GT, MS><<<opt_grid(n), 256, 0, st>>>(                                                         \
-      (PT*)p.data_ptr(), MS ? master->data_ptr<float>() : nullptr, (const GT*)g.data_ptr(), m.data_ptr<float>(), \
-      v.data_ptr<float>(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cp,  \
+#define ALM(PT, GT, MS, MT)                                                                                      \
+  adamw_kernel<PT, GT, MS, MT><<<opt_grid(n), 256, 0, st>>>(                                                     \
+      (PT*)p.data_ptr(), MS ? master->data_ptr<float>() : nullptr, (const GT*)g.data_ptr(), (MT*)m.data_ptr(),   \
+      (MT*)v.data_ptr(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cp,    \
       adam_l2 ? 1 : 0, hp)
+#define AL(PT, GT, MS) ALM(PT, GT, MS, float)
   const bool pb = p.scalar_type() == at::kBFloat16, gb = g.scalar_type() == at::kBFloat16;
-  if (pb && gb) { TORCH_CHECK(master.has_value(), "bf16 params need an fp32 master"); AL(bf16, bf16, true); }
+  if (mb) {
+    TORCH_CHECK(master.has_value(), "adamw: bf16 moments need an fp32 master");
+    if (pb && gb) ALM(bf16, bf16, true, bf16);
+    else if (pb) ALM(bf16, float, true, bf16);
+    else if (gb) ALM(float, bf16, true, bf16);
+    else ALM(float, float, true, bf16);
+  } else if (pb && gb) { TORCH_CHECK(master.has_value(), "bf16 params need an fp32 master"); AL(bf16, bf16, true); }
   else if (pb && !gb) { TORCH_CHECK(master.has_value(), "bf16 params need an fp32 master"); AL(bf16, float, true); }
   else if (!pb && gb) { if (master) AL(float, bf16, true); else AL(float, bf16, false); }
   else { if (master) AL(float, float, true); else AL(float, float, false); }
 #undef AL
+#undef ALM
   SPA_LAUNCH_CHECK();
 }
 

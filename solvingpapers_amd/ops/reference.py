@@ -147,14 +147,16 @@ def adamw_(p, master, g, m, v, lr, b1, b2, eps, wd, step, coef=None, adam_l2=Fal
     gf = g.float() * (coef.float() if coef is not None else 1.0)
     if adam_l2:
         gf = gf + wd * pf
-    m.mul_(b1).add_(gf, alpha=1 - b1)
-    v.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+    mf = m.float().mul_(b1).add_(gf, alpha=1 - b1)      # bf16 moments: update in fp32, store rounded
+    vf = v.float().mul_(b2).addcmul_(gf, gf, value=1 - b2)
+    m.copy_(mf)
+    v.copy_(vf)
     bc1 = 1 - b1 ** step
     bc2 = 1 - b2 ** step
-    denom = v.sqrt() / math.sqrt(bc2) + eps
+    denom = vf.sqrt() / math.sqrt(bc2) + eps
     if not adam_l2:
         pf = pf * (1 - lr * wd)
-    pf = pf - (lr / bc1) * m / denom
+    pf = pf - (lr / bc1) * mf / denom
     if master is not None:
         master.copy_(pf)
     p.copy_(pf.to(p.dtype))

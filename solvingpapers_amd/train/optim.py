@@ -214,13 +214,18 @@ def _subtract(ranges, holes):
 
 class FlatAdamW(FlatOptimizer):
     def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=None,
-                 adam_l2=False, shard=None, ep_group=None, tp_group=None, graph_safe=False):
+                 adam_l2=False, shard=None, ep_group=None, tp_group=None, graph_safe=False,
+                 moment_dtype=torch.float32):
+        """moment_dtype bf16: the DeepSeek-V3 recipe (moments in BF16, fp32 master weights;
+        arXiv 2412.19437 sec. 3.3.2) -- needs an fp32 master (low-precision params)."""
         super().__init__(flat, lr, weight_decay, max_grad_norm, shard, ep_group, tp_group, graph_safe)
         self.b1, self.b2 = betas
         self.eps = eps
         self.adam_l2 = adam_l2
-        self.m = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device)
-        self.v = torch.zeros(self.state_numel, dtype=torch.float32, device=flat.device)
+        if moment_dtype != torch.float32 and self.master is None:
+            moment_dtype = torch.float32      # fp32 params: keep the moments at their precision
+        self.m = torch.zeros(self.state_numel, dtype=moment_dtype, device=flat.device)
+        self.v = torch.zeros(self.state_numel, dtype=moment_dtype, device=flat.device)
 
     @torch.no_grad()
     def step(self, lr: Optional[float] = None, overlap: bool = False):

@@ -165,6 +165,30 @@ def test_adamw_matches_torch():
     assert abs(K.sqsum(grads[0]).item() - grads[0].pow(2).sum().item()) < 1e-2 * grads[0].pow(2).sum().item()
 
 
+def test_adamw_bf16_moments_match_cpu_oracle():
+    """bf16 moments (DeepSeek-V3 recipe) with an fp32 master: the HIP kernel against the CPU
+    oracle doing the same rounding, and close to the fp32-moment trajectory."""
+    from solvingpapers_amd.ops import optim_kernels as K
+    n = 10007
+    torch.manual_seed(0)
+    p0 = torch.randn(n)
+    grads = [torch.randn(n) for _ in range(4)]
+    res = {}
+    for dev in ("cpu", DEV):
+        pb, master = p0.bfloat16().to(dev), p0.clone().to(dev)
+        m = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        v = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        for s, g in enumerate(grads, 1):
+            K.adamw_(pb, master, g.bfloat16().to(dev), m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, s)
+        res[dev] = (master.cpu(), m.float().cpu(), v.float().cpu())
+    for a, b in zip(res["cpu"], res[DEV]):
+        assert rel(b, a) < 2e-3        # fp32 math in a different order, then one bf16 rounding
+    pf, mf32, vf32 = p0.clone(), torch.zeros(n), torch.zeros(n)
+    for s, g in enumerate(grads, 1):
+        K.adamw_(pf, None, g.bfloat16().float(), mf32, vf32, 1e-2, 0.9, 0.95, 1e-8, 0.1, s)
+    assert rel(res[DEV][0], pf) < 1e-3
+
+
 ATTN_CASES = [
     # B, Tq, Tk, H, Hkv, hd, causal
     (2, 128, 128, 4, 4, 64, True),
