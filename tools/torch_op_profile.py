@@ -1,0 +1,45 @@
+"""Which framework ops launch the non-GEMM "glue" kernels (fills, copies, casts, cats) of a
+DeepSeek-V3-style training step: torch.profiler over one fwd+bwd+AdamW step, ops sorted by
+device time with their input shapes.
+    python tools/torch_op_profile.py [--fp8] [--rows 40]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from solvingpapers_amd.models import deepseekv3 as ds  # noqa: E402
+from solvingpapers_amd.train.optim import FlatAdamW  # noqa: E402
+from solvingpapers_amd.utils.flat import FlatParams  # noqa: E402
+
+
+def main():
+    fp8 = "--fp8" in sys.argv
+    rows = int(sys.argv[sys.argv.index("--rows") + 1]) if "--rows" in sys.argv else 40
+    c = ds.config("dsv3_v3", n_layers=4, n_experts=32, n_dense_layers=1, block_size=4096, moe_fp8=fp8,
+                  fp8_linears=fp8)
+    m = ds.DeepSeekV3(c, device="cuda", dtype=torch.bfloat16, seed=1)
+    flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
+    opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
+    for l in m.moe_layers():
+        l.balance_group = None
+    t = torch.randint(0, c.vocab_size, (1, 4097), device="cuda")
+
+    def step():
+        opt.zero_grad()
+        loss = m(t[:, :-1], t[:, 1:])
+        loss.backward()
+        opt.step()
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+    with torch.profiler.profile(activities=acts, record_shapes=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=rows,
+                                                             max_name_column_width=60, max_shapes_column_width=70))
+
+
+if __name__ == "__main__":
+    main()
