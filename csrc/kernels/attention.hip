@@ -1023,8 +1023,12 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   bf16* pme = pimg + pair * (MT * 2 * 64 * 8) + lane * 8;   // + slot * PSLOT + (t * 2 + half) * 512
   bool prev_act = false;
   // interval k (slot SC = k % 3): tiles k-1 (slot (SC+2)%3) and k (slot SC) resident; commits k+1
-  auto interval = [&](const int k, auto slotc) {
+  // ROLE is a compile-time constant and each role runs its own copy of the interval loop (same
+  // barrier count): with one loop branching on the role per interval, the accumulators of the
+  // two roles met in phi nodes and hipcc re-homed all 64 of them (32 v_mov_b64) every interval
+  auto interval = [&](const int k, auto slotc, auto rolec) {
     constexpr int SC = decltype(slotc)::value, SP = (SC + 2) % 3;
+    constexpr int ROLE = decltype(rolec)::value;
     if (k + 1 < total) {
       commit_tile((SC + 1) % 3);
       if (k + 2 < total) fetch(k + 2);
@@ -1034,7 +1038,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
     const bf16* Qp = smem + SP * TB;
     const bf16* Dp = Qp + TQ;
     const bf16* pr = pme + ((k + 1) & 1) * PSLOT;        // P(k-1)
-    if (role == 0) {
+    if constexpr (ROLE == 0) {
       if (prev_act) {                                    // dV^T += dO(k-1)^T P(k-1)
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -1075,7 +1079,13 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-    } else if (prev_act) {                               // tile k-1: dP, dS, dK^T
+    } else {
+      if (!prev_act) {
+        prev_act = cur;
+        __syncthreads();
+        return;
+      }
+      // tile k-1: dP, dS, dK^T
       const bf16* Dpr = Dp;
       const float* rc = rowc[SP];
 #pragma unroll
@@ -1109,10 +1119,18 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
     prev_act = cur;
     __syncthreads();
   };
-  for (int k = 0; k <= total; k += 3) {
-    interval(k, IC<0>{});
-    if (k + 1 <= total) interval(k + 1, IC<1>{});
-    if (k + 2 <= total) interval(k + 2, IC<2>{});
+  if (role == 0) {
+    for (int k = 0; k <= total; k += 3) {
+      interval(k, IC<0>{}, IC<0>{});
+      if (k + 1 <= total) interval(k + 1, IC<1>{}, IC<0>{});
+      if (k + 2 <= total) interval(k + 2, IC<2>{}, IC<0>{});
+    }
+  } else {
+    for (int k = 0; k <= total; k += 3) {
+      interval(k, IC<0>{}, IC<1>{});
+      if (k + 1 <= total) interval(k + 1, IC<1>{}, IC<1>{});
+      if (k + 2 <= total) interval(k + 2, IC<2>{}, IC<1>{});
+    }
   }
   store_kv_grad<HD>(p, acc, role == 1, b, hk, key, split, hh);
 }
