@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--fp8-experts-only", action="store_true", help="with --fp8: dense projections stay bf16")
     ap.add_argument("--bf16-moments", action="store_true",
                     help="AdamW moments in bf16 (DeepSeek-V3 sec. 3.3.2; fp32 master weights kept)")
+    ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
@@ -53,6 +54,9 @@ def main():
     dp = DataParallel(m, flat) if world > 1 else None
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, ep_group=ep,
                     moment_dtype=torch.bfloat16 if a.bf16_moments else torch.float32)
+    overlap = not a.no_opt_overlap and torch.cuda.is_available()
+    if overlap:   # AdamW per bucket on a side stream, each layer's forward waits for its bucket
+        m.param_wait_cb = flat.wait_bucket
     for l in m.moe_layers():
         l.balance_group = None
     gen = torch.Generator(device=dev).manual_seed(7 + info.rank)
@@ -69,7 +73,7 @@ def main():
                 loss.backward()
         if dp is not None:
             dp.finish_grad_sync()
-        opt.step()
+        opt.step(overlap=overlap)
         last[0] = loss * a.accum
 
     el = timed(step, a.steps, a.warmup)
