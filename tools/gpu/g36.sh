@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 400 python -u bench.py --steps 8 --warmup 2 > gpurun_out/g36.log 2>&1; echo brc=$?
+grep -v amdgpu.ids gpurun_out/g36.log | cut -c1-250
+timeout -k 10 300 python -u bench/vit_train.py --steps 8 --warmup 2 >> gpurun_out/g36.log 2>&1; echo vrc=$?
+tail -1 gpurun_out/g36.log | cut -c1-200
