@@ -73,7 +73,37 @@ at::Tensor transpose2d(const at::Tensor& x_) {
   return y;
 }
 
+// Collective-footprint proxy (tools/overlap_interference.py): nwg workgroups of 256 threads
+// stream src -> dst `reps` times with 16-byte accesses, the way an RCCL ring kernel keeps one
+// workgroup per channel busy moving bytes for the whole collective. Lets a 1-GPU box measure
+// what a concurrent all-reduce costs the backward's GEMMs (which CUs it takes, for how long)
+// without a second GPU.
+__global__ __launch_bounds__(256) void stream_copy_wg_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                             long n, int reps) {
+  for (int r = 0; r < reps; ++r)
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
+void stream_copy_wg(const at::Tensor& src, at::Tensor& dst, int64_t nwg, int64_t reps) {
+  SPA_CHECK_CUDA(src);
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && src.nbytes() == dst.nbytes() && src.nbytes() % 16 == 0,
+              "stream_copy_wg: contiguous, equal sizes, 16-byte multiple");
+  TORCH_CHECK(nwg > 0 && nwg <= 65536 && reps >= 0, "stream_copy_wg: nwg in [1, 65536], reps >= 0");
+  DeviceGuard g(src.device());
+  const long n = (long)(src.nbytes() / 16);
+  if (n == 0 || reps == 0) return;
+  stream_copy_wg_kernel<<<(int)nwg, 256, 0, stream()>>>((const uint4*)src.data_ptr(), (uint4*)dst.data_ptr(), n,
+                                                       (int)reps);
+  SPA_LAUNCH_CHECK();
+}
+
 }  // namespace spa
 
-TORCH_LIBRARY_FRAGMENT(spa, m) { m.def("transpose2d(Tensor x) -> Tensor"); }
-TORCH_LIBRARY_IMPL(spa, CUDA, m) { m.impl("transpose2d", &spa::transpose2d); }
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("transpose2d(Tensor x) -> Tensor");
+  m.def("stream_copy_wg(Tensor src, Tensor(a!) dst, int nwg, int reps) -> ()");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("transpose2d", &spa::transpose2d);
+  m.impl("stream_copy_wg", &spa::stream_copy_wg);
+}
