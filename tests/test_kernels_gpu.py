@@ -295,6 +295,37 @@ def test_packed_attention_matches_split():
     assert rel(qkv.grad, q2.grad.reshape(B, T, -1)) < 1e-3
 
 
+@pytest.mark.parametrize("B,Tq,Tk,H,causal", [(4, 197, 197, 12, False), (2, 256, 256, 4, True), (3, 33, 33, 2, True),
+                                              (2, 100, 100, 3, False), (1, 64, 200, 2, True), (2, 256, 131, 2, False)])
+def test_attention_short_bwd(B, Tq, Tk, H, causal, monkeypatch):
+    """Fused short-sequence backward (T <= 256, hd 64: one block per (b, h), whole sequence in
+    LDS) against the fp32 oracle and against the split dq + dK/dV kernels (SPA_ATTN_SHORT=0)."""
+    ops = _ext.ops()
+    torch.manual_seed(5)
+    hd = 64
+    q = torch.randn(B, Tq, H, hd, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Tk, H, hd, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Tk, H, hd, device=DEV, dtype=torch.bfloat16)
+    sc = 1 / math.sqrt(hd)
+    o, lse = ops.attn_fwd(q, k, v, sc, causal)
+    do = torch.randn_like(o)
+    grads = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SPA_ATTN_SHORT", mode)
+        g = (torch.full_like(q, float("nan")), torch.full_like(k, float("nan")), torch.full_like(v, float("nan")))
+        ops.attn_bwd(do, q, k, v, o, lse, *g, sc, causal)
+        grads[mode] = g
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention(qf, kf, vf, causal)
+    of.backward(do.float())
+    assert rel(o, of) < 2e-2, rel(o, of)
+    for a, ref in zip(grads["1"], (qf.grad, kf.grad, vf.grad)):
+        assert torch.isfinite(a).all()
+        assert rel(a, ref) < 3e-2, rel(a, ref)
+    for a, b in zip(grads["1"], grads["0"]):
+        assert rel(a, b) < 1e-2, rel(a, b)
+
+
 @pytest.mark.parametrize("env", [{"SPA_ATTN_BWD_FUSED": "1"}, {"SPA_ATTN_DKDV": "0"}, {"SPA_ATTN_DKDV": "2"},
                                  {"SPA_ATTN_DKDV": "3"}])
 def test_attention_bwd_variants_match_default(env):
