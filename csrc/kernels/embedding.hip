@@ -10,6 +10,9 @@
 // MI355X; the fp32 accumulator is then cast to the parameter dtype.
 #include "spa_common.h"
 
+#include <map>
+#include <tuple>
+
 namespace spa {
 
 template <typename T, bool POS>
@@ -38,7 +41,8 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const T* __restrict__ W, c
 
 template <typename T>
 __global__ __launch_bounds__(256) void emb_bwd_kernel(const T* __restrict__ dout, const int64_t* __restrict__ idx,
-                                                      float* __restrict__ dW, long N, int D, float scale) {
+                                                      float* __restrict__ dW, long N, int D, float scale,
+                                                      int* __restrict__ flag) {
   // one wave per (row n, 256-column chunk): lane l adds column chunk*256 + 4l .. +3
   const int lane = threadIdx.x & 63;
   const int nchunk = (D + 255) / 256;
@@ -48,11 +52,45 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const T* __restrict__ dout
     const int c = (w % nchunk) * 256 + lane * 4;
     if (c >= D) continue;
     const int64_t r = idx[n];
+    if (flag && c == 0) flag[r] = 1;  // row touched (every writer stores the same value)
     float* dst = dW + r * D + c;
     const T* src = dout + n * D + c;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (c + k < D) atomicAdd(dst + k, (float)src[k] * scale);
+  }
+}
+
+// Flush the touched rows of the persistent fp32 accumulator into the parameter-dtype gradient:
+// one block per token; the block that wins the row's flag (atomic exchange) adds the row into
+// `out` and re-zeroes it in `acc`, so repeated tokens flush once and the scratch is all zeros
+// again for the next call. Untouched rows are never read.
+template <typename T>
+__global__ __launch_bounds__(256) void emb_flush_kernel(float* __restrict__ acc, int* __restrict__ flag,
+                                                        const int64_t* __restrict__ idx, T* __restrict__ out,
+                                                        long N, int D) {
+  __shared__ int own;
+  for (long n = blockIdx.x; n < N; n += gridDim.x) {
+    const int64_t r = idx[n];
+    if (threadIdx.x == 0) own = atomicExch(flag + r, 0);
+    __syncthreads();
+    if (own) {
+      float* a = acc + r * D;
+      T* o = out + r * D;
+      for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+        float v[8], w[8];
+        load8(a + c, v);
+        load8(o + c, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          w[k] += v[k];
+          v[k] = 0.f;
+        }
+        store8(o + c, w);
+        store8(a + c, v);
+      }
+    }
+    __syncthreads();  // `own` is rewritten next iteration
   }
 }
 
@@ -112,10 +150,10 @@ at::Tensor emb_bwd(const at::Tensor& dout_, const at::Tensor& idx, int64_t V, do
     const int grid = (int)std::min<long>((nw + 3) / 4, 16384);
     if (dout.scalar_type() == at::kBFloat16)
       emb_bwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dout.data_ptr(), ix.data_ptr<int64_t>(),
-                                                 acc.data_ptr<float>(), N, D, (float)scale);
+                                                 acc.data_ptr<float>(), N, D, (float)scale, nullptr);
     else
       emb_bwd_kernel<float><<<grid, 256, 0, st>>>(dout.data_ptr<float>(), ix.data_ptr<int64_t>(),
-                                                  acc.data_ptr<float>(), N, D, (float)scale);
+                                                  acc.data_ptr<float>(), N, D, (float)scale, nullptr);
     SPA_LAUNCH_CHECK();
   }
   if (dtype_like.scalar_type() == at::kFloat) return acc;
@@ -127,13 +165,60 @@ at::Tensor emb_bwd(const at::Tensor& dout_, const at::Tensor& idx, int64_t V, do
   return outp;
 }
 
+// Table gradient written into / added to `out` ([V, D], the parameter's main_grad view) touching
+// only the rows of the batch's tokens: fp32 atomics into a persistent zero-initialised scratch
+// with per-row flags, then a flush of the flagged rows. With accumulate=false `out` is zeroed
+// first. Against emb_bwd + commit this drops the per-call [V, D] fp32 zero-fill, the dense cast
+// and the dense bf16 add (LLaMA3-8B: 2.1 GB fill + 3.1 GB cast + 3 GB add per micro-batch).
+void emb_bwd_into(const at::Tensor& dout_, const at::Tensor& idx, double scale, at::Tensor& out, bool accumulate) {
+  SPA_CHECK_CUDA(out); SPA_CHECK_CONTIG(out);
+  TORCH_CHECK(idx.scalar_type() == at::kLong && out.dim() == 2, "emb_bwd_into: int64 ids, [V, D] out");
+  auto dout = dout_.contiguous();
+  auto ix = idx.contiguous();
+  const long V = out.size(0);
+  const int D = out.size(1);
+  TORCH_CHECK(D % 8 == 0 && dout.numel() == ix.numel() * D && dout.scalar_type() == out.scalar_type(),
+              "emb_bwd_into: dout [N, D] in out's dtype, D % 8 == 0");
+  DeviceGuard g(out.device());
+  auto st = stream();
+  // scratch per (device, V, D): all zeros between calls
+  static std::map<std::tuple<int, long, int>, std::pair<at::Tensor, at::Tensor>> cache;
+  auto& sc = cache[std::make_tuple(out.get_device(), V, D)];
+  if (!sc.first.defined()) {
+    sc.first = at::zeros({V, D}, out.options().dtype(at::kFloat));
+    sc.second = at::zeros({V}, out.options().dtype(at::kInt));
+  }
+  if (!accumulate) out.zero_();
+  const long N = ix.numel();
+  if (N == 0) return;
+  const long nw = N * ((D + 255) / 256);
+  const int grid = (int)std::min<long>((nw + 3) / 4, 16384);
+  const int fgrid = (int)std::min<long>(N, 16384);
+  float* acc = sc.first.data_ptr<float>();
+  int* flag = sc.second.data_ptr<int>();
+  if (out.scalar_type() == at::kBFloat16) {
+    emb_bwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dout.data_ptr(), ix.data_ptr<int64_t>(), acc, N, D,
+                                               (float)scale, flag);
+    emb_flush_kernel<bf16><<<fgrid, 256, 0, st>>>(acc, flag, ix.data_ptr<int64_t>(), (bf16*)out.data_ptr(), N, D);
+  } else if (out.scalar_type() == at::kFloat) {
+    emb_bwd_kernel<float><<<grid, 256, 0, st>>>(dout.data_ptr<float>(), ix.data_ptr<int64_t>(), acc, N, D,
+                                                (float)scale, flag);
+    emb_flush_kernel<float><<<fgrid, 256, 0, st>>>(acc, flag, ix.data_ptr<int64_t>(), out.data_ptr<float>(), N, D);
+  } else {
+    TORCH_CHECK(false, "emb_bwd_into: bf16/fp32");
+  }
+  SPA_LAUNCH_CHECK();
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("emb_fwd(Tensor W, Tensor idx, Tensor? pos, float scale) -> Tensor");
   m.def("emb_bwd(Tensor dout, Tensor idx, int V, float scale, Tensor dtype_like) -> Tensor");
+  m.def("emb_bwd_into(Tensor dout, Tensor idx, float scale, Tensor(a!) out, bool accumulate) -> ()");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("emb_fwd", &spa::emb_fwd);
   m.impl("emb_bwd", &spa::emb_bwd);
+  m.impl("emb_bwd_into", &spa::emb_bwd_into);
 }

@@ -2,14 +2,16 @@
 
 Optional fused additive position table (GPT learned pos_embed, DeepSeek
 sinusoidal pe) and multiplicative scale (Gemma sqrt(D)). The table gradient is
-committed to ``W.main_grad`` when present.
+committed to ``W.main_grad`` when present: written in place by ``emb_bwd_into``, which
+touches only the rows of the batch's tokens (fp32 scratch + row flags, then a flush of the
+flagged rows) instead of materialising a dense [V, D] gradient per call.
 """
 from __future__ import annotations
 
 import torch
 
 from . import _ext, reference
-from ..utils.grad import commit_tensor
+from ..utils.grad import claim_main_grad, commit_tensor
 
 
 class _EmbFn(torch.autograd.Function):
@@ -25,8 +27,14 @@ class _EmbFn(torch.autograd.Function):
         W = ctx.W
         gw = gp = None
         if ctx.needs_input_grad[0]:
-            dW = _ext.ops().emb_bwd(g.contiguous(), idx, W.shape[0], ctx.scale, W)
-            gw = commit_tensor(W, dW)
+            claim = claim_main_grad(W)
+            if claim is not None and g.dtype == W.dtype:
+                # straight into the flat gradient buffer, touching only the batch's rows
+                mg, accumulate = claim
+                _ext.ops().emb_bwd_into(g.contiguous(), idx, ctx.scale, mg, accumulate)
+            else:
+                dW = _ext.ops().emb_bwd(g.contiguous(), idx, W.shape[0], ctx.scale, W)
+                gw = commit_tensor(W, dW)
         if ctx.pos is not None and ctx.needs_input_grad[2]:
             T = idx.shape[-1]
             D = W.shape[1]

@@ -52,6 +52,18 @@ def direct_out(p: torch.Tensor):
     return mg
 
 
+def claim_main_grad(p: torch.Tensor):
+    """For a kernel that writes OR accumulates into the gradient buffer itself: returns
+    ``(main_grad, accumulate)`` -- accumulate is False on the first commit of this iteration --
+    and marks the commit, or None when ``p`` has no contiguous main_grad of its own dtype."""
+    mg = getattr(p, "main_grad", None)
+    if mg is None or mg.dtype != p.dtype or not mg.is_contiguous():
+        return None
+    accumulate = getattr(p, "_spa_gen", -1) == _Gen.value
+    p._spa_gen = _Gen.value
+    return mg, accumulate
+
+
 def commit_tensor(p: torch.Tensor, g: torch.Tensor):
     """Commit an already-computed gradient tensor."""
     def _c(out, acc):

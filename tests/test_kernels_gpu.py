@@ -140,6 +140,26 @@ def test_embedding():
     assert rel(W.grad, ref) < 1e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_embedding_grad_into_main_grad(dtype):
+    """emb_bwd_into: sparse row flush into a main_grad view (overwrite, then accumulate), repeated
+    tokens, and a scratch that is clean again for the next call (three calls, fresh ids each)."""
+    ops = _ext.ops()
+    V, D = 5000, 264
+    out = torch.full((V, D), float("nan"), device=DEV, dtype=dtype)
+    ref = torch.zeros(V, D, device=DEV)
+    for call in range(3):
+        idx = torch.randint(0, V, (3, 70), device=DEV)
+        idx[0, :9] = 11 + call      # repeated rows: one flush per row
+        g = torch.randn(3, 70, D, device=DEV, dtype=dtype)
+        ops.emb_bwd_into(g, idx, 0.5, out, call > 0)
+        if call == 0:
+            ref.zero_()
+        ref.index_add_(0, idx.reshape(-1), 0.5 * g.reshape(-1, D).float())
+        assert torch.isfinite(out).all()
+        assert rel(out, ref) < (1e-2 if dtype == torch.bfloat16 else 1e-5), call
+
+
 def test_adamw_matches_torch():
     from solvingpapers_amd.ops import optim_kernels as K
     n = 10007
