@@ -31,8 +31,12 @@ def main():
     ap.add_argument("--fp8", action="store_true",
                     help="DeepSeek-V3 fp8 recipe: routed experts + dense projections in block-scaled e4m3")
     ap.add_argument("--fp8-experts-only", action="store_true", help="with --fp8: dense projections stay bf16")
-    ap.add_argument("--bf16-moments", action="store_true",
-                    help="AdamW moments in bf16 (DeepSeek-V3 sec. 3.3.2; fp32 master weights kept)")
+    # DeepSeek-V3's own recipe (sec. 3.3.2) keeps the AdamW moments in bf16 next to fp32 master
+    # weights; at 8K tokens per step the optimizer over 7.3B parameters is ~24 % of the
+    # dsv3_style step with fp32 moments, so bf16 is the default here
+    ap.add_argument("--bf16-moments", dest="bf16_moments", action="store_true", default=True,
+                    help="AdamW moments in bf16 (DeepSeek-V3 sec. 3.3.2; fp32 master weights kept; default)")
+    ap.add_argument("--fp32-moments", dest="bf16_moments", action="store_false", help="AdamW moments in fp32")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
     a = ap.parse_args()
     info = sdist.init_distributed()

@@ -40,9 +40,9 @@ import torch.distributed as dist
 import torch.nn as tnn
 
 from ..ops import apply_rope, embedding, glu, layer_norm, linear, linear_cross_entropy, rms_norm
-from ..ops.attention import attention_dropout, flash_attention
+from ..ops.attention import attention_dropout, flash_attention, mla_attention, split_last
 from ..ops.misc import dropout
-from ..ops.moe import route
+from ..ops.moe import route, router_logits
 from ..utils.grad import mark_ready
 from ..infer.sampling import sample
 
@@ -243,6 +243,13 @@ class MLA(tnn.Module):
         H, dn, dr, dv = c.n_heads, c.qk_nope_dim, c.qk_rope_dim, c.v_head_dim
         scale = 1.0 / math.sqrt(dn + dr)
         q = self._q(xn).view(B, T, H, dn + dr)
+        if cache is None and isinstance(pos, int):
+            # training / prefill: head assembly fused around the flash kernels (ops.mla_attention)
+            ckv_in, kr = split_last(linear(xn, self.wdkv, fp8=c.fp8_linears), c.kv_lora_rank)
+            ckv = rms_norm(ckv_in, self.kv_norm, c.norm_eps)
+            kv = linear(ckv, self.wukv, fp8=c.fp8_linears).view(B, T, H, dn + dv)
+            o = mla_attention(q, kv, kr.view(B, T, 1, dr), dn, scale, c.rope_theta, pos)
+            return linear(o.reshape(B, T, H * dv), self.wo, fp8=c.fp8_linears)
         qr = self._rope(q[..., dn:], pos)
         ckv, kr = self._latent(xn, pos)
         if cache is not None:
@@ -360,7 +367,7 @@ class MoE(tnn.Module):
         c = self.c
         B, T, D = x.shape
         x2 = x.reshape(-1, D)
-        logits = torch.mm(x2.float(), self.gate.float().t())
+        logits = router_logits(x2, self.gate)
         idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
         y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group,
                              fp8=c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0)
@@ -417,17 +424,26 @@ class DSV3Layer(tnn.Module):
     def expert_params(self):
         return self.ffn.expert_params() if isinstance(self.ffn, MoE) else []
 
-    def forward(self, x, L0=None, cache=None, pos=0):
+    def forward_split(self, res, delta, L0=None, cache=None, pos=0):
+        """Pre-norm layer on a split residual stream (as LlamaBlock): the input is res + delta and
+        the output (h, f) means h + f; both residual adds happen inside the fused RMSNorms, so
+        neither the forward nor the backward launches a separate add."""
         c = self.c
-        xn = rms_norm(x, self.attn_norm, c.norm_eps)
+        if res is None:
+            xn, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
+        else:
+            xn, h = rms_norm(delta, self.attn_norm, c.norm_eps, residual=res)
         if c.attention == "ref" and L0 is None:
             L0 = self.attn.latent0(xn)                 # the only latent anybody attends to (Q1)
             if cache is not None:
-                cache[:, pos:pos + x.shape[1]] = L0.to(cache.dtype)
+                cache[:, pos:pos + xn.shape[1]] = L0.to(cache.dtype)
         a = self.attn(xn, L0, cache, pos)
-        x = x + a
-        x = x + self.ffn(rms_norm(x, self.ffn_norm, c.norm_eps))
-        return x, L0
+        n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
+        return h2, self.ffn(n2), L0
+
+    def forward(self, x, L0=None, cache=None, pos=0):
+        h, f, L0 = self.forward_split(None, x, L0, cache, pos)
+        return h + f, L0
 
 
 class DeepSeekV3(tnn.Module):
@@ -496,19 +512,24 @@ class DeepSeekV3(tnn.Module):
         x0 = x
         L0 = None
         cb = self.grad_ready_cb
+        res, delta = None, x
         for i, layer in enumerate(self.layers):
             wait(i + 1)
-            x = mark_ready(x, cb, i + 1)
+            delta = mark_ready(delta, cb, i + 1)
             if c.attention == "ref":
-                x, L0 = layer(x, L0, None if caches is None else caches[0], pos)
+                res, delta, L0 = layer.forward_split(res, delta, L0, None if caches is None else caches[0], pos)
             else:
-                x, _ = layer(x, None, None if caches is None else caches[i], pos)
+                res, delta, _ = layer.forward_split(res, delta, None, None if caches is None else caches[i], pos)
         wait(len(self.layers) + 1)
-        x = mark_ready(x, cb, len(self.layers) + 1)
-        x = dropout(x, c.dropout, self.training)
-        if c.final_scale:
-            x = x * (2.0 * c.n_layers ** -0.5)
-        return rms_norm(x, self.norm_f, c.norm_eps), x0
+        delta = mark_ready(delta, cb, len(self.layers) + 1)
+        if (c.dropout > 0 and self.training) or c.final_scale or res is None:
+            x = delta if res is None else res + delta
+            x = dropout(x, c.dropout, self.training)
+            if c.final_scale:
+                x = x * (2.0 * c.n_layers ** -0.5)
+            return rms_norm(x, self.norm_f, c.norm_eps), x0
+        n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
+        return n, x0
 
     def logits(self, n):
         return linear(n, self.embed)

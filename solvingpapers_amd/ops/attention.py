@@ -191,6 +191,97 @@ def flash_attention(q, k, v, causal=True, scale=None, dropout_p=0.0, seed=None):
     return reference.attention(q, k, v, causal, scale)[0]
 
 
+class _MLAFn(torch.autograd.Function):
+    """DeepSeek-V3 MLA attention core on the (192, 128) flash kernels with the head assembly
+    fused around them (deepseekv3/deepseekv3.ipynb:1152-1189 for the reference's latent heads):
+
+    forward:  q = q_raw with RoPE on its last dr columns (one copy + one in-place rope),
+              k = [kv_nope | rope(kr) broadcast over heads] (two strided copies),
+              v = the strided view kv[..., dn:] (no copy);
+    backward: the flash backward writes dV straight into the dkv buffer's v columns,
+              dK's nope columns are copied next to it, dK's rope columns are summed over heads
+              in one fp32 reduction, and both rope gradients are rotated back in place.
+
+    The op-by-op form (slices, two torch.cat, out-of-place rope) paid a zero-fill + copy per
+    sliced input and an add per reused tensor in the backward."""
+
+    @staticmethod
+    def forward(ctx, q_raw, kv, kr, dn, scale, pos_off, theta):
+        from .rope import RopeCache
+        ops = _ext.ops()
+        B, T, H, dqk = q_raw.shape
+        dr = dqk - dn
+        cos, sin = RopeCache.get(pos_off + T, dr, theta, q_raw.device)
+        q = q_raw.contiguous().clone()
+        ops.rope_(q[..., dn:], cos, sin, None, H, pos_off, 0, False)
+        krr = kr.contiguous().clone()
+        ops.rope_(krr, cos, sin, None, 1, pos_off, 0, False)
+        k = torch.empty(B, T, H, dqk, device=q.device, dtype=q.dtype)
+        k[..., :dn].copy_(kv[..., :dn])
+        k[..., dn:].copy_(krr.expand(B, T, H, dr))
+        out, lse = ops.attn_fwd(q, k, kv[..., dn:], scale, True, 0.0, 0, None)
+        ctx.save_for_backward(q, k, kv, out, lse)
+        ctx.args = (dn, scale, pos_off, cos, sin)
+        return out
+
+    @staticmethod
+    def backward(ctx, do):
+        ops = _ext.ops()
+        q, k, kv, out, lse = ctx.saved_tensors
+        dn, scale, pos_off, cos, sin = ctx.args
+        H = q.shape[2]
+        dq, dk, dkv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(kv)
+        ops.attn_bwd(do.contiguous(), q, k, kv[..., dn:], out, lse, dq, dk, dkv[..., dn:], scale, True, 0.0, 0,
+                     None)
+        dkv[..., :dn].copy_(dk[..., :dn])
+        dkr = dk[..., dn:].sum(2, keepdim=True, dtype=torch.float32).to(q.dtype)
+        ops.rope_(dkr, cos, sin, None, 1, pos_off, 0, True)
+        ops.rope_(dq[..., dn:], cos, sin, None, H, pos_off, 0, True)
+        return dq, dkv, dkr, None, None, None, None
+
+
+def mla_attention(q_raw, kv, kr, dn, scale, theta, pos_off=0):
+    """Causal MLA attention: q_raw [B, T, H, dn+dr] (rope columns not yet rotated), kv
+    [B, T, H, dn+dv] (the W_ukv up-projection: k_nope | v per head), kr [B, T, 1, dr] (the shared
+    rope key, not yet rotated). Returns o [B, T, H, dv]. RoPE is interleaved (apply_rope's
+    default) at positions pos_off.. ."""
+    dr = q_raw.shape[-1] - dn
+    dv = kv.shape[-1] - dn
+    if (q_raw.is_cuda and q_raw.dtype == torch.bfloat16 and (dn + dr, dv) == (192, 128)
+            and kv.stride(-1) == 1 and kr.shape[2] == 1):
+        return _MLAFn.apply(q_raw, kv, kr, int(dn), float(scale), int(pos_off), float(theta))
+    from .rope import apply_rope
+    B, T, H, _ = q_raw.shape
+    qr = apply_rope(q_raw[..., dn:], theta, pos_off)
+    krr = apply_rope(kr, theta, pos_off)
+    qf = torch.cat([q_raw[..., :dn], qr], dim=-1)
+    k = torch.cat([kv[..., :dn], krr.expand(B, T, H, dr)], dim=-1)
+    return flash_attention(qf, k, kv[..., dn:], causal=True, scale=scale)
+
+
+class _SplitLastFn(torch.autograd.Function):
+    """x [..., a + b] -> (x[..., :a], x[..., a:]) as contiguous tensors; the backward writes both
+    gradients into one buffer (one cat) instead of two zero-filled slice gradients and an add."""
+
+    @staticmethod
+    def forward(ctx, x, a):
+        ctx.a, ctx.shape = a, x.shape
+        return x[..., :a].contiguous(), x[..., a:].contiguous()
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        if ga is None:
+            ga = torch.zeros(ctx.shape[:-1] + (ctx.a,), device=gb.device, dtype=gb.dtype)
+        if gb is None:
+            gb = torch.zeros(ctx.shape[:-1] + (ctx.shape[-1] - ctx.a,), device=ga.device, dtype=ga.dtype)
+        return torch.cat([ga, gb], dim=-1), None
+
+
+def split_last(x, a):
+    """(x[..., :a], x[..., a:]) as contiguous tensors with a single-buffer backward."""
+    return _SplitLastFn.apply(x, int(a))
+
+
 def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None, dropout_p=0.0, seed=None):
     """qkv [B, T, H+2Hkv, hd] (or [B, T, (H+2Hkv)*hd] with head_dim) -> out [B, T, H*hd]."""
     hd = head_dim if head_dim is not None else qkv.shape[-1]

@@ -60,6 +60,34 @@ class _RouteFn(torch.autograd.Function):
         return dl, None, None, None
 
 
+class _RouterLogitsFn(torch.autograd.Function):
+    """logits = x2 @ gate^T as one bf16 GEMM with fp32 accumulation AND fp32 output (hipBLASLt
+    ``mm(out_dtype=float32)``): the router keeps fp32 logits without the fp32 copies of x2
+    ([N, D]) and of the gate that an fp32 GEMM needs, and the backward runs two bf16 GEMMs on
+    the bf16-rounded fp32 dlogits."""
+
+    @staticmethod
+    def forward(ctx, x2, gate):
+        ctx.save_for_backward(x2, gate)
+        return torch.mm(x2, gate.t(), out_dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, dl):
+        from ..utils.grad import commit_tensor
+        x2, gate = ctx.saved_tensors
+        dlb = dl.to(x2.dtype)
+        dx = torch.mm(dlb, gate) if ctx.needs_input_grad[0] else None
+        dg = commit_tensor(gate, torch.mm(dlb.t(), x2)) if ctx.needs_input_grad[1] else None
+        return dx, dg
+
+
+def router_logits(x2, gate):
+    """fp32 router logits [N, E] of x2 [N, D] and gate [E, D]."""
+    if x2.is_cuda and x2.dtype == torch.bfloat16 and gate.dtype == torch.bfloat16:
+        return _RouterLogitsFn.apply(x2, gate)
+    return torch.mm(x2.float(), gate.float().t())
+
+
 def route(logits, k, bias=None, bias_in_weights=True):
     """Top-k expert choice + softmax over the selected logits.
 

@@ -261,6 +261,27 @@ def test_flash_attention_mixed_head_dims(Hkv, dqk, dv):
         assert a.shape == b.shape and rel(a, b) < 3e-2, rel(a, b)
 
 
+@pytest.mark.parametrize("pos_off", [0, 5])
+def test_mla_attention_fused_matches_composition(pos_off):
+    """ops.mla_attention (rope + head assembly fused around the (192, 128) flash kernels, dV
+    written into the dkv buffer, rope key grad summed over heads) vs the op-by-op fp32 CPU path."""
+    from solvingpapers_amd.ops.attention import mla_attention
+    torch.manual_seed(7)
+    B, T, H, dn, dr, dv = 2, 300, 4, 128, 64, 128
+    q = torch.randn(B, T, H, dn + dr, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    kv = torch.randn(B, T, H, dn + dv, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    kr = torch.randn(B, T, 1, dr, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = mla_attention(q, kv, kr, dn, 0.07, 10000.0, pos_off)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qc, kvc, krc = (t.detach().float().cpu().requires_grad_() for t in (q, kv, kr))
+    oc = mla_attention(qc, kvc, krc, dn, 0.07, 10000.0, pos_off)
+    oc.backward(do.float().cpu())
+    assert rel(o.cpu(), oc) < 2e-2, rel(o.cpu(), oc)
+    for a, b in ((q.grad, qc.grad), (kv.grad, kvc.grad), (kr.grad, krc.grad)):
+        assert rel(a.cpu(), b) < 3e-2, rel(a.cpu(), b)
+
+
 def test_flash_lse_and_spike():
     """Force the online-softmax rescale: one key spiked against one query (rule 26)."""
     B, T, H, hd = 1, 300, 2, 128

@@ -13,6 +13,22 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
+def test_router_logits_fp32_output():
+    """bf16 GEMM with fp32 output (and its two bf16 backward GEMMs) vs the fp32 oracle."""
+    torch.manual_seed(0)
+    x = torch.randn(777, 512, device=dev).bfloat16().requires_grad_()
+    g = (torch.randn(64, 512, device=dev) * 0.05).bfloat16().requires_grad_()
+    lg = M.router_logits(x, g)
+    assert lg.dtype == torch.float32 and lg.shape == (777, 64)
+    dl = torch.randn_like(lg)
+    lg.backward(dl)
+    xf, gf = x.detach().float().requires_grad_(), g.detach().float().requires_grad_()
+    ref = xf @ gf.t()
+    ref.backward(dl)
+    assert _rel(lg, ref) < 1e-3
+    assert _rel(x.grad, xf.grad) < 1e-2 and _rel(g.grad, gf.grad) < 1e-2
+
+
 @pytest.mark.parametrize("E,k,bias_in_w", [(8, 2, True), (64, 6, False), (256, 8, False), (5, 1, True)])
 def test_route(E, k, bias_in_w):
     torch.manual_seed(0)

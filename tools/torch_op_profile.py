@@ -1,7 +1,7 @@
 """Which framework ops launch the non-GEMM "glue" kernels (fills, copies, casts, cats) of a
 DeepSeek-V3-style training step: torch.profiler over one fwd+bwd+AdamW step, ops sorted by
 device time with their input shapes.
-    python tools/torch_op_profile.py [--fp8] [--rows 40]"""
+    python tools/torch_op_profile.py [--fp8] [--rows 40] [--preset dsv3_style --mb 2]"""
 import os
 import sys
 
@@ -16,14 +16,16 @@ from solvingpapers_amd.utils.flat import FlatParams  # noqa: E402
 def main():
     fp8 = "--fp8" in sys.argv
     rows = int(sys.argv[sys.argv.index("--rows") + 1]) if "--rows" in sys.argv else 40
-    c = ds.config("dsv3_v3", n_layers=4, n_experts=32, n_dense_layers=1, block_size=4096, moe_fp8=fp8,
-                  fp8_linears=fp8)
+    preset = sys.argv[sys.argv.index("--preset") + 1] if "--preset" in sys.argv else "dsv3_v3"
+    mb = int(sys.argv[sys.argv.index("--mb") + 1]) if "--mb" in sys.argv else 1
+    kw = dict(n_layers=4, n_experts=32, n_dense_layers=1) if preset == "dsv3_v3" else {}
+    c = ds.config(preset, block_size=4096, moe_fp8=fp8, fp8_linears=fp8, **kw)
     m = ds.DeepSeekV3(c, device="cuda", dtype=torch.bfloat16, seed=1)
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
     for l in m.moe_layers():
         l.balance_group = None
-    t = torch.randint(0, c.vocab_size, (1, 4097), device="cuda")
+    t = torch.randint(0, c.vocab_size, (mb, 4097), device="cuda")
 
     def step():
         opt.zero_grad()
