@@ -1432,7 +1432,9 @@ static void check_qkv(const at::Tensor& t, const char* n) {
 // forward uses 8 waves (2 per SIMD) for head dims <= 192, 4 waves for 256; dq keeps q, dO and
 // the dQ accumulator in registers and needs one wave per SIMD (the AGPR half of the register
 // file) beyond square 128
-template <int HDK, int HDV> constexpr int fwd_waves() { return (HDK <= 192 && HDV <= 192) ? 8 : 4; }
+template <int HDK, int HDV> constexpr int fwd_waves() {
+  return (HDK <= 192 && HDV <= 192) || (HDK == 256 && HDV == 128) ? 8 : 4;
+}
 template <int HDK, int HDV> constexpr int dq_waves() { return (HDK <= 128 && HDV <= 128) ? 8 : 4; }
 
 // (q/k head dim, v head dim) instantiations: the square 64/128/256 and MLA's 192/128
@@ -1490,6 +1492,23 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   p.hsplit = 1;
   if (B * Tq * H == 0) return {out, lse};
   auto st = stream();
+  // head dim 256 (Gemma MQA) as two launches of the (256, 128) kernel, each producing half of the
+  // output columns: the 128-wide O accumulator lets 8 waves (2 per SIMD) share a CU, where the
+  // full 256-wide one holds a wave per SIMD, at the price of computing S twice (1.5x the MFMA
+  // work). SPA_ATTN_SPLITV=0 (read per call) keeps the single 4-wave launch.
+  const char* sve = getenv("SPA_ATTN_SPLITV");
+  if (!(sve && atoi(sve) == 0) && HDK == 256 && HDV == 256 && !drop) {
+    const int grid = cdiv(Tq, 32 * 8) * H * B;
+    for (int half = 0; half < 2; ++half) {
+      AttnParams ph = p;
+      ph.v = p.v + 128 * half;
+      ph.out = p.out + 128 * half;
+      if (causal) attn_fwd_kernel<256, 128, 8, true, false><<<grid, 512, 0, st>>>(ph);
+      else attn_fwd_kernel<256, 128, 8, false, false><<<grid, 512, 0, st>>>(ph);
+    }
+    SPA_LAUNCH_CHECK();
+    return {out, lse};
+  }
   // two-sub-tile pipelined body at head dim 128 (default; SPA_ATTN_FWD_PIPE=0, read per call, keeps
   // the one-sub-tile-at-a-time body). Same-process A/B at the LLaMA3-8B shape on MI355X:
   // 0.584 vs 0.593-0.600 ms, identical output (profiles/r2_attn_fwd_pipe_ab.txt)

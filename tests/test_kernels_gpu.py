@@ -298,6 +298,22 @@ def test_attn_fwd_pipe_variant_matches(causal, monkeypatch):
     assert rel(o1, o0) < 5e-3 and (l1 - l0).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("causal,Hkv", [(True, 1), (False, 2)])
+def test_attn_fwd_hd256_splitv_matches(causal, Hkv, monkeypatch):
+    """Head dim 256 forward as two (256, 128) half-V launches (default) == the single 4-wave
+    launch (SPA_ATTN_SPLITV=0), output and lse."""
+    ops = _ext.ops()
+    torch.manual_seed(4)
+    q = torch.randn(2, 333, 4, 256, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(2, 333, Hkv, 256, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(2, 333, Hkv, 256, device=DEV, dtype=torch.bfloat16)
+    monkeypatch.setenv("SPA_ATTN_SPLITV", "0")
+    o0, l0 = ops.attn_fwd(q, k, v, 0.0625, causal)
+    monkeypatch.setenv("SPA_ATTN_SPLITV", "1")
+    o1, l1 = ops.attn_fwd(q, k, v, 0.0625, causal)
+    assert rel(o1, o0) < 5e-3 and (l1 - l0).abs().max().item() < 1e-3
+
+
 def test_flash_lse_and_spike():
     """Force the online-softmax rescale: one key spiked against one query (rule 26)."""
     B, T, H, hd = 1, 300, 2, 128
