@@ -100,7 +100,7 @@ __device__ __forceinline__ bool drop_keep(unsigned base, int q, int key, unsigne
 // ---------------------------------------------------------------------------
 template <int HDK, int HDV> constexpr int attn_bn() { return (HDK >= 256 || HDV >= 256) ? 32 : 64; }
 
-template <int HDK, int HDV, int NW, bool CAUSAL, bool DROP, bool PIPE = false>
+template <int HDK, int HDV, int NW, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   constexpr int BN = attn_bn<HDK, HDV>(), NSUB = BN / 32, BM = 32 * NW, KS = HDK / 16, DT = HDV / 32;
   constexpr int NT = NW * 64, IK = img_w<HDK>(), IV = img_w<HDV>();
@@ -214,41 +214,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
       lk.store(Kn);
       lv.store(Kn + TK);
       if (j + 2 < ntiles) { lk.load(kbase, p.skt, k0 + 2 * BN, p.Tk); lv.load(vbase, p.svt, k0 + 2 * BN, p.Tk); }
-    }
-    // PIPE (T15-style): with both 32-key sub-tiles of the tile fully unmasked for this wave, issue
-    // both QK^T chains first, so the second chain's MFMAs run under the first sub-tile's softmax
-    // VALU work, and only then the two softmax + PV steps (one straight-line block, no branches
-    // between them for the scheduler to respect)
-    if constexpr (PIPE && NSUB == 2 && !DROP) {
-      if (k0 + 64 <= p.Tk && (!CAUSAL || k0 + 63 <= q0 + p.causal_off)) {
-        f32x16 sa0 = mfma32(ld_row(Ks, offk.row[0]), qf[0], splat16(0.f));
-        f32x16 sa1 = mfma32(ld_row(Ks + 32 * IK, offk.row[0]), qf[0], splat16(0.f));
-#pragma unroll
-        for (int ks = 1; ks < KS; ++ks) {
-          sa0 = mfma32(ld_row(Ks, offk.row[ks]), qf[ks], sa0);
-          sa1 = mfma32(ld_row(Ks + 32 * IK, offk.row[ks]), qf[ks], sa1);
-        }
-        softmax(sa0);
-        {
-          const bf16x8 pa = pack_acc(sa0, 0), pb = pack_acc(sa0, 1);
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            o[dt] = mfma32(ld_tr(Vs, offv.tra[dt], offv.trb[dt]), pa, o[dt]);
-            o[dt] = mfma32(ld_tr(Vs + 16 * IV, offv.tra[dt], offv.trb[dt]), pb, o[dt]);
-          }
-        }
-        softmax(sa1);
-        {
-          const bf16x8 pa = pack_acc(sa1, 0), pb = pack_acc(sa1, 1);
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            o[dt] = mfma32(ld_tr(Vs + 32 * IV, offv.tra[dt], offv.trb[dt]), pa, o[dt]);
-            o[dt] = mfma32(ld_tr(Vs + 48 * IV, offv.tra[dt], offv.trb[dt]), pb, o[dt]);
-          }
-        }
-        __syncthreads();
-        return;
-      }
     }
 #pragma unroll
     for (int t = 0; t < NSUB; ++t) {
@@ -1509,11 +1474,6 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
     SPA_LAUNCH_CHECK();
     return {out, lse};
   }
-  // two-sub-tile pipelined body at head dim 128 (default; SPA_ATTN_FWD_PIPE=0, read per call, keeps
-  // the one-sub-tile-at-a-time body). Same-process A/B at the LLaMA3-8B shape on MI355X:
-  // 0.584 vs 0.593-0.600 ms, identical output (profiles/r2_attn_fwd_pipe_ab.txt)
-  const char* fpe = getenv("SPA_ATTN_FWD_PIPE");
-  const bool pipe = !(fpe && atoi(fpe) == 0);
   HDKV_SWITCH(HDK, HDV, {
     constexpr int NW = fwd_waves<HDK_, HDV_>();
     constexpr bool SQ = HDK_ == HDV_;
@@ -1523,9 +1483,6 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
         if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, true><<<grid, NW * 64, 0, st>>>(p);
         else attn_fwd_kernel<HDK_, HDV_, NW, false, true><<<grid, NW * 64, 0, st>>>(p);
       }
-    } else if (pipe && HDK_ == 128 && HDV_ == 128) {
-      if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, false, true><<<grid, NW * 64, 0, st>>>(p);
-      else attn_fwd_kernel<HDK_, HDV_, NW, false, false, true><<<grid, NW * 64, 0, st>>>(p);
     } else {
       if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, false><<<grid, NW * 64, 0, st>>>(p);
       else attn_fwd_kernel<HDK_, HDV_, NW, false, false><<<grid, NW * 64, 0, st>>>(p);

@@ -282,22 +282,6 @@ def test_mla_attention_fused_matches_composition(pos_off):
         assert rel(a.cpu(), b) < 3e-2, rel(a.cpu(), b)
 
 
-@pytest.mark.parametrize("causal", [True, False])
-def test_attn_fwd_pipe_variant_matches(causal, monkeypatch):
-    """The two-sub-tile pipelined forward body (default at hd 128) == the one-sub-tile body
-    (SPA_ATTN_FWD_PIPE=0)."""
-    ops = _ext.ops()
-    torch.manual_seed(2)
-    q = torch.randn(2, 700, 8, 128, device=DEV, dtype=torch.bfloat16)
-    k = torch.randn(2, 700, 2, 128, device=DEV, dtype=torch.bfloat16)
-    v = torch.randn(2, 700, 2, 128, device=DEV, dtype=torch.bfloat16)
-    monkeypatch.setenv("SPA_ATTN_FWD_PIPE", "0")
-    o0, l0 = ops.attn_fwd(q, k, v, 0.088, causal)
-    monkeypatch.setenv("SPA_ATTN_FWD_PIPE", "1")
-    o1, l1 = ops.attn_fwd(q, k, v, 0.088, causal)
-    assert rel(o1, o0) < 5e-3 and (l1 - l0).abs().max().item() < 1e-3
-
-
 @pytest.mark.parametrize("causal,Hkv", [(True, 1), (False, 2)])
 def test_attn_fwd_hd256_splitv_matches(causal, Hkv, monkeypatch):
     """Head dim 256 forward as two (256, 128) half-V launches (default) == the single 4-wave

@@ -1,8 +1,9 @@
 """Attention kernel micro-benchmark (LLaMA3-8B shape by default): TFLOP/s fwd / bwd.
 
---ab ENV=VAL[,ENV=VAL...]: also time the backward with those env settings in the same
-process (the dK/dV kernel choice is read per call), since MI355X devices differ by up to
-~10 % and cross-box comparisons are noise."""
+--ab ENV=VAL[,ENV=VAL...]: also time both passes with those env settings in the same
+process (the kernel choices are read per call), since MI355X devices differ by up to
+~10 % and cross-box comparisons are noise. Each A/B runs in ABBA order (default, variant,
+variant, default) and averages the two arms, because the clock drifts within a run."""
 import argparse, math, time, sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -52,18 +53,37 @@ if a.pad:
     tbp = t(lambda: ops.attn_bwd(dop, qp, kp, vp, op_, lp, dqp, dkp, dvp, sc, causal))
     print(f"   same problem zero-padded to hd {a.pad}: fwd {tfp*1e3:.3f} ms ({fl/tfp/1e12:.0f} useful TF) | "
           f"bwd {tbp*1e3:.3f} ms ({flb/tbp/1e12:.0f} useful TF)", flush=True)
+def _arm(key, val):
+    """(fwd s, bwd s, out) with env key=val (val None: unset) for the duration of the call."""
+    old = os.environ.get(key)
+    if val is None:
+        os.environ.pop(key, None)
+    else:
+        os.environ[key] = val
+    try:
+        tfx = t(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
+        tbx = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
+        ox, _ = ops.attn_fwd(q, k, v, sc, causal, P, SEED)
+    finally:
+        if old is None:
+            os.environ.pop(key, None)
+        else:
+            os.environ[key] = old
+    return tfx, tbx, ox
+
+
 for setting in filter(None, a.ab.split(",")):
     key, val = setting.split("=")
-    old = os.environ.get(key)
-    os.environ[key] = val
-    tf2 = t(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
-    o2, _ = ops.attn_fwd(q, k, v, sc, causal, P, SEED)
-    err = ((o2.float() - out.float()).norm() / out.float().norm()).item()
-    tb2 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
-    if old is None: os.environ.pop(key)
-    else: os.environ[key] = old
-    tf3 = t(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
-    tb3 = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
+    base = os.environ.get(key)
+    # ABBA order (default, variant, variant, default): the chip's clock drifts over a run, so a
+    # fixed variant-then-default order biases the comparison
+    d1 = _arm(key, base)
+    v1 = _arm(key, val)
+    v2 = _arm(key, val)
+    d2 = _arm(key, base)
+    tf2, tb2 = (v1[0] + v2[0]) / 2, (v1[1] + v2[1]) / 2
+    tf3, tb3 = (d1[0] + d2[0]) / 2, (d1[1] + d2[1]) / 2
+    err = ((v1[2].float() - d1[2].float()).norm() / d1[2].float().norm()).item()
     print(f"   with {key}={val}: fwd {tf2*1e3:.3f} ms ({fl/tf2/1e12:.0f} TF, out rel diff {err:.1e}) vs default "
           f"{tf3*1e3:.3f} ms ({fl/tf3/1e12:.0f} TF) | bwd {tb2*1e3:.3f} ms ({flb/tb2/1e12:.0f} TF) vs "
           f"{tb3*1e3:.3f} ms", flush=True)
