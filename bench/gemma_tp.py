@@ -23,8 +23,12 @@ def main():
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")
+    ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (tuning/*.csv) to look up")
     a = ap.parse_args()
     info = sdist.init_distributed()
+    if a.gemm_table:   # after init: the device is set, so every rank loads it on its own GPU
+        from solvingpapers_amd.utils.tuning import load_gemm_tuning
+        assert load_gemm_tuning(a.gemm_table), a.gemm_table
     world, dev = info.world_size, info.device
     kw = {"max_seq_len": a.seq}
     if a.layers:

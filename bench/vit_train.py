@@ -22,8 +22,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mb", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (tuning/*.csv) to look up")
     a = ap.parse_args()
     info = sdist.init_distributed()
+    if a.gemm_table:   # after init: the device is set, so every rank loads it on its own GPU
+        from solvingpapers_amd.utils.tuning import load_gemm_tuning
+        assert load_gemm_tuning(a.gemm_table), a.gemm_table
     world, dev = info.world_size, info.device
     c = vit.config("vit_b16")
     m = vit.ViT(c, device=dev, dtype=torch.bfloat16)
