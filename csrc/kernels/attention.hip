@@ -73,6 +73,7 @@ struct AttnParams {
   const int64_t* seed_ptr;  // device seed (graph-safe: a fresh mask per HIP-graph replay) or null
   // profiling only (SPA_ATTN_STAMP): per-wave s_memtime segment sums of the dK/dV loop, or null
   long long* stamp;
+  int xcd;  // query-parallel kernels: XCD-aware block order (q_block_map)
 };
 
 // ---- dropout counter hash (bit-identical in ops/attention.py dropout_keep_mask) ------
@@ -95,6 +96,34 @@ __device__ __forceinline__ bool drop_keep(unsigned base, int q, int key, unsigne
 }
 
 
+
+// Query-parallel block -> (q-block, batch, q-head). Default: q-block major over (b, h), heaviest
+// causal q-blocks first. XCD-aware (p.xcd, needs B*Hkv % 8 == 0): the hardware hands block i to
+// XCD i % 8, so logical tile L = (i % 8) * (grid / 8) + i / 8 gives each XCD a contiguous chunk
+// of an order that is (b, kv-head) major: every q-head of a GQA group, and every q-block of it,
+// runs on the XCD whose private L2 already holds that kv-head's K / V (LLaMA3-8B: one kv-head per
+// XCD). Within an XCD the q-blocks still go heaviest first.
+__device__ __forceinline__ void q_block_map(const AttnParams& p, int nqb, bool causal, int& qb, int& b, int& h) {
+  const int G = p.H / p.Hkv;
+  if (p.xcd) {
+    const int cpx = gridDim.x / 8;
+    const int L = (blockIdx.x % 8) * cpx + blockIdx.x / 8;
+    const int per_unit = nqb * G;
+    const int u = L / per_unit, rem = L % per_unit;
+    const int qr = rem / G, g = rem % G;
+    qb = causal ? nqb - 1 - qr : qr;
+    b = u / p.Hkv;
+    h = (u % p.Hkv) * G + g;
+  } else {
+    const int nbh = p.H * p.B;
+    const int bh = blockIdx.x % nbh;
+    qb = blockIdx.x / nbh;
+    if (causal) qb = nqb - 1 - qb;  // heaviest q-blocks first
+    h = bh % p.H;
+    b = bh / p.H;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Forward: block = NW waves x 32 query rows; K/V tiles of BN keys.
 // ---------------------------------------------------------------------------
@@ -110,10 +139,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   const int lq = lane & 31, hh = lane >> 5;
   const int nqb = cdiv(p.Tq, BM);
   const int nbh = p.H * p.B;
-  int qb = blockIdx.x / nbh;
-  const int bh = blockIdx.x % nbh;
-  if (CAUSAL) qb = nqb - 1 - qb;  // heaviest q-blocks first
-  const int h = bh % p.H, b = bh / p.H;
+  int qb, b, h;
+  q_block_map(p, nqb, CAUSAL, qb, b, h);
   const int hk = h / (p.H / p.Hkv);
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
@@ -274,10 +301,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const int lq = lane & 31, hh = lane >> 5;
   const int nqb = cdiv(p.Tq, BM);
   const int nbh = p.H * p.B;
-  int qb = blockIdx.x / nbh;
-  const int bh = blockIdx.x % nbh;
-  if (CAUSAL) qb = nqb - 1 - qb;
-  const int h = bh % p.H, b = bh / p.H;
+  int qb, b, h;
+  q_block_map(p, nqb, CAUSAL, qb, b, h);
   const int hk = h / (p.H / p.Hkv);
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
@@ -1416,6 +1441,14 @@ static void fill_strides(AttnParams& p, const at::Tensor& q, const at::Tensor& k
   p.svb = v.stride(0); p.svt = v.stride(1); p.svh = v.stride(2);
 }
 
+// XCD-aware block order for the query-parallel kernels (q_block_map) when B * Hkv % 8 == 0;
+// SPA_ATTN_XCD=0 (read per call) keeps the q-block-major order
+static int xcd_order(int B, int Hkv) {
+  const char* e = getenv("SPA_ATTN_XCD");
+  if (e && atoi(e) == 0) return 0;
+  return ((long)B * Hkv) % 8 == 0 ? 1 : 0;
+}
+
 static void fill_dropout(AttnParams& p, double dropout_p, int64_t seed, const c10::optional<at::Tensor>& seed_t) {
   if (seed_t) {
     TORCH_CHECK(seed_t->is_cuda() && seed_t->scalar_type() == at::kLong && seed_t->numel() >= 1,
@@ -1455,6 +1488,7 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal_off = Tk - Tq;
   p.hsplit = 1;
+  p.xcd = xcd_order(B, Hkv);
   if (B * Tq * H == 0) return {out, lse};
   auto st = stream();
   // head dim 256 (Gemma MQA) as two launches of the (256, 128) kernel, each producing half of the
@@ -1578,6 +1612,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   p.sdvb = dv.stride(0); p.sdvt = dv.stride(1); p.sdvh = dv.stride(2);
   p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal_off = Tk - Tq;
+  p.xcd = xcd_order(B, Hkv);
   if (B * H == 0) return;
   auto st = stream();
   if (Tq == 0) { dk.zero_(); dv.zero_(); return; }
