@@ -76,20 +76,26 @@ class _LinearXentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (h2,) = ctx.saved_tensors
-        G = ctx.grad_buf
+        G = ctx.grad_buf                      # d(loss)/d(logits) for an upstream grad of 1
         ctx.grad_buf = None
-        G.mul_(g.to(G.dtype))                 # padded columns are exactly 0
+        # the upstream grad g (a device scalar: 1 / accum in a gradient-accumulation loop) scales
+        # the [N, D] / [N] sides of the products, never the [N, V] buffer: dh = g (G W),
+        # dW = G^T (g h) -- a pass over G would stream 2 x N x V x 2 bytes (4.2 GB per LLaMA3-8B
+        # micro-batch) through a broadcast-scalar elementwise kernel
+        gs = g.to(G.dtype)
         w, b, wp = ctx.w, ctx.b, ctx.wp
         ctx.wp = None
-        dh = torch.mm(G, wp).view(ctx.hshape) if ctx.needs_input_grad[0] else None
-        G = G[:, :ctx.V]
+        dh = torch.mm(G, wp).mul_(gs).view(ctx.hshape) if ctx.needs_input_grad[0] else None
+        G = G[:, :ctx.V]                      # padded columns are exactly 0
         gw = gb = None
         if ctx.needs_input_grad[1]:
+            h2s = h2 * gs
+
             def _w(out, acc):
-                return wgrad(G, h2, out, acc)
+                return wgrad(G, h2s, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
-            gb = commit_tensor(b, bias_grad(G).to(b.dtype))
+            gb = commit_tensor(b, (bias_grad(G) * g.to(torch.float32)).to(b.dtype))
         return dh, gw, gb, None, None, None
 
 
