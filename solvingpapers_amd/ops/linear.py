@@ -8,6 +8,7 @@ no per-parameter grad allocation and no extra accumulate pass.
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -18,6 +19,47 @@ from .layout import bias_grad, wgrad
 # decode-time products with <= 4 token rows go to the GEMV kernel; SPA_GEMV=0 -> torch.mm
 GEMV = os.environ.get("SPA_GEMV", "1") != "0"
 GEMV_MAX_ROWS = 4
+
+# dX = dY W runs as the NT product dY (W^T)^T on a transposed copy of W (K-contiguous, like the
+# forward's operands) rebuilt once per optimizer step: hipBLASLt at LLaMA3-8B shapes, ABBA-timed
+# (profiles/r2_dgrad_layouts.txt): qkv 0.336 -> 0.296 ms, o 0.217 -> 0.205, gate/up 1.365 -> 1.251,
+# down 0.717 -> 0.601, LM head 6.07 -> 5.25, against one transpose per weight per step (≈ 6 ms for
+# all of LLaMA3-8B with layout.hip's kernel). SPA_DGRAD_WT=0 keeps the NN product.
+DGRAD_WT = os.environ.get("SPA_DGRAD_WT", "1") != "0"
+DGRAD_WT_MIN_NUMEL = 1 << 22
+# id(w) -> (validity key, W^T, weakref(w)); entries leave with their tensor (weakref.finalize).
+# Not a WeakKeyDictionary: its lookups compare tensor keys with ==, which is elementwise.
+_WT_CACHE: dict = {}
+
+
+def transposed_weight(w: torch.Tensor):
+    """Contiguous W^T for the dgrad product, or None where it does not apply. Valid while the
+    optimizer's weight epoch (bumped by every fused optimizer step) and the tensor's version
+    counter (bumped by any torch in-place update) are unchanged."""
+    if not (DGRAD_WT and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
+            and w.numel() >= DGRAD_WT_MIN_NUMEL and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
+            and w.data_ptr() % 16 == 0):
+        return None
+    from .layout import transpose2d
+    from .moe import _WEIGHT_EPOCH
+    key = (_WEIGHT_EPOCH[0], w._version, w.data_ptr())
+    hit = _WT_CACHE.get(id(w))
+    if hit is not None and hit[2]() is not w:
+        hit = None                               # defensive: never another tensor's entry
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        wt = transpose2d(w)
+    if hit is None:
+        weakref.finalize(w, _WT_CACHE.pop, id(w), None)
+    _WT_CACHE[id(w)] = (key, wt, weakref.ref(w))
+    return wt
+
+
+def dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dX = dY W for dY [T, N], W [N, K] (NT form on the cached W^T where it applies)."""
+    wt = transposed_weight(w)
+    return torch.mm(dy2, w) if wt is None else torch.mm(dy2, wt.t())
 
 
 class _LinearFn(torch.autograd.Function):
@@ -40,7 +82,7 @@ class _LinearFn(torch.autograd.Function):
         w, b = ctx.w, ctx.b
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
-        dx = torch.mm(dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = dgrad(dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
         gw = gb = None
         if ctx.needs_input_grad[1]:
             def _w(out, acc):

@@ -15,6 +15,7 @@ import torch.distributed as dist
 from . import _ext
 from . import reference
 from .layout import bias_grad, wgrad, wgrad_operand
+from .linear import dgrad
 from ..utils.grad import commit, commit_tensor
 
 
@@ -85,7 +86,9 @@ class _LinearXentFn(torch.autograd.Function):
         gs = g.to(G.dtype)
         w, b, wp = ctx.w, ctx.b, ctx.wp
         ctx.wp = None
-        dh = torch.mm(G, wp).mul_(gs).view(ctx.hshape) if ctx.needs_input_grad[0] else None
+        dh = None
+        if ctx.needs_input_grad[0]:   # the cached-W^T form only for the persistent weight (not a padded copy)
+            dh = (dgrad(G, wp) if wp is w else torch.mm(G, wp)).mul_(gs).view(ctx.hshape)
         G = G[:, :ctx.V]                      # padded columns are exactly 0
         gw = gb = None
         if ctx.needs_input_grad[1]:

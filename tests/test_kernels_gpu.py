@@ -160,6 +160,34 @@ def test_embedding_grad_into_main_grad(dtype):
         assert rel(out, ref) < (1e-2 if dtype == torch.bfloat16 else 1e-5), call
 
 
+def test_dgrad_transposed_weight_cache_tracks_updates():
+    """dX through the cached W^T (ops/linear.py transposed_weight) equals dY W after every kind of
+    weight update: none (cache hit), a torch in-place op (version counter), and a write the
+    version counter cannot see, as a fused optimizer kernel makes, announced by the weight epoch."""
+    from solvingpapers_amd.ops import linear
+    from solvingpapers_amd.ops.linear import _WT_CACHE
+    from solvingpapers_amd.ops.moe import bump_weight_epoch
+    torch.manual_seed(0)
+    w = (torch.randn(2048, 2048, device=DEV) * 0.02).bfloat16().requires_grad_()
+    x = torch.randn(64, 2048, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    dy = torch.randn(64, 2048, device=DEV, dtype=torch.bfloat16)
+
+    def dx():
+        x.grad = None
+        linear(x, w).backward(dy)
+        return x.grad
+
+    assert rel(dx(), dy.float() @ w.detach().float()) < 1e-2
+    assert id(w) in _WT_CACHE
+    assert rel(dx(), dy.float() @ w.detach().float()) < 1e-2          # hit
+    with torch.no_grad():
+        w.mul_(-0.5)                                                 # version bump
+    assert rel(dx(), dy.float() @ w.detach().float()) < 1e-2
+    w.data.mul_(3.0)                                                 # invisible to the version counter
+    bump_weight_epoch()
+    assert rel(dx(), dy.float() @ w.detach().float()) < 1e-2
+
+
 def test_adamw_matches_torch():
     from solvingpapers_amd.ops import optim_kernels as K
     n = 10007
