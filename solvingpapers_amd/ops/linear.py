@@ -26,7 +26,9 @@ GEMV_MAX_ROWS = 4
 # down 0.717 -> 0.601, LM head 6.07 -> 5.25, against one transpose per weight per step (≈ 6 ms for
 # all of LLaMA3-8B with layout.hip's kernel). SPA_DGRAD_WT=0 keeps the NN product.
 DGRAD_WT = os.environ.get("SPA_DGRAD_WT", "1") != "0"
-DGRAD_WT_MIN_NUMEL = 1 << 22
+# weights below SPA_DGRAD_WT_MIN elements keep NN (ViT-B/16's 0.6-2.4M-element weights gain too:
+# 6,115 -> 6,180 img/s ABBA, profiles/r2_vit_dgrad_abba.txt)
+DGRAD_WT_MIN_NUMEL = int(os.environ.get("SPA_DGRAD_WT_MIN", str(1 << 18)))
 # id(w) -> (validity key, W^T, weakref(w)); entries leave with their tensor (weakref.finalize).
 # Not a WeakKeyDictionary: its lookups compare tensor keys with ==, which is elementwise.
 _WT_CACHE: dict = {}
