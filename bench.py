@@ -22,8 +22,9 @@ per step). Every micro-batch runs its full forward + backward inside the timed
 region; only the inner micro-batches skip the gradient all-reduce (no_sync) and
 the last one launches it, so the per-step optimizer / grad-norm / all-reduce
 cost (~40 ms on 1 GPU, more at N=8) is paid once per 32K tokens as in a real
-LLaMA-scale run (global batches of millions of tokens). Measured on 1 MI355X:
-accum 1: 18.6K tok/s, 2: 19.4K, 4: 20.35K, 8: 20.6K.
+LLaMA-scale run (global batches of millions of tokens). Measured on 1 MI355X in round 1:
+accum 1: 18.6K tok/s, 2: 19.4K, 4: 20.35K, 8: 20.6K; accum 4 at the end of round 2: 21.0K
+(BASELINE.md).
 """
 from __future__ import annotations
 
