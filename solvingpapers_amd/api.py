@@ -111,14 +111,21 @@ def compute_mtp_loss(logits, targets, ignore_index: int = -100):
 @torch.no_grad()
 def topk_sampling(model, input_ids, max_length=50, top_k=50, temperature=1.0, eos_token_id: Optional[int] = None,
                   generator=None):
-    """deepseekv3.ipynb:1849-1873 (softmax -> top-k -> multinomial until max_length or EOS),
-    on the model's cached decoder."""
+    """deepseekv3.ipynb:1849-1873 (softmax -> top-k -> multinomial until max_length or EOS) as ONE
+    cached ``generate`` call: the prompt is prefilled once and every further token is a single
+    decode step against the model's KV / latent cache (the reference re-runs the whole prefix
+    per token). With ``eos_token_id`` a finished sequence is padded with EOS; a single sequence
+    is cut right after its first EOS, exactly where the reference's loop breaks."""
     remaining = max(0, max_length - input_ids.shape[1])
-    out = input_ids
-    for _ in range(remaining):
-        out = model.generate(out, 1, temperature=temperature, top_k=top_k, generator=generator)
-        if eos_token_id is not None and int(out[0, -1]) == eos_token_id:
-            break
+    if remaining == 0:
+        return input_ids
+    out = model.generate(input_ids, remaining, temperature=temperature, top_k=top_k, greedy=False,
+                         generator=generator, eos_token_id=eos_token_id)
+    if eos_token_id is not None and out.shape[0] == 1:
+        gen = out[0, input_ids.shape[1]:]
+        hit = (gen == eos_token_id).nonzero()
+        if hit.numel():
+            out = out[:, :input_ids.shape[1] + int(hit[0, 0]) + 1]
     return out
 
 

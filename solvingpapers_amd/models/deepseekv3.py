@@ -73,6 +73,7 @@ class DSV3Config:
     dense_hidden: int = 0
     moe_fp8: bool = False           # routed-expert fwd/dX GEMMs in OCP e4m3 (BASELINE config #5)
     fp8_linears: bool = False       # dense projections too (MLA, shared / dense FFN): the V3 recipe
+    noisy_topk: bool = False        # ref (deepseekv3.ipynb:390,1026-1039): + softplus(noise(x)) * N(0,1)
     aux_free: bool = True
     bias_update_rate: float = 1e-3
     bias_in_weights: bool = True    # ref: softmax over (logits + bias); paper: bias steers selection only
@@ -126,7 +127,7 @@ PRESETS = {
                              balance_stat="counts", final_scale=False, norm_eps=1e-6, dropout=0.0,
                              attn_dropout=0.0, mtp_heads=1, batch_size=1),
     # DeepSeek-V3 (arXiv 2412.19437) widths: D7168, 128 heads, q_lora 1536, kv_lora 512,
-    # qk 128 nope + 64 rope = 192 and v 128 (flash kernel via zero-padding to 256), 256 routed
+    # qk 128 nope + 64 rope = 192 and v 128 (native (192, 128) flash kernels, no padding), 256 routed
     # experts top-8 + 1 shared of hidden 2048, 3 dense layers of 18432, V 129280. 61 layers is
     # the model card; benches override depth and (for 1 GPU) the expert count.
     "dsv3_v3": DSV3Config(vocab_size=129280, block_size=4096, dim=7168, n_layers=61, n_heads=128,
@@ -328,6 +329,9 @@ class MoE(tnn.Module):
         D, F = c.dim, c.ffn_hidden
         self.F, self.Fp = F, _pad8(F)
         self.gate = tnn.Parameter(torch.empty(c.n_experts, D, **fk))
+        # noisy top-k gating (deepseekv3.ipynb:1026-1027): a second router GEMM whose softplus
+        # scales the per-(token, expert) Gaussian noise added to the gate logits
+        self.noise = tnn.Parameter(torch.empty(c.n_experts, D, **fk)) if c.noisy_topk else None
         self.w13 = tnn.Parameter(torch.zeros(El, 2 * self.Fp, D, **fk))
         self.w2 = tnn.Parameter(torch.zeros(El, D, self.Fp, **fk))
         self.w13.expert_parallel = self.ep > 1
@@ -341,6 +345,8 @@ class MoE(tnn.Module):
     def reset_parameters(self, std, g):
         F, Fp = self.F, self.Fp
         self.gate.normal_(0, std, generator=g)
+        if self.noise is not None:
+            self.noise.normal_(0, std, generator=g)
         # under EP draw all E experts exactly as the unsharded model does and keep this rank's
         # slice: every EP rank then holds distinct experts, and rank r's shard equals
         # shard_experts(unsharded init, r, P) (a per-rank E/P draw from the shared generator
@@ -368,6 +374,10 @@ class MoE(tnn.Module):
         B, T, D = x.shape
         x2 = x.reshape(-1, D)
         logits = router_logits(x2, self.gate)
+        if self.noise is not None:
+            # deepseekv3.ipynb:1037-1039 -- applied in eval too, exactly as the reference does;
+            # the fp32 logits keep the noise draw at full precision
+            logits = logits + torch.nn.functional.softplus(router_logits(x2, self.noise)) * torch.randn_like(logits)
         idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
         y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group,
                              fp8=c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0)
@@ -690,6 +700,8 @@ def _layer_to_ref(l: DSV3Layer, p):
     sd[p + "mhla.linear.weight"] = a.wo
     m = l.ffn
     sd[p + "moe_block.gate.weight"] = m.gate
+    if m.noise is not None:
+        sd[p + "moe_block.noise.weight"] = m.noise
     sd[p + "moe_block.routing_bias"] = m.routing_bias
     for e in range(m.w13.shape[0]):
         _ffn_to_ref(m, m.F, f"{p}moe_block.experts.{e}.", sd, e)
@@ -711,6 +723,8 @@ def _layer_from_ref(l: DSV3Layer, sd, p):
     a.wo.copy_(sd[p + "mhla.linear.weight"])
     m = l.ffn
     m.gate.copy_(sd[p + "moe_block.gate.weight"])
+    if m.noise is not None:
+        m.noise.copy_(sd[p + "moe_block.noise.weight"])
     m.routing_bias.copy_(sd[p + "moe_block.routing_bias"])
     for e in range(m.w13.shape[0]):
         _ffn_from_ref(m.w13[e], m.w2[e], m.F, sd, f"{p}moe_block.experts.{e}.")

@@ -59,39 +59,72 @@ class _RMS(tnn.Module):
         return self.rmsnorm_layer(x)
 
 
+def _stacked_state_alias(module, pname, pieces):
+    """Keep the reference's state-dict keys for a parameter stored stacked: ``pname`` [sum rows, K]
+    is saved as the reference's separate ``pieces`` = [(key, rows)] and rebuilt from them on
+    load, so one GEMM runs where the notebook runs several (gemma.ipynb state dict)."""
+    def save(mod, sd, prefix, _meta):
+        w = sd.pop(prefix + pname)
+        r = 0
+        for key, n in pieces:
+            sd[prefix + key] = w[r:r + n]
+            r += n
+        return sd
+
+    def load(sd, prefix, *_):
+        keys = [prefix + k for k, _ in pieces]
+        if all(k in sd for k in keys):
+            sd[prefix + pname] = torch.cat([sd.pop(k) for k in keys], 0)
+
+    module._register_state_dict_hook(save)
+    module._register_load_state_dict_pre_hook(load)
+
+
 class MQARef(tnn.Module):
+    """gemma.ipynb:218-259. The notebook's 2 query projections, key and value (four D x D
+    Linears) run as ONE GEMM on a stacked [2D + 2D, D] weight; the state dict still holds
+    ``multi_query.{j}.weight``, ``key.weight`` and ``value.weight``."""
+
     def __init__(self, c: GemmaRefConfig):
         super().__init__()
         D = c.embeddings_dims
         self.c = c
         self.no_of_q_heads = c.no_of_heads // c.no_kv_heads if c.no_kv_heads > 0 else 1
-        self.multi_query = tnn.ModuleList([snn.Linear(D, D, bias=False) for _ in range(self.no_of_q_heads)])
-        self.key = snn.Linear(D, D, bias=False)
-        self.value = snn.Linear(D, D, bias=False)
-        self.linear_layer = snn.Linear(D * self.no_of_q_heads, D, bias=False)
+        Hq = self.no_of_q_heads
+        self.wqkv = tnn.Parameter(torch.empty((Hq + 2) * D, D))
+        with torch.no_grad():                               # nn.Linear's default init, per piece
+            for i in range(Hq + 2):
+                tnn.init.kaiming_uniform_(self.wqkv[i * D:(i + 1) * D], a=math.sqrt(5))
+        _stacked_state_alias(self, "wqkv", [(f"multi_query.{j}.weight", D) for j in range(Hq)]
+                             + [("key.weight", D), ("value.weight", D)])
+        self.linear_layer = snn.Linear(D * Hq, D, bias=False)
 
     def forward(self, x):
         B, T, D = x.shape
+        Hq = self.no_of_q_heads
         p = self.c.attn_dropout if self.training else 0.0
-        q = torch.stack([qp(x) for qp in self.multi_query], dim=2)      # [B, T, Hq, D]
-        k = self.key(x).unsqueeze(2)                                      # [B, T, 1, D]
-        v = self.value(x).unsqueeze(2)
+        qkv = linear(x, self.wqkv).view(B, T, Hq + 2, D)
+        q, k, v = qkv[:, :, :Hq], qkv[:, :, Hq:Hq + 1], qkv[:, :, Hq + 1:]
         o = flash_attention(gemma_ref_rotate(q), gemma_ref_rotate(k), v, causal=True, scale=1.0 / math.sqrt(D))
         o = dropout(o, p, self.training)                                  # dropout on each head's output
         return dropout(self.linear_layer(o.reshape(B, T, -1)), p, self.training)
 
 
 class GeGLURef(tnn.Module):
+    """gemma.ipynb:269-286: gelu(l1 x) * (l2 x) -> l3. l1 and l2 are ONE GEMM on a stacked
+    [8D, D] weight feeding the fused HIP glu kernel (state dict keeps ``linear_layer{1,2}``)."""
+
     def __init__(self, D):
         super().__init__()
-        self.linear_layer1 = snn.Linear(D, 4 * D, bias=False)
-        self.linear_layer2 = snn.Linear(D, 4 * D, bias=False)
+        self.w12 = tnn.Parameter(torch.empty(8 * D, D))
+        with torch.no_grad():
+            for i in range(2):
+                tnn.init.kaiming_uniform_(self.w12[i * 4 * D:(i + 1) * 4 * D], a=math.sqrt(5))
+        _stacked_state_alias(self, "w12", [("linear_layer1.weight", 4 * D), ("linear_layer2.weight", 4 * D)])
         self.linear_layer3 = snn.Linear(4 * D, D, bias=False)
 
     def forward(self, x):
-        # act(l1 x) * (l2 x) through the fused HIP glu kernel on the concatenated outputs
-        gu = torch.cat([self.linear_layer1(x), self.linear_layer2(x)], dim=-1)
-        return self.linear_layer3(glu(gu, "gelu"))
+        return self.linear_layer3(glu(linear(x, self.w12), "gelu"))
 
 
 class FFNRef(tnn.Module):

@@ -23,7 +23,7 @@ import torch.nn as tnn
 
 from .. import nn as snn
 from ..ops import act, attention_packed, embedding, layer_norm, linear, linear_cross_entropy
-from ..ops.attention import attention_dropout
+from ..ops.attention import attention_dropout, decode_attention
 from ..ops.misc import dropout
 from ..utils.grad import mark_ready
 
@@ -73,11 +73,22 @@ class Block(tnn.Module):
         for b in (self.proj.bias, self.fc1.bias, self.fc2.bias):
             b.zero_()
 
-    def attn(self, x):
+    def attn(self, x, cache=None, pos=0):
         c = self.c
         B, T, D = x.shape
         qkv = linear(x, self.qkv)
         hd = D // c.num_heads
+        if cache is not None:
+            # cached decoding (inference): K/V rows [pos, pos+T) into the preallocated cache, the
+            # queries attend to every cached row (causal with offset) -- split-K decode kernel for
+            # single tokens, flash for the prompt (ops/attention.py decode_attention)
+            H = c.num_heads
+            q4 = qkv.view(B, T, 3 * H, hd)
+            kc, vc = cache
+            kc[:, pos:pos + T] = q4[:, :, H:2 * H]
+            vc[:, pos:pos + T] = q4[:, :, 2 * H:]
+            o = decode_attention(q4[:, :, :H], kc[:, :pos + T], vc[:, :pos + T], causal=True)
+            return self.proj(o.reshape(B, T, D))
         p = c.dropout_rate if self.training else 0.0
         if p > 0:
             q4 = qkv.view(B, T, 3 * c.num_heads, hd)
@@ -88,10 +99,10 @@ class Block(tnn.Module):
             o = attention_packed(qkv, c.num_heads, c.num_heads, causal=True, head_dim=hd)
         return dropout(self.proj(o), p, self.training)
 
-    def forward(self, x):
+    def forward(self, x, cache=None, pos=0):
         c = self.c
         p = c.dropout_rate if self.training else 0.0
-        a = self.attn(self.ln1(x))
+        a = self.attn(self.ln1(x), cache, pos)
         n2, h = self.ln2(a, residual=x)
         m = self.fc2(dropout(act(self.fc1(n2), "gelu_tanh"), p, self.training))
         return h + m
@@ -123,15 +134,15 @@ class GPT(tnn.Module):
         return [[self.token_embed, self.pos_embed]] + [list(l.parameters()) for l in self.layers] + \
             [list(self.ln_f.parameters()) + [self.lm_head]]
 
-    def hidden(self, idx):
+    def hidden(self, idx, cache=None, pos=0):
         c = self.c
         T = idx.shape[1]
-        assert T <= c.block_size
-        x = embedding(self.token_embed, idx, pos=self.pos_embed.view(c.block_size, c.emb_dim)[:T])
+        assert pos + T <= c.block_size
+        x = embedding(self.token_embed, idx, pos=self.pos_embed.view(c.block_size, c.emb_dim)[pos:pos + T])
         x = dropout(x, c.dropout_rate, self.training)
         for i, l in enumerate(self.layers):
             x = mark_ready(x, self.grad_ready_cb, i + 1)
-            x = l(x)
+            x = l(x, None if cache is None else cache[i], pos)
         x = mark_ready(x, self.grad_ready_cb, len(self.layers) + 1)
         return self.ln_f(x)
 
@@ -141,13 +152,39 @@ class GPT(tnn.Module):
             return linear(h, self.lm_head)
         return linear_cross_entropy(h.reshape(-1, h.shape[-1]), self.lm_head, targets.reshape(-1))
 
+    # ------------------------------------------------------------ cached decoding
+    @property
+    def max_context(self):
+        return self.c.block_size
+
+    def new_cache(self, B, Tmax):
+        from ..infer.cache import KVCache
+        c = self.c
+        return KVCache(c.num_layers, B, Tmax, c.num_heads, c.emb_dim // c.num_heads,
+                       device=self.token_embed.device, dtype=self.token_embed.dtype)
+
+    def step(self, ids, cache, pos):
+        """Write ids' K/V at cache rows [pos, pos+T) (learned positions pos..pos+T-1), return the
+        last position's logits [B, V]."""
+        h = self.hidden(ids, cache, pos)
+        return linear(h[:, -1:], self.lm_head).float()[:, -1]
+
     @torch.no_grad()
-    def generate(self, idx, max_new_tokens, greedy=True, temperature=1.0, top_k=None, generator=None):
-        """gpt-jax.ipynb:821-829: crop to block_size, argmax (greedy by default)."""
+    def generate(self, idx, max_new_tokens, greedy=True, temperature=1.0, top_k=None, generator=None,
+                 eos_token_id=None, stats=None):
+        """gpt-jax.ipynb:821-829 (greedy by default). While prompt + new tokens fit the learned
+        position table (block_size) this is KV-cached: one prefill, then one token per step. Past
+        block_size the reference crops the window to the last block_size tokens, which shifts
+        every token's position embedding, so no cache can stand in: that tail re-forwards the
+        cropped window exactly as the reference does."""
+        from ..infer.generate import generate
         from ..infer.sampling import sample
         was = self.training
         self.eval()
-        for _ in range(max_new_tokens):
+        n_cached = max(0, min(max_new_tokens, self.c.block_size - idx.shape[1]))
+        if n_cached:
+            idx = generate(self, idx, n_cached, temperature, top_k, None, greedy, eos_token_id, generator, stats)
+        for _ in range(max_new_tokens - n_cached):
             lg = self(idx[:, -self.c.block_size:])[:, -1].float()
             idx = torch.cat([idx, sample(lg, temperature, top_k, greedy, generator)], 1)
         self.train(was)

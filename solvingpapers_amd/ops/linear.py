@@ -31,19 +31,42 @@ DGRAD_WT = os.environ.get("SPA_DGRAD_WT", "1") != "0"
 DGRAD_WT_MIN_NUMEL = int(os.environ.get("SPA_DGRAD_WT_MIN", str(1 << 18)))
 # id(w) -> (validity key, W^T, weakref(w)); entries leave with their tensor (weakref.finalize).
 # Not a WeakKeyDictionary: its lookups compare tensor keys with ==, which is elementwise.
+#
+# CONTRACT (also for the fp8 weight images of ops/moe.py): a cached image is reused while
+#   (a) the global weight epoch (ops.moe.bump_weight_epoch) and (b) the tensor's own _version
+# are unchanged. Every in-framework writer of parameters bumps the epoch: the fused optimizers
+# (train/optim.py _run), checkpoint.load, DataParallel.broadcast_params / gather_params
+# (ZeRO-1). (b) catches torch in-place ops ON THE PARAMETER TENSOR ITSELF, but NOT writes
+# through the FlatParams buffer (utils/flat.py attaches params as views with ``p.data = view``,
+# so each keeps its own version counter) nor raw kernels. Any other code that rewrites weights
+# (e.g. a custom optimizer, ``flat.param.copy_``) must call ``invalidate_weight_caches()``
+# before the next backward, or dX silently uses the stale W^T. Trainer checks the epoch moved
+# after each optimizer step (train/trainer.py). While a HIP graph is captured the cache is
+# bypassed: the transpose is recorded into the graph, so replays rebuild it from the live W.
 _WT_CACHE: dict = {}
+
+
+def invalidate_weight_caches():
+    """Mark every cached weight image (W^T, fp8) stale; call after writing weights by hand."""
+    from .moe import bump_weight_epoch
+    bump_weight_epoch()
 
 
 def transposed_weight(w: torch.Tensor):
     """Contiguous W^T for the dgrad product, or None where it does not apply. Valid while the
     optimizer's weight epoch (bumped by every fused optimizer step) and the tensor's version
-    counter (bumped by any torch in-place update) are unchanged."""
+    counter (bumped by any torch in-place update) are unchanged -- see CONTRACT above."""
     if not (DGRAD_WT and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
             and w.numel() >= DGRAD_WT_MIN_NUMEL and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
             and w.data_ptr() % 16 == 0):
         return None
     from .layout import transpose2d
     from .moe import _WEIGHT_EPOCH
+    if torch.cuda.is_current_stream_capturing():
+        # never hand an eager image to a graph (replays would not refresh it) and never keep a
+        # capture-time tensor in the global cache
+        with torch.no_grad():
+            return transpose2d(w)
     key = (_WEIGHT_EPOCH[0], w._version, w.data_ptr())
     hit = _WT_CACHE.get(id(w))
     if hit is not None and hit[2]() is not w:

@@ -131,6 +131,7 @@ class DataParallel:
                                                      group=self.group, async_op=True))
         for w in works:
             w.wait()
+        _invalidate()
 
     def broadcast_params(self, src: int = 0):
         """Make every replica start from the same parameters: dense buckets from rank ``src``
@@ -152,3 +153,11 @@ class DataParallel:
                 for b in self.flat.buckets:
                     if b.index in self.expert_buckets:
                         dist.broadcast(self.flat.param[b.start:b.end], src=esrc, group=grp)
+        _invalidate()
+
+
+def _invalidate():
+    """params were rewritten through the flat buffer: cached W^T / fp8 images are stale
+    (ops/linear.py CONTRACT)."""
+    from ..ops.linear import invalidate_weight_caches
+    invalidate_weight_caches()

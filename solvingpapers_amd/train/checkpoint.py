@@ -118,6 +118,8 @@ def load(path: str, flat, optimizer=None, buffers: Optional[Dict[str, torch.Tens
         raise RuntimeError(f"checkpoint written with world size {obj['world_size']}, running {world}")
     with torch.no_grad():
         flat.param.copy_(obj["param"].to(flat.param.device))
+    from ..ops.linear import invalidate_weight_caches
+    invalidate_weight_caches()          # written through the flat buffer (ops/linear.py CONTRACT)
     if optimizer is not None and obj["optimizer"] is not None:
         dev = flat.param.device
         optimizer.load_state_dict({k: (v.to(dev) if isinstance(v, torch.Tensor) else v)

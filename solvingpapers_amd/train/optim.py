@@ -24,12 +24,19 @@ class FlatOptimizer:
                  graph_safe: bool = False, skip_nonfinite: bool = True):
         self.flat = flat
         # skip_nonfinite: compute the global grad norm even without clipping so a non-finite
-        # gradient skips the update on every rank alike (clip_coef)
+        # gradient skips the update on every rank alike (clip_coef). Cost: one extra
+        # memory-bound pass over the gradients (sqsum, ~2 bytes/param) plus the norm's
+        # all-reduces per optimizer step when no clipping was asked for.
         self.skip_nonfinite = skip_nonfinite
-        # graph_safe: lr and step live on the device ([lr, step] fp32) so a captured HIP graph of
-        # the whole training step replays with the right bias correction / schedule (set_lr)
+        # On the GPU lr and step live on the device ([lr, step] fp32): a skipped step (NaN
+        # coefficient) then does not advance Adam's bias correction -- the step counter moves by
+        # isfinite(coef) without a host sync -- and a captured HIP graph of the whole training
+        # step replays with the right bias correction / schedule (set_lr). ``graph_safe`` is
+        # kept for API compatibility; the device form is always used on the GPU.
+        self.graph_safe = graph_safe
         self.hyper = (torch.tensor([lr, 0.0], dtype=torch.float32, device=flat.device)
-                      if graph_safe and flat.device.type == "cuda" else None)
+                      if flat.device.type == "cuda" else None)
+        self._host_steps = 0          # CPU: applied (finite) steps
         # tensor parallelism: params tagged ``tp_replicated`` are identical on every TP rank and
         # counted once; the squared norm of everything else is summed over the TP group
         self.tp_group = tp_group
@@ -85,12 +92,17 @@ class FlatOptimizer:
         step (see FlatParams.wait_bucket)."""
         self.step_count += 1
         from ..ops.moe import bump_weight_epoch
-        bump_weight_epoch()                  # cached fp8 expert-weight images go stale now
+        bump_weight_epoch()                  # cached fp8 / W^T weight images go stale now
+        coef = self.clip_coef()
         if self.hyper is not None:
             if not torch.cuda.is_current_stream_capturing():
                 self.hyper[0].fill_(lr)
-            self.hyper[1].add_(1.0)
-        coef = self.clip_coef()
+            if coef is None:
+                self.hyper[1].add_(1.0)
+            else:                            # a skipped (non-finite) step does not count
+                self.hyper[1].add_(torch.isfinite(coef).to(torch.float32)[0])
+        elif coef is None or bool(torch.isfinite(coef).all()):
+            self._host_steps += 1
         segs = self._segments()
         if overlap and self.flat.device.type == "cuda":
             main = torch.cuda.current_stream(self.flat.device)
@@ -194,7 +206,12 @@ class FlatOptimizer:
             self.hyper[0].fill_(lr)
 
     def device_step(self) -> int:
-        return int(self.hyper[1].item()) if self.hyper is not None else self.step_count
+        """Applied optimizer steps (skipped non-finite steps excluded)."""
+        return int(self.hyper[1].item()) if self.hyper is not None else self._host_steps
+
+    def _kstep(self) -> int:
+        """host step handed to the kernels (ignored on the GPU, where hyper[1] is used)."""
+        return self.step_count if self.hyper is not None else max(1, self._host_steps)
 
 
 def _subtract(ranges, holes):
@@ -236,13 +253,13 @@ class FlatAdamW(FlatOptimizer):
         n = b - a
         K.adamw_(f.param[a:b], self.master[so:so + n] if self.master is not None else None, f.grad[a:b],
                  self.m[so:so + n], self.v[so:so + n], lr, self.b1, self.b2, self.eps,
-                 self.weight_decay if dec else 0.0, self.step_count, coef, self.adam_l2, self.hyper)
+                 self.weight_decay if dec else 0.0, self._kstep(), coef, self.adam_l2, self.hyper)
 
     def state_dict(self):
         return {"step": self.device_step(), "m": self.m, "v": self.v, "master": self.master, "lr": self.lr}
 
     def load_state_dict(self, sd):
-        self.step_count = int(sd["step"])
+        self.step_count = self._host_steps = int(sd["step"])
         if self.hyper is not None:
             self.hyper[1].fill_(float(self.step_count))
         self.m.copy_(sd["m"])
@@ -275,10 +292,12 @@ class FlatSGD(FlatOptimizer):
                self.weight_decay if dec else 0.0, coef, self.hyper)
 
     def state_dict(self):
-        return {"step": self.step_count, "buf": self.buf, "master": self.master, "lr": self.lr}
+        return {"step": self.device_step(), "buf": self.buf, "master": self.master, "lr": self.lr}
 
     def load_state_dict(self, sd):
-        self.step_count = int(sd["step"])
+        self.step_count = self._host_steps = int(sd["step"])
+        if self.hyper is not None:
+            self.hyper[1].fill_(float(self.step_count))
         if self.buf is not None and sd.get("buf") is not None:
             self.buf.copy_(sd["buf"])
         if self.master is not None and sd.get("master") is not None:

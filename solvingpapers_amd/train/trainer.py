@@ -83,13 +83,21 @@ class Trainer:
             ep_group, expert_dp_group = groups.ep_group, groups.expert_dp_group
         self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-        self.dp_size = (dist.get_world_size(dp_group) if dp_group is not None else self.world) \
-            if self.world > 1 else 1
-        groups = model.param_groups() if hasattr(model, "param_groups") else None
-        self.flat = FlatParams(model, groups=groups, align=64 * max(1, self.world),
+        if self.groups is not None:
+            # an explicit layout: dp_group None means dp == 1 (e.g. tp == world), NOT the world
+            # group -- a DataParallel there would broadcast rank 0's TP shards to every rank and
+            # average the gradients of different shards
+            self.dp_size = self.groups.dp
+            use_dp = self.groups.dp > 1
+        else:
+            self.dp_size = (dist.get_world_size(dp_group) if dp_group is not None else self.world) \
+                if self.world > 1 else 1
+            use_dp = self.world > 1
+        pgroups = model.param_groups() if hasattr(model, "param_groups") else None
+        self.flat = FlatParams(model, groups=pgroups, align=64 * max(1, self.world),
                                grad_dtype=cfg.grad_dtype, param_dtype=cfg.param_dtype)
         self.dp = DataParallel(model, self.flat, group=dp_group, zero1=cfg.zero1,
-                               expert_dp_group=expert_dp_group) if self.world > 1 else None
+                               expert_dp_group=expert_dp_group) if use_dp else None
         if self.dp is not None:
             # before the optimizer is built: FlatOptimizer copies its fp32 master from the
             # params at construction, so a later broadcast would be undone by the first step
@@ -211,8 +219,12 @@ class Trainer:
         sync_sp = getattr(self.model, "sync_sequence_parallel_grads", None)
         if sync_sp is not None:
             sync_sp()
+        from ..ops.moe import _WEIGHT_EPOCH
+        epoch = _WEIGHT_EPOCH[0]
         with annotate("optimizer"):
             self.opt.step(lr=self.lr_at(step), overlap=c.opt_overlap)
+        # cached W^T / fp8 weight images are keyed on this epoch (ops/linear.py CONTRACT)
+        assert _WEIGHT_EPOCH[0] != epoch, "optimizer step did not invalidate the cached weight images"
         if self.dp is not None:
             self.dp.gather_params()
         ok = self.opt.last_step_ok()

@@ -38,11 +38,12 @@ class _Args:
     ignore_pad_token_in_loss = False
 
 
-def _ref_model():
+def _ref_model(noisy=False):
     from torch.nn import RMSNorm
+    args = type("_NoisyArgs", (_Args,), {"noisy_topk": True}) if noisy else _Args
     ns = refexec.exec_cells(NB, ["precompute_pos_embeddings", "apply_pos_embeddings", "Normalization", "swish",
                                  "SWiGLUExpert", "MoeLayer", "LatentAttention", "MHLA", "DecoderLayer", "Block",
-                                 "DeepSeekV3"], {"modelargs": _Args, "RMSNorm": RMSNorm, "dataclass": dataclass})
+                                 "DeepSeekV3"], {"modelargs": args, "RMSNorm": RMSNorm, "dataclass": dataclass})
     torch.manual_seed(0)
     ref = ns["DeepSeekV3"](embeddings_dim=64, vocab_size=97, dropout=0.0, mtp_heads=0, device="cpu")
     with torch.no_grad():
@@ -51,9 +52,9 @@ def _ref_model():
     return ref
 
 
-def _ours():
+def _ours(noisy=False):
     c = ds.config("dsv3_ref", vocab_size=97, block_size=16, dim=64, n_layers=2, n_heads=4, latent_dim=16,
-                  n_experts=4, top_k=2, dropout=0.0, attn_dropout=0.0)
+                  n_experts=4, top_k=2, dropout=0.0, attn_dropout=0.0, noisy_topk=noisy)
     return ds.DeepSeekV3(c)
 
 
@@ -118,6 +119,48 @@ def test_dsv3_ref_training_grads_and_bias_update():
             assert mo.w13.grad[e, F_:mo.Fp].abs().max() == 0          # padding stays inert
         sh = l.moe_block.shared_expert
         assert torch.allclose(sh.w1.weight.grad, mo.shared.w13.grad[:F_], atol=1e-5)
+
+
+def test_dsv3_ref_noisy_topk_matches_reference():
+    """noisy_topk=True (deepseekv3.ipynb:390,1026-1039): the extra ``noise`` Linear round-trips
+    through the reference state dict, and with the same torch RNG state both models draw the
+    same N(0,1) noise per (token, expert) in the same order -> equal logits, loss, gate / noise
+    gradients and routing-bias update. The noise is on in eval too, as in the reference."""
+    import torch.nn.functional as F
+    ref, m = _ref_model(noisy=True), _ours(noisy=True)
+    sd = ref.state_dict()
+    assert any(k.endswith("moe_block.noise.weight") for k in sd)
+    m.from_reference_state_dict(sd)
+    out = m.to_reference_state_dict()
+    assert set(sd) == set(out)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(0, 97, (2, 16), generator=g)
+    y = torch.randint(0, 97, (2, 16), generator=g)
+    ref.eval()
+    m.eval()
+    with torch.no_grad():
+        torch.manual_seed(11)
+        a = ref(x, inference=True)
+        torch.manual_seed(11)
+        b = m(x)
+        torch.manual_seed(12)
+        c = m(x)
+    assert torch.allclose(a, b, atol=1e-5), (a - b).abs().max()
+    assert not torch.allclose(b, c, atol=1e-6)                      # a different draw moves the routing
+    ref.train()
+    m.train()
+    torch.manual_seed(13)
+    lr = F.cross_entropy(ref(x).view(-1, 97), y.view(-1))
+    lr.backward()
+    torch.manual_seed(13)
+    lo = m(x, y)
+    lo.backward()
+    assert abs(lr.item() - lo.item()) < 1e-5
+    for i, l in enumerate(ref.decoder.decoder):
+        mo = m.layers[i].ffn
+        assert torch.allclose(l.moe_block.routing_bias, mo.routing_bias, atol=1e-7)
+        assert torch.allclose(l.moe_block.gate.weight.grad, mo.gate.grad, atol=1e-5)
+        assert torch.allclose(l.moe_block.noise.weight.grad, mo.noise.grad, atol=1e-5)
 
 
 def test_dsv3_ref_cached_generate_matches_recompute():

@@ -41,8 +41,17 @@ def test_cached_generation_matches_reforward(family):
 def test_generic_driver_uncached_model_crops_window():
     torch.manual_seed(0)
     m = gpt.GPT(gpt.config("gpt_tiny_cpu", block_size=8)).eval()
+
+    class Uncached(torch.nn.Module):       # forward only: no new_cache / step protocol
+        def __init__(self, inner):
+            super().__init__()
+            self.inner, self.c = inner, inner.c
+
+        def forward(self, x):
+            return self.inner(x)
+
     ids = torch.randint(0, 60, (1, 3))
-    out = generate(m, ids, 12, greedy=True)
+    out = generate(Uncached(m).eval(), ids, 12, greedy=True)
     assert out.shape == (1, 15)
     ref = ids
     with torch.no_grad():
@@ -91,3 +100,48 @@ def test_kv_cache_write_and_overflow():
     assert c.nbytes() == 2 * 2 * 4 * 2 * 8 * 4
     with pytest.raises(ValueError):
         c.write(0, torch.randn(1, 2, 2, 8), torch.randn(1, 2, 2, 8), 3)
+
+
+def test_topk_sampling_single_cached_call_and_eos_stop():
+    """api.topk_sampling (deepseekv3.ipynb:1849-1873) runs ONE cached generate call: with
+    top_k=1 it equals the reference's per-token full re-forward, and it stops right after EOS."""
+    from solvingpapers_amd import api
+    from solvingpapers_amd.models import deepseekv3 as ds
+    m = ds.DeepSeekV3(ds.config("dsv3_tiny"), seed=0).eval()
+    calls = {"n": 0}
+    orig = m.generate
+
+    def counted(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+
+    m.generate = counted
+    x = torch.randint(0, 512, (1, 4), generator=torch.Generator().manual_seed(0))
+    out = api.topk_sampling(m, x, max_length=12, top_k=1)
+    assert calls["n"] == 1 and out.shape == (1, 12)
+    cur = x
+    with torch.no_grad():
+        for _ in range(8):
+            cur = torch.cat([cur, m(cur)[:, -1].argmax(-1, keepdim=True)], 1)
+    assert torch.equal(out, cur)
+    eos = int(cur[0, 6])                         # the 3rd generated token
+    first = int((cur[0, 4:] == eos).nonzero()[0, 0]) + 4
+    out2 = api.topk_sampling(m, x, max_length=12, top_k=1, eos_token_id=eos)
+    assert torch.equal(out2, cur[:, :first + 1])
+
+
+def test_gpt_cached_generate_matches_window_reforward():
+    """GPT now has a KV cache (learned positions): cached greedy decoding equals the reference's
+    crop-and-re-forward loop (gpt/gpt-jax.ipynb:821-829), including past block_size where the
+    window slides and the tail falls back to re-forwarding."""
+    from solvingpapers_amd.models import gpt
+    c = gpt.config("gpt_ref", num_layers=2, block_size=24, emb_dim=64)
+    m = gpt.GPT(c, seed=0).eval()
+    x = torch.randint(0, 65, (2, 5), generator=torch.Generator().manual_seed(1))
+    out = m.generate(x, 30)
+    cur = x
+    with torch.no_grad():
+        for _ in range(30):
+            cur = torch.cat([cur, m(cur[:, -24:])[:, -1].argmax(-1, keepdim=True)], 1)
+    assert torch.equal(out, cur)
+    assert m.new_cache(2, 24)[0][0].shape == (2, 24, 1, 64)

@@ -188,6 +188,63 @@ def test_dgrad_transposed_weight_cache_tracks_updates():
     assert rel(dx(), dy.float() @ w.detach().float()) < 1e-2
 
 
+def test_dgrad_weight_cache_flat_writes_and_capture(tmp_path):
+    """Writes through the FlatParams buffer (checkpoint.load's flat.param.copy_) invalidate the
+    cached W^T; a HIP-graph capture never reads the eager cache (replays see weight updates)."""
+    from solvingpapers_amd.ops import linear
+    from solvingpapers_amd.train import checkpoint as ckpt
+    from solvingpapers_amd.utils.flat import FlatParams
+    torch.manual_seed(1)
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter((torch.randn(1024, 512, device=DEV) * 0.02).bfloat16())
+
+    m = M()
+    flat = FlatParams(m)
+    x = torch.randn(64, 512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    dy = torch.randn(64, 1024, device=DEV, dtype=torch.bfloat16)
+
+    def dx():
+        x.grad = None
+        linear(x, m.w).backward(dy)
+        return x.grad
+
+    ckpt.save(str(tmp_path), 0, flat, None, {})
+    saved = m.w.detach().clone()
+    assert rel(dx(), dy.float() @ m.w.detach().float()) < 1e-2            # fills the cache
+    with torch.no_grad():
+        flat.param.mul_(-2.0)                                               # change the weights ...
+    ckpt.load(str(tmp_path), flat, None, {}, restore_rng=False)            # ... and restore them
+    assert torch.equal(m.w.detach(), saved)
+    with torch.no_grad():
+        flat.param.mul_(3.0)
+    ckpt.load(str(tmp_path), flat, None, {}, restore_rng=False)
+    assert rel(dx(), dy.float() @ saved.float()) < 1e-2
+
+    # capture fwd + bwd with the cache warm, then change W eagerly (epoch bump) and replay
+    static_x = x.detach().clone().requires_grad_()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            static_x.grad = None
+            linear(static_x, m.w).backward(dy)
+    torch.cuda.current_stream().wait_stream(s)
+    static_x.grad = None
+    with torch.cuda.graph(g):
+        linear(static_x, m.w).backward(dy)
+    with torch.no_grad():
+        flat.param.mul_(-0.25)
+    from solvingpapers_amd.ops.linear import invalidate_weight_caches
+    invalidate_weight_caches()
+    g.replay()
+    torch.cuda.synchronize()
+    assert rel(static_x.grad, dy.float() @ m.w.detach().float()) < 1e-2
+
+
 def test_adamw_matches_torch():
     from solvingpapers_amd.ops import optim_kernels as K
     n = 10007
@@ -270,7 +327,9 @@ def test_flash_attention(B, Tq, Tk, H, Hkv, hd, causal):
 
 @pytest.mark.parametrize("Hkv,dqk,dv", [(4, 192, 128), (1, 96, 64), (2, 128, 64)])
 def test_flash_attention_mixed_head_dims(Hkv, dqk, dv):
-    """MLA-shaped heads (q/k 128 nope + 64 rope, v 128) zero-padded onto the flash kernel."""
+    """Mixed q/k vs v head dims: (192, 128) is the MLA shape (q/k 128 nope + 64 rope, v 128) and
+    runs its own unpadded kernel pair; the other pairs have no instantiation and are zero-padded
+    onto the smallest kernel pair (ops/attention.py flash_attention)."""
     from solvingpapers_amd.ops import flash_attention
     torch.manual_seed(3)
     B, T, H = 2, 300, 4

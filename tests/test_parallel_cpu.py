@@ -354,3 +354,59 @@ def test_expert_parallel_fp8_dispatch_matches_local_fp8():
         ref13 = W13r.grad[rank * 2:(rank + 1) * 2]
         assert ((torch.from_numpy(g13) - ref13).norm() / ref13.norm()) < 5e-2
         assert torch.allclose(torch.from_numpy(g2), W2r.grad[rank * 2:(rank + 1) * 2], atol=1e-4)
+
+
+def _gemma_tp_cfg():
+    from solvingpapers_amd.models import gemma
+    return gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
+
+
+def _trainer_batches():
+    ids = torch.randint(0, 64, (2, 13), generator=torch.Generator().manual_seed(3))
+    return lambda i: (ids[:, :-1], ids[:, 1:])
+
+
+def _trainer_tp_worker(rank, world, port, q):
+    _init(rank, world, port)
+    from solvingpapers_amd.models import gemma
+    from solvingpapers_amd.parallel.groups import build_groups
+    from solvingpapers_amd.train.trainer import TrainConfig, Trainer
+    groups = build_groups(tp=2)
+    local = gemma.Gemma(_gemma_tp_cfg(), tp_group=groups.tp_group, seed=5)
+    tr = Trainer(local, TrainConfig(steps=3, lr=1e-2, clip=1.0, resume="never"), _trainer_batches(), groups=groups)
+    assert tr.dp is None and tr.dp_size == 1
+    tr.fit()
+    q.put((rank, {n: p.detach().clone().numpy() for n, p in local.named_parameters()}))
+    dist.destroy_process_group()
+
+
+def test_trainer_tensor_parallel_keeps_shards_and_matches_unsharded():
+    """Trainer(groups=tp=world) must not wrap a DataParallel over the world (it would
+    broadcast rank 0's shards and average different shards' gradients). After 3 AdamW steps with
+    TP-aware clipping each rank's shards equal the slices of the unsharded run."""
+    from solvingpapers_amd.models import gemma
+    from solvingpapers_amd.train.trainer import TrainConfig, Trainer
+    full = gemma.Gemma(_gemma_tp_cfg(), seed=5)
+    Trainer(full, TrainConfig(steps=3, lr=1e-2, clip=1.0, resume="never"), _trainer_batches()).fit()
+    fp = {n: p.detach() for n, p in full.named_parameters()}
+    out = _run(_trainer_tp_worker, 2)
+    world = 2
+    assert not torch.equal(torch.from_numpy(out[0][1]["layers.0.wq"]), torch.from_numpy(out[1][1]["layers.0.wq"]))
+    for rank, params in out:
+        for n, g in params.items():
+            g = torch.from_numpy(g)
+            f = fp[n]
+            if n == "embed":
+                vl = f.shape[0] // world
+                f = f[rank * vl:(rank + 1) * vl]
+            elif n.endswith(".wq"):
+                h = f.shape[0] // world
+                f = f[rank * h:(rank + 1) * h]
+            elif n.endswith(".wo") or n.endswith(".w2"):
+                h = f.shape[1] // world
+                f = f[:, rank * h:(rank + 1) * h]
+            elif n.endswith(".w13"):
+                F2 = f.shape[0] // 2
+                fl = F2 // world
+                f = torch.cat([f[rank * fl:(rank + 1) * fl], f[F2 + rank * fl:F2 + (rank + 1) * fl]])
+            assert torch.allclose(g, f, atol=1e-4, rtol=1e-3), (rank, n, (g - f).abs().max())
