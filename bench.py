@@ -57,7 +57,11 @@ def self_launch(n: int, argv) -> int:
     exec: nothing here has touched the GPU, and the parent only waits) and return its exit
     code. Rendezvous on 127.0.0.1 (the container hostname may not resolve)."""
     env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    # RCCL moves buffers between the ranks' GPUs through HIP IPC; on these hosts the driver only
+    # supports dmabuf IPC (HSA_ENABLE_IPC_MODE_LEGACY=0), which the harness already exports. Only
+    # default it when the caller's environment says nothing, never override a set value.
+    if "HSA_ENABLE_IPC_MODE_LEGACY" not in env:
+        env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
     env["SPA_BENCH_SELF"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
@@ -202,6 +206,7 @@ def run(a):
             "world_size": world,
             "backend": tdist.get_backend() if tdist.is_initialized() else "none",
             "device_count": torch.cuda.device_count() if cuda else 0,
+            "streamk_data_parallel": os.environ.get("TENSILE_STREAMK_DATA_PARALLEL"),
             "launcher": "bench.py self-launch" if os.environ.get("SPA_BENCH_SELF") else
                         ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "direct"),
         }

@@ -38,6 +38,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 import torch.nn as tnn
+from types import SimpleNamespace
 
 from ..ops import apply_rope, embedding, glu, layer_norm, linear, linear_cross_entropy, rms_norm
 from ..ops.attention import attention_dropout, flash_attention, mla_attention, split_last
@@ -314,16 +315,50 @@ class DenseFFN(tnn.Module):
         return linear(glu(linear(x, self.w13, fp8=self.fp8), "silu"), self.w2, fp8=self.fp8)
 
 
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class _JoinSide(torch.autograd.Function):
+    """Identity joining the side stream back; its backward queues an end-of-backward wait of the
+    caller's stream on the side stream (weight gradients committed there are then complete)."""
+
+    @staticmethod
+    def forward(ctx, x, side):
+        ctx.side = side
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        side, main = ctx.side, torch.cuda.current_stream()
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
+        return g, None
+
+
 class MoE(tnn.Module):
     """DeepSeekMoE: shared experts + top-k routed experts with aux-free load balancing.
     Under EP (``ep_group`` of size P) this rank holds experts [r*E/P, (r+1)*E/P)."""
 
-    def __init__(self, c: DSV3Config, ep_group=None, **fk):
+    def __init__(self, c: DSV3Config, ep_group=None, ep_group2=None, **fk):
+        """``ep_group2``: a second communicator over the same EP ranks. Given (EP > 1), the
+        layer's tokens run as two chunks -- chunk A on the current stream with ``ep_group``,
+        chunk B on a side compute stream with ``ep_group2`` -- so one chunk's dispatch /
+        combine all-to-alls are on the wire while the other chunk's experts (and the shared
+        expert, issued before the count sync) compute; see _forward_pipelined."""
         super().__init__()
         from ..parallel.expert_parallel import ep_rank_size
         self.c = c
         self.ep_group = ep_group
         self.ep_rank, self.ep = ep_rank_size(ep_group)
+        self.ep_group2 = ep_group2 if self.ep > 1 else None
+        self._side = None
+        if self.ep_group2 is not None:
+            from ..utils.grad import set_multi_stream
+            set_multi_stream(True)        # weight-grad commits come from two streams
         assert c.n_experts % self.ep == 0
         El = c.n_experts // self.ep
         D, F = c.dim, c.ffn_hidden
@@ -368,16 +403,22 @@ class MoE(tnn.Module):
     def expert_params(self):
         return [self.w13, self.w2]
 
-    def forward(self, x):
-        from ..parallel.expert_parallel import ep_moe_ffn
-        c = self.c
-        B, T, D = x.shape
-        x2 = x.reshape(-1, D)
+    def _logits(self, x2):
         logits = router_logits(x2, self.gate)
         if self.noise is not None:
             # deepseekv3.ipynb:1037-1039 -- applied in eval too, exactly as the reference does;
             # the fp32 logits keep the noise draw at full precision
             logits = logits + torch.nn.functional.softplus(router_logits(x2, self.noise)) * torch.randn_like(logits)
+        return logits
+
+    def forward(self, x):
+        from ..parallel.expert_parallel import ep_moe_ffn
+        c = self.c
+        B, T, D = x.shape
+        x2 = x.reshape(-1, D)
+        if self.ep_group2 is not None and x2.shape[0] >= 2:
+            return self._forward_pipelined(x2).view(B, T, D)
+        logits = self._logits(x2)
         idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
         y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group,
                              fp8=c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0)
@@ -387,6 +428,60 @@ class MoE(tnn.Module):
         if c.aux_free and self.training:
             self._update_bias(idx, w, plan)
         return y.view(B, T, D)
+
+    def _forward_pipelined(self, x2):
+        """Two token chunks on two streams / two EP communicators (see __init__). Host order:
+        route + permute + count exchange + shared expert of BOTH chunks, then one host sync per
+        chunk for its split sizes (the GPU is busy with the shared experts meanwhile), then each
+        chunk's dispatch -> experts -> combine on its own stream. A stream waits only for its own
+        chunk's all-to-alls, so the other chunk's grouped GEMMs fill those gaps; autograd runs
+        each backward op on its forward's stream, so the backward overlaps the same way."""
+        from ..parallel.expert_parallel import ep_prepare, ep_run
+        c = self.c
+        N = x2.shape[0]
+        half = N // 2
+        groups = (self.ep_group, self.ep_group2)
+        cuda = x2.is_cuda
+        main = torch.cuda.current_stream(x2.device) if cuda else None
+        if cuda and self._side is None:
+            self._side = torch.cuda.Stream(x2.device)
+        side = self._side if cuda else None
+
+        def on(i):
+            return torch.cuda.stream(side) if (i == 1 and side is not None) else _NullCtx()
+
+        if side is not None:
+            side.wait_stream(main)
+        parts = (x2[:half], x2[half:])
+        fp8 = c.moe_fp8 and cuda and self.Fp % 16 == 0
+        st = []
+        for i in range(2):
+            with on(i):
+                logits = self._logits(parts[i])
+                idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
+                prep = ep_prepare(idx, c.n_experts, groups[i])
+                ys = self.shared(parts[i]) if self.shared is not None else None
+                st.append((idx, w, prep, ys))
+        outs = []
+        for i in range(2):
+            idx, w, prep, ys = st[i]
+            with on(i):
+                y, _ = ep_run(parts[i], w, prep, self.w13, self.w2, c.n_experts, groups[i], fp8=fp8)
+                outs.append(y + ys if ys is not None else y)
+        idx = torch.cat([st[0][0], st[1][0]])
+        w = torch.cat([st[0][1], st[1][1]])
+        counts = st[0][2].plan.counts + st[1][2].plan.counts
+        if side is not None:
+            main.wait_stream(side)
+            for t in (outs[1], st[1][0], st[1][1], st[1][2].plan.counts):
+                t.record_stream(main)
+        y = torch.cat(outs)
+        if side is not None:
+            y = _JoinSide.apply(y, side)
+        self.last_counts = counts
+        if c.aux_free and self.training:
+            self._update_bias(idx, w, SimpleNamespace(counts=counts))
+        return y
 
     @torch.no_grad()
     def _update_bias(self, idx, w, plan):
@@ -404,7 +499,7 @@ class MoE(tnn.Module):
 
 # =============================================================================== layers
 class DSV3Layer(tnn.Module):
-    def __init__(self, c: DSV3Config, dense: bool, ep_group=None, **fk):
+    def __init__(self, c: DSV3Config, dense: bool, ep_group=None, ep_group2=None, **fk):
         super().__init__()
         self.c = c
         self.attn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
@@ -413,7 +508,7 @@ class DSV3Layer(tnn.Module):
         if dense:
             self.ffn = DenseFFN(c.dim, c.dense_hidden or c.ffn_hidden, fp8=c.fp8_linears, **fk)
         else:
-            self.ffn = MoE(c, ep_group, **fk)
+            self.ffn = MoE(c, ep_group, ep_group2, **fk)
 
     @torch.no_grad()
     def reset_parameters(self, g):
@@ -457,12 +552,13 @@ class DSV3Layer(tnn.Module):
 
 
 class DeepSeekV3(tnn.Module):
-    def __init__(self, c: DSV3Config, device=None, dtype=torch.float32, seed: int = 0, ep_group=None):
+    def __init__(self, c: DSV3Config, device=None, dtype=torch.float32, seed: int = 0, ep_group=None,
+                 ep_group2=None):
         super().__init__()
         self.c = c
         fk = dict(device=device, dtype=dtype)
         self.embed = tnn.Parameter(torch.empty(c.vocab_size, c.dim, **fk))     # tied LM head
-        self.layers = tnn.ModuleList([DSV3Layer(c, i < c.n_dense_layers, ep_group, **fk)
+        self.layers = tnn.ModuleList([DSV3Layer(c, i < c.n_dense_layers, ep_group, ep_group2, **fk)
                                       for i in range(c.n_layers)])
         self.norm_f = tnn.Parameter(torch.ones(c.dim, **fk))
         # MTP (deepseekv3.ipynb:1466-1485): norm1 on the shifted-token embedding, norm2 on the
@@ -474,7 +570,7 @@ class DeepSeekV3(tnn.Module):
         self.mtp_norm2_b = tnn.Parameter(torch.zeros(D, **fk))
         self.mtp_proj = tnn.Parameter(torch.empty(D, 2 * D, **fk))
         self.mtp_heads = tnn.ParameterList([tnn.Parameter(torch.empty(D, D, **fk)) for _ in range(c.mtp_heads)])
-        self.mtp_layers = tnn.ModuleList([DSV3Layer(c, False, ep_group, **fk) for _ in range(c.mtp_heads)])
+        self.mtp_layers = tnn.ModuleList([DSV3Layer(c, False, ep_group, ep_group2, **fk) for _ in range(c.mtp_heads)])
         if c.pos_emb == "sinusoidal":
             self.register_buffer("pe", sinusoidal_pe(c.block_size, c.dim, device=device).to(dtype))
         else:

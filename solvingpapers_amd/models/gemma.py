@@ -242,9 +242,13 @@ class GemmaBlock(tnn.Module):
         self.w13.copy_(torch.cat([full["w13"][r * fl:(r + 1) * fl], full["w13"][F + r * fl:F + (r + 1) * fl]]))
         self.w2.copy_(full["w2"][:, r * fl:(r + 1) * fl])
 
-    def forward(self, res, delta, tp_group=None, cache=None, pos=0, sp=False):
+    def forward(self, res, delta, tp_group=None, cache=None, pos=0, sp=False, kv_prefix=None, want_kv=False):
         """``sp``: sequence parallel -- res/delta are [B, T/tp, D] shards; the TP regions
-        open with an all-gather over T and close with a reduce-scatter over T."""
+        open with an all-gather over T and close with a reduce-scatter over T.
+        ``kv_prefix`` / ``want_kv`` (training, TP chunk pipelining in Gemma.hidden): this call
+        holds tokens [pos, pos+T) of the sequence; its queries also attend to the (RoPE'd) K/V
+        of the earlier tokens ``kv_prefix`` = (k, v), and ``want_kv`` returns this chunk's own
+        (k, v) for the next chunk."""
         from ..parallel.tensor_parallel import (copy_to_tp, gather_seq, reduce_from_tp, reduce_grad_tp,
                                                 reduce_scatter_seq, scale_grad)
         c = self.c
@@ -278,7 +282,16 @@ class GemmaBlock(tnn.Module):
             f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
             return h2, reduce_from_tp(linear(f, self.w2), tp_group)
         qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, pos, interleaved=False, head_dim=hd)
-        if cache is None:
+        kv_out = None
+        if cache is None and (kv_prefix is not None or want_kv):
+            x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
+            k4, v4 = x4[:, :, self.hl:self.hl + KV], x4[:, :, self.hl + KV:]
+            kv_out = (k4, v4)
+            if kv_prefix is not None:     # causal with offset: query i sees keys <= prefix + i
+                k4 = torch.cat([kv_prefix[0], k4], 1)
+                v4 = torch.cat([kv_prefix[1], v4], 1)
+            o = flash_attention(x4[:, :, :self.hl], k4, v4, causal=True).reshape(B, T, self.hl * hd)
+        elif cache is None:
             o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
         else:  # KV-cached inference: write this step's K/V, attend over the cache
             x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
@@ -291,18 +304,57 @@ class GemmaBlock(tnn.Module):
         a = close(linear(o, self.wo), tp_group)
         n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
         f = glu(linear(gather_seq(n2, tp_group) if sp else copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
-        return h2, close(linear(f, self.w2), tp_group)
+        out = close(linear(f, self.w2), tp_group)
+        return (h2, out, kv_out) if want_kv else (h2, out)
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class _JoinStreams(torch.autograd.Function):
+    """Identity at the end of the two-stream forward. Its backward runs first in the backward
+    pass and queues an end-of-backward callback that makes the caller's stream wait for the
+    side stream: weight gradients committed from it (utils/grad.py) are complete before the
+    optimizer (or a DP bucket launched after backward) reads them."""
+
+    @staticmethod
+    def forward(ctx, x, side):
+        ctx.side = side
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        side, main = ctx.side, torch.cuda.current_stream()
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
+        return g, None
 
 
 class Gemma(tnn.Module):
     def __init__(self, c: GemmaConfig, device=None, dtype=torch.float32, tp_group=None, seed=0,
-                 sequence_parallel=False):
+                 sequence_parallel=False, tp_group2=None):
+        """``tp_group2``: a second communicator over the SAME TP ranks. Given (TP > 1, no
+        sequence parallelism), training splits each sequence into two halves that run as two
+        pipelines -- half A on the current stream with ``tp_group``, half B on a second compute
+        stream with ``tp_group2`` -- so every TP all-reduce of one half overlaps the other
+        half's GEMMs / attention, forward AND backward (autograd runs each backward op on its
+        forward's stream). Half B's queries attend to half A's K/V (causal with offset), so
+        the result equals the unsplit model; see hidden()."""
         super().__init__()
         from ..parallel.tensor_parallel import tp_rank_size
         self.c = c
         self.tp_group = tp_group
         self.tp_rank, self.tp = tp_rank_size(tp_group)
         self.sp = bool(sequence_parallel) and self.tp > 1
+        self.tp_group2 = tp_group2 if (self.tp > 1 and not self.sp) else None
+        self._side = None
+        if self.tp_group2 is not None:
+            from ..utils.grad import set_multi_stream
+            set_multi_stream(True)        # weight-grad commits come from two streams
         assert c.vocab_size % self.tp == 0
         fk = dict(device=device, dtype=dtype)
         self.embed = tnn.Parameter(torch.empty(c.vocab_size // self.tp, c.dim, **fk))   # vocab-parallel, tied head
@@ -327,10 +379,64 @@ class Gemma(tnn.Module):
     def param_groups(self):
         return [[self.embed]] + [list(l.parameters()) for l in self.layers] + [[self.norm_f]]
 
+    def _pipelined(self, ids, cache):
+        return (self.tp_group2 is not None and cache is None and torch.is_grad_enabled() and self.training
+                and ids.shape[1] % 2 == 0 and ids.shape[1] >= 2)
+
+    def _hidden_pipelined(self, ids):
+        """Two-chunk TP pipeline (see __init__): per layer, half A runs on the current stream
+        (``tp_group``), then half B on the side stream (``tp_group2``) once A's K/V exist.
+        Each stream waits only on its own communicator, so while one half's all-reduce is on
+        the wire the other half's kernels run; the backward replays the same two streams."""
+        from ..parallel.tensor_parallel import vocab_parallel_embedding
+        c = self.c
+        T = ids.shape[1]
+        half = T // 2
+        groups = (self.tp_group, self.tp_group2)
+        cuda = ids.is_cuda
+        main = torch.cuda.current_stream(ids.device) if cuda else None
+        if cuda and self._side is None:
+            self._side = torch.cuda.Stream(ids.device)
+        side = self._side if cuda else None
+
+        def on(i):
+            return torch.cuda.stream(side) if (i == 1 and side is not None) else _Null()
+
+        if side is not None:
+            side.wait_stream(main)
+        chunks = (ids[:, :half], ids[:, half:])
+        delta = [None, None]
+        for i in range(2):
+            with on(i):
+                delta[i] = vocab_parallel_embedding(self.embed, chunks[i], groups[i], scale=math.sqrt(c.dim))
+        res = [None, None]
+        for l in self.layers:
+            with on(0):
+                res[0], delta[0], kv = l(res[0], delta[0], groups[0], None, 0, False, want_kv=True)
+            if side is not None:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                for t in kv:
+                    t.record_stream(side)
+            with on(1):
+                res[1], delta[1] = l(res[1], delta[1], groups[1], None, half, False, kv_prefix=kv)
+        outs = [None, None]
+        for i in range(2):
+            with on(i):
+                outs[i], _ = rms_norm(delta[i], self.norm_f, c.norm_eps, residual=res[i])
+        if side is not None:
+            main.wait_stream(side)
+            outs[1].record_stream(main)
+            return _JoinStreams.apply(torch.cat(outs, 1), side)
+        return torch.cat(outs, 1)
+
     def hidden(self, ids, cache=None, pos=0):
         """Final-norm hidden states; a [B, T/tp, D] sequence shard under sequence parallelism."""
         from ..parallel.tensor_parallel import vocab_parallel_embedding
         c = self.c
+        if self._pipelined(ids, cache):
+            return self._hidden_pipelined(ids)
         sp = self.sp and cache is None
         x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim), sequence_parallel=sp)
         res, delta = None, x

@@ -161,8 +161,9 @@ class _ChunkedLinearXent(torch.autograd.Function):
         D = h.shape[-1]
         h2 = h.reshape(-1, D)
         N, Vl = h2.shape[0], w.shape[0]
-        tp = dist.get_world_size(group) if group is not None else 1
-        v_off = (dist.get_rank(group) * Vl) if group is not None else 0
+        from ..parallel import comm
+        rank, tp = comm.group_rank_size(group)
+        v_off = rank * Vl
         Vtot = Vl * tp
         t = target.reshape(-1).contiguous().long()
         # running statistics in fp32 (fp64 for fp64 inputs: CPU oracle checks)
@@ -176,10 +177,10 @@ class _ChunkedLinearXent(torch.autograd.Function):
             del lc
         if tp > 1:
             gm = m.clone()
-            dist.all_reduce(gm, op=dist.ReduceOp.MAX, group=group)
+            comm.all_reduce(gm, group, op=dist.ReduceOp.MAX)
             s = torch.where(m == -float("inf"), torch.zeros_like(s), s * torch.exp(m - gm))
             pack = torch.stack([s, tl, sx])            # tl is 0 on ranks not owning the target
-            dist.all_reduce(pack, group=group)
+            comm.all_reduce(pack, group)
             s, tl, sx, m = pack[0], pack[1], pack[2], gm
         lse = m + torch.log(s)
         valid = t != ignore_index
@@ -225,8 +226,9 @@ class _ChunkedLinearXent(torch.autograd.Function):
                 gb[v0:v1] = G.to(acc_dt).sum(0)
             del lc, G
         if need_h:
-            if group is not None and dist.get_world_size(group) > 1:
-                dist.all_reduce(dh, group=group)      # h is replicated over TP: sum the vocab partials
+            from ..parallel import comm
+            if comm.group_rank_size(group)[1] > 1:
+                comm.all_reduce(dh, group)      # h is replicated over TP: sum the vocab partials
             dh = dh.to(h2.dtype).view(ctx.hshape)
         if need_b:
             gb = commit_tensor(b, gb.to(b.dtype))

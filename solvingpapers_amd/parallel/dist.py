@@ -32,7 +32,9 @@ _INFO = DistInfo()
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> DistInfo:
-    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*). With more than
+    one RCCL rank it also selects hipBLASLt's data-parallel stream-K grid (SPA_STREAMK_DP=0
+    keeps the default persistent grid), see below."""
     global _INFO
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -41,6 +43,14 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> Di
     if backend is None:
         # SPA_DIST_BACKEND=gloo: rehearse the multi-rank paths on a box with fewer GPUs than ranks
         backend = os.environ.get("SPA_DIST_BACKEND") or ("nccl" if cuda else "gloo")
+    if world > 1 and backend == "nccl" and os.environ.get("SPA_STREAMK_DP", "1") != "0":
+        # Gradient buckets all-reduce on RCCL's stream while the backward runs. hipBLASLt's
+        # stream-K GEMMs size a persistent grid to the whole chip, so a co-running RCCL kernel
+        # stalls their workgroups: a 1-GPU stand-in (tools/overlap_interference.py) slowed the
+        # LLaMA-8B-shape backward 1.39x; with Tensile's data-parallel stream-K grid 1.18x, and
+        # backward+collective overlapped 65.5 -> 57.1 ms (profiles/r2_overlap_streamk_env.jsonl)
+        # for +0.9 % GEMM time standalone. Set before the first GEMM loads hipBLASLt.
+        os.environ.setdefault("TENSILE_STREAMK_DATA_PARALLEL", "1")
     if cuda:
         ndev = torch.cuda.device_count()
         dev_idx = local if (backend == "nccl" or local < ndev) else local % ndev

@@ -26,8 +26,8 @@ from __future__ import annotations
 from types import SimpleNamespace
 
 import torch
-import torch.distributed as dist
 
+from . import comm
 from ..ops._ext import ops
 from ..ops.activation import glu
 from ..ops.moe import (combine, commit_weight_grad, dequant_act_fp8_blk, gather, grouped_gemm_fp8_blk, grouped_linear,
@@ -35,29 +35,13 @@ from ..ops.moe import (combine, commit_weight_grad, dequant_act_fp8_blk, gather,
 
 
 def ep_rank_size(group):
-    if group is None or not dist.is_initialized():
-        return 0, 1
-    return dist.get_rank(group), dist.get_world_size(group)
-
-
-class _AllToAll(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, out_splits, in_splits, group):
-        ctx.splits, ctx.group = (out_splits, in_splits), group
-        out = x.new_empty((sum(out_splits),) + tuple(x.shape[1:]))
-        dist.all_to_all_single(out, x.contiguous(), out_splits, in_splits, group=group)
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        out_splits, in_splits = ctx.splits
-        dx = g.new_empty((sum(in_splits),) + tuple(g.shape[1:]))
-        dist.all_to_all_single(dx, g.contiguous(), in_splits, out_splits, group=ctx.group)
-        return dx, None, None, None
+    """(rank, size) in the EP group: a torch.distributed group, a comm.ProxyGroup, or None."""
+    return comm.group_rank_size(group)
 
 
 def all_to_all(x, out_splits, in_splits, group):
-    return _AllToAll.apply(x, list(out_splits), list(in_splits), group)
+    """Autograd all-to-all (the reverse exchange in backward) through parallel/comm.py."""
+    return comm.a2a(x, out_splits, in_splits, group)
 
 
 def _em_dest(rc):
@@ -116,7 +100,7 @@ class _Fp8DispatchW13(torch.autograd.Function):
         pad = (-KB) % 16
         pay = torch.cat([q.view(torch.uint8), torch.nn.functional.pad(sx, (0, pad))], 1).contiguous()
         pr = pay.new_empty((sum(recv_splits), pay.shape[1]))
-        dist.all_to_all_single(pr, pay, recv_splits, send_splits, group=group)
+        comm.all_to_all_single(pr, pay, recv_splits, send_splits, group)
         pl = regroup_rows(pr, rc, True)
         xq_l = pl[:, :D].contiguous().view(torch.float8_e4m3fn)
         sx_l = pl[:, D:D + KB].contiguous()
@@ -138,37 +122,67 @@ class _Fp8DispatchW13(torch.autograd.Function):
             dxl = grouped_gemm_fp8_blk(dq, sd, wtq, swt, offsets).to(dh.dtype)
             dxr = regroup_rows(dxl, rc, False)
             dxp = dxr.new_empty((sum(send_splits), dxr.shape[1]))
-            dist.all_to_all_single(dxp, dxr, send_splits, recv_splits, group=ctx.group)
+            comm.all_to_all_single(dxp, dxr, send_splits, recv_splits, ctx.group)
         gw = None
         if ctx.needs_input_grad[1]:
             gw = commit_weight_grad(W, dh, dequant_act_fp8_blk(xq_l, sx_l, dh.dtype), lplan)
         return dxp, gw, None, None, None, None, None
 
 
-def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
-    """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
-    [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
-    ``W2`` [E/P, D, F] are this rank's experts. Returns (y [N, D], local plan)."""
-    rank, P = ep_rank_size(group)
+class EPPrep:
+    """Routing plan of one token chunk, with its per-(rank, expert) counts on their way to the
+    host (``ep_prepare``); ``ep_run`` reads them after one host sync."""
+
+    def __init__(self, plan, counts=None, recv=None, host=None, ev=None):
+        self.plan, self.counts, self.recv, self.host, self.ev = plan, counts, recv, host, ev
+
+    def splits(self, P, El):
+        """(send_splits, recv count matrix rc [P, El] on the host); waits for the D2H copy."""
+        if self.ev is not None:
+            self.ev.synchronize()
+        both = self.host
+        return both[0].view(P, El).sum(1).tolist(), both[1].view(P, El)
+
+
+def ep_prepare(idx, n_experts, group):
+    """Local permutation + the count exchange of a chunk, all on the device; the counts are
+    copied to (pinned) host memory asynchronously. Issue the prepare of every chunk, plus any
+    independent work (the shared expert), before the first ``ep_run``: its host sync then
+    waits while the GPU is busy."""
     plan = permute(idx, n_experts)
+    rank, P = ep_rank_size(group)
+    if P == 1:
+        return EPPrep(plan)
+    counts = plan.counts.to(torch.int64)
+    recv = torch.empty_like(counts)
+    comm.all_to_all_counts(recv, counts, group)              # recv[(src, e_local)]
+    both = torch.stack([counts, recv])
+    if both.is_cuda:
+        host = torch.empty(both.shape, dtype=both.dtype, pin_memory=True)
+        host.copy_(both, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return EPPrep(plan, counts, recv, host, ev)
+    return EPPrep(plan, counts, recv, both.clone())
+
+
+def ep_run(x, w, prep, W13, W2, n_experts, group, act="silu", fp8=False):
+    """Dispatch -> local grouped experts -> combine for a chunk prepared by ``ep_prepare``."""
+    plan = prep.plan
+    rank, P = ep_rank_size(group)
     if P == 1:
         xp = gather(x, plan)
         h = glu(grouped_linear(xp, W13, plan, fp8), act)
         return combine(grouped_linear(h, W2, plan, fp8), w, plan), plan
     El = n_experts // P
     assert El * P == n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
-    counts = plan.counts.to(torch.int64)
-    recv = torch.empty_like(counts)
-    dist.all_to_all_single(recv, counts, group=group)       # recv[(src, e_local)]
-    both = torch.stack([counts, recv]).cpu()                 # the single host sync
-    send_splits = both[0].view(P, El).sum(1).tolist()
-    rc = both[1].view(P, El)
+    send_splits, rc = prep.splits(P, El)                     # the single host sync of the chunk
     recv_splits = rc.sum(1).tolist()
     xp = gather(x, plan)                                      # [A, D] sorted by global expert
     per_e = rc.sum(0)
     loff = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
     dev = x.device
-    rc_dev = recv.view(P, El)                                # device copy of the counts
+    rc_dev = prep.recv.view(P, El)                           # device copy of the counts
     lplan = SimpleNamespace(offsets=loff.to(device=dev, dtype=torch.int32))
     D = x.shape[-1]
     if fp8 and D % 128 == 0 and W13.shape[1] % 128 == 0:
@@ -183,6 +197,13 @@ def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     yr = _Regroup.apply(yl, rc_dev, False)
     yp = all_to_all(yr, send_splits, recv_splits, group)
     return combine(yp, w, plan), plan
+
+
+def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
+    """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
+    [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
+    ``W2`` [E/P, D, F] are this rank's experts. Returns (y [N, D], local plan)."""
+    return ep_run(x, w, ep_prepare(idx, n_experts, group), W13, W2, n_experts, group, act, fp8)
 
 
 def shard_experts(full_w, rank, P):

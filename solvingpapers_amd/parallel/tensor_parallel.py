@@ -19,17 +19,17 @@ import torch.distributed as dist
 
 from ..ops import embedding, linear_cross_entropy
 from ..ops.xent import chunked_linear_cross_entropy
+from . import comm
 
 
 def tp_rank_size(group):
-    if group is None or not dist.is_initialized():
-        return 0, 1
-    return dist.get_rank(group), dist.get_world_size(group)
+    """(rank, size) in the TP group: a torch.distributed group, a comm.ProxyGroup, or None."""
+    return comm.group_rank_size(group)
 
 
 def _ar(x, group):
     x = x.contiguous()
-    dist.all_reduce(x, group=group)
+    comm.all_reduce(x, group)
     return x
 
 
@@ -75,6 +75,8 @@ reduce_grad_tp = copy_to_tp  # identity fwd, sum of activation grads over the TP
 
 def _gather_seq_raw(x, group):
     rank, tp = tp_rank_size(group)
+    if comm.is_proxy(group):
+        raise NotImplementedError("sequence parallelism is not modelled by the proxy group")
     if dist.get_backend(group) == "gloo":
         parts = [torch.empty_like(x) for _ in range(tp)]
         dist.all_gather(parts, x.contiguous(), group=group)
@@ -88,6 +90,8 @@ def _gather_seq_raw(x, group):
 def _reduce_scatter_seq_raw(x, group):
     rank, tp = tp_rank_size(group)
     assert x.shape[1] % tp == 0, "sequence parallelism needs T divisible by the TP size"
+    if comm.is_proxy(group):
+        raise NotImplementedError("sequence parallelism is not modelled by the proxy group")
     if dist.get_backend(group) == "gloo":                               # gloo has no reduce-scatter
         y = x.contiguous().clone()
         dist.all_reduce(y, group=group)
@@ -156,7 +160,7 @@ def sync_sequence_parallel_grads(params, group):
         g = getattr(p, "main_grad", None)
         g = g if g is not None else p.grad
         if g is not None:
-            dist.all_reduce(g, group=group)
+            comm.all_reduce(g, group)
 
 
 def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=False):
@@ -192,6 +196,8 @@ def gather_vocab_logits(logits_local, group):
     rank, tp = tp_rank_size(group)
     if tp == 1:
         return logits_local
+    if comm.is_proxy(group):
+        return torch.cat([logits_local] * tp, dim=-1)
     parts = [torch.empty_like(logits_local) for _ in range(tp)]
     dist.all_gather(parts, logits_local.contiguous(), group=group)
     return torch.cat(parts, dim=-1)

@@ -16,11 +16,41 @@ import torch
 
 class _Gen:
     value = 0
+    # > 0 while a model runs its backward on more than one compute stream (tensor-parallel
+    # chunk pipelining, models/gemma.py): weight-gradient commits are then ordered across streams
+    multi_stream = 0
 
 
 def next_generation():
     """Start a new gradient iteration: the next commit to each param overwrites."""
     _Gen.value += 1
+
+
+def set_multi_stream(on: bool):
+    """Enter / leave multi-stream mode: every commit to a param waits for the previous commit
+    to it (an event recorded on the stream that made it) when that came from another stream,
+    so the first-writer-overwrites / later-writers-accumulate order decided on the host is the
+    order the device applies. The direct-write shortcuts (direct_out, claim_main_grad) are off
+    in this mode: their writes happen after they return, outside the ordering."""
+    _Gen.multi_stream += 1 if on else -1
+
+
+def _order_before(p, t):
+    if not _Gen.multi_stream or not t.is_cuda:
+        return None
+    cur = torch.cuda.current_stream(t.device)
+    ev = getattr(p, "_spa_ev", None)
+    if ev is not None and getattr(p, "_spa_stream", None) != cur:
+        cur.wait_event(ev)
+    return cur
+
+
+def _order_after(p, cur):
+    if cur is None:
+        return
+    ev = torch.cuda.Event()
+    ev.record(cur)
+    p._spa_ev, p._spa_stream = ev, cur
 
 
 def commit(p: torch.Tensor, compute: Callable[[Optional[torch.Tensor], bool], Optional[torch.Tensor]]):
@@ -33,11 +63,13 @@ def commit(p: torch.Tensor, compute: Callable[[Optional[torch.Tensor], bool], Op
     mg = getattr(p, "main_grad", None)
     if mg is None:
         return compute(None, False)
+    cur = _order_before(p, mg)
     if getattr(p, "_spa_gen", -1) != _Gen.value:
         compute(mg, False)
         p._spa_gen = _Gen.value
     else:
         compute(mg, True)
+    _order_after(p, cur)
     return None
 
 
@@ -46,7 +78,8 @@ def direct_out(p: torch.Tensor):
     with p's dtype, claim it and return it so a kernel can write the gradient
     straight into it (no temporary + copy). Returns None otherwise."""
     mg = getattr(p, "main_grad", None)
-    if mg is None or getattr(p, "_spa_gen", -1) == _Gen.value or mg.dtype != p.dtype or not mg.is_contiguous():
+    if mg is None or getattr(p, "_spa_gen", -1) == _Gen.value or mg.dtype != p.dtype or not mg.is_contiguous() \
+            or _Gen.multi_stream:
         return None
     p._spa_gen = _Gen.value
     return mg
@@ -57,7 +90,7 @@ def claim_main_grad(p: torch.Tensor):
     ``(main_grad, accumulate)`` -- accumulate is False on the first commit of this iteration --
     and marks the commit, or None when ``p`` has no contiguous main_grad of its own dtype."""
     mg = getattr(p, "main_grad", None)
-    if mg is None or mg.dtype != p.dtype or not mg.is_contiguous():
+    if mg is None or mg.dtype != p.dtype or not mg.is_contiguous() or _Gen.multi_stream:
         return None
     accumulate = getattr(p, "_spa_gen", -1) == _Gen.value
     p._spa_gen = _Gen.value

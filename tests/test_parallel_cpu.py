@@ -134,7 +134,7 @@ def test_zero1_matches_dp():
         assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
 
 
-def _tp_worker(rank, world, port, q, sp=False):
+def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
     _init(rank, world, port)
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.parallel.tensor_parallel import shard_gemma_from_full
@@ -142,11 +142,16 @@ def _tp_worker(rank, world, port, q, sp=False):
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     grp = dist.new_group([0, 1])
-    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=sp)
+    grp2 = dist.new_group([0, 1]) if pipelined else None
+    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=sp, tp_group2=grp2)
+    assert not pipelined or local.tp_group2 is not None
     shard_gemma_from_full(full, local, rank, world)
     flat = FlatParams(local)
     ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
-    loss = local(ids[:, :-1], ids[:, 1:]) if not sp else local(ids[:, :-2], ids[:, 1:-1])
+    even = sp or pipelined                       # SP shards T; the pipeline splits T in halves
+    loss = local(ids[:, :-1], ids[:, 1:]) if not even else local(ids[:, :-2], ids[:, 1:-1])
+    if pipelined:
+        assert local._pipelined(ids[:, :-2], None)
     loss.backward()
     local.sync_sequence_parallel_grads()
     grads = {n: p.main_grad.clone().numpy() for n, p in local.named_parameters()}
@@ -156,20 +161,22 @@ def _tp_worker(rank, world, port, q, sp=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("sp", [False, True])
-def test_tensor_parallel_gemma_matches_unsharded(sp):
+@pytest.mark.parametrize("sp,pipelined", [(False, False), (True, False), (False, True)])
+def test_tensor_parallel_gemma_matches_unsharded(sp, pipelined):
     """TP=2 (and TP=2 with Megatron sequence parallelism: reduce-scatter / all-gather over T,
-    norms on sequence shards, norm-weight grads summed over TP) == the unsharded model."""
+    norms on sequence shards, norm-weight grads summed over TP; and the two-chunk pipeline on a
+    second communicator, half B attending to half A's K/V) == the unsharded model."""
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.utils.flat import FlatParams
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     FlatParams(full)
     ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
-    loss = full(ids[:, :-1], ids[:, 1:]) if not sp else full(ids[:, :-2], ids[:, 1:-1])  # SP: T even
+    even = sp or pipelined
+    loss = full(ids[:, :-1], ids[:, 1:]) if not even else full(ids[:, :-2], ids[:, 1:-1])  # SP / pipeline: T even
     loss.backward()
     fg = {n: p.main_grad for n, p in full.named_parameters()}
-    out = _run(_tp_worker, 2, sp)
+    out = _run(_tp_worker, 2, sp, pipelined)
     world = 2
     full_norm = torch.sqrt(sum((g.float() ** 2).sum() for g in fg.values())).item()
     for rank, l, (grads, gn) in out:
@@ -206,7 +213,7 @@ def _moe_inputs():
     return x, gy
 
 
-def _ep_worker(rank, world, port, q):
+def _ep_worker(rank, world, port, q, pipelined=False):
     _init(rank, world, port)
     from solvingpapers_amd.models import deepseekv3 as ds
     from solvingpapers_amd.parallel.expert_parallel import shard_experts
@@ -215,7 +222,9 @@ def _ep_worker(rank, world, port, q):
     full = ds.MoE(c)
     full.reset_parameters(0.1, torch.Generator().manual_seed(3))
     grp = dist.new_group([0, 1])
-    m = ds.MoE(c, ep_group=grp)
+    grp2 = dist.new_group([0, 1]) if pipelined else None
+    m = ds.MoE(c, ep_group=grp, ep_group2=grp2)
+    assert (m.ep_group2 is not None) == pipelined
     # the EP constructor's own init: rank r holds shard_experts(unsharded init, r, P), i.e.
     # distinct experts on every rank (not E/P experts drawn again from the shared sequence)
     m.reset_parameters(0.1, torch.Generator().manual_seed(3))
@@ -230,10 +239,12 @@ def _ep_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_expert_parallel_moe_matches_local():
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_expert_parallel_moe_matches_local(pipelined):
     """EP=2 (all-to-all dispatch/combine, 2 experts per rank) == one process holding all
     4 experts: outputs, input grads, and each rank's expert grads (which collect the
-    contributions of BOTH ranks' tokens)."""
+    contributions of BOTH ranks' tokens). ``pipelined``: the two-chunk form on a second EP
+    communicator (each chunk its own count exchange, dispatch and combine)."""
     from solvingpapers_amd.models import deepseekv3 as ds
     c = _moe_cfg()
     torch.manual_seed(0)
@@ -243,7 +254,7 @@ def test_expert_parallel_moe_matches_local():
     xs = x.clone().requires_grad_(True)
     ys = [full(xs[r]) for r in range(2)]
     sum((y * gy[r]).sum() for r, y in enumerate(ys)).backward()
-    out = _run(_ep_worker, 2)
+    out = _run(_ep_worker, 2, pipelined)
     for rank, y, gx, g13, g2, gg in out:
         assert torch.allclose(torch.from_numpy(y), ys[rank].detach(), atol=1e-5)
         assert torch.allclose(torch.from_numpy(gx), xs.grad[rank], atol=1e-5)
