@@ -38,6 +38,8 @@ def main():
                     help="AdamW moments in bf16 (DeepSeek-V3 sec. 3.3.2; fp32 master weights kept; default)")
     ap.add_argument("--fp32-moments", dest="bf16_moments", action="store_false", help="AdamW moments in fp32")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="no two-chunk EP pipeline (default: token halves on two streams / communicators)")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
@@ -53,7 +55,8 @@ def main():
         kw["fp8_linears"] = not a.fp8_experts_only
     c = ds.config(a.preset, **kw)
     ep = torch.distributed.group.WORLD if world > 1 else None
-    m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep)
+    ep2 = torch.distributed.new_group(list(range(world))) if (world > 1 and a.pipeline) else None
+    m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep, ep_group2=ep2)
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16, align=64 * world)
     dp = DataParallel(m, flat) if world > 1 else None
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, ep_group=ep,
@@ -87,7 +90,8 @@ def main():
            tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
             + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum, "adam_moments": "bf16" if a.bf16_moments else "fp32",
-            "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu", "params": m.num_params(),
+            "parallelism": (f"ep{world}-dp{world}" + ("-pipe2" if ep2 is not None else "")) if world > 1 else "1gpu",
+            "params": m.num_params(),
             "active_params": m.num_params(active=True)},
            tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4))
     sdist.cleanup()

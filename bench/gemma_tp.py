@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="no two-chunk TP pipeline (default: halves on two streams / communicators)")
     ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (tuning/*.csv) to look up")
     a = ap.parse_args()
     info = sdist.init_distributed()
@@ -35,7 +37,8 @@ def main():
         kw["n_layers"] = a.layers
     c = gemma.config("gemma_7b_mqa", **kw)
     tp = dist.group.WORLD if world > 1 else None
-    m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=tp, seed=1, sequence_parallel=a.sp)
+    tp2 = dist.new_group(list(range(world))) if (world > 1 and a.pipeline and not a.sp) else None
+    m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=tp, seed=1, sequence_parallel=a.sp, tp_group2=tp2)
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     # global grad norm: TP-sharded squares summed over the group, replicated params counted once
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, tp_group=tp)
@@ -56,7 +59,7 @@ def main():
     tf = tok_s * m.flops_per_token(a.seq) / world / 1e12
     report("training tokens/sec, Gemma-7B-shape MQA bf16 (TP)", tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": "gemma_7b_mqa" + (f"-L{a.layers}" if a.layers else ""), "global_batch": 1, "seq_len": a.seq,
-            "parallelism": f"tp{world}" + ("-sp" if a.sp and world > 1 else "")}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
+            "parallelism": f"tp{world}" + ("-sp" if a.sp and world > 1 else "") + ("-pipe2" if tp2 is not None else "")}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
            loss=round(float(last[0].detach()), 4))
     sdist.cleanup()
 

@@ -445,6 +445,8 @@ class MoE(tnn.Module):
         main = torch.cuda.current_stream(x2.device) if cuda else None
         if cuda and self._side is None:
             self._side = torch.cuda.Stream(x2.device)
+            from ..utils.grad import register_side_stream
+            register_side_stream(self._side)
         side = self._side if cuda else None
 
         def on(i):

@@ -397,6 +397,8 @@ class Gemma(tnn.Module):
         main = torch.cuda.current_stream(ids.device) if cuda else None
         if cuda and self._side is None:
             self._side = torch.cuda.Stream(ids.device)
+            from ..utils.grad import register_side_stream
+            register_side_stream(self._side)
         side = self._side if cuda else None
 
         def on(i):

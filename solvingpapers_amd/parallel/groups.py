@@ -41,6 +41,10 @@ class ProcessGroups:
     dp_group: Optional[object] = None
     ep_group: Optional[object] = None
     expert_dp_group: Optional[object] = None
+    # second communicators over the same TP / EP ranks (two-chunk comm/compute pipelines:
+    # models/gemma.py tp_group2, models/deepseekv3.py ep_group2); None unless requested
+    tp_group2: Optional[object] = None
+    ep_group2: Optional[object] = None
     tp_ranks: Optional[List[int]] = None
     dp_ranks: Optional[List[int]] = None
     ep_ranks: Optional[List[int]] = None
@@ -70,14 +74,17 @@ def layout_ranks(world: int, tp: int = 1, ep: int = 1):
     return {"tp": tp_groups, "dp": dp_groups, "ep": ep_groups, "expert_dp": edp_groups}
 
 
-def build_groups(tp: int = 1, ep: int = 1) -> ProcessGroups:
+def build_groups(tp: int = 1, ep: int = 1, pipeline: bool = False) -> ProcessGroups:
+    """``pipeline``: also build a second communicator for every TP and EP group (each chunk of
+    the two-chunk pipelines runs its collectives on its own RCCL communicator / stream)."""
     initialized = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size() if initialized else 1
     rank = dist.get_rank() if initialized else 0
     lay = layout_ranks(world, tp, ep)
     mine = {}
-    for kind in ("tp", "dp", "ep", "expert_dp"):
-        for ranks in lay[kind]:
+    kinds = ("tp", "dp", "ep", "expert_dp") + (("tp2", "ep2") if pipeline else ())
+    for kind in kinds:
+        for ranks in lay[kind.rstrip("2")]:
             # new_group is collective over the WORLD: create every group on every rank, in order
             g = dist.new_group(ranks) if (initialized and len(ranks) > 1) else None
             if rank in ranks:
@@ -88,4 +95,5 @@ def build_groups(tp: int = 1, ep: int = 1) -> ProcessGroups:
         tp_rank=tp_ranks.index(rank), dp_rank=dp_ranks.index(rank), ep_rank=ep_ranks.index(rank),
         tp_group=mine["tp"][0], dp_group=mine["dp"][0], ep_group=mine["ep"][0],
         expert_dp_group=mine["expert_dp"][0],
+        tp_group2=mine["tp2"][0] if pipeline else None, ep_group2=mine["ep2"][0] if pipeline else None,
         tp_ranks=tp_ranks, dp_ranks=dp_ranks, ep_ranks=ep_ranks, expert_dp_ranks=mine["expert_dp"][1])

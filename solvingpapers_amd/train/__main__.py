@@ -64,7 +64,7 @@ def _lm(args, info):
     dev = info.device if args.device is None else torch.device(args.device)
     # world = tp x data, data = ep x expert-dp (parallel/groups.py); the data loader shards by the
     # DATA coordinate: TP peers read the same batch, DP/EP ranks different ones
-    pg = build_groups(args.tp, args.ep)
+    pg = build_groups(args.tp, args.ep, pipeline=args.pipeline and (args.tp > 1 or args.ep > 1))
     if args.tp > 1 and args.model != "gemma":
         raise SystemExit("--tp is implemented for gemma (Megatron column/row-parallel + vocab-parallel CE)")
     if args.ep > 1 and args.model != "dsv3":
@@ -100,11 +100,12 @@ def _lm(args, info):
             V, T, B = c.vocab_size, c.block_size, c.batch_size
         else:
             model = gemma.Gemma(c, device=dev, dtype=dtype, seed=args.seed, tp_group=pg.tp_group,
-                                sequence_parallel=args.sp)
+                                sequence_parallel=args.sp, tp_group2=pg.tp_group2)
             V, T, B = c.vocab_size, args.seq or c.max_seq_len, c.batch_size
     elif fam == "dsv3":
         c = deepseekv3.config(args.preset or "dsv3_ref", **sets)
-        model = deepseekv3.DeepSeekV3(c, device=dev, dtype=dtype, seed=args.seed, ep_group=pg.ep_group)
+        model = deepseekv3.DeepSeekV3(c, device=dev, dtype=dtype, seed=args.seed, ep_group=pg.ep_group,
+                                      ep_group2=pg.ep_group2)
         V, T, B = c.vocab_size, c.block_size, c.batch_size
     else:
         raise SystemExit(f"unknown model {fam}")
@@ -185,6 +186,8 @@ def main(argv=None):
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (gemma)")
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism with --tp")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree (dsv3)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="with --tp / --ep: no two-chunk comm/compute pipeline (one communicator)")
     ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--device", default=None)
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"])

@@ -35,6 +35,24 @@ def set_multi_stream(on: bool):
     _Gen.multi_stream += 1 if on else -1
 
 
+_SIDE_STREAMS: list = []
+
+
+def register_side_stream(stream):
+    """A model's second compute stream (chunk pipelines): consumers of the gradient buffer that
+    launch work mid-backward (DataParallel buckets) order themselves after it."""
+    if stream is not None and all(stream != s for s in _SIDE_STREAMS):
+        _SIDE_STREAMS.append(stream)
+
+
+def wait_side_streams():
+    """Make the current stream wait for every registered side stream (no-op when none)."""
+    if _SIDE_STREAMS:
+        cur = torch.cuda.current_stream()
+        for s in _SIDE_STREAMS:
+            cur.wait_stream(s)
+
+
 def _order_before(p, t):
     if not _Gen.multi_stream or not t.is_cuda:
         return None
