@@ -49,32 +49,11 @@
 // q/k/v/o and grads are addressed with (batch, seq, head) strides so the kernels
 // read/write a fused [B, T, H + 2*Hkv, hd] qkv buffer in place.
 #include "attn_common.h"
+#include "attn_params.h"
 
 namespace spa {
 
-struct AttnParams {
-  const bf16* q; const bf16* k; const bf16* v; const bf16* o; const bf16* dout;
-  bf16* out; bf16* dq; bf16* dk; bf16* dv;
-  float* lse; const float* lse_in; float* delta; float* dqacc;  // dqacc: fused bwd fp32 dQ [B,Tq,H,HD]
-  int B, H, Hkv, Tq, Tk;
-  long sqb, sqt, sqh, skb, skt, skh, svb, svt, svh, sob, sot, soh;
-  long sdob, sdot, sdoh;
-  long sdqb, sdqt, sdqh, sdkb, sdkt, sdkh, sdvb, sdvt, sdvh;
-  float scale;       // softmax scale (natural)
-  float scale_log2;  // scale * log2(e)
-  int causal_off;    // key j visible to query i iff j <= i + causal_off
-  // dK/dV q-head split (small Hkv x key-block grids, e.g. MQA): hsplit blocks per key block,
-  // each summing G/hsplit q-heads into fp32 partials dkacc/dvacc [hsplit, B, Tk, Hkv, HD]
-  int hsplit;
-  float* dkacc; float* dvacc;
-  // fused dropout on P (DROP kernels): keep iff hash(seed, b, h, q, key) >> 8 >= drop_thr
-  unsigned seed_lo, seed_hi, drop_thr;
-  float drop_scale;  // 1 / (1 - p)
-  const int64_t* seed_ptr;  // device seed (graph-safe: a fresh mask per HIP-graph replay) or null
-  // profiling only (SPA_ATTN_STAMP): per-wave s_memtime segment sums of the dK/dV loop, or null
-  long long* stamp;
-  int xcd;  // query-parallel kernels: XCD-aware block order (q_block_map)
-};
+
 
 // ---- dropout counter hash (bit-identical in ops/attention.py dropout_keep_mask) ------
 __device__ __forceinline__ unsigned mix32(unsigned x) {
@@ -426,41 +405,6 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) w[i] = (bf16)(acc[dt][4 * g + i] * p.scale);
         *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * hh) = w;
-      }
-  }
-}
-
-// dK^T / dV^T accumulator (rows d = 32dt + (r&3) + 8(r>>2) + 4hh, column = key) -> global:
-// bf16 (dk scaled) when the block owns all q-heads of its kv-head, else fp32 partials.
-template <int HD>
-__device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 (&acc)[HD / 32], bool is_k,
-                                              int b, int hk, int key, int split, int hh) {
-  if (key >= p.Tk) return;
-  constexpr int DT = HD / 32;
-  if (p.hsplit == 1) {
-    bf16* dst = is_k ? p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh
-                     : p.dv + b * p.sdvb + (long)key * p.sdvt + hk * p.sdvh;
-    const float sc = is_k ? p.scale : 1.f;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 w;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = (bf16)(acc[dt][4 * g + i] * sc);
-        *reinterpret_cast<bf16x4*>(dst + 32 * dt + 8 * g + 4 * hh) = w;
-      }
-  } else {
-    float* dst = (is_k ? p.dkacc : p.dvacc) +
-                 ((((long)split * p.B + b) * p.Tk + key) * p.Hkv + hk) * HD;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 w;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = acc[dt][4 * g + i];
-        *reinterpret_cast<f32x4*>(dst + 32 * dt + 8 * g + 4 * hh) = w;
       }
   }
 }
@@ -1551,8 +1495,11 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
   else attn_bwd_dq_kernel<HDK, HDV, NW, false, DROP><<<grid, NW * 64, 0, st>>>(p);
   if (p.Tk == 0) return;
   const bool paired = PAIRED_OK && dkdv_mode == 2;
+  const bool single4 = PAIRED_OK && HDK == 128 && dkdv_mode == 4;
   const bool piped = PAIRED_OK && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
-  if (piped) {
+  if (single4) {
+    if constexpr (PAIRED_OK && HDK == 128) launch_dkdv4_128(p, causal, g2, st);   // attention_bwd4.hip
+  } else if (piped) {
     if constexpr (PAIRED_OK) {
       if (causal) attn_bwd_dkdv3_kernel<HDK, true><<<g2, 512, 0, st>>>(p);
       else attn_bwd_dkdv3_kernel<HDK, false><<<g2, 512, 0, st>>>(p);

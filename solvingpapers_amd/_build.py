@@ -25,6 +25,10 @@ CSRC = ROOT / "csrc"
 BUILD = ROOT / "build"
 OUT = PKG / "_C.so"
 ARCH = os.environ.get("SPA_OFFLOAD_ARCH", "gfx950")
+# per-file device flags. attention_bwd4.hip (one-wave-per-SIMD dK/dV): the max-ILP machine
+# scheduler issues a chain's LDS operand reads ahead of its MFMAs; the default (occupancy-
+# driven) scheduler re-uses one register quad and waits out every LDS round trip there.
+EXTRA_FLAGS = {"attention_bwd4.hip": "-mllvm -amdgpu-sched-strategy=max-ilp"}
 
 
 def _torch_paths():
@@ -88,6 +92,8 @@ def write_ninja(debug: bool = False) -> Path:
         o = BUILD / "obj" / (s.stem + ".hip.o")
         objs.append(o)
         lines.append(f"build {o}: hip {s}")
+        if s.name in EXTRA_FLAGS:
+            lines.append(f"  devflags = {dev_flags} {EXTRA_FLAGS[s.name]}")
     for s in hosts:
         o = BUILD / "obj" / (s.stem + ".cpp.o")
         objs.append(o)

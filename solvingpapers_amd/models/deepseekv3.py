@@ -343,18 +343,20 @@ class MoE(tnn.Module):
     """DeepSeekMoE: shared experts + top-k routed experts with aux-free load balancing.
     Under EP (``ep_group`` of size P) this rank holds experts [r*E/P, (r+1)*E/P)."""
 
-    def __init__(self, c: DSV3Config, ep_group=None, ep_group2=None, **fk):
-        """``ep_group2``: a second communicator over the same EP ranks. Given (EP > 1), the
-        layer's tokens run as two chunks -- chunk A on the current stream with ``ep_group``,
-        chunk B on a side compute stream with ``ep_group2`` -- so one chunk's dispatch /
-        combine all-to-alls are on the wire while the other chunk's experts (and the shared
-        expert, issued before the count sync) compute; see _forward_pipelined."""
+    def __init__(self, c: DSV3Config, ep_group=None, ep_group2=None, ep_chunks=2, **fk):
+        """Under EP (P > 1) the layer's tokens run as ``ep_chunks`` chunks whose dispatch /
+        combine all-to-alls overlap the other chunks' expert GEMMs and the shared expert on
+        ONE stream (expert_parallel.ep_run_interleaved; ``ep_chunks=1``: no overlap).
+        ``ep_group2``: instead a second communicator over the same EP ranks -- two chunks on two
+        compute streams (chunk A with ``ep_group``, chunk B on a side stream with
+        ``ep_group2``); see _forward_pipelined."""
         super().__init__()
         from ..parallel.expert_parallel import ep_rank_size
         self.c = c
         self.ep_group = ep_group
         self.ep_rank, self.ep = ep_rank_size(ep_group)
         self.ep_group2 = ep_group2 if self.ep > 1 else None
+        self.ep_chunks = int(ep_chunks) if self.ep > 1 else 1
         self._side = None
         if self.ep_group2 is not None:
             from ..utils.grad import set_multi_stream
@@ -418,6 +420,8 @@ class MoE(tnn.Module):
         x2 = x.reshape(-1, D)
         if self.ep_group2 is not None and x2.shape[0] >= 2:
             return self._forward_pipelined(x2).view(B, T, D)
+        if self.ep_chunks > 1 and x2.shape[0] >= self.ep_chunks:
+            return self._forward_interleaved(x2).view(B, T, D)
         logits = self._logits(x2)
         idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
         y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group,
@@ -428,6 +432,31 @@ class MoE(tnn.Module):
         if c.aux_free and self.training:
             self._update_bias(idx, w, plan)
         return y.view(B, T, D)
+
+    def _forward_interleaved(self, x2):
+        """``ep_chunks`` token chunks, one stream (expert_parallel.ep_run_interleaved): routing,
+        permutation and count exchange of every chunk first (one host sync per chunk, all
+        issued before the first dispatch), then the interleaved dispatch / experts / combine."""
+        from ..parallel.expert_parallel import ep_prepare, ep_run_interleaved
+        c = self.c
+        n = self.ep_chunks
+        parts = torch.tensor_split(x2, n)
+        idxs, ws, preps = [], [], []
+        for xp in parts:
+            idx, w = route(self._logits(xp), c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
+            idxs.append(idx)
+            ws.append(w)
+            preps.append(ep_prepare(idx, c.n_experts, self.ep_group))
+        fp8 = c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0
+        ys = ep_run_interleaved(parts, ws, preps, self.w13, self.w2, c.n_experts, self.ep_group, fp8=fp8,
+                                shared=self.shared)
+        counts = preps[0].plan.counts
+        for p_ in preps[1:]:
+            counts = counts + p_.plan.counts
+        self.last_counts = counts
+        if c.aux_free and self.training:
+            self._update_bias(torch.cat(idxs), torch.cat(ws), SimpleNamespace(counts=counts))
+        return torch.cat(ys)
 
     def _forward_pipelined(self, x2):
         """Two token chunks on two streams / two EP communicators (see __init__). Host order:

@@ -286,7 +286,11 @@ class GemmaBlock(tnn.Module):
         if cache is None and (kv_prefix is not None or want_kv):
             x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
             k4, v4 = x4[:, :, self.hl:self.hl + KV], x4[:, :, self.hl + KV:]
-            kv_out = (k4, v4)
+            ev = None
+            if want_kv and qkv.is_cuda:      # the next chunk waits for THIS point only, not for the
+                ev = torch.cuda.Event()      # rest of the layer (its all-reduces) on this stream
+                ev.record()
+            kv_out = (k4, v4, ev)
             if kv_prefix is not None:     # causal with offset: query i sees keys <= prefix + i
                 k4 = torch.cat([kv_prefix[0], k4], 1)
                 v4 = torch.cat([kv_prefix[1], v4], 1)
@@ -416,11 +420,10 @@ class Gemma(tnn.Module):
             with on(0):
                 res[0], delta[0], kv = l(res[0], delta[0], groups[0], None, 0, False, want_kv=True)
             if side is not None:
-                ev = torch.cuda.Event()
-                ev.record(main)
-                side.wait_event(ev)
-                for t in kv:
+                side.wait_event(kv[2])       # half A's K/V are rope'd: half B may start its layer
+                for t in kv[:2]:
                     t.record_stream(side)
+            kv = kv[:2]
             with on(1):
                 res[1], delta[1] = l(res[1], delta[1], groups[1], None, half, False, kv_prefix=kv)
         outs = [None, None]

@@ -42,7 +42,7 @@ class ProxyGroup:
     kernel at all (compute-only reference)."""
 
     def __init__(self, size: int, device=None, ar_busbw_gbps: float = PROXY_AR_BUSBW_GBPS,
-                 a2a_gbps: float = PROXY_A2A_GBPS, nwg: int = 16, buf_mb: int = 64, mode: str = "overlap"):
+                 a2a_gbps: float = PROXY_A2A_GBPS, nwg: int = 16, buf_mb: int = 8, mode: str = "overlap"):
         self.size, self.rank = int(size), 0
         self.device = torch.device(device or "cuda")
         self.ar_bw, self.a2a_bw = ar_busbw_gbps * 1e9, a2a_gbps * 1e9
@@ -77,8 +77,12 @@ class ProxyGroup:
         from ..ops._ext import ops
         if self._rep_s is None:
             self._calibrate()
-        reps = max(1, int(round(seconds / self._rep_s)))
+        reps = int(round(seconds / self._rep_s))
         cur = torch.cuda.current_stream(self.device)
+        if reps == 0:          # below the stand-in's granularity (a few tens of us): latency only
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            return _DoneWork()
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             ops().stream_copy_wg(self._src, self._dst, self.nwg, reps)

@@ -199,6 +199,52 @@ def ep_run(x, w, prep, W13, W2, n_experts, group, act="silu", fp8=False):
     return combine(yp, w, plan), plan
 
 
+def ep_run_interleaved(parts, ws, preps, W13, W2, n_experts, group, act="silu", fp8=False, shared=None):
+    """Token chunks of ONE MoE layer on ONE compute stream, their all-to-alls interleaved so
+    that each exchange is on the wire while another chunk's experts compute:
+
+        start dispatch(0..n-1), shared(first half) | for c: finish dispatch(c), experts(c),
+        start combine(c) | shared(second half) | for c: finish combine(c), combine(c)
+
+    (comm.a2a_start / a2a_finish; autograd replays the same interleave in reverse, each
+    reverse exchange launched before the other chunks' backward and waited after it). One
+    stream, so chunks never compete for the CUs the way two concurrent grouped GEMMs do.
+    ``shared(x_part)`` (the shared expert) covers the first dispatch and the last combine.
+    Returns the per-chunk outputs (shared expert added)."""
+    from . import comm as _c
+    rank, P = ep_rank_size(group)
+    El = n_experts // P
+    assert El * P == n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
+    n = len(parts)
+    meta, hd = [], []
+    for i in range(n):
+        send_splits, rc = preps[i].splits(P, El)
+        recv_splits = rc.sum(1).tolist()
+        per_e = rc.sum(0)
+        loff = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
+        lplan = SimpleNamespace(offsets=loff.to(device=parts[i].device, dtype=torch.int32))
+        meta.append((send_splits, recv_splits, preps[i].recv.view(P, El), lplan))
+        hd.append(_c.a2a_start(gather(parts[i], preps[i].plan), recv_splits, send_splits, group))
+    sh = [None] * n
+    if shared is not None:                                   # under the first dispatch
+        sh[0] = shared(parts[0])
+    hc = []
+    for i in range(n):
+        send_splits, recv_splits, rc_dev, lplan = meta[i]
+        xl = _Regroup.apply(_c.a2a_finish(hd[i]), rc_dev, True)
+        h = glu(grouped_linear(xl, W13, lplan, fp8), act)
+        yr = _Regroup.apply(grouped_linear(h, W2, lplan, fp8), rc_dev, False)
+        hc.append(_c.a2a_start(yr, send_splits, recv_splits, group))
+    if shared is not None:                                   # under the last combines
+        for i in range(1, n):
+            sh[i] = shared(parts[i])
+    out = []
+    for i in range(n):
+        y = combine(_c.a2a_finish(hc[i]), ws[i], preps[i].plan)
+        out.append(y + sh[i] if sh[i] is not None else y)
+    return out
+
+
 def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
     [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and

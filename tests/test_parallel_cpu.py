@@ -213,7 +213,7 @@ def _moe_inputs():
     return x, gy
 
 
-def _ep_worker(rank, world, port, q, pipelined=False):
+def _ep_worker(rank, world, port, q, mode="interleaved"):
     _init(rank, world, port)
     from solvingpapers_amd.models import deepseekv3 as ds
     from solvingpapers_amd.parallel.expert_parallel import shard_experts
@@ -222,9 +222,8 @@ def _ep_worker(rank, world, port, q, pipelined=False):
     full = ds.MoE(c)
     full.reset_parameters(0.1, torch.Generator().manual_seed(3))
     grp = dist.new_group([0, 1])
-    grp2 = dist.new_group([0, 1]) if pipelined else None
-    m = ds.MoE(c, ep_group=grp, ep_group2=grp2)
-    assert (m.ep_group2 is not None) == pipelined
+    grp2 = dist.new_group([0, 1]) if mode == "two_stream" else None
+    m = ds.MoE(c, ep_group=grp, ep_group2=grp2, ep_chunks={"plain": 1, "interleaved": 2, "chunks3": 3}.get(mode, 2))
     # the EP constructor's own init: rank r holds shard_experts(unsharded init, r, P), i.e.
     # distinct experts on every rank (not E/P experts drawn again from the shared sequence)
     m.reset_parameters(0.1, torch.Generator().manual_seed(3))
@@ -239,11 +238,12 @@ def _ep_worker(rank, world, port, q, pipelined=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined", [False, True])
-def test_expert_parallel_moe_matches_local(pipelined):
+@pytest.mark.parametrize("mode", ["plain", "interleaved", "chunks3", "two_stream"])
+def test_expert_parallel_moe_matches_local(mode):
     """EP=2 (all-to-all dispatch/combine, 2 experts per rank) == one process holding all
     4 experts: outputs, input grads, and each rank's expert grads (which collect the
-    contributions of BOTH ranks' tokens). ``pipelined``: the two-chunk form on a second EP
+    contributions of BOTH ranks' tokens). Modes: one exchange per layer; 2 / 3 token chunks
+    with interleaved all-to-alls on one stream; two chunks on two streams with a second EP
     communicator (each chunk its own count exchange, dispatch and combine)."""
     from solvingpapers_amd.models import deepseekv3 as ds
     c = _moe_cfg()
@@ -254,7 +254,7 @@ def test_expert_parallel_moe_matches_local(pipelined):
     xs = x.clone().requires_grad_(True)
     ys = [full(xs[r]) for r in range(2)]
     sum((y * gy[r]).sum() for r, y in enumerate(ys)).backward()
-    out = _run(_ep_worker, 2, pipelined)
+    out = _run(_ep_worker, 2, mode)
     for rank, y, gx, g13, g2, gg in out:
         assert torch.allclose(torch.from_numpy(y), ys[rank].detach(), atol=1e-5)
         assert torch.allclose(torch.from_numpy(gx), xs.grad[rank], atol=1e-5)

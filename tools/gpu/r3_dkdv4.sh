@@ -1,0 +1,17 @@
+#!/bin/bash
+# dkdv4 (one-wave-per-SIMD dK/dV) correctness vs the single-wave kernel + ABBA timing at the
+# LLaMA3-8B shape; then the overlap proxy at the default and 8 HW queues
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
+  tests/test_kernels_gpu.py -k "bwd_variants" > gpurun_out/r3d4_pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -8 gpurun_out/r3d4_pytest.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u tools/bench_attn.py --iters 20 --ab SPA_ATTN_DKDV=4 > gpurun_out/r3d4_attn.log 2>&1; echo "attn rc=$?"
+grep -v amdgpu.ids gpurun_out/r3d4_attn.log
+timeout -k 10 400 python -u tools/overlap_proxy.py --layers 2 > gpurun_out/r3o2_q4.log 2>&1; echo "q4 rc=$?"
+grep -v amdgpu.ids gpurun_out/r3o2_q4.log | cut -c1-900
+GPU_MAX_HW_QUEUES=8 timeout -k 10 400 python -u tools/overlap_proxy.py --layers 2 > gpurun_out/r3o2_q8.log 2>&1; echo "q8 rc=$?"
+grep -v amdgpu.ids gpurun_out/r3o2_q8.log | cut -c1-900

@@ -47,10 +47,15 @@ def _time(fn, iters):
     return s.elapsed_time(e) / iters
 
 
+ARMS = None   # --arms: run only these (profiling one arm under rocprofv3)
+
+
 def _arms(make_step, groups, iters, rounds):
     """make_step(pipelined) -> step fn. groups: the ProxyGroups whose mode is switched."""
     steps = {"compute": (make_step(False), "off"), "blocking": (make_step(False), "blocking"),
              "pipelined": (make_step(True), "overlap"), "pipe_comp": (make_step(True), "off")}
+    if ARMS:
+        steps = {k: v for k, v in steps.items() if k in ARMS}
     res = {k: [] for k in steps}
     comm_ms = {}
     for r in range(rounds):
@@ -63,6 +68,8 @@ def _arms(make_step, groups, iters, rounds):
             res[k].append(_time(fn, iters))
             comm_ms[k] = sum(g.modelled_s for g in groups) * 1e3 / iters
     med = {k: statistics.median(v) for k, v in res.items()}
+    if ARMS:
+        return med, {k: comm_ms.get(k, 0.0) for k in ("blocking",)}, 0.0, 0.0
     exposed = med["pipelined"] - med["pipe_comp"]
     total = med["blocking"] - med["compute"]
     return med, comm_ms, exposed, total
@@ -99,23 +106,27 @@ def tp_gemma(a):
 
 
 def ep_moe(a):
+    """Variants: plain (one exchange per layer), one-stream interleaved chunks (2 and 4), and two
+    chunks on two streams / communicators; each timed with collectives modelled and skipped."""
     from solvingpapers_amd.models import deepseekv3 as ds
     dev = torch.device("cuda")
     c = ds.config("dsv3_v3", moe_fp8=a.fp8)
     g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
     g2 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
+    variants = {"plain": dict(ep_chunks=1), "interleaved2": dict(ep_chunks=2), "interleaved4": dict(ep_chunks=4),
+                "two_stream": dict(ep_group2=g2)}
+    if a.variants:
+        variants = {k: v for k, v in variants.items() if k in a.variants.split(",") or k == "plain"}
     mods = {}
-    for pipe in (False, True):
-        m = ds.MoE(c, ep_group=g1, ep_group2=g2 if pipe else None, device=dev, dtype=torch.bfloat16)
+    for name, kw in variants.items():
+        m = ds.MoE(c, ep_group=g1, device=dev, dtype=torch.bfloat16, **kw)
         m.reset_parameters(0.02, torch.Generator(device=dev).manual_seed(3))
         FlatParams(m, grad_dtype=torch.bfloat16)
-        mods[pipe] = m.train()
+        mods[name] = m.train()
     x = (torch.randn(1, a.tokens, c.dim, device=dev) * 0.5).bfloat16().requires_grad_()
     gy = torch.randn_like(x)
 
-    def make(pipe):
-        m = mods[pipe]
-
+    def step_of(m):
         def step():
             from solvingpapers_amd.utils.grad import next_generation
             next_generation()
@@ -123,12 +134,37 @@ def ep_moe(a):
             m(x).backward(gy)
         return step
 
-    med, comm_ms, exposed, total = _arms(make, (g1, g2), a.iters, a.rounds)
-    return {"config": f"dsv3_v3 MoE layer EP=8 local shard (32 of 256 experts, top-8, D 7168, F 2048, 1 shared)"
-                      f"{' fp8' if a.fp8 else ''}", "tokens": a.tokens,
-            "ms": {k: round(v, 3) for k, v in med.items()}, "modelled_comm_ms": round(comm_ms["blocking"], 3),
-            "comm_added_blocking_ms": round(total, 3), "comm_exposed_pipelined_ms": round(exposed, 3),
-            "hidden": round(1 - exposed / total, 3) if total > 0 else None}
+    arms = {}
+    for name, m in mods.items():
+        arms[name + ":off"] = (step_of(m), "off")
+        arms[name + ":overlap" if name != "plain" else "plain:blocking"] = (step_of(m), "overlap" if name != "plain" else "blocking")
+    if ARMS:
+        arms = {k: v for k, v in arms.items() if k in ARMS}
+    res = {k: [] for k in arms}
+    comm = 0.0
+    for r in range(a.rounds):
+        for k, (fn, mode) in arms.items():
+            for g in (g1, g2):
+                g.mode = mode
+            fn()
+            for g in (g1, g2):
+                g.reset_stats()
+            res[k].append(_time(fn, a.iters))
+            if k == "plain:blocking":
+                comm = (g1.modelled_s + g2.modelled_s) * 1e3 / a.iters
+    med = {k: round(statistics.median(v), 3) for k, v in res.items()}
+    out = {"config": f"dsv3_v3 MoE layer EP=8 local shard (32 of 256 experts, top-8, D 7168, F 2048, 1 shared)"
+                     f"{' fp8' if a.fp8 else ''}", "tokens": a.tokens, "ms": med, "modelled_comm_ms": round(comm, 3)}
+    if not ARMS:
+        total = med["plain:blocking"] - med["plain:off"]
+        out["comm_added_blocking_ms"] = round(total, 3)
+        for name in variants:
+            if name == "plain":
+                continue
+            exposed = med[name + ":overlap"] - med[name + ":off"]
+            out[f"hidden_{name}"] = round(1 - exposed / total, 3) if total > 0 else None
+            out[f"vs_blocking_{name}"] = round(med["plain:blocking"] / med[name + ":overlap"], 3)
+    return out
 
 
 def main():
@@ -143,7 +179,11 @@ def main():
     ap.add_argument("--nwg", type=int, default=16)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--arms", default="", help="comma list: compute,blocking,pipelined,pipe_comp (default all)")
+    ap.add_argument("--variants", default="", help="EP: subset of interleaved2,interleaved4,two_stream")
     a = ap.parse_args()
+    global ARMS
+    ARMS = [x for x in a.arms.split(",") if x] or None
     assert _ext.load(), "HIP extension missing"
     base = {"ar_busbw_gbps": a.ar_gbps, "a2a_gbps": a.a2a_gbps, "proxy_nwg": a.nwg}
     for w in a.which.split(","):

@@ -1,38 +1,85 @@
-"""Per-kernel time summary from a rocprofv3 rocpd SQLite database (--kernel-trace output).
+"""Summarise a rocprofv3 rocpd database (ROCm 7.2 default output, ``run_results.db``).
 
-usage: python tools/rocpd_summary.py run_results.db [--top N] [--steps S]
-Groups dispatches by a shortened kernel name, prints total ms, share, calls and, with
---steps, ms per step."""
+Per kernel: calls, total / mean device ms, share; per queue: busy ms; the span from the first
+kernel start to the last kernel end and the sum of kernel time (busy union per queue shows
+whether two streams' kernels ran side by side).
+
+  python tools/rocpd_summary.py gpurun_out/<dir>/run_results.db [--top 25] [--grep attn]
+"""
+from __future__ import annotations
+
 import argparse
-import re
+import glob
 import sqlite3
-from collections import defaultdict
+import sys
 
 
-def short(name):
-    n = re.sub(r"\(.*$", "", name)
-    return n[:110]
+def _tab(con, prefix):
+    for (name,) in con.execute("select name from sqlite_master where type='table'"):
+        if name.startswith(prefix + "_"):
+            return name
+    raise KeyError(prefix)
+
+
+def load(path):
+    con = sqlite3.connect(path)
+    kd, ks = _tab(con, "rocpd_kernel_dispatch"), _tab(con, "rocpd_info_kernel_symbol")
+    rows = con.execute(f"select d.start, d.end, d.queue_id, d.stream_id, s.display_name, s.kernel_name "
+                       f"from {kd} d join {ks} s on d.kernel_id = s.id").fetchall()
+    return rows
+
+
+def _union(iv):
+    iv = sorted(iv)
+    tot, cur_s, cur_e = 0, None, None
+    for s, e in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
+
+
+def summarise(rows, top=25, grep=None, out=sys.stdout):
+    if grep:
+        rows = [r for r in rows if grep in (r[4] or r[5])]
+    if not rows:
+        print("no kernels", file=out)
+        return
+    agg = {}
+    for s, e, q, st, disp, name in rows:
+        k = (disp or name)[:110]
+        a = agg.setdefault(k, [0, 0])
+        a[0] += 1
+        a[1] += e - s
+    total = sum(v[1] for v in agg.values())
+    span = max(r[1] for r in rows) - min(r[0] for r in rows)
+    print(f"kernels {len(rows)}  kernel-time {total / 1e6:.3f} ms  span {span / 1e6:.3f} ms  "
+          f"busy-union {_union([(r[0], r[1]) for r in rows]) / 1e6:.3f} ms", file=out)
+    byq = {}
+    for s, e, q, st, *_ in rows:
+        byq.setdefault((q, st), []).append((s, e))
+    for (q, st), iv in sorted(byq.items()):
+        print(f"  queue {q} stream {st}: {len(iv)} kernels, busy {_union(iv) / 1e6:.3f} ms", file=out)
+    print(f"{'ms':>10} {'%':>6} {'calls':>6}  kernel", file=out)
+    for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"{t / 1e6:10.3f} {100 * t / total:6.2f} {n:6d}  {k}", file=out)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("db")
-    ap.add_argument("--top", type=int, default=30)
-    ap.add_argument("--steps", type=int, default=0)
+    ap.add_argument("db", nargs="+")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--grep", default=None)
     a = ap.parse_args()
-    c = sqlite3.connect(a.db)
-    tot = defaultdict(float)
-    calls = defaultdict(int)
-    for name, dur in c.execute("select name, duration from kernels"):
-        k = short(name)
-        tot[k] += dur / 1e6
-        calls[k] += 1
-    all_ms = sum(tot.values())
-    print(f"total kernel time {all_ms:.1f} ms over {sum(calls.values())} dispatches")
-    print(f"{'ms':>10} {'share':>6} {'calls':>6} {'ms/step':>8}  kernel")
-    for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
-        ps = f"{v / a.steps:8.2f}" if a.steps else "       -"
-        print(f"{v:10.2f} {100 * v / all_ms:5.1f}% {calls[k]:6d} {ps}  {k}")
+    for pat in a.db:
+        for path in sorted(glob.glob(pat)):
+            print(f"== {path}")
+            summarise(load(path), a.top, a.grep)
 
 
 if __name__ == "__main__":
