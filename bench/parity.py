@@ -12,8 +12,18 @@ the numbers the reference published on Tesla T4s.
       with the reference epochs on synthetic MNIST-like digits (no dataset access) —
       quality parity unpinned, reported for completeness with wall-clock.
 
+  B3  LLaMA-tiny generation tok/s  (prompt 10 tokens, 20 sampled at T=1, batch 1)   ref 0.33 tok/s (1xT4 fp32)
+  B7  GPT-tiny greedy generation   (prompt "ROMEO:\\n" = 7 chars, 200 tokens)          ref 0.31 tok/s (1xT4 fp32)
+
 Throughput runs use synthetic token ids; ``--graph`` captures the whole training step
 (forward + backward + optimizer) in one HIP graph (these tiny configs are launch-bound).
+``--ref-loop`` runs the reference's own loop instead of K timed steps: B1 one 1000-step epoch
+(llama3/LLaMA-jax.ipynb:1059-1080, 30 of them in the reference; the rate is per step), B5 the
+whole 1000 steps with an evaluation every 100 steps of 100 train + 100 val batches
+(gpt/gpt-jax.ipynb:302, :542-551, :795-802), all inside the timed region as in the reference's
+2026 s. ``--dtype fp32`` is the reference's precision (B1/B3/B5/B7 were published in fp32).
+Generation rows time the whole call (prefill + every new token), KV-cached, and also the
+reference's algorithm (re-forward the whole window per token) on the same model.
 Prints one JSON line per run. ``python bench/parity.py [--which B1,B5,B9,B14,...]``
 """
 from __future__ import annotations
@@ -26,10 +36,11 @@ import torch
 
 from common import sdist
 
-REF = {"B1": 29.0e3, "B5": 16.2e3, "B9": 5.3e3, "B13": None, "B14": 97.25, "B15": 0.012954, "B16": 13881.32, "B17": 97.50}
+REF = {"B1": 29.0e3, "B3": 0.33, "B5": 16.2e3, "B7": 0.31, "B9": 5.3e3, "B13": None, "B14": 97.25, "B15": 0.012954, "B16": 13881.32, "B17": 97.50}
 
 
-def _lm_throughput(tag, model, flat, opt, V, B, T, steps, warmup, dtype_name, graph):
+def _lm_throughput(tag, model, flat, opt, V, B, T, steps, warmup, dtype_name, graph, evals=None):
+    """evals: (every, iters_per_split) -- the reference's periodic loss estimate inside the loop."""
     from solvingpapers_amd.utils.graphs import StepGraph
     dev = flat.device
     g = torch.Generator(device=dev).manual_seed(0)
@@ -44,22 +55,83 @@ def _lm_throughput(tag, model, flat, opt, V, B, T, steps, warmup, dtype_name, gr
         opt.step()
         out["loss"] = loss
 
+    @torch.no_grad()
+    def estimate():
+        model.eval()
+        tot = torch.zeros((), device=dev)
+        for _ in range(2 * evals[1]):                     # train split, then val split
+            x.random_(0, V, generator=g)
+            y.random_(0, V, generator=g)
+            tot += model(x, y).float()
+        model.train()
+        out["eval_loss"] = tot / (2 * evals[1])
+
     run = StepGraph(step, warmup=2).replay if graph else step  # opt built graph_safe below
     for _ in range(warmup):
         x.random_(0, V, generator=g)
         run()
+    if evals:
+        estimate()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
+        x.random_(0, V, generator=g)
         run()
+        if evals and (i + 1) % evals[0] == 0:
+            estimate()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     tok_s = B * T * steps / el
-    print(json.dumps({"run": tag, "metric": "training tokens/sec", "value": round(tok_s, 1), "unit": "tokens/s",
-                      "reference": REF[tag], "vs_reference": round(tok_s / REF[tag], 2) if REF[tag] else None,
-                      "dtype": dtype_name,
-                      "ms_per_step": round(el / steps * 1e3, 3), "hip_graph": graph,
-                      "loss": round(float(out["loss"].detach()), 4), "n_gpus": 1}), flush=True)
+    rec = {"run": tag, "metric": "training tokens/sec", "value": round(tok_s, 1), "unit": "tokens/s",
+           "reference": REF[tag], "vs_reference": round(tok_s / REF[tag], 2) if REF[tag] else None,
+           "dtype": dtype_name, "steps": steps, "wall_s": round(el, 3),
+           "ms_per_step": round(el / steps * 1e3, 3), "hip_graph": graph,
+           "loss": round(float(out["loss"].detach()), 4), "n_gpus": 1, "data": "synthetic ids"}
+    if evals:
+        rec["evals"] = f"{steps // evals[0]} x {2 * evals[1]} batches (inside the timed region)"
+    print(json.dumps(rec), flush=True)
+
+
+def _gen_rate(tag, model, prompt_len, new, V, greedy, dtype_name, reps=3):
+    """Whole-call generation rate, KV-cached (ours) and re-forwarding the window per token
+    (the reference's algorithm), batch 1."""
+    from solvingpapers_amd.infer.sampling import sample
+    dev = next(model.parameters()).device
+    g = torch.Generator(device=dev).manual_seed(0)
+    ids = torch.randint(0, V, (1, prompt_len), device=dev, generator=g)
+    model.eval()
+    win = model.max_context
+
+    @torch.no_grad()
+    def reforward():
+        idx = ids
+        for _ in range(new):
+            lg = model(idx[:, -win:])
+            lg = (lg[0] if isinstance(lg, tuple) else lg)[:, -1].float()
+            idx = torch.cat([idx, sample(lg, 1.0, None, greedy, g)], 1)
+        return idx
+
+    def cached():
+        return model.generate(ids, new, greedy=greedy, generator=g)
+
+    res = {}
+    for name, fn in (("kv_cached", cached), ("reforward", reforward)):
+        fn()                                          # warm (allocator, kernels)
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            o = fn()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        assert o.shape[1] == prompt_len + new
+        res[name] = new / best
+    print(json.dumps({"run": tag, "metric": "generated tokens/sec (batch 1, whole call incl. prefill)",
+                      "value": round(res["kv_cached"], 1), "unit": "tokens/s", "reference": REF[tag],
+                      "vs_reference": round(res["kv_cached"] / REF[tag], 1),
+                      "reforward_tok_s": round(res["reforward"], 1), "prompt": prompt_len, "new_tokens": new,
+                      "sampling": "greedy" if greedy else "categorical T=1", "dtype": dtype_name,
+                      "data": "random-init weights, synthetic prompt ids", "n_gpus": 1}), flush=True)
 
 
 def run_b1(a, dev, dt, name):
@@ -70,7 +142,22 @@ def run_b1(a, dev, dt, name):
     m = llama3.Llama3(c, device=dev, dtype=dt, seed=0)
     flat = FlatParams(m, groups=m.param_groups())
     opt = FlatSGD(flat, lr=3e-4, graph_safe=a.graph)
-    _lm_throughput("B1", m, flat, opt, c.vocab_size, 16, 128, a.steps, a.warmup, name, a.graph)
+    _lm_throughput("B1", m, flat, opt, c.vocab_size, 16, 128, 1000 if a.ref_loop else a.steps, a.warmup, name,
+                   a.graph)
+
+
+def run_b3(a, dev, dt, name):
+    from solvingpapers_amd.models import llama3
+    c = llama3.config("llama3_ref")
+    m = llama3.Llama3(c, device=dev, dtype=dt, seed=0)
+    _gen_rate("B3", m, 10, 20, c.vocab_size, False, name)
+
+
+def run_b7(a, dev, dt, name):
+    from solvingpapers_amd.models import gpt
+    c = gpt.config("gpt_ref")
+    m = gpt.GPT(c, device=dev, dtype=dt, seed=0)
+    _gen_rate("B7", m, 7, 200, c.vocab_size, True, name)
 
 
 def run_b5(a, dev, dt, name):
@@ -81,7 +168,8 @@ def run_b5(a, dev, dt, name):
     m = gpt.GPT(c, device=dev, dtype=dt, seed=0)
     flat = FlatParams(m, groups=m.param_groups() if hasattr(m, "param_groups") else None)
     opt = FlatAdamW(flat, lr=3e-4, weight_decay=0.01, graph_safe=a.graph)
-    _lm_throughput("B5", m, flat, opt, c.vocab_size, c.batch_size, c.block_size, a.steps, a.warmup, name, a.graph)
+    _lm_throughput("B5", m, flat, opt, c.vocab_size, c.batch_size, c.block_size, 1000 if a.ref_loop else a.steps,
+                   a.warmup, name, a.graph, evals=(100, 100) if a.ref_loop else None)
 
 
 def run_b9(a, dev, dt, name):
@@ -135,14 +223,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--ref-loop", action="store_true", help="B1: 1000-step epoch; B5: 1000 steps + 10 evals")
     a = ap.parse_args()
     info = sdist.init_distributed()
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.dtype]
     for tag in a.which.split(","):
         if tag == "B1":
             run_b1(a, info.device, dt, a.dtype)
+        elif tag == "B3":
+            run_b3(a, info.device, dt, a.dtype)
         elif tag == "B5":
             run_b5(a, info.device, dt, a.dtype)
+        elif tag == "B7":
+            run_b7(a, info.device, dt, a.dtype)
         elif tag == "B9":
             run_b9(a, info.device, dt, a.dtype)
         elif tag == "B13":

@@ -117,6 +117,9 @@ inline at::Tensor dense_like(const at::Tensor& t, const at::Tensor& like) {
   return at::empty_like(like, t.options()).copy_(t);
 }
 
+// fp32 [P, N] row partials -> fp32 [N] column sums into out (or a new tensor); norm.hip
+at::Tensor reduce_col_parts(const at::Tensor& part, c10::optional<at::Tensor> out = c10::nullopt);
+
 }  // namespace spa
 
 #define SPA_CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a HIP tensor")

@@ -10,64 +10,9 @@
 //
 // Memory bound: 16-byte vector I/O (8 bf16 or 2x4 fp32 per thread), grid-stride,
 // fp32 math; one kernel template per (kind, dtype).
-#include "spa_common.h"
+#include "act_common.h"
 
 namespace spa {
-
-enum ActKind : int { RELU = 0, LEAKY = 1, PRELU = 2, ELU = 3, GELU_TANH = 4, GELU_ERF = 5, SILU = 6,
-                     SIGMOID = 7, TANH = 8, IDENT = 9 };
-
-__device__ __forceinline__ float act_f(int kind, float x, float a) {
-  switch (kind) {
-    case RELU: return x > 0.f ? x : 0.f;
-    case LEAKY:
-    case PRELU: return x > 0.f ? x : a * x;
-    case ELU: return x > 0.f ? x : a * (__expf(x) - 1.f);
-    case GELU_TANH: {
-      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-      const float u = k0 * (x + k1 * x * x * x);
-      return 0.5f * x * (1.f + tanhf(u));
-    }
-    case GELU_ERF: return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
-    case SILU: return x / (1.f + __expf(-x));
-    case SIGMOID: return 1.f / (1.f + __expf(-x));
-    case TANH: return tanhf(x);
-    default: return x;
-  }
-}
-// derivative d act / dx
-__device__ __forceinline__ float act_df(int kind, float x, float a) {
-  switch (kind) {
-    case RELU: return x > 0.f ? 1.f : 0.f;
-    case LEAKY:
-    case PRELU: return x > 0.f ? 1.f : a;
-    case ELU: return x > 0.f ? 1.f : a * __expf(x);
-    case GELU_TANH: {
-      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-      const float u = k0 * (x + k1 * x * x * x);
-      const float th = tanhf(u);
-      return 0.5f * (1.f + th) + 0.5f * x * (1.f - th * th) * k0 * (1.f + 3.f * k1 * x * x);
-    }
-    case GELU_ERF: {
-      const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
-      const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-      return cdf + x * pdf;
-    }
-    case SILU: {
-      const float s = 1.f / (1.f + __expf(-x));
-      return s * (1.f + x * (1.f - s));
-    }
-    case SIGMOID: {
-      const float s = 1.f / (1.f + __expf(-x));
-      return s * (1.f - s);
-    }
-    case TANH: {
-      const float t = tanhf(x);
-      return 1.f - t * t;
-    }
-    default: return 1.f;
-  }
-}
 
 template <typename T, int KIND>
 __global__ __launch_bounds__(256) void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long n, float a) {
@@ -136,6 +81,62 @@ __global__ __launch_bounds__(256) void glu_bwd_kernel(const T* __restrict__ dy, 
   }
 }
 
+// Backward of act(u) fused with the bias gradient of the Linear that produced u: dU = dY * act'(u)
+// is written AND summed over rows (the bias gradient is colsum(dU)), so dU is not read a second
+// time. Layout of rowsum_part_kernel (norm.hip): block (bx, by) covers 256 columns x rows
+// [by*rpb, (by+1)*rpb); 32 lanes x 8 columns span a 512-byte row segment, 8 row groups stride
+// the rows two at a time (4 16-byte loads in flight per lane); fp32 partials part[by, :] are
+// summed by reduce_col_parts (deterministic).
+template <int KIND>
+__global__ __launch_bounds__(256) void act_bwd_colsum_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ u,
+                                                             bf16* __restrict__ du, float* __restrict__ part,
+                                                             long R, int N, long rpb, float a) {
+  __shared__ __attribute__((aligned(16))) float red[8][256];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c0 = blockIdx.x * 256 + cl * 8;
+  const long r0 = (long)blockIdx.y * rpb, r1 = min(R, r0 + rpb);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto one = [&](const float* g, const float* x, long r) {
+    float d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      d[k] = g[k] * act_df(KIND, x[k], a);
+    }
+    store8(du + r * N + c0, d);
+    // sum what was stored (bf16-rounded), as a separate bias-grad pass over dU would
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += (float)(bf16)d[k];
+  };
+  if (c0 < N) {
+    long r = r0 + rg;
+    for (; r + 8 < r1; r += 16) {
+      float g0[8], x0[8], g1[8], x1[8];
+      load8(dy + r * N + c0, g0);
+      load8(u + r * N + c0, x0);
+      load8(dy + (r + 8) * N + c0, g1);
+      load8(u + (r + 8) * N + c0, x1);
+      one(g0, x0, r);
+      one(g1, x1, r + 8);
+    }
+    for (; r < r1; r += 8) {
+      float g0[8], x0[8];
+      load8(dy + r * N + c0, g0);
+      load8(u + r * N + c0, x0);
+      one(g0, x0, r);
+    }
+  }
+  *reinterpret_cast<float4*>(&red[rg][cl * 8]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(&red[rg][cl * 8 + 4]) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][threadIdx.x];
+    part[(long)blockIdx.y * N + c] = t;
+  }
+}
+
 static int ew_grid(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
 
 #define ACT_SWITCH(KIND, ...)                                         \
@@ -186,6 +187,33 @@ at::Tensor act_bwd(const at::Tensor& dy_, const at::Tensor& x_, int64_t kind, do
   SPA_LAUNCH_CHECK();
   return dx;
 }
+// (dU [R, N] bf16, colsum(dU) fp32 [N]) for dy, u [R, N] bf16 contiguous, N % 8 == 0
+std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dy, const at::Tensor& u, int64_t kind, double alpha) {
+  SPA_CHECK_CUDA(u);
+  TORCH_CHECK(u.dim() == 2 && u.scalar_type() == at::kBFloat16 && u.is_contiguous(), "act_bwd_colsum: [R, N] bf16");
+  TORCH_CHECK(dy.sizes() == u.sizes() && dy.scalar_type() == at::kBFloat16 && dy.is_contiguous(),
+              "act_bwd_colsum: dy must match u");
+  const long R = u.size(0);
+  const int N = u.size(1);
+  TORCH_CHECK(N % 8 == 0 && (uintptr_t)u.data_ptr() % 16 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0,
+              "act_bwd_colsum: 16-byte rows");
+  DeviceGuard g(u.device());
+  auto du = at::empty_like(u);
+  auto opts = u.options().dtype(at::kFloat);
+  if (N == 0) return {du, at::empty({0}, opts)};
+  if (R == 0) return {du, at::zeros({N}, opts)};
+  auto st = stream();
+  const int nx = cdiv(N, 256);
+  const long want = std::max<long>(1, std::min<long>(cdiv(1024, nx), cdiv(R, 64)));
+  const long rpb = (R + want - 1) / want;
+  const int P = (int)cdiv(R, rpb);
+  auto part = at::empty({P, N}, opts);
+  ACT_SWITCH(kind, act_bwd_colsum_kernel<K_><<<dim3(nx, P), 256, 0, st>>>(
+                       (const bf16*)dy.data_ptr(), (const bf16*)u.data_ptr(), (bf16*)du.data_ptr(),
+                       part.data_ptr<float>(), R, N, rpb, (float)alpha));
+  SPA_LAUNCH_CHECK();
+  return {du, reduce_col_parts(part)};
+}
 at::Tensor glu_fwd(const at::Tensor& gu_, int64_t kind) {
   SPA_CHECK_CUDA(gu_);
   auto gu = gu_.contiguous();
@@ -226,12 +254,14 @@ at::Tensor glu_bwd(const at::Tensor& dy_, const at::Tensor& gu_, int64_t kind) {
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("act_fwd(Tensor x, int kind, float alpha) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int kind, float alpha) -> Tensor");
+  m.def("act_bwd_colsum(Tensor dy, Tensor u, int kind, float alpha) -> Tensor[]");
   m.def("glu_fwd(Tensor gu, int kind) -> Tensor");
   m.def("glu_bwd(Tensor dy, Tensor gu, int kind) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("act_fwd", &spa::act_fwd);
   m.impl("act_bwd", &spa::act_bwd);
+  m.impl("act_bwd_colsum", &spa::act_bwd_colsum);
   m.impl("glu_fwd", &spa::glu_fwd);
   m.impl("glu_bwd", &spa::glu_bwd);
 }

@@ -225,9 +225,16 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     for (int t = 0; t < NSUB; ++t) {
       const int ks0 = k0 + 32 * t;
       if (ks0 < wave_kend) {
-        f32x16 s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[0]), qf[0], splat16(0.f));
+        // every K-row operand read issued before the chain (sched_group_barrier: DS reads, then
+        // MFMAs): hipcc's default order re-used one register quad and waited out each LDS read
+        bf16x8 kr[KS];
 #pragma unroll
-        for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[ks]), qf[ks], s);
+        for (int ks = 0; ks < KS; ++ks) kr[ks] = ld_row(Ks + 32 * t * IK, offk.row[ks]);
+        f32x16 s = mfma32(kr[0], qf[0], splat16(0.f));
+#pragma unroll
+        for (int ks = 1; ks < KS; ++ks) s = mfma32(kr[ks], qf[ks], s);
+        __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
         const bool need_mask = (ks0 + 32 > p.Tk) || (CAUSAL && ks0 + 31 > q0 + p.causal_off);
         if (need_mask) mask(s, ks0);
         softmax(s);
@@ -242,6 +249,12 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     }
     __syncthreads();
   };
+  // the loop's prefetch is conditional (no loads on the last tiles), so hipcc cannot count the
+  // q-fragment loads of the prologue past it and waited vmcnt(0) -- draining the prefetch just
+  // issued -- at every tile's first MFMA. An empty asm that USES the fragments makes it wait for
+  // them here, once (an asm s_waitcnt is invisible to its waitcnt pass)
+#pragma unroll
+  for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(qf[s]));
   for (int j = 0; j < ntiles; j += 2) {
     body(j, IC<0>{});
     if (j + 1 < ntiles) body(j + 1, IC<1>{});
@@ -365,12 +378,29 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     for (int t = 0; t < NSUB; ++t) {
       const int ks0 = k0 + 32 * t;
       if (ks0 < wave_kend) {
-        f32x16 s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[0]), qf[0], splat16(0.f));
+        // K rows up front, V rows issued between the S MFMAs (sched_group_barrier), so neither
+        // chain waits out an LDS round trip per MFMA
+        bf16x8 kr[KSK], vr[KSV];
 #pragma unroll
-        for (int ks = 1; ks < KSK; ++ks) s = mfma32(ld_row(Ks + 32 * t * IK, offk.row[ks]), qf[ks], s);
-        f32x16 dp = mfma32(ld_row(Vs + 32 * t * IV, offv.row[0]), df[0], splat16(DROP ? 0.f : -dlt));
+        for (int ks = 0; ks < KSK; ++ks) kr[ks] = ld_row(Ks + 32 * t * IK, offk.row[ks]);
 #pragma unroll
-        for (int ks = 1; ks < KSV; ++ks) dp = mfma32(ld_row(Vs + 32 * t * IV, offv.row[ks]), df[ks], dp);
+        for (int ks = 0; ks < KSV; ++ks) vr[ks] = ld_row(Vs + 32 * t * IV, offv.row[ks]);
+        f32x16 s = mfma32(kr[0], qf[0], splat16(0.f));
+#pragma unroll
+        for (int ks = 1; ks < KSK; ++ks) s = mfma32(kr[ks], qf[ks], s);
+        f32x16 dp = mfma32(vr[0], df[0], splat16(DROP ? 0.f : -dlt));
+#pragma unroll
+        for (int ks = 1; ks < KSV; ++ks) dp = mfma32(vr[ks], df[ks], dp);
+        constexpr int KMIN = KSK < KSV ? KSK : KSV;
+        __builtin_amdgcn_sched_group_barrier(0x100, KSK, 0);
+#pragma unroll
+        for (int ks = 0; ks < KMIN; ++ks) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if constexpr (KSK > KSV) __builtin_amdgcn_sched_group_barrier(0x008, KSK - KSV, 0);
+        if constexpr (KSV > KSK) __builtin_amdgcn_sched_group_barrier(0x100, KSV - KSK, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KSV, 0);
         if constexpr (DROP) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {

@@ -36,7 +36,7 @@
 //     f(r) = ((r & 3) << 2) | ((r >> 2) & 3) -- read with ds_read_b64_tr_b16 (conflict-free).
 // Out-of-range rows / columns / tokens read as zero through the buffer descriptor range check
 // (dW descriptors start at the expert's first token and end at its last).
-#include "spa_common.h"
+#include "act_common.h"
 #include "gemm_common.h"
 
 #include <map>
@@ -122,12 +122,24 @@ __device__ __forceinline__ bf16x8 rd_ks(const char* half, int col0, int s, int l
 // results by construction and are never selected by the op unless SPA_GG8_ABLATE is set.
 // PART (mode 2 only): the "experts" are token slices of one dense dW product (split-K) and each
 // writes its fp32 partial [M, N] at C + e * strideC floats, summed by wgrad_reduce_kernel.
-template <int MODE, int ABL = 0, bool ILV = false, bool PART = false>
+// EPI (single group, E == 1, no accumulate; gemm8_epi below): fused epilogues of a Linear +
+// activation pair, applied to the bf16-rounded C values exactly as the separate kernels would:
+//   1 (mode 0)  u = C + bias[n] -> ep.aux, C = act(u)                    (fc1 + act forward)
+//   2 (mode 1)  C = C * act'(ep.aux[m, n]), fp32 column sums of C per 256-row tile -> ep.part
+//               [m-tile, N] (the bias gradient of the Linear that produced aux)   (fc2 dgrad + act')
+struct G8Epi {
+  const bf16* bias;
+  bf16* aux;
+  float* part;
+  float alpha;
+};
+
+template <int MODE, int ABL = 0, bool ILV = false, bool PART = false, int EPI = 0, int KIND = 0>
 __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                                bf16* __restrict__ C, const int* __restrict__ offsets,
                                                                int E, int M, int N, int K, long lda, long ldb, long ldc,
                                                                long strideB, long strideC, int accumulate, long a_rows,
-                                                               long b_rows) {
+                                                               long b_rows, G8Epi ep) {
   using namespace g8;
   constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
   // ONE LDS array (a second __shared__ object can make hipcc drain the DMA queue before ds_reads);
@@ -393,6 +405,21 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   // distinct bank pairs) -> whole-row 16-byte global stores (a per-lane 8-byte store at a row
   // stride would touch 16 cache lines per instruction)
   constexpr int RS = 256 * 2 + 16;
+  // EPI 1: this lane's bias values (columns n0 + nh*128 + wn*32 + 16j + 4(l>>4) + q), added in fp32
+  float bv[2][2][4];
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
+        bf16x4 b4 = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+        if (gn < N) b4 = *reinterpret_cast<const bf16x4*>(ep.bias + gn);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[nh][j][q] = (float)b4[q];
+      }
+  }
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // EPI 2: column sums of this lane's chunk
   __syncthreads();
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
@@ -405,7 +432,10 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
           const f32x4 v = acc[mh * 4 + i][nh * 2 + j];
           bf16x4 w4;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+          for (int q = 0; q < 4; ++q) {
+            if constexpr (EPI == 1) w4[q] = (bf16)(v[q] + bv[nh][j][q]);
+            else w4[q] = (bf16)v[q];
+          }
           const int r = wm * 64 + 16 * i + (lane & 15);
           const int cn = nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
           *reinterpret_cast<bf16x4*>(smem + r * RS + cn * 2) = w4;
@@ -419,7 +449,19 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       if ((MODE == 2 ? gm < M : gm < mend) && gn < N) {
         bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * RS + ch * 16);
         bf16* cp = Cp + gm * ldc + gn;
-        if (accumulate) {
+        if constexpr (EPI == 1) {
+          *reinterpret_cast<bf16x8*>(ep.aux + gm * ldc + gn) = v;       // pre-activation u
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = (bf16)act_f(KIND, (float)v[q], ep.alpha);
+        } else if constexpr (EPI == 2) {
+          const bf16x8 u = *reinterpret_cast<const bf16x8*>(ep.aux + gm * ldc + gn);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            v[q] = (bf16)((float)v[q] * act_df(KIND, (float)u[q], ep.alpha));
+            csum[q] += (float)v[q];
+          }
+        }
+        if (EPI == 0 && accumulate) {
           const bf16x8 old = *reinterpret_cast<const bf16x8*>(cp);
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)old[q]);
@@ -428,6 +470,21 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       }
     }
     __syncthreads();
+  }
+  if constexpr (EPI == 2) {
+    // every thread owns column chunk tid & 31 on rows (tid >> 5) + 16c: 16 partial rows per column
+    float* red = reinterpret_cast<float*>(smem);          // [16][256]
+#pragma unroll
+    for (int q = 0; q < 8; q += 4)
+      *reinterpret_cast<f32x4*>(red + (tid >> 5) * 256 + (tid & 31) * 8 + q) =
+          f32x4{csum[q], csum[q + 1], csum[q + 2], csum[q + 3]};
+    __syncthreads();
+    if (tid < 256 && n0 + tid < N) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) t += red[g * 256 + tid];
+      ep.part[(long)(m0 / BM) * N + n0 + tid] = t;
+    }
   }
 }
 
@@ -508,7 +565,7 @@ at::Tensor wgrad8(const at::Tensor& dy, const at::Tensor& x, const c10::optional
   auto part = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
   grouped_gemm8_kernel<2, 0, false, true><<<S * tiles, 512, 0, st>>>(
       (const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(), reinterpret_cast<bf16*>(part.data_ptr<float>()),
-      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T);
+      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T, G8Epi{});
   SPA_LAUNCH_CHECK();
   const long n = (long)N * K;
   const int rb = (int)std::min<long>((n / 4 + 255) / 256, 4096);
@@ -553,10 +610,10 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 #define G8_L(MD, AB)                                                                                          \
   if (abl == 4) grouped_gemm8_kernel<MD, 0, true><<<grid, 512, 0, st>>>(                                     \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,  \
-      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw);                                           \
+      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{});                                  \
   else grouped_gemm8_kernel<MD, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),     \
                                                      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
-                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw)
+                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{})
     const int abl = ablation();
     if (mode == 0) {
       if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else { G8_L(0, 0); }
@@ -578,10 +635,10 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 #define G8_L2(AB)                                                                                             \
   if (abl == 4) grouped_gemm8_kernel<2, 0, true><<<grid, 512, 0, st>>>(                                      \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N,  \
-      K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, T, T);                                              \
+      K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{});                                     \
   else grouped_gemm8_kernel<2, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),      \
                                                     (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, \
-                                                    K, 0, (long)N * K, accumulate ? 1 : 0, T, T)
+                                                    K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{})
   const int abl = ablation();
   if (abl == 1) { G8_L2(1); } else if (abl == 2) { G8_L2(2); } else if (abl == 3) { G8_L2(3); } else { G8_L2(0); }
 #undef G8_L2
@@ -589,13 +646,74 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
   return out;
 }
 
+// Linear + activation epilogues on the 8-phase kernel (one group), see G8Epi:
+//   epi 1: a = x [M, K], w = W [N, K], aux = bias [N]      -> (act(x W^T + b), u = x W^T + b)
+//   epi 2: a = dY [M, K], w = W [K, N] (weight [out, in]), aux = u [M, N]
+//                                                           -> (dU = (dY W) * act'(u), colsum(dU) fp32 [N])
+// K % 64 == 0, N % 8 == 0; offsets = the device tensor [0, M].
+std::vector<at::Tensor> gemm8_epi(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t epi,
+                                  const at::Tensor& aux, int64_t kind, double alpha) {
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  aux.scalar_type() == at::kBFloat16, "gemm8_epi: bf16");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.is_contiguous() && w.is_contiguous() && aux.is_contiguous(),
+              "gemm8_epi: contiguous 2-D operands");
+  TORCH_CHECK(offsets.scalar_type() == at::kInt && offsets.numel() == 2, "gemm8_epi: offsets [0, M]");
+  TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)w.data_ptr() % 16 == 0 &&
+                  (uintptr_t)aux.data_ptr() % 16 == 0, "gemm8_epi: 16-B aligned");
+  const int M = a.size(0), K = a.size(1);
+  const int mode = epi == 1 ? 0 : 1;
+  TORCH_CHECK(epi == 1 || epi == 2, "gemm8_epi: epi 1 or 2");
+  const int N = mode == 0 ? w.size(0) : w.size(1);
+  TORCH_CHECK((mode == 0 ? w.size(1) : w.size(0)) == K, "gemm8_epi: A/W shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && N % 8 == 0, "gemm8_epi: reduction % 64, output cols % 8");
+  if (epi == 1) {
+    TORCH_CHECK(aux.numel() == N, "gemm8_epi: bias [N]");
+  } else {
+    TORCH_CHECK(aux.dim() == 2 && aux.size(0) == M && aux.size(1) == N, "gemm8_epi: u [M, N]");
+  }
+  TORCH_CHECK((long)(M + 256) * K * 2 < (1L << 32) && (long)(w.numel() + 256L * K) * 2 < (1L << 32),
+              "gemm8_epi: operands < 4 GiB");
+  TORCH_CHECK(kind == GELU_ERF || kind == GELU_TANH || kind == RELU || kind == SILU, "gemm8_epi: act kind");
+  DeviceGuard g(a.device());
+  auto st = stream();
+  auto out = at::empty({M, N}, a.options());
+  const int mtiles = cdiv(M, 256);
+  at::Tensor second = epi == 1 ? at::empty({M, N}, a.options()) : at::empty({mtiles, N}, a.options().dtype(at::kFloat));
+  if (M == 0) return {out, epi == 1 ? second : at::zeros({N}, a.options().dtype(at::kFloat))};
+  G8Epi ep{};
+  ep.alpha = (float)alpha;
+  if (epi == 1) { ep.bias = (const bf16*)aux.data_ptr(); ep.aux = (bf16*)second.data_ptr(); }
+  else { ep.aux = (bf16*)aux.data_ptr(); ep.part = second.data_ptr<float>(); }
+  const int grid = (mtiles + 1) * cdiv(N, 256);
+  const int Nw = w.size(0), Kw = w.size(1);
+#define G8E(MD, EP, KD)                                                                                      \
+  grouped_gemm8_kernel<MD, 0, false, false, EP, KD><<<grid, 512, 0, st>>>(                                   \
+      (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), 1, M, \
+      N, K, K, Kw, N, (long)Nw * Kw, 0, 0, M, Nw, ep)
+#define G8E_KIND(MD, EP)                                  \
+  switch (kind) {                                         \
+    case GELU_ERF: G8E(MD, EP, GELU_ERF); break;          \
+    case GELU_TANH: G8E(MD, EP, GELU_TANH); break;        \
+    case RELU: G8E(MD, EP, RELU); break;                  \
+    default: G8E(MD, EP, SILU); break;                    \
+  }
+  if (epi == 1) { G8E_KIND(0, 1); } else { G8E_KIND(1, 2); }
+#undef G8E_KIND
+#undef G8E
+  SPA_LAUNCH_CHECK();
+  if (epi == 1) return {out, second};
+  return {out, reduce_col_parts(second)};
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("grouped_gemm8(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def("wgrad8(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate, int splits) -> Tensor");
+  m.def("gemm8_epi(Tensor a, Tensor w, Tensor offsets, int epi, Tensor aux, int kind, float alpha) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("grouped_gemm8", &spa::grouped_gemm8);
   m.impl("wgrad8", &spa::wgrad8);
+  m.impl("gemm8_epi", &spa::gemm8_epi);
 }

@@ -422,8 +422,20 @@ at::Tensor rowsum_bf16(const at::Tensor& x) {
   const int P = (int)cdiv(R, rpb);
   auto part = at::empty({P, N}, opts);
   rowsum_part_kernel<<<dim3(nx, P), 256, 0, st>>>((const bf16*)x.data_ptr(), part.data_ptr<float>(), R, N, ld, rpb);
+  SPA_LAUNCH_CHECK();
+  return reduce_col_parts(part, out);
+}
+
+// fp32 [P, N] row partials -> fp32 [N] column sums (two levels when P > 64; deterministic)
+at::Tensor reduce_col_parts(const at::Tensor& part, c10::optional<at::Tensor> out_) {
+  TORCH_CHECK(part.dim() == 2 && part.scalar_type() == at::kFloat && part.is_contiguous());
+  const int PP0 = part.size(0), N = part.size(1);
+  auto opts = part.options();
+  auto out = out_ ? *out_ : at::empty({N}, opts);
+  if (N == 0) return out;
+  auto st = stream();
   const float* src = part.data_ptr<float>();
-  int PP = P;
+  int PP = PP0;
   at::Tensor p2;
   if (PP > 64) {
     const int Y = std::min(64, cdiv(PP, 16));

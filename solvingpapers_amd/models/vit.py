@@ -23,6 +23,7 @@ import torch.nn as tnn
 
 from .. import nn as snn
 from ..ops import act, attention_packed, cross_entropy, layer_norm, linear
+from ..ops.linear import mlp
 from ..ops.misc import patch_embed
 from ..utils.grad import mark_ready
 
@@ -112,7 +113,9 @@ class TransformerEncoder(tnn.Module):
             n1, x = self.layer_norm1(m, residual=h)
         a = self.multihead_attention(n1)
         n2, h2 = self.layer_norm2(a, residual=x)     # h2 = x + attn, n2 = LN2(h2)
-        return h2, self.mlp(n2)
+        fc1, gelu, fc2 = self.mlp
+        # one op: fc1 + bias + GELU forward epilogue, fc2-dX + GELU' + fc1 bias-grad backward epilogue
+        return h2, mlp(n2, fc1.weight, fc1.bias, fc2.weight, fc2.bias, gelu.kind, gelu.alpha)
 
 
 class MLPHead(tnn.Module):

@@ -87,6 +87,18 @@ def dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.mm(dy2, w) if wt is None else torch.mm(dy2, wt.t())
 
 
+def _commit_bias(b, s):
+    """Commit the fp32 column sum ``s`` as the gradient of bias ``b`` (flat buffer or .grad)."""
+    def _b(out, acc):
+        if out is None:
+            return s.to(b.dtype)
+        if acc:
+            out.add_(s.to(out.dtype))
+        else:
+            out.copy_(s)
+    return commit(b, _b)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -114,16 +126,121 @@ class _LinearFn(torch.autograd.Function):
                 return wgrad(dy2, x2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
-            def _b(out, acc):
-                s = bias_grad(dy2)
-                if out is None:
-                    return s.to(b.dtype)
-                if acc:
-                    out.add_(s.to(out.dtype))
-                else:
-                    out.copy_(s)
-            gb = commit(b, _b)
+            gb = _commit_bias(b, bias_grad(dy2))
         return dx, gw, gb
+
+
+class _LinearActFn(torch.autograd.Function):
+    """y = act(x W^T + b) (ViT / GPT MLP fc1 + GELU). Forward: library GEMM with the bias
+    epilogue, then the activation kernel; the pre-activation u is kept for backward. Backward:
+    ONE pass over (dY, u) writes dU = dY act'(u) and its column sums -- the bias gradient --
+    (activation.hip act_bwd_colsum), instead of an activation-backward pass and a second read of
+    dU for the bias; then dX = dU W and dW = dU^T X as in :class:`_LinearFn`."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, kind, alpha):
+        x2 = x.reshape(-1, x.shape[-1])
+        u = torch.addmm(b, x2, w.t())
+        y = _ext.ops().act_fwd(u, kind, alpha)
+        ctx.save_for_backward(x, u)
+        ctx.w, ctx.b, ctx.kind, ctx.alpha = w, b, kind, alpha
+        return torch.ops.aten._unsafe_view(y, (*x.shape[:-1], w.shape[0]))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, u = ctx.saved_tensors
+        w, b = ctx.w, ctx.b
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        gb = None
+        if ctx.needs_input_grad[2]:
+            du, s = _ext.ops().act_bwd_colsum(dy2, u, ctx.kind, ctx.alpha)
+            gb = _commit_bias(b, s)
+        else:
+            du = _ext.ops().act_bwd(dy2, u, ctx.kind, ctx.alpha)
+        dx = dgrad(du, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            def _w(out, acc):
+                return wgrad(du, x2, out, acc)
+            gw = commit(w, _w)
+        return dx, gw, gb, None, None
+
+
+def linear_act(x, w, b, kind="gelu", alpha=None):
+    """act(linear(x, w, b)) with the activation backward and the bias gradient fused into one
+    pass on the GPU (bf16, bias present, widths % 8); elsewhere the two ops in sequence."""
+    from .activation import act
+    from .reference import ACT_KINDS
+    if (b is not None and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and w.shape[0] % 8 == 0 and x.shape[-1] % 8 == 0 and x.numel() > 0):
+        if alpha is None:
+            alpha = 0.01 if kind == "leaky_relu" else (1.0 if kind == "elu" else 0.0)
+        return _LinearActFn.apply(x, w, b, ACT_KINDS[kind], float(alpha))
+    return act(linear(x, w, b), kind, alpha)
+
+
+# fc1 + act forward and fc2-dgrad + act' backward on the 8-phase kernel's fused epilogues
+# (csrc/kernels/gemm8.hip gemm8_epi); SPA_MLP_EPI=0 -> library GEMMs + separate passes
+MLP_EPI = os.environ.get("SPA_MLP_EPI", "1") != "0"
+
+
+def _mlp_epi_ok(x2, w1, w2):
+    F, D = w1.shape
+    return (MLP_EPI and x2.is_cuda and x2.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16
+            and w2.dtype == torch.bfloat16 and D % 64 == 0 and F % 64 == 0 and w2.shape == (D, F)
+            and x2.shape[0] > 0 and x2.is_contiguous() and w1.is_contiguous() and w2.is_contiguous())
+
+
+class _MLPFn(torch.autograd.Function):
+    """fc2(act(fc1(x))) with both biases (ViT / transformer MLP without inner dropout).
+
+    Forward: fc1 on the 8-phase kernel with the bias + activation epilogue (writes y = act(u) and
+    the pre-activation u in the same pass), fc2 on the library GEMM. Backward: fc2's dX product
+    runs on the same kernel with the act' epilogue -- dU = (dOut W2) * act'(u) and the column
+    sums of dU (fc1's bias gradient) leave the GEMM together -- so the [T, F] activation
+    gradient is written once and never re-read for the bias; then the usual dX / dW products.
+    Rounding matches the unfused chain (bf16 u and y; dY W2 rounded to bf16 before act')."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, kind, alpha):
+        x2 = x.reshape(-1, x.shape[-1])
+        grp = _one_group(x2.shape[0], x2.device)
+        y, u = _ext.ops().gemm8_epi(x2, w1, grp, 1, b1, kind, alpha)
+        out = torch.addmm(b2, y, w2.t())
+        ctx.save_for_backward(x, u, y)
+        ctx.ws, ctx.kind, ctx.alpha = (w1, b1, w2, b2), kind, alpha
+        return torch.ops.aten._unsafe_view(out, (*x.shape[:-1], w2.shape[0]))
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, u, y = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.ws
+        d2 = dout.reshape(-1, dout.shape[-1]).contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        g = [None] * 7
+        if ctx.needs_input_grad[3]:
+            g[3] = commit(w2, lambda out, acc: wgrad(d2, y, out, acc))
+        if ctx.needs_input_grad[4]:
+            g[4] = _commit_bias(b2, bias_grad(d2))
+        du, s1 = _ext.ops().gemm8_epi(d2, w2, _one_group(d2.shape[0], d2.device), 2, u, ctx.kind, ctx.alpha)
+        if ctx.needs_input_grad[2]:
+            g[2] = _commit_bias(b1, s1)
+        if ctx.needs_input_grad[1]:
+            g[1] = commit(w1, lambda out, acc: wgrad(du, x2, out, acc))
+        if ctx.needs_input_grad[0]:
+            g[0] = dgrad(du, w1).view(x.shape)
+        return tuple(g)
+
+
+def mlp(x, w1, b1, w2, b2, kind="gelu", alpha=None):
+    """fc2(act(fc1(x))) -- the fused kernel path where it applies, else linear_act + linear."""
+    from .reference import ACT_KINDS
+    if b1 is not None and b2 is not None and kind in ("gelu", "gelu_erf", "gelu_tanh", "relu", "silu"):
+        x2 = x.reshape(-1, x.shape[-1])
+        if _mlp_epi_ok(x2, w1, w2):
+            return _MLPFn.apply(x, w1, b1, w2, b2, ACT_KINDS[kind], 0.0)
+    return linear(linear_act(x, w1, b1, kind, alpha), w2, b2)
 
 
 def _gemv_ok(x, w, b) -> bool:
@@ -178,15 +295,7 @@ class _LinearFP8Fn(torch.autograd.Function):
                 return wgrad(dy2, x2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
-            def _b(out, acc):
-                s = bias_grad(dy2)
-                if out is None:
-                    return s.to(b.dtype)
-                if acc:
-                    out.add_(s.to(out.dtype))
-                else:
-                    out.copy_(s)
-            gb = commit(b, _b)
+            gb = _commit_bias(b, bias_grad(dy2))
         return dx, gw, gb
 
 

@@ -80,6 +80,53 @@ def test_activation(kind, dtype):
     assert rel(x.grad, xf.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("kind,R", [("gelu", 1000), ("gelu", 50432 // 8), ("relu", 77)])
+def test_linear_act_fused_bias_grad(kind, R):
+    """fc1 + activation with the fused activation-backward + bias-gradient pass vs fp32 torch."""
+    from solvingpapers_amd.ops.linear import linear_act
+    K, N = 256, 768
+    x = (torch.randn(R, K, device=DEV) * 0.5).bfloat16().requires_grad_()
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16().requires_grad_()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16().requires_grad_()
+    y = linear_act(x, w, b, kind)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yf = R_act(xf @ wf.t() + bf, kind)
+    (yf * g.float()).sum().backward()
+    assert rel(y, yf) < 1e-2
+    for got, ref in ((x.grad, xf.grad), (w.grad, wf.grad), (b.grad, bf.grad)):
+        assert rel(got, ref) < 2e-2
+
+
+@pytest.mark.parametrize("kind,R,D,F", [("gelu", 1000, 256, 1024), ("gelu", 6304, 768, 3072), ("relu", 300, 128, 192)])
+def test_mlp_fused_epilogues(kind, R, D, F):
+    """fc2(act(fc1 x)) on the 8-phase kernel's bias+act / act'+colsum epilogues vs fp32 torch."""
+    from solvingpapers_amd.ops import linear as L
+    assert L._mlp_epi_ok(torch.empty(R, D, device=DEV, dtype=torch.bfloat16),
+                         torch.empty(F, D, device=DEV, dtype=torch.bfloat16),
+                         torch.empty(D, F, device=DEV, dtype=torch.bfloat16))
+    x = (torch.randn(R, D, device=DEV) * 0.5).bfloat16().requires_grad_()
+    w1 = (torch.randn(F, D, device=DEV) * D ** -0.5).bfloat16().requires_grad_()
+    b1 = (torch.randn(F, device=DEV) * 0.1).bfloat16().requires_grad_()
+    w2 = (torch.randn(D, F, device=DEV) * F ** -0.5).bfloat16().requires_grad_()
+    b2 = (torch.randn(D, device=DEV) * 0.1).bfloat16().requires_grad_()
+    y = L.mlp(x, w1, b1, w2, b2, kind)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    ps = (x, w1, b1, w2, b2)
+    fs = [t.detach().float().requires_grad_() for t in ps]
+    yf = R_act(fs[0] @ fs[1].t() + fs[2], kind) @ fs[3].t() + fs[4]
+    (yf * g.float()).sum().backward()
+    assert rel(y, yf) < 1e-2
+    for p_, f_ in zip(ps, fs):
+        assert rel(p_.grad, f_.grad) < 2e-2, p_.shape
+
+
+def R_act(x, kind):
+    return R.act(x, kind, 0.0)
+
+
 @pytest.mark.parametrize("kind", ["silu", "gelu", "gelu_tanh"])
 def test_glu(kind):
     from solvingpapers_amd.ops import glu
