@@ -112,6 +112,22 @@ __device__ __forceinline__ bf16x8 ld_tr(const bf16* img, int offa, int offb) {
 }
 template <int V> using IC = std::integral_constant<int, V>;
 
+// Instruction order for an MFMA chain whose operands come from LDS (sched_group_barrier masks:
+// 0x100 DS read, 0x008 MFMA): PRE + AHEAD * PER reads first, then (1 MFMA, PER reads) for the
+// next N - AHEAD MFMAs, then the last AHEAD MFMAs -- each MFMA's operand was requested AHEAD
+// MFMAs earlier, so the counted lgkmcnt waits overlap LDS latency with the chain instead of the
+// default schedule's read -> lgkmcnt(0) -> MFMA serialisation. Place right after the chain.
+template <int N, int PER, int AHEAD, int PRE = 0>
+__device__ __forceinline__ void chain_sched() {
+  __builtin_amdgcn_sched_group_barrier(0x100, PRE + AHEAD * PER, 0);
+#pragma unroll
+  for (int i = 0; i < N - AHEAD; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, PER, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, AHEAD, 0);
+}
+
 // Register-staged tile loader: ROWS x HDC bf16 tile of a strided tensor -> regs -> LDS image
 // with IW-element rows (IW = img_w<HDC>, >= HDC).
 // Global side: one buffer descriptor per tile (scalar work), its range ending at the

@@ -109,14 +109,15 @@ __global__ __launch_bounds__(256) void act_bwd_colsum_kernel(const bf16* __restr
   };
   if (c0 < N) {
     long r = r0 + rg;
-    for (; r + 8 < r1; r += 16) {
-      float g0[8], x0[8], g1[8], x1[8];
-      load8(dy + r * N + c0, g0);
-      load8(u + r * N + c0, x0);
-      load8(dy + (r + 8) * N + c0, g1);
-      load8(u + (r + 8) * N + c0, x1);
-      one(g0, x0, r);
-      one(g1, x1, r + 8);
+    for (; r + 24 < r1; r += 32) {                 // 8 16-byte loads in flight per lane
+      float g[4][8], x[4][8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        load8(dy + (r + 8 * k) * N + c0, g[k]);
+        load8(u + (r + 8 * k) * N + c0, x[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) one(g[k], x[k], r + 8 * k);
     }
     for (; r < r1; r += 8) {
       float g0[8], x0[8];
@@ -204,7 +205,8 @@ std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dy, const at::Tensor& u
   if (R == 0) return {du, at::zeros({N}, opts)};
   auto st = stream();
   const int nx = cdiv(N, 256);
-  const long want = std::max<long>(1, std::min<long>(cdiv(1024, nx), cdiv(R, 64)));
+  // >= 2048 blocks (8 per CU), each at least 128 rows
+  const long want = std::max<long>(1, std::min<long>(cdiv(2048, nx), cdiv(R, 128)));
   const long rpb = (R + want - 1) / want;
   const int P = (int)cdiv(R, rpb);
   auto part = at::empty({P, N}, opts);

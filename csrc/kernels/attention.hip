@@ -937,6 +937,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
 // in MFMA-operand order (role A re-reads its own P for dV). Q / dO tiles live in a 3-deep LDS
 // ring (tiles k-1 and k are read while k+1 is committed); lse / delta travel with their tile.
 // ---------------------------------------------------------------------------
+#ifndef DKDV3_SCHED
+#define DKDV3_SCHED 0   // 1: chain_sched hints (no effect at 256 VGPRs: one operand register quad; kept for experiments)
+#endif
 template <int HD, bool CAUSAL>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 512, IW = img_w<HD>();
@@ -1048,6 +1051,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
             acc[dt] = mfma32(ld_tr(Dp + 32 * t * IW, off.tra[dt], off.trb[dt]), pa, acc[dt]);
             acc[dt] = mfma32(ld_tr(Dp + (32 * t + 16) * IW, off.tra[dt], off.trb[dt]), pb, acc[dt]);
           }
+          if (DKDV3_SCHED) chain_sched<2 * DT, 2, 2, 2>();
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -1060,6 +1064,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           f32x16 s = mfma32(ld_row(Qc + 32 * t * IW, off.row[0]), xf[0], splat16(0.f));
 #pragma unroll
           for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Qc + 32 * t * IW, off.row[ks]), xf[ks], s);
+          if (DKDV3_SCHED) chain_sched<KS, 1, 2>();
           const int qt0 = qq0 + 32 * t;
           if (CAUSAL && qt0 + p.causal_off < kw0 + 31) {
             const int d = key - qt0 - 4 * hh - p.causal_off;   // row offsets below d are masked
@@ -1098,6 +1103,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
         }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) dp = mfma32(ld_row(Dpr + 32 * t * IW, off.row[ks]), xf[ks], dp);
+        if (DKDV3_SCHED) chain_sched<KS, 1, 2, 4>();      // + the 4 delta reads
         const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 0) * 512);
         const bf16x8 pb = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 1) * 512);
         f32x16 ds;
@@ -1112,6 +1118,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           acc[dt] = mfma32(ld_tr(Qp + 32 * t * IW, off.tra[dt], off.trb[dt]), sa, acc[dt]);
           acc[dt] = mfma32(ld_tr(Qp + (32 * t + 16) * IW, off.tra[dt], off.trb[dt]), sb, acc[dt]);
         }
+        if (DKDV3_SCHED) chain_sched<2 * DT, 2, 2, 2>();  // + the P(k-1) reads
         __builtin_amdgcn_sched_barrier(0);
       }
     }

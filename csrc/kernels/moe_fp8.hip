@@ -175,17 +175,73 @@ __global__ __launch_bounds__(256) void dequant_act_blk_kernel(const uint8_t* __r
   }
 }
 
+// Weight-gradient operands (dW_e = dY_e^T X_e, reduction over the expert's tokens): x [T, C] bf16
+// with rows grouped by expert (offsets [E+1]) -> q [C, ldq] e4m3 TRANSPOSED (token-contiguous)
+// with each expert's segment starting at the 128-aligned padded offset poff[e] and zero-filled to
+// it, and s [C, ldq/128] E8M0: one scale per (channel, 128-token block) -- the 128 x 1 tiles of the
+// DeepSeek-V3 recipe for the Wgrad operands. Block (tb, cb): padded tokens [128 tb, +128) x
+// channels [64 cb, +64); tile through LDS in fp32, per-channel amax over the 128 tokens, then
+// 128-byte rows of the transposed image.
+__global__ __launch_bounds__(256) void quant_t_fp8_seg_kernel(const bf16* __restrict__ x, const int* __restrict__ offsets,
+                                                              const int* __restrict__ poff, int E, int C,
+                                                              uint8_t* __restrict__ q, uint8_t* __restrict__ s, long ldq) {
+  __shared__ float tile[128][65];
+  __shared__ float inv_s[64];
+  const int tb = blockIdx.x, cb = blockIdx.y, tid = threadIdx.x;
+  const int p0 = tb * 128;
+  if (p0 >= poff[E]) return;
+  int lo = 0, hi = E;                                   // expert e: poff[e] <= p0 < poff[e + 1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (poff[mid] <= p0) lo = mid; else hi = mid;
+  }
+  const int e = lo;
+  const long src0 = offsets[e] + (p0 - poff[e]), send = offsets[e + 1];
+  const int c8 = (tid & 7) * 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (tid >> 3) + 32 * i;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (src0 + r < send) load8(x + (src0 + r) * C + cb * 64 + c8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[r][c8 + j] = v[j];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float amax = 0.f;
+    for (int r = 0; r < 128; ++r) amax = fmaxf(amax, fabsf(tile[r][tid]));
+    const int ex = e8m0_exp(amax);
+    inv_s[tid] = e8m0_inv(ex);
+    s[(long)(cb * 64 + tid) * (ldq / 128) + tb] = (uint8_t)(ex + 127);
+  }
+  __syncthreads();
+  const int c = tid >> 2, seg = tid & 3;               // channel c, tokens [32 seg, +32)
+  const float inv = inv_s[c];
+  uint8_t* qr = q + (long)(cb * 64 + c) * ldq + p0 + 32 * seg;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[32 * seg + 8 * h + j][c];
+    *reinterpret_cast<int2*>(qr + 8 * h) = q8(v, inv);
+  }
+}
+
 // --------------------------------------------------------------------------- GEMM
 __device__ __forceinline__ int f8_off(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
 
 // BLK = false: per-row fp32 scales sa [M], sb [E, N] applied in the epilogue (unit MFMA scales).
 // BLK = true: E8M0 block scales sa [M, K/128] (1 x 128 activation tiles), sb [E, N/128, K/128]
 // (128 x 128 weight blocks) fed to the MFMA scale operands per k-step; no epilogue scaling.
-template <int BM, int BN, int WGM, int WGN, bool BLK>
+// WG (weight gradient, with BLK): C_e [M, N] (+)= A[:, seg_e] B[:, seg_e]^T over expert e's
+// padded token segment [poff[e], poff[e+1]) (offsets = poff) of the transposed images of
+// quant_t_fp8_seg (row stride ld, per-row E8M0 scales [rows, ld/128] for BOTH operands);
+// grid = E x M-tiles x N-tiles; fp32 or bf16 output straight from the fragments.
+template <int BM, int BN, int WGM, int WGN, bool BLK, bool WG = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
     const uint8_t* __restrict__ A, const void* __restrict__ sa_, const uint8_t* __restrict__ B,
     const void* __restrict__ sb_, bf16* __restrict__ C, const int* __restrict__ offsets, int E, int N, int K,
-    long strideB) {
+    long strideB, int Mw, long ld, int accumulate, int out_f32) {
   const float* sa = static_cast<const float*>(sa_);
   const float* sb = static_cast<const float*>(sb_);
   const uint8_t* sa8 = static_cast<const uint8_t*>(sa_);
@@ -197,7 +253,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
   constexpr int CA = AB / 16 / NT, CB = BB / 16 / NT;
   static_assert(CA * 16 * NT == AB && CB * 16 * NT == BB, "tile/threads mismatch");
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (AB + BB)];
-  __shared__ uint8_t scl[2][BM + BN / 128];                 // BLK: E8M0 scales of the staged k-tile
+  __shared__ uint8_t scl[2][BM + BN];                      // BLK: E8M0 scales of the staged k-tile
   __shared__ int s_e, s_mt;
   __shared__ int wsum[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -206,7 +262,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = lid % nnt;
   int mt = lid / nnt;
-  {  // tile -> expert (block scan of per-expert tile counts; thread e owns expert e)
+  if (WG) {
+    const int mtn = (Mw + BM - 1) / BM;
+    if (tid == 0) { s_e = mt / mtn; s_mt = mt % mtn; }
+    __syncthreads();
+  } else {  // tile -> expert (block scan of per-expert tile counts; thread e owns expert e)
     const int cnt = tid < E ? offsets[tid + 1] - offsets[tid] : 0;
     const int tiles = (cnt + BM - 1) / BM;
     int inc = tiles;
@@ -224,19 +284,25 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
     __syncthreads();
   }
   const int e = s_e;
-  if (e < 0) return;
+  if (e < 0 || e >= E) return;
   mt = s_mt;
-  const int m0 = offsets[e] + mt * BM, mend = offsets[e + 1];
+  // WG: rows m of A run over [0, Mw); the k (token) range is the expert's padded segment
+  const int m0 = WG ? mt * BM : offsets[e] + mt * BM, mend = WG ? Mw : offsets[e + 1];
   const int n0 = nt * BN;
-  const uint8_t* Bp = B + e * strideB;
+  const long kbeg = WG ? offsets[e] : 0, kstop = WG ? offsets[e + 1] : K;
+  const long lda = WG ? ld : K;
+  const uint8_t* Bp = WG ? B : B + e * strideB;
   uint4 ra[CA], rb[CB];
   int rs = 127;                                             // BLK: this thread's staged scale byte
-  const int KB = K / 128, NB = (N + 127) / 128;
-  auto load_tiles = [&](int kk) {
+  const int KB = WG ? (int)(ld / 128) : K / 128, NB = (N + 127) / 128;
+  auto load_tiles = [&](long kk) {
     if (BLK) {
-      const int kb = kk / 128;
+      const int kb = (int)(kk / 128);
       if (tid < BM) rs = (m0 + tid < mend) ? sa8[(long)(m0 + tid) * KB + kb] : 127;
-      else if (tid < BM + BN / 128) {
+      else if (WG) {
+        const int gn = n0 + (tid - BM);
+        rs = (tid < BM + BN && gn < N) ? sb8[(long)gn * KB + kb] : 127;
+      } else if (tid < BM + BN / 128) {
         const int nb = n0 / 128 + (tid - BM);
         rs = nb < NB ? sb8[((long)e * NB + nb) * KB + kb] : 127;
       }
@@ -244,18 +310,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT, r = idx >> 3, ch = idx & 7;
-      const int gm = m0 + r, gk = kk + 16 * ch;
-      ra[c] = (gm < mend && gk < K) ? *reinterpret_cast<const uint4*>(A + (long)gm * K + gk) : uint4{0, 0, 0, 0};
+      const long gm = m0 + r, gk = kk + 16 * ch;
+      ra[c] = (gm < mend && gk < kstop) ? *reinterpret_cast<const uint4*>(A + gm * lda + gk) : uint4{0, 0, 0, 0};
     }
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
       const int idx = tid + c * NT, r = idx >> 3, ch = idx & 7;
-      const int gn = n0 + r, gk = kk + 16 * ch;
-      rb[c] = (gn < N && gk < K) ? *reinterpret_cast<const uint4*>(Bp + (long)gn * K + gk) : uint4{0, 0, 0, 0};
+      const long gn = n0 + r, gk = kk + 16 * ch;
+      rb[c] = (gn < N && gk < kstop) ? *reinterpret_cast<const uint4*>(Bp + gn * (WG ? ld : (long)K) + gk)
+                                     : uint4{0, 0, 0, 0};
     }
   };
   auto store_tiles = [&](int buf) {
-    if (BLK && tid < BM + BN / 128) scl[buf][tid] = (uint8_t)rs;
+    if (BLK && tid < BM + (WG ? BN : BN / 128)) scl[buf][tid] = (uint8_t)rs;
     uint8_t* At = smem + buf * (AB + BB);
     uint8_t* Bt = At + AB;
 #pragma unroll
@@ -283,17 +350,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
     for (int j = 0; j < IM; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const int kt = (K + BK - 1) / BK;
+  const int kt = (int)((kstop - kbeg + BK - 1) / BK);
   const int l32 = lane & 31, hh = lane >> 5;
-  load_tiles(0);
-  store_tiles(0);
-  if (kt > 1) load_tiles(BK);
+  if (kt > 0) {
+    load_tiles(kbeg);
+    store_tiles(0);
+    if (kt > 1) load_tiles(kbeg + BK);
+  }
   __syncthreads();
   for (int t = 0; t < kt; ++t) {
     const int buf = t & 1;
     if (t + 1 < kt) {
       store_tiles(buf ^ 1);
-      if (t + 2 < kt) load_tiles((t + 2) * BK);
+      if (t + 2 < kt) load_tiles(kbeg + (long)(t + 2) * BK);
     }
     const uint8_t* At = smem + buf * (AB + BB);
     const uint8_t* Bt = At + AB;
@@ -304,18 +373,54 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
       for (int j = 0; j < IM; ++j) af[j] = frag(At, wm * TM + j * 32 + l32, s, hh);
 #pragma unroll
       for (int i = 0; i < IN; ++i) bfr[i] = frag(Bt, wn * TN + i * 32 + l32, s, hh);
-      int sca[IM], scb = 127;
+      int sca[IM], scb[IN];
 #pragma unroll
       for (int j = 0; j < IM; ++j) sca[j] = BLK ? (int)scl[buf][wm * TM + j * 32 + l32] : 127;
-      if (BLK) scb = scl[buf][BM + (wn * TN) / 128];
+#pragma unroll
+      for (int i = 0; i < IN; ++i)
+        scb[i] = !BLK ? 127 : WG ? (int)scl[buf][BM + wn * TN + i * 32 + l32] : (int)scl[buf][BM + (wn * TN) / 128];
 #pragma unroll
       for (int i = 0; i < IN; ++i)
 #pragma unroll
         for (int j = 0; j < IM; ++j)   // e4m3 x e4m3; MX scales: weight block (A), token tile (B)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[i], af[j], acc[i][j], 0, 0, 0, scb, 0,
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[i], af[j], acc[i][j], 0, 0, 0, scb[i], 0,
                                                                       sca[j]);
     }
     __syncthreads();
+  }
+  if constexpr (WG) {
+    // C_e [Mw, N]: lane holds rows m = wm*TM + 32j + l32, columns n = wn*TN + 32i + 8g + 4hh + q
+    const long cbase = (long)e * Mw * N;
+#pragma unroll
+    for (int j = 0; j < IM; ++j) {
+      const long gm = m0 + wm * TM + j * 32 + l32;
+      if (gm >= mend) continue;
+#pragma unroll
+      for (int i = 0; i < IN; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int gn = n0 + wn * TN + i * 32 + 8 * g + 4 * hh;
+          if (gn >= N) continue;
+          f32x4 v{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+          if (out_f32) {
+            float* cp = reinterpret_cast<float*>(C) + cbase + gm * N + gn;
+            if (accumulate) v += *reinterpret_cast<const f32x4*>(cp);
+            *reinterpret_cast<f32x4*>(cp) = v;
+          } else {
+            bf16* cp = C + cbase + gm * N + gn;
+            bf16x4 w4;
+            if (accumulate) {
+              const bf16x4 o = *reinterpret_cast<const bf16x4*>(cp);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] += (float)o[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+            *reinterpret_cast<bf16x4*>(cp) = w4;
+          }
+        }
+    }
+    return;
   }
   // epilogue through LDS, one 128-token half (= the waves with wm == half) at a time: C^T
   // fragments (lane = token m, rows n = 8g + 4hh + {0..3}) -> padded [m][n] bf16 image ->
@@ -394,7 +499,7 @@ at::Tensor grouped_gemm_fp8(const at::Tensor& xq, const at::Tensor& sx, const at
   const int grid = (cdiv(M, BM) + E) * cdiv(N, BN);
   grouped_gemm_fp8_kernel<BM, BN, 2, 4, false><<<grid, 512, 0, stream()>>>(
       (const uint8_t*)xq.data_ptr(), sx.data_ptr<float>(), (const uint8_t*)wq.data_ptr(), sw.data_ptr<float>(),
-      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, (long)N * K);
+      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, (long)N * K, 0, 0, 0, 0);
   SPA_LAUNCH_CHECK();
   return out;
 }
@@ -475,7 +580,59 @@ at::Tensor grouped_gemm_fp8_blk(const at::Tensor& xq, const at::Tensor& sx, cons
   const int grid = (cdiv(M, BM) + E) * cdiv(N, BN);
   grouped_gemm_fp8_kernel<BM, BN, 2, 4, true><<<grid, 512, 0, stream()>>>(
       (const uint8_t*)xq.data_ptr(), sx.data_ptr<uint8_t>(), (const uint8_t*)wq.data_ptr(), sw.data_ptr<uint8_t>(),
-      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, (long)N * K);
+      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, (long)N * K, 0, 0, 0, 0);
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+// x [T, C] bf16 (rows grouped by offsets [E+1]), poff [E+1] (128-aligned padded segment starts,
+// poff[E] <= ldq) -> (q [C, ldq] e4m3, s [C, ldq/128] E8M0): transposed Wgrad operand
+std::vector<at::Tensor> quant_t_fp8_seg(const at::Tensor& x_, const at::Tensor& offsets, const at::Tensor& poff,
+                                        int64_t ldq) {
+  SPA_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "quant_t_fp8_seg: bf16 [T, C]");
+  TORCH_CHECK(offsets.scalar_type() == at::kInt && poff.scalar_type() == at::kInt && offsets.numel() == poff.numel(),
+              "quant_t_fp8_seg: int32 offsets / padded offsets [E+1]");
+  const int C = x.size(1), E = offsets.numel() - 1;
+  TORCH_CHECK(C % 64 == 0 && ldq % 128 == 0 && ldq >= x.size(0), "quant_t_fp8_seg: C % 64, ldq % 128");
+  DeviceGuard g(x.device());
+  auto q = at::empty({C, ldq}, x.options().dtype(at::kFloat8_e4m3fn));
+  auto s = at::empty({C, ldq / 128}, x.options().dtype(at::kByte));
+  if (ldq == 0 || C == 0) return {q, s};
+  quant_t_fp8_seg_kernel<<<dim3((unsigned)(ldq / 128), C / 64), 256, 0, stream()>>>(
+      (const bf16*)x.data_ptr(), offsets.data_ptr<int>(), poff.data_ptr<int>(), E, C, (uint8_t*)q.data_ptr(),
+      s.data_ptr<uint8_t>(), ldq);
+  SPA_LAUNCH_CHECK();
+  return {q, s};
+}
+
+// dW_e [M, N] (+)= aq[:, seg_e] bq[:, seg_e]^T for the quant_t_fp8_seg images aq [M, ld], bq [N, ld]
+// (scales [rows, ld/128]); out [E, M, N] bf16 or fp32 (a main_grad view), new bf16 if absent
+at::Tensor wgrad_fp8_blk(const at::Tensor& aq, const at::Tensor& sa, const at::Tensor& bq, const at::Tensor& sb,
+                         const at::Tensor& poff, const c10::optional<at::Tensor>& out_, bool accumulate) {
+  TORCH_CHECK(aq.scalar_type() == at::kFloat8_e4m3fn && bq.scalar_type() == at::kFloat8_e4m3fn, "e4m3 operands");
+  TORCH_CHECK(sa.scalar_type() == at::kByte && sb.scalar_type() == at::kByte, "E8M0 (uint8) scales");
+  TORCH_CHECK(aq.is_contiguous() && bq.is_contiguous() && sa.is_contiguous() && sb.is_contiguous());
+  TORCH_CHECK(poff.scalar_type() == at::kInt, "wgrad_fp8_blk: int32 padded offsets");
+  const int E = poff.numel() - 1;
+  const int M = aq.size(0), N = bq.size(0);
+  const long ld = aq.size(1);
+  TORCH_CHECK(bq.size(1) == ld && ld % 128 == 0 && N % 8 == 0, "wgrad_fp8_blk: shapes");
+  TORCH_CHECK(sa.size(0) == M && sb.size(0) == N && sa.size(1) == ld / 128 && sb.size(1) == ld / 128,
+              "wgrad_fp8_blk: scale shapes");
+  DeviceGuard g(aq.device());
+  auto out = out_ ? *out_ : at::empty({E, M, N}, aq.options().dtype(at::kBFloat16));
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * M * N &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "wgrad_fp8_blk: out [E, M, N] bf16/fp32 contiguous");
+  if (E == 0 || M == 0 || N == 0) return out;
+  constexpr int BM = 256, BN = 256;
+  const int grid = E * cdiv(M, BM) * cdiv(N, BN);
+  grouped_gemm_fp8_kernel<BM, BN, 2, 4, true, true><<<grid, 512, 0, stream()>>>(
+      (const uint8_t*)aq.data_ptr(), sa.data_ptr<uint8_t>(), (const uint8_t*)bq.data_ptr(), sb.data_ptr<uint8_t>(),
+      (bf16*)out.data_ptr(), poff.data_ptr<int>(), E, N, 0, 0, M, ld, accumulate ? 1 : 0,
+      out.scalar_type() == at::kFloat ? 1 : 0);
   SPA_LAUNCH_CHECK();
   return out;
 }
@@ -489,6 +646,8 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("dequant_act_fp8_blk(Tensor q, Tensor s) -> Tensor");
   m.def("quant_weight_fp8_blk(Tensor w) -> Tensor[]");
   m.def("grouped_gemm_fp8_blk(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor offsets) -> Tensor");
+  m.def("quant_t_fp8_seg(Tensor x, Tensor offsets, Tensor poff, int ldq) -> Tensor[]");
+  m.def("wgrad_fp8_blk(Tensor aq, Tensor sa, Tensor bq, Tensor sb, Tensor poff, Tensor(a!)? out, bool accumulate) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("quant_rows_fp8", &spa::quant_rows_fp8);
@@ -497,4 +656,6 @@ TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("dequant_act_fp8_blk", &spa::dequant_act_fp8_blk);
   m.impl("quant_weight_fp8_blk", &spa::quant_weight_fp8_blk);
   m.impl("grouped_gemm_fp8_blk", &spa::grouped_gemm_fp8_blk);
+  m.impl("quant_t_fp8_seg", &spa::quant_t_fp8_seg);
+  m.impl("wgrad_fp8_blk", &spa::wgrad_fp8_blk);
 }

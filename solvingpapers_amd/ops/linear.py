@@ -181,8 +181,12 @@ def linear_act(x, w, b, kind="gelu", alpha=None):
 
 
 # fc1 + act forward and fc2-dgrad + act' backward on the 8-phase kernel's fused epilogues
-# (csrc/kernels/gemm8.hip gemm8_epi); SPA_MLP_EPI=0 -> library GEMMs + separate passes
-MLP_EPI = os.environ.get("SPA_MLP_EPI", "1") != "0"
+# (csrc/kernels/gemm8.hip gemm8_epi). Off by default: at ViT-B/16 widths (K = 768, 12 K-tiles)
+# the 8-phase kernel runs fc1 at 630-770 TF against hipBLASLt's ~1 PF, which costs more than the
+# activation pass it saves (tools/bench_vit_mlp.py: fwd+bwd 1.955 vs 1.901 ms,
+# profiles/r3_vit_mlp_epilogue_ab.txt); hipBLASLt's own GELU epilogues are the tanh form, not the
+# exact erf GELU of the reference ViT. SPA_MLP_EPI=1 selects it.
+MLP_EPI = os.environ.get("SPA_MLP_EPI", "0") == "1"
 
 
 def _mlp_epi_ok(x2, w1, w2):

@@ -424,10 +424,86 @@ def grouped_gemm_fp8_blk(xq, sx, wq, sw, offsets):
     return _cpu_grouped(x.view(xq.shape), w.view(E, N, K), offsets, 0).to(torch.bfloat16)
 
 
+# fp8 weight gradient of the routed experts (block-scaled path): dW_e = dY_e^T X_e with both
+# operands quantized along the token (reduction) dimension in 128 x 1 tiles -- the DeepSeek-V3
+# recipe's Wgrad quantization -- on the block-scaled MFMA (csrc/kernels/moe_fp8.hip
+# quant_t_fp8_seg + wgrad_fp8_blk). SPA_FP8_WGRAD=0 keeps the bf16 grouped dW.
+FP8_WGRAD = os.environ.get("SPA_FP8_WGRAD", "1") != "0"
+
+
+def padded_offsets(offsets):
+    """[E+1] device offsets -> [E+1] int32 offsets with every expert's segment padded to a
+    multiple of 128 tokens (device ops only: no host sync)."""
+    cnt = offsets[1:] - offsets[:-1]
+    pc = (cnt + 127) // 128 * 128
+    return torch.cat([offsets.new_zeros(1), torch.cumsum(pc, 0)]).to(torch.int32)
+
+
+def quant_t_fp8_seg(x, offsets, poff, ld):
+    """x [T, C] (rows grouped by expert) -> (q [C, ld] e4m3 transposed, each expert's tokens at its
+    128-aligned padded offset, zero-filled; s [C, ld/128] E8M0 per (channel, 128-token block))."""
+    if x.is_cuda:
+        return tuple(ops().quant_t_fp8_seg(x.contiguous(), offsets, poff, int(ld)))
+    C = x.shape[1]
+    xt = torch.zeros(C, ld, dtype=torch.float32)
+    for e in range(offsets.numel() - 1):
+        a, b, p0 = int(offsets[e]), int(offsets[e + 1]), int(poff[e])
+        xt[:, p0:p0 + (b - a)] = x[a:b].float().t()
+    t = xt.view(C, ld // 128, 128)
+    ex = _e8m0(t.abs().amax(-1))
+    q = (t * torch.exp2(-ex.float())[..., None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    return q.view(C, ld), (ex + 127).to(torch.uint8)
+
+
+def wgrad_fp8_blk(aq, sa, bq, sb, poff, out=None, accumulate=False):
+    """dW_e [M, N] (+)= aq[:, seg_e] bq[:, seg_e]^T on the images of :func:`quant_t_fp8_seg`."""
+    if aq.is_cuda:
+        return ops().wgrad_fp8_blk(aq, sa, bq, sb, poff, out, accumulate)
+    M, ld = aq.shape
+    a = (aq.float().view(M, ld // 128, 128) * torch.exp2(sa.float() - 127)[..., None]).view(M, ld)
+    b = (bq.float().view(bq.shape[0], ld // 128, 128) * torch.exp2(sb.float() - 127)[..., None]).view(-1, ld)
+    res = torch.stack([a[:, int(poff[e]):int(poff[e + 1])] @ b[:, int(poff[e]):int(poff[e + 1])].t()
+                       for e in range(poff.numel() - 1)])
+    if out is None:
+        return res.to(torch.bfloat16)
+    if accumulate:
+        out.add_(res.to(out.dtype).view_as(out))
+    else:
+        out.copy_(res.view_as(out))
+    return out
+
+
+def _wgrad_fp8_ok(dy, xp, W):
+    return FP8_WGRAD and W.shape[1] % 64 == 0 and W.shape[2] % 64 == 0 and dy.shape[0] > 0
+
+
+def commit_weight_grad_fp8(W, dy, xp, plan):
+    """fp8 dW_e = dy_e^T xp_e (128 x 1 token tiles), committed into W's gradient storage."""
+    T, E = dy.shape[0], W.shape[0]
+    ld = (T + E * 127 + 127) // 128 * 128          # host bound on the padded token count
+    poff = padded_offsets(plan.offsets)
+    aq, sa = quant_t_fp8_seg(dy, plan.offsets, poff, ld)
+    bq, sb = quant_t_fp8_seg(xp, plan.offsets, poff, ld)
+
+    def _w(out, acc):
+        if out is None:
+            return wgrad_fp8_blk(aq, sa, bq, sb, poff).view(W.shape)
+        if out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32):
+            wgrad_fp8_blk(aq, sa, bq, sb, poff, out.view(W.shape), acc)
+        else:
+            g = wgrad_fp8_blk(aq, sa, bq, sb, poff)
+            if acc:
+                out.add_(g.view_as(out))
+            else:
+                out.copy_(g.view_as(out))
+    return commit(W, _w)
+
+
 class _GroupedLinearFP8Fn(torch.autograd.Function):
     """fp8 expert projection. Block-scaled path (N, K % 128): X in 1 x 128 tiles, W in 128 x 128
-    blocks, W^T for dX from the same quantized bytes; weights quantized once per optimizer step.
-    Otherwise per-row scales. dW is a bf16 grouped GEMM."""
+    blocks, W^T for dX from the same quantized bytes; weights quantized once per optimizer step;
+    dW on the same MFMA with dY and X quantized in 128 x 1 token tiles (FP8_WGRAD). Otherwise
+    per-row scales and a bf16 grouped dW."""
 
     @staticmethod
     def forward(ctx, xp, W, plan):
@@ -459,7 +535,9 @@ class _GroupedLinearFP8Fn(torch.autograd.Function):
                 wtq, swt = _quant_weight(transpose2d(W))          # [E, in, out]
                 dx = grouped_gemm_fp8(dq, sd, wtq, swt, plan.offsets).to(xp.dtype)
         gw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and ctx.blk and _wgrad_fp8_ok(dy, xp, W):
+            gw = commit_weight_grad_fp8(W, dy, xp, plan)
+        elif ctx.needs_input_grad[1]:
             def _w(out, acc):
                 if out is None:
                     return grouped_gemm(dy, xp, plan.offsets, 2)

@@ -312,6 +312,39 @@ def test_grouped_gemm_fp8_blk_exact_on_dequantized(counts):
     assert _rel(dx.cpu(), _oracle(dyd, wd, off, 1)) < 5e-3
 
 
+@pytest.mark.parametrize("counts", [[300, 0, 129, 1, 64, 700, 0, 33], [256] * 4])
+def test_fp8_wgrad_exact_on_dequantized_and_close_to_fp32(counts):
+    """fp8 expert dW: the transposed 128-token-tile quantizer == its torch reference bit for bit;
+    the block-scaled Wgrad GEMM == fp32 GEMM of the dequantized operands; and the whole fp8 dW is
+    within fp8 rounding of the fp32 dW_e = dy_e^T x_e (fp32 and bf16 outputs, accumulate)."""
+    g = torch.Generator().manual_seed(4)
+    E, N, K = len(counts), 384, 256
+    T = sum(counts)
+    offc = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32)
+    off = offc.to(dev)
+    dy = (torch.randn(T, N, generator=g) * torch.logspace(-2, 1, N)).to(torch.bfloat16)
+    x = (torch.randn(T, K, generator=g)).to(torch.bfloat16)
+    poff = M.padded_offsets(off)
+    ld = (T + E * 127 + 127) // 128 * 128
+    aq, sa = M.quant_t_fp8_seg(dy.to(dev), off, poff, ld)
+    aqr, sar = M.quant_t_fp8_seg(dy, offc, poff.cpu(), ld)
+    used = int(poff[-1])
+    assert torch.equal(sa.cpu()[:, :used // 128], sar[:, :used // 128])
+    assert torch.equal(aq.cpu().view(torch.uint8)[:, :used], aqr.view(torch.uint8)[:, :used])
+    bq, sb = M.quant_t_fp8_seg(x.to(dev), off, poff, ld)
+    dw = M.wgrad_fp8_blk(aq, sa, bq, sb, poff)                      # bf16 [E, N, K]
+    ad = (aq.float().view(N, -1, 128) * torch.exp2(sa.float() - 127)[..., None]).view(N, ld)
+    bd = (bq.float().view(K, -1, 128) * torch.exp2(sb.float() - 127)[..., None]).view(K, ld)
+    pc = poff.cpu()
+    ref_dq = torch.stack([ad[:, int(pc[e]):int(pc[e + 1])] @ bd[:, int(pc[e]):int(pc[e + 1])].t() for e in range(E)])
+    assert _rel(dw.cpu(), ref_dq.cpu()) < 5e-3
+    ref = torch.stack([dy[offc[e]:offc[e + 1]].float().t() @ x[offc[e]:offc[e + 1]].float() for e in range(E)])
+    assert _rel(dw.cpu(), ref) < 4e-2
+    out = torch.ones(E, N, K, device=dev)
+    M.wgrad_fp8_blk(aq, sa, bq, sb, poff, out, True)                 # fp32 main_grad, accumulate
+    assert _rel(out.cpu() - 1, ref_dq.cpu()) < 1e-4
+
+
 def test_fp8_weight_cache_follows_optimizer_steps():
     W = torch.randn(2, 256, 256, device=dev, dtype=torch.bfloat16) * 0.02
     a = M.quant_weight_fp8_blk(W)

@@ -351,8 +351,9 @@ def _ep_fp8_worker(rank, world, port, q):
 def test_expert_parallel_fp8_dispatch_matches_local_fp8():
     """fp8 dispatch (e4m3 rows + E8M0 1x128 scales over the all-to-all, fused with the
     block-scaled W13 GEMM) == the single-process block-scaled fp8 MoE: outputs and input grads
-    to fp32 rounding; expert grads to the fp8 rounding of the dW operand (the EP path forms dW13
-    from the dequantized received rows, as DeepSeek-V3 does)."""
+    to fp32 rounding; expert grads to the fp8 rounding of the dW operands (the EP path forms dW13
+    from the dequantized received rows, as DeepSeek-V3 does, and both paths quantize the dW
+    operands in 128-token tiles that group the two ranks' tokens differently)."""
     from solvingpapers_amd.ops.moe import moe_ffn
     x, idx, w, W13, W2, gy = _ep_fp8_inputs()
     W13r, W2r = W13.clone().requires_grad_(True), W2.clone().requires_grad_(True)
@@ -364,7 +365,8 @@ def test_expert_parallel_fp8_dispatch_matches_local_fp8():
         assert torch.allclose(torch.from_numpy(gx), xs.grad[rank], atol=1e-4)
         ref13 = W13r.grad[rank * 2:(rank + 1) * 2]
         assert ((torch.from_numpy(g13) - ref13).norm() / ref13.norm()) < 5e-2
-        assert torch.allclose(torch.from_numpy(g2), W2r.grad[rank * 2:(rank + 1) * 2], atol=1e-4)
+        ref2 = W2r.grad[rank * 2:(rank + 1) * 2]           # fp8 dW: 128-token quantization blocks
+        assert ((torch.from_numpy(g2) - ref2).norm() / ref2.norm()) < 5e-2   # group tokens differently
 
 
 def _gemma_tp_cfg():

@@ -12,7 +12,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from solvingpapers_amd.ops import _ext  # noqa: E402
-from solvingpapers_amd.ops import linear as L  # noqa: E402
+import importlib  # noqa: E402
+
+L = importlib.import_module("solvingpapers_amd.ops.linear")   # (ops.linear is also a function)
 
 
 def main():

@@ -27,7 +27,13 @@ import os
 import statistics
 import sys
 
-import torch
+# a real TP / EP run (world > 1 over RCCL) selects hipBLASLt's data-parallel stream-K grid in
+# parallel/dist.py init_distributed (a persistent whole-chip grid stalls next to a collective);
+# the one-process proxy must run the same GEMM configuration. Set before hipBLASLt loads.
+if os.environ.get("SPA_STREAMK_DP", "1") != "0":
+    os.environ.setdefault("TENSILE_STREAMK_DATA_PARALLEL", "1")
+
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -185,7 +191,8 @@ def main():
     global ARMS
     ARMS = [x for x in a.arms.split(",") if x] or None
     assert _ext.load(), "HIP extension missing"
-    base = {"ar_busbw_gbps": a.ar_gbps, "a2a_gbps": a.a2a_gbps, "proxy_nwg": a.nwg}
+    base = {"ar_busbw_gbps": a.ar_gbps, "a2a_gbps": a.a2a_gbps, "proxy_nwg": a.nwg,
+            "streamk_data_parallel": os.environ.get("TENSILE_STREAMK_DATA_PARALLEL") == "1"}
     for w in a.which.split(","):
         out = tp_gemma(a) if w == "tp" else ep_moe(a)
         print(json.dumps({**out, **base}), flush=True)
