@@ -32,6 +32,7 @@ exporter slices the padding off.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, replace
 from typing import Dict, List, Optional
 
@@ -343,19 +344,24 @@ class MoE(tnn.Module):
     """DeepSeekMoE: shared experts + top-k routed experts with aux-free load balancing.
     Under EP (``ep_group`` of size P) this rank holds experts [r*E/P, (r+1)*E/P)."""
 
-    def __init__(self, c: DSV3Config, ep_group=None, ep_group2=None, ep_chunks=2, **fk):
+    def __init__(self, c: DSV3Config, ep_group=None, ep_group2=None, ep_chunks=2, ep_schedule=None, **fk):
         """Under EP (P > 1) the layer's tokens run as ``ep_chunks`` chunks whose dispatch /
         combine all-to-alls overlap the other chunks' expert GEMMs and the shared expert on
-        ONE stream (expert_parallel.ep_run_interleaved; ``ep_chunks=1``: no overlap).
-        ``ep_group2``: instead a second communicator over the same EP ranks -- two chunks on two
-        compute streams (chunk A with ``ep_group``, chunk B on a side stream with
-        ``ep_group2``); see _forward_pipelined."""
+        ONE stream (expert_parallel.ep_run_interleaved; ``ep_chunks=1``: no overlap) -- the
+        default ``ep_schedule="interleave"``. ``ep_schedule="two_stream"`` with ``ep_group2`` (a
+        second communicator over the same EP ranks): two chunks on two compute streams (chunk A
+        with ``ep_group``, chunk B on a side stream with ``ep_group2``); see _forward_pipelined.
+        1-GPU proxy (profiles/r3_overlap_proxy_streamk_dp.jsonl): interleave hides 0.47-0.55 of
+        the all-to-all time, two_stream 0.42-0.48 (its chunks share the CUs). SPA_EP_SCHEDULE
+        overrides the default."""
         super().__init__()
         from ..parallel.expert_parallel import ep_rank_size
         self.c = c
         self.ep_group = ep_group
         self.ep_rank, self.ep = ep_rank_size(ep_group)
-        self.ep_group2 = ep_group2 if self.ep > 1 else None
+        sched = ep_schedule or os.environ.get("SPA_EP_SCHEDULE", "interleave")
+        assert sched in ("interleave", "two_stream"), sched
+        self.ep_group2 = ep_group2 if (self.ep > 1 and sched == "two_stream") else None
         self.ep_chunks = int(ep_chunks) if self.ep > 1 else 1
         self._side = None
         if self.ep_group2 is not None:
@@ -473,7 +479,8 @@ class MoE(tnn.Module):
         cuda = x2.is_cuda
         main = torch.cuda.current_stream(x2.device) if cuda else None
         if cuda and self._side is None:
-            self._side = torch.cuda.Stream(x2.device)
+            from ..parallel.comm import side_stream
+            self._side = side_stream(x2.device)
             from ..utils.grad import register_side_stream
             register_side_stream(self._side)
         side = self._side if cuda else None

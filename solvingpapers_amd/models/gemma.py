@@ -18,6 +18,7 @@ process group (K/V replicated because Hkv = 1 < tp; see parallel/tensor_parallel
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, replace
 from typing import Optional
 
@@ -312,6 +313,53 @@ class GemmaBlock(tnn.Module):
         return (h2, out, kv_out) if want_kv else (h2, out)
 
 
+    # ---- one-stream interleaved TP schedule (Gemma._hidden_interleaved): the layer in four
+    # stages, each ending where a collective would block; the caller runs the other chunk's
+    # stage between two stages of one chunk, so every collective has a stage to hide behind.
+    def stage1(self, st, g):
+        """norm1 on (res, delta | pending all-reduce of the previous layer's output)."""
+        from ..parallel import comm
+        c = self.c
+        x = comm.ar_finish(st["out"]) if st.get("out") is not None else st["delta"]
+        st["out"] = None
+        if st["res"] is None:
+            n1, h = rms_norm(x, self.attn_norm, c.norm_eps), x
+        else:
+            n1, h = rms_norm(x, self.attn_norm, c.norm_eps, residual=st["res"])
+        st["n1"], st["h"] = n1, h
+        st["sq"] = comm.grad_ar_start(n1, g)            # q path: gradient all-reduce (bwd)
+
+    def stage2(self, st, g, pos, kv_prefix=None):
+        """q / kv projections, RoPE, attention (queries of this chunk over kv_prefix + own K/V),
+        o projection; starts its all-reduce. Returns this chunk's (k, v)."""
+        from ..parallel import comm
+        from ..parallel.tensor_parallel import reduce_grad_tp
+        c = self.c
+        hd, KV = c.head_dim, c.n_kv_heads
+        q = linear(comm.grad_ar_finish(st.pop("sq")), self.wq)
+        kv = reduce_grad_tp(linear(st.pop("n1"), self.wkv), g)
+        B, T = q.shape[0], q.shape[1]
+        qkv = rope_packed_(torch.cat([q, kv], dim=-1), self.hl + KV, c.rope_theta, pos, interleaved=False,
+                           head_dim=hd)
+        x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
+        k4, v4 = x4[:, :, self.hl:self.hl + KV], x4[:, :, self.hl + KV:]
+        kk, vv = (k4, v4) if kv_prefix is None else (torch.cat([kv_prefix[0], k4], 1), torch.cat([kv_prefix[1], v4], 1))
+        o = flash_attention(x4[:, :, :self.hl], kk, vv, causal=True).reshape(B, T, self.hl * hd)
+        st["sa"] = comm.ar_start(linear(o, self.wo), g)
+        return k4, v4
+
+    def stage3(self, st, g):
+        from ..parallel import comm
+        n2, h2 = rms_norm(comm.ar_finish(st.pop("sa")), self.ffn_norm, self.c.norm_eps, residual=st.pop("h"))
+        st["res"] = h2
+        st["sm"] = comm.grad_ar_start(n2, g)
+
+    def stage4(self, st, g):
+        from ..parallel import comm
+        f = glu(linear(comm.grad_ar_finish(st.pop("sm")), self.w13), "gelu_tanh")
+        st["out"] = comm.ar_start(linear(f, self.w2), g)
+
+
 class _Null:
     def __enter__(self):
         return self
@@ -340,7 +388,7 @@ class _JoinStreams(torch.autograd.Function):
 
 class Gemma(tnn.Module):
     def __init__(self, c: GemmaConfig, device=None, dtype=torch.float32, tp_group=None, seed=0,
-                 sequence_parallel=False, tp_group2=None):
+                 sequence_parallel=False, tp_group2=None, tp_schedule=None):
         """``tp_group2``: a second communicator over the SAME TP ranks. Given (TP > 1, no
         sequence parallelism), training splits each sequence into two halves that run as two
         pipelines -- half A on the current stream with ``tp_group``, half B on a second compute
@@ -355,8 +403,12 @@ class Gemma(tnn.Module):
         self.tp_rank, self.tp = tp_rank_size(tp_group)
         self.sp = bool(sequence_parallel) and self.tp > 1
         self.tp_group2 = tp_group2 if (self.tp > 1 and not self.sp) else None
+        # "interleave": one-stream staged schedule (_hidden_interleaved); "two_stream": half B on
+        # a second compute stream (_hidden_pipelined). SPA_TP_SCHEDULE overrides the default.
+        self.tp_schedule = tp_schedule or os.environ.get("SPA_TP_SCHEDULE", "interleave")
+        assert self.tp_schedule in ("interleave", "two_stream"), self.tp_schedule
         self._side = None
-        if self.tp_group2 is not None:
+        if self.tp_group2 is not None and self.tp_schedule == "two_stream":
             from ..utils.grad import set_multi_stream
             set_multi_stream(True)        # weight-grad commits come from two streams
         assert c.vocab_size % self.tp == 0
@@ -387,7 +439,61 @@ class Gemma(tnn.Module):
         return (self.tp_group2 is not None and cache is None and torch.is_grad_enabled() and self.training
                 and ids.shape[1] % 2 == 0 and ids.shape[1] >= 2)
 
-    def _hidden_pipelined(self, ids):
+    def _hidden_interleaved(self, ids, targets=None):
+        """One-stream two-chunk TP schedule. Each layer is four stages per chunk (GemmaBlock
+        stage1..4, each ending at a collective: the q-path and MLP-input gradient all-reduces of
+        the backward, the o-projection and MLP-output all-reduces of the forward), issued as
+
+            A.s1(l) B.s3(l-1) A.s2(l) B.s4(l-1) A.s3(l) B.s1(l) A.s4(l) B.s2(l) | A.s1(l+1) ...
+
+        with every collective started at the end of one stage of its chunk and finished at the
+        start of the next (parallel/comm ar_start / ar_finish, grad_ar_start / grad_ar_finish).
+        Half B runs half a layer behind half A (its attention needs A's K/V of the same layer),
+        so between the two halves of any collective the other chunk's stage runs -- in the
+        forward, and, since autograd replays nodes in reverse creation order, in the backward.
+        One compute stream: the chunks never share the CUs (the two-stream form's chunks fall
+        into lockstep and their collectives coincide, profiles/r3_overlap_proxy_v2.jsonl)."""
+        from ..parallel import comm
+        from ..parallel.tensor_parallel import vocab_parallel_cross_entropy, vocab_parallel_embedding
+        c = self.c
+        half = ids.shape[1] // 2
+        g = (self.tp_group, self.tp_group2 if self.tp_group2 is not None else self.tp_group)
+        st = [dict(res=None, delta=vocab_parallel_embedding(self.embed, ids[:, i * half:(i + 1) * half], g[i],
+                                                            scale=math.sqrt(c.dim)), out=None) for i in range(2)]
+        L = self.layers
+        for i, l in enumerate(L):
+            l.stage1(st[0], g[0])
+            if i > 0:
+                L[i - 1].stage3(st[1], g[1])
+            kv = l.stage2(st[0], g[0], 0)
+            if i > 0:
+                L[i - 1].stage4(st[1], g[1])
+            l.stage3(st[0], g[0])
+            l.stage1(st[1], g[1])
+            l.stage4(st[0], g[0])
+            l.stage2(st[1], g[1], half, kv_prefix=kv)
+        L[-1].stage3(st[1], g[1])
+        outs, hs = [None, None], [None, None]
+        for i in range(2):
+            if i == 0:
+                x = comm.ar_finish(st[0]["out"])
+            else:
+                L[-1].stage4(st[1], g[1])
+                x = comm.ar_finish(st[1]["out"])
+            outs[i], _ = rms_norm(x, self.norm_f, c.norm_eps, residual=st[i]["res"])
+            if targets is not None:
+                hs[i] = comm.grad_ar_start(outs[i], g[i])   # head input grads: all-reduced async
+        if targets is None:
+            return torch.cat(outs, 1)
+        ls, nv = [None, None], [None, None]
+        for i in range(2):
+            t = targets[:, i * half:(i + 1) * half].reshape(-1)
+            h = comm.grad_ar_finish(hs[i])
+            ls[i] = vocab_parallel_cross_entropy(h.reshape(-1, c.dim), self.embed, t, g[i], reduce_dh=False)
+            nv[i] = (t != -100).sum().clamp_min(1).to(ls[i].dtype)
+        return (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
+
+    def _hidden_pipelined(self, ids, targets=None):
         """Two-chunk TP pipeline (see __init__): per layer, half A runs on the current stream
         (``tp_group``), then half B on the side stream (``tp_group2``) once A's K/V exist.
         Each stream waits only on its own communicator, so while one half's all-reduce is on
@@ -400,7 +506,8 @@ class Gemma(tnn.Module):
         cuda = ids.is_cuda
         main = torch.cuda.current_stream(ids.device) if cuda else None
         if cuda and self._side is None:
-            self._side = torch.cuda.Stream(ids.device)
+            from ..parallel.comm import side_stream
+            self._side = side_stream(ids.device)
             from ..utils.grad import register_side_stream
             register_side_stream(self._side)
         side = self._side if cuda else None
@@ -430,6 +537,24 @@ class Gemma(tnn.Module):
         for i in range(2):
             with on(i):
                 outs[i], _ = rms_norm(delta[i], self.norm_f, c.norm_eps, residual=res[i])
+        if targets is not None:
+            # the vocab-parallel head + CE per chunk, each on its own stream and communicator: the
+            # [T/2, D] hidden-gradient all-reduce of one chunk's head backward overlaps the other
+            # chunk's head GEMMs (one [T, D] all-reduce here was the longest exposed collective)
+            from ..parallel.tensor_parallel import vocab_parallel_cross_entropy
+            tg = (targets[:, :half], targets[:, half:])
+            ls, nv = [None, None], [None, None]
+            for i in range(2):
+                with on(i):
+                    t = tg[i].reshape(-1)
+                    ls[i] = vocab_parallel_cross_entropy(outs[i].reshape(-1, c.dim), self.embed, t, groups[i])
+                    nv[i] = (t != -100).sum().clamp_min(1).to(ls[i].dtype)
+            if side is not None:
+                main.wait_stream(side)
+                ls[1].record_stream(main)
+                nv[1].record_stream(main)
+            loss = (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
+            return _JoinStreams.apply(loss, side) if side is not None else loss
         if side is not None:
             main.wait_stream(side)
             outs[1].record_stream(main)
@@ -441,6 +566,8 @@ class Gemma(tnn.Module):
         from ..parallel.tensor_parallel import vocab_parallel_embedding
         c = self.c
         if self._pipelined(ids, cache):
+            if self.tp_schedule == "interleave":
+                return self._hidden_interleaved(ids)
             return self._hidden_pipelined(ids)
         sp = self.sp and cache is None
         x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim), sequence_parallel=sp)
@@ -455,6 +582,10 @@ class Gemma(tnn.Module):
     def forward(self, ids, targets=None):
         from ..parallel.tensor_parallel import gather_seq, scale_grad, vocab_parallel_cross_entropy
         c = self.c
+        if targets is not None and self._pipelined(ids, None):
+            if self.tp_schedule == "interleave":
+                return self._hidden_interleaved(ids, targets)
+            return self._hidden_pipelined(ids, targets)
         n = self.hidden(ids)
         if self.sp:  # the vocab-parallel head needs every token on every rank; its input grad is
             n = scale_grad(gather_seq(n, self.tp_group), 1.0 / self.tp)  # complete on each rank

@@ -439,11 +439,14 @@ def padded_offsets(offsets):
     return torch.cat([offsets.new_zeros(1), torch.cumsum(pc, 0)]).to(torch.int32)
 
 
-def quant_t_fp8_seg(x, offsets, poff, ld):
+def quant_t_fp8_seg(x, offsets, poff, ld, rows=False):
     """x [T, C] (rows grouped by expert) -> (q [C, ld] e4m3 transposed, each expert's tokens at its
-    128-aligned padded offset, zero-filled; s [C, ld/128] E8M0 per (channel, 128-token block))."""
+    128-aligned padded offset, zero-filled; s [C, ld/128] E8M0 per (channel, 128-token block)).
+    ``rows``: also return quant_act_fp8_blk(x) (the 1 x 128 row image) from the same read."""
     if x.is_cuda:
-        return tuple(ops().quant_t_fp8_seg(x.contiguous(), offsets, poff, int(ld)))
+        return tuple(ops().quant_t_fp8_seg(x.contiguous(), offsets, poff, int(ld), bool(rows)))
+    if rows:
+        return quant_t_fp8_seg(x, offsets, poff, ld) + quant_act_fp8_blk(x)
     C = x.shape[1]
     xt = torch.zeros(C, ld, dtype=torch.float32)
     for e in range(offsets.numel() - 1):
@@ -474,17 +477,17 @@ def wgrad_fp8_blk(aq, sa, bq, sb, poff, out=None, accumulate=False):
 
 
 def _wgrad_fp8_ok(dy, xp, W):
-    return FP8_WGRAD and W.shape[1] % 64 == 0 and W.shape[2] % 64 == 0 and dy.shape[0] > 0
+    return FP8_WGRAD and W.shape[1] % 128 == 0 and W.shape[2] % 128 == 0 and dy.shape[0] > 0
 
 
-def commit_weight_grad_fp8(W, dy, xp, plan):
-    """fp8 dW_e = dy_e^T xp_e (128 x 1 token tiles), committed into W's gradient storage."""
-    T, E = dy.shape[0], W.shape[0]
-    ld = (T + E * 127 + 127) // 128 * 128          # host bound on the padded token count
-    poff = padded_offsets(plan.offsets)
-    aq, sa = quant_t_fp8_seg(dy, plan.offsets, poff, ld)
-    bq, sb = quant_t_fp8_seg(xp, plan.offsets, poff, ld)
+def wgrad_ld(T, E):
+    """host bound (multiple of 128) on the padded token count of T rows over E experts"""
+    return (T + E * 127 + 127) // 128 * 128
 
+
+def commit_weight_grad_fp8(W, aq, sa, bq, sb, poff):
+    """fp8 dW_e = dy_e^T xp_e from the transposed images (aq, sa) of dy and (bq, sb) of xp
+    (:func:`quant_t_fp8_seg`), committed into W's gradient storage."""
     def _w(out, acc):
         if out is None:
             return wgrad_fp8_blk(aq, sa, bq, sb, poff).view(W.shape)
@@ -508,8 +511,18 @@ class _GroupedLinearFP8Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xp, W, plan):
         ctx.plan, ctx.W = plan, W
-        ctx.save_for_backward(xp)
         ctx.blk = _blk_ok(W)
+        ctx.wg8 = ctx.blk and _wgrad_fp8_ok(xp, xp, W)
+        if ctx.wg8:
+            # one read of xp: the 1 x 128 row image for this GEMM and the transposed 128 x 1 image
+            # the fp8 dW needs -- saved INSTEAD of xp (half its bytes)
+            ctx.poff, ctx.ld = padded_offsets(plan.offsets), wgrad_ld(xp.shape[0], W.shape[0])
+            xtq, xts, xq, sx = quant_t_fp8_seg(xp, plan.offsets, ctx.poff, ctx.ld, rows=True)
+            ctx.save_for_backward(xtq, xts)
+            ctx.xshape = xp.shape
+            wq, _, sw, _ = quant_weight_fp8_blk(W)
+            return grouped_gemm_fp8_blk(xq, sx, wq, sw, plan.offsets).to(xp.dtype)
+        ctx.save_for_backward(xp)
         if ctx.blk:
             xq, sx = quant_act_fp8_blk(xp)
             wq, _, sw, _ = quant_weight_fp8_blk(W)
@@ -521,9 +534,18 @@ class _GroupedLinearFP8Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         from .layout import transpose2d
-        (xp,) = ctx.saved_tensors
         W, plan = ctx.W, ctx.plan
         dy = dy.contiguous()
+        if ctx.wg8:
+            xtq, xts = ctx.saved_tensors
+            dtq, dts, dq, sd = quant_t_fp8_seg(dy, plan.offsets, ctx.poff, ctx.ld, rows=True)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                _, wtq, _, swt = quant_weight_fp8_blk(W)              # [E, in, out], cached
+                dx = grouped_gemm_fp8_blk(dq, sd, wtq, swt, plan.offsets).to(dy.dtype)
+            gw = commit_weight_grad_fp8(W, dtq, dts, xtq, xts, ctx.poff) if ctx.needs_input_grad[1] else None
+            return dx, gw, None
+        (xp,) = ctx.saved_tensors
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.blk:
@@ -535,9 +557,7 @@ class _GroupedLinearFP8Fn(torch.autograd.Function):
                 wtq, swt = _quant_weight(transpose2d(W))          # [E, in, out]
                 dx = grouped_gemm_fp8(dq, sd, wtq, swt, plan.offsets).to(xp.dtype)
         gw = None
-        if ctx.needs_input_grad[1] and ctx.blk and _wgrad_fp8_ok(dy, xp, W):
-            gw = commit_weight_grad_fp8(W, dy, xp, plan)
-        elif ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1]:
             def _w(out, acc):
                 if out is None:
                     return grouped_gemm(dy, xp, plan.offsets, 2)

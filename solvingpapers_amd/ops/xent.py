@@ -157,7 +157,7 @@ class _ChunkedLinearXent(torch.autograd.Function):
     and dh, a partial sum over the local vocabulary, is all-reduced in backward."""
 
     @staticmethod
-    def forward(ctx, h, w, b, target, ignore_index, smoothing, group, Vc):
+    def forward(ctx, h, w, b, target, ignore_index, smoothing, group, Vc, reduce_dh=True):
         D = h.shape[-1]
         h2 = h.reshape(-1, D)
         N, Vl = h2.shape[0], w.shape[0]
@@ -189,6 +189,7 @@ class _ChunkedLinearXent(torch.autograd.Function):
         loss = torch.where(valid, rows, torch.zeros_like(rows)).sum() / nvalid
         ctx.save_for_backward(h2, w, t, lse, (1.0 / nvalid).reshape(1))
         ctx.b, ctx.hshape, ctx.cfg = b, h.shape, (ignore_index, smoothing, group, Vc, v_off, Vtot)
+        ctx.reduce_dh = reduce_dh
         return loss
 
     @staticmethod
@@ -227,12 +228,15 @@ class _ChunkedLinearXent(torch.autograd.Function):
             del lc, G
         if need_h:
             from ..parallel import comm
-            if comm.group_rank_size(group)[1] > 1:
-                comm.all_reduce(dh, group)      # h is replicated over TP: sum the vocab partials
-            dh = dh.to(h2.dtype).view(ctx.hshape)
+            # h is replicated over TP: sum the vocab partials -- in h's dtype (bf16 on the wire,
+            # half the bytes of the fp32 accumulator; each partial is already fp32-accumulated)
+            dh = dh.to(h2.dtype)
+            if ctx.reduce_dh and comm.group_rank_size(group)[1] > 1:
+                comm.all_reduce(dh, group)
+            dh = dh.view(ctx.hshape)
         if need_b:
             gb = commit_tensor(b, gb.to(b.dtype))
-        return dh, gw, gb, None, None, None, None, None
+        return dh, gw, gb, None, None, None, None, None, None
 
 
 _ADDMM_F32 = None
@@ -269,12 +273,15 @@ def _commit_rows(w, compute, first_chunk):  # w has main_grad
 
 
 def chunked_linear_cross_entropy(h, w, target, bias=None, ignore_index=-100, label_smoothing=0.0, group=None,
-                                 chunk_cols=None):
+                                 chunk_cols=None, reduce_dh=True):
     """Vocab-chunked fused LM head + CE (never holds [N, V]); ``group``: W is this TP rank's
-    vocab shard and the CE is over the full (sharded) vocabulary."""
+    vocab shard and the CE is over the full (sharded) vocabulary. ``reduce_dh=False``: return
+    this rank's vocab-partial input gradient (the caller all-reduces it, e.g. asynchronously with
+    parallel/comm.grad_ar_start / grad_ar_finish around ``h``)."""
     N = h.numel() // h.shape[-1]
     Vc = chunk_cols or _chunk_cols(N, w.shape[0], h.element_size())
-    return _ChunkedLinearXent.apply(h, w, bias, target, ignore_index, float(label_smoothing), group, int(Vc))
+    return _ChunkedLinearXent.apply(h, w, bias, target, ignore_index, float(label_smoothing), group, int(Vc),
+                                    bool(reduce_dh))
 
 
 def linear_cross_entropy(h, w, target, bias=None, ignore_index=-100, label_smoothing=0.0):

@@ -21,6 +21,7 @@ xGMI links of an MI355X (defaults below; override per run).
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import List
 
@@ -31,6 +32,21 @@ import torch.distributed as dist
 # ring all-reduce bus bandwidth ~ per-link bound x channels; all-to-all uses all 7 links
 PROXY_AR_BUSBW_GBPS = 300.0
 PROXY_A2A_GBPS = 300.0
+
+# Stream priorities of the two-chunk pipelines (models/gemma.py, models/deepseekv3.py) and of
+# the TP / EP collective streams (RCCL is_high_priority_stream; the proxy's comm stream). The
+# idea: the chunk running ahead keeps its lead instead of sharing the chip evenly with the one
+# behind (lockstep makes both chunks' collectives coincide). Measured on the 1-GPU proxy
+# (profiles/r3_overlap_proxy_priorities.jsonl): TP hidden 0.30 -> 0.35, but the EP layer's
+# two-stream compute slowed 15 % and its overlap vanished, so both default to normal (0);
+# SPA_SIDE_PRIO=-1 / SPA_COMM_PRIO=-1 select high priority.
+SIDE_PRIORITY = int(os.environ.get("SPA_SIDE_PRIO", "0"))
+COMM_PRIORITY = int(os.environ.get("SPA_COMM_PRIO", "0"))
+
+
+def side_stream(device):
+    """The second compute stream of a two-chunk pipeline (priority SIDE_PRIORITY)."""
+    return torch.cuda.Stream(device, priority=SIDE_PRIORITY)
 
 
 class ProxyGroup:
@@ -47,7 +63,8 @@ class ProxyGroup:
         self.device = torch.device(device or "cuda")
         self.ar_bw, self.a2a_bw = ar_busbw_gbps * 1e9, a2a_gbps * 1e9
         self.nwg, self.mode = int(nwg), mode
-        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.stream = (torch.cuda.Stream(self.device, priority=COMM_PRIORITY) if self.device.type == "cuda"
+                       else None)
         n = buf_mb << 20
         self._src = torch.empty(n, dtype=torch.uint8, device=self.device)
         self._dst = torch.empty_like(self._src)
@@ -282,5 +299,54 @@ def ar_finish(handle):
     return _ARFinish.apply(y, box)
 
 
-__all__ = ["ProxyGroup", "is_proxy", "group_rank_size", "backend", "all_reduce", "all_to_all_single",
+class _GradARStart(torch.autograd.Function):
+    """Identity forward; backward waits for the gradient all-reduce launched by
+    _GradARFinish.backward and returns its result."""
+
+    @staticmethod
+    def forward(ctx, x, box):
+        ctx.box = box
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        box = ctx.box
+        box.bwork.wait()
+        dx, box.dx = box.dx, None
+        return dx, None
+
+
+class _GradARFinish(torch.autograd.Function):
+    """Identity forward; backward launches the all-reduce of the incoming gradient (in place,
+    async) and hands it to _GradARStart.backward."""
+
+    @staticmethod
+    def forward(ctx, x, box):
+        ctx.box = box
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        box = ctx.box
+        box.dx = g.contiguous()
+        box.bwork = all_reduce(box.dx, box.group, async_op=True)
+        return g, None
+
+
+def grad_ar_start(x, group):
+    """Megatron's f operator (identity forward, all-reduce of the gradient backward) split in
+    two: ops created between ``grad_ar_start`` and :func:`grad_ar_finish` in the forward run, in
+    the backward, while the gradient all-reduce is on the wire (it is launched at the finish
+    node's backward and waited at the start node's)."""
+    box = _Box()
+    box.group = group
+    return _GradARStart.apply(x, box), box
+
+
+def grad_ar_finish(handle):
+    y, box = handle
+    return _GradARFinish.apply(y, box)
+
+
+__all__ = ["grad_ar_start", "grad_ar_finish", "ProxyGroup", "side_stream", "SIDE_PRIORITY", "COMM_PRIORITY", "is_proxy", "group_rank_size", "backend", "all_reduce", "all_to_all_single",
            "all_to_all_counts", "a2a_start", "a2a_finish", "a2a", "ar_start", "ar_finish"]

@@ -74,6 +74,21 @@ def layout_ranks(world: int, tp: int = 1, ep: int = 1):
     return {"tp": tp_groups, "dp": dp_groups, "ep": ep_groups, "expert_dp": edp_groups}
 
 
+def _hp_options(kind):
+    """RCCL options for the TP / EP communicators: their collectives sit between compute on the
+    critical path (or between the two chunks of a pipeline), so their internal stream is high
+    priority (parallel/comm.py COMM_PRIORITY); DP buckets keep the default."""
+    from .comm import COMM_PRIORITY
+    if kind in ("dp", "expert_dp") or COMM_PRIORITY >= 0 or dist.get_backend() != "nccl":
+        return None
+    try:
+        o = dist.ProcessGroupNCCL.Options()
+        o.is_high_priority_stream = True
+        return o
+    except (AttributeError, RuntimeError):
+        return None
+
+
 def build_groups(tp: int = 1, ep: int = 1, pipeline: bool = False) -> ProcessGroups:
     """``pipeline``: also build a second communicator for every TP and EP group (each chunk of
     the two-chunk pipelines runs its collectives on its own RCCL communicator / stream)."""
@@ -86,7 +101,7 @@ def build_groups(tp: int = 1, ep: int = 1, pipeline: bool = False) -> ProcessGro
     for kind in kinds:
         for ranks in lay[kind.rstrip("2")]:
             # new_group is collective over the WORLD: create every group on every rank, in order
-            g = dist.new_group(ranks) if (initialized and len(ranks) > 1) else None
+            g = dist.new_group(ranks, pg_options=_hp_options(kind)) if (initialized and len(ranks) > 1) else None
             if rank in ranks:
                 mine[kind] = (g, ranks)
     tp_ranks, dp_ranks, ep_ranks = mine["tp"][1], mine["dp"][1], mine["ep"][1]

@@ -178,7 +178,7 @@ def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=F
     return reduce_scatter_seq(x, group) if sequence_parallel else reduce_from_tp(x, group)
 
 
-def vocab_parallel_cross_entropy(h, w_local, target, group, chunk_cols=None):
+def vocab_parallel_cross_entropy(h, w_local, target, group, chunk_cols=None, reduce_dh=True):
     """mean CE(h @ W^T, target) with W sharded by rows (vocab) over the TP group.
 
     Runs the vocab-chunked fused head (ops/xent.py ``_ChunkedLinearXent``, HIP kernels
@@ -189,7 +189,7 @@ def vocab_parallel_cross_entropy(h, w_local, target, group, chunk_cols=None):
     [N, D] dh partials (h is replicated over TP)."""
     if tp_rank_size(group)[1] == 1:
         return linear_cross_entropy(h, w_local, target)
-    return chunked_linear_cross_entropy(h, w_local, target, group=group, chunk_cols=chunk_cols)
+    return chunked_linear_cross_entropy(h, w_local, target, group=group, chunk_cols=chunk_cols, reduce_dh=reduce_dh)
 
 
 def gather_vocab_logits(logits_local, group):

@@ -7,14 +7,18 @@ import torch
 from solvingpapers_amd.parallel.comm import ProxyGroup, group_rank_size
 
 
-def test_proxy_group_tp_gemma_pipelined_matches_plain():
+import pytest
+
+
+@pytest.mark.parametrize("schedule", ["interleave", "two_stream"])
+def test_proxy_group_tp_gemma_pipelined_matches_plain(schedule):
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.utils.flat import FlatParams
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=8, head_dim=16, ffn_hidden=128)
     g1, g2 = ProxyGroup(8, "cpu"), ProxyGroup(8, "cpu")
     assert group_rank_size(g1) == (0, 8)
     plain = gemma.Gemma(c, tp_group=g1, seed=3)
-    pipe = gemma.Gemma(c, tp_group=g1, tp_group2=g2, seed=3)
+    pipe = gemma.Gemma(c, tp_group=g1, tp_group2=g2, seed=3, tp_schedule=schedule)
     assert plain.layers[0].hl == 1 and plain.embed.shape[0] == 8     # TP=8 local shard shapes
     ids = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(0))
     grads = []
@@ -36,7 +40,7 @@ def test_proxy_group_ep_moe_pipelined_matches_plain():
     g1, g2 = ProxyGroup(8, "cpu"), ProxyGroup(8, "cpu")
     outs = []
     for pipe in (False, True):
-        m = ds.MoE(c, ep_group=g1, ep_group2=g2 if pipe else None)
+        m = ds.MoE(c, ep_group=g1, ep_group2=g2 if pipe else None, ep_schedule="two_stream" if pipe else None)
         m.reset_parameters(0.1, torch.Generator().manual_seed(3))
         assert m.w13.shape[0] == 2                                    # 16 experts / EP 8
         x = torch.randn(2, 6, 32, generator=torch.Generator().manual_seed(1)).requires_grad_()

@@ -331,7 +331,9 @@ def test_fp8_wgrad_exact_on_dequantized_and_close_to_fp32(counts):
     used = int(poff[-1])
     assert torch.equal(sa.cpu()[:, :used // 128], sar[:, :used // 128])
     assert torch.equal(aq.cpu().view(torch.uint8)[:, :used], aqr.view(torch.uint8)[:, :used])
-    bq, sb = M.quant_t_fp8_seg(x.to(dev), off, poff, ld)
+    bq, sb, xq, sx = M.quant_t_fp8_seg(x.to(dev), off, poff, ld, rows=True)
+    xqr, sxr = M.quant_act_fp8_blk(x.to(dev))                        # the fused row image == the
+    assert torch.equal(sx, sxr) and torch.equal(xq.view(torch.uint8), xqr.view(torch.uint8))  # plain one
     dw = M.wgrad_fp8_blk(aq, sa, bq, sb, poff)                      # bf16 [E, N, K]
     ad = (aq.float().view(N, -1, 128) * torch.exp2(sa.float() - 127)[..., None]).view(N, ld)
     bd = (bq.float().view(K, -1, 128) * torch.exp2(sb.float() - 127)[..., None]).view(K, ld)

@@ -135,6 +135,9 @@ def test_zero1_matches_dp():
 
 
 def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
+    schedule = None
+    if isinstance(pipelined, str):                # "interleave" / "two_stream"
+        schedule, pipelined = pipelined, True
     _init(rank, world, port)
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.parallel.tensor_parallel import shard_gemma_from_full
@@ -143,7 +146,7 @@ def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
     full = gemma.Gemma(c, seed=5)
     grp = dist.new_group([0, 1])
     grp2 = dist.new_group([0, 1]) if pipelined else None
-    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=sp, tp_group2=grp2)
+    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=sp, tp_group2=grp2, tp_schedule=schedule)
     assert not pipelined or local.tp_group2 is not None
     shard_gemma_from_full(full, local, rank, world)
     flat = FlatParams(local)
@@ -161,7 +164,8 @@ def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("sp,pipelined", [(False, False), (True, False), (False, True)])
+@pytest.mark.parametrize("sp,pipelined", [(False, False), (True, False), (False, "interleave"),
+                                          (False, "two_stream")])
 def test_tensor_parallel_gemma_matches_unsharded(sp, pipelined):
     """TP=2 (and TP=2 with Megatron sequence parallelism: reduce-scatter / all-gather over T,
     norms on sequence shards, norm-weight grads summed over TP; and the two-chunk pipeline on a
@@ -223,7 +227,8 @@ def _ep_worker(rank, world, port, q, mode="interleaved"):
     full.reset_parameters(0.1, torch.Generator().manual_seed(3))
     grp = dist.new_group([0, 1])
     grp2 = dist.new_group([0, 1]) if mode == "two_stream" else None
-    m = ds.MoE(c, ep_group=grp, ep_group2=grp2, ep_chunks={"plain": 1, "interleaved": 2, "chunks3": 3}.get(mode, 2))
+    m = ds.MoE(c, ep_group=grp, ep_group2=grp2, ep_chunks={"plain": 1, "interleaved": 2, "chunks3": 3}.get(mode, 2),
+               ep_schedule="two_stream" if mode == "two_stream" else "interleave")
     # the EP constructor's own init: rank r holds shard_experts(unsharded init, r, P), i.e.
     # distinct experts on every rank (not E/P experts drawn again from the shared sequence)
     m.reset_parameters(0.1, torch.Generator().manual_seed(3))

@@ -9,13 +9,14 @@ xGMI at the modelled bandwidth (``--ar-gbps`` RCCL all-reduce bus bandwidth,
 ``--a2a-gbps`` all-to-all bytes leaving a rank per second -- inputs, not measurements).
 
 Arms (fwd + bwd, same process, interleaved rounds):
-  compute   collectives skipped                                  (proxy mode "off")
-  blocking  collectives modelled, the caller waits at each one   (no overlap; = compute + comm)
-  pipelined collectives modelled, two-chunk two-stream pipeline  (models/gemma.py, models/deepseekv3.py)
-  pipe_comp the pipelined form with collectives skipped          (chunking's own compute cost)
+  compute       plain layer, collectives skipped                      (proxy mode "off")
+  blocking      plain layer, collectives modelled, each one waited    (= compute + comm)
+  <form>:overlap  a two-chunk form, collectives modelled and overlapped (models/gemma.py,
+                models/deepseekv3.py: TP interleave / two_stream; EP interleaved2/4 / two_stream)
+  <form>:off    the same form with collectives skipped                (chunking's own cost)
 
-hidden = 1 - (pipelined - pipe_comp) / (blocking - compute): the fraction of the collective
-time that no longer adds to the layer time. One JSON line per config.
+hidden = 1 - (overlap - off) / (blocking - compute): the fraction of the collective time that
+no longer adds to the layer time. One JSON line per config.
 
   python tools/overlap_proxy.py [--which tp,ep] [--layers 2] [--seq 8192]
 """
@@ -56,59 +57,63 @@ def _time(fn, iters):
 ARMS = None   # --arms: run only these (profiling one arm under rocprofv3)
 
 
-def _arms(make_step, groups, iters, rounds):
-    """make_step(pipelined) -> step fn. groups: the ProxyGroups whose mode is switched."""
-    steps = {"compute": (make_step(False), "off"), "blocking": (make_step(False), "blocking"),
-             "pipelined": (make_step(True), "overlap"), "pipe_comp": (make_step(True), "off")}
-    if ARMS:
-        steps = {k: v for k, v in steps.items() if k in ARMS}
-    res = {k: [] for k in steps}
-    comm_ms = {}
-    for r in range(rounds):
-        for k, (fn, mode) in steps.items():
-            for g in groups:
-                g.mode = mode
-            fn()                                         # warm (allocator, proxy calibration)
-            for g in groups:
-                g.reset_stats()
-            res[k].append(_time(fn, iters))
-            comm_ms[k] = sum(g.modelled_s for g in groups) * 1e3 / iters
-    med = {k: statistics.median(v) for k, v in res.items()}
-    if ARMS:
-        return med, {k: comm_ms.get(k, 0.0) for k in ("blocking",)}, 0.0, 0.0
-    exposed = med["pipelined"] - med["pipe_comp"]
-    total = med["blocking"] - med["compute"]
-    return med, comm_ms, exposed, total
-
-
 def tp_gemma(a):
+    """Plain layer (compute / blocking arms) and both two-chunk schedules of models/gemma.py:
+    "interleave" (one stream, staged) and "two_stream" (half B on a second compute stream)."""
     from solvingpapers_amd.models import gemma
     dev = torch.device("cuda")
     c = gemma.config("gemma_7b_mqa", n_layers=a.layers, max_seq_len=a.seq)
     g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
     g2 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
     models = {}
-    for pipe in (False, True):
-        m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=g1, tp_group2=g2 if pipe else None, seed=1)
+    for name, kw in (("plain", {}), ("interleave", dict(tp_group2=g2, tp_schedule="interleave")),
+                     ("two_stream", dict(tp_group2=g2, tp_schedule="two_stream"))):
+        if a.variants and name != "plain" and name not in a.variants.split(","):
+            continue
+        m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=g1, seed=1, **kw)
         FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
-        models[pipe] = m
+        models[name] = m
     ids = torch.randint(0, c.vocab_size, (1, a.seq + 1), device=dev)
 
-    def make(pipe):
-        m = models[pipe]
-
+    def step_of(m):
         def step():
             from solvingpapers_amd.utils.grad import next_generation
             next_generation()
             m(ids[:, :-1], ids[:, 1:]).backward()
         return step
 
-    med, comm_ms, exposed, total = _arms(make, (g1, g2), a.iters, a.rounds)
-    return {"config": "gemma_7b_mqa TP=8 local shard (2 q-heads x 256, GeGLU 3072, V/8)", "layers": a.layers,
-            "seq": a.seq, "ms": {k: round(v, 3) for k, v in med.items()},
-            "modelled_comm_ms": round(comm_ms["blocking"], 3), "comm_added_blocking_ms": round(total, 3),
-            "comm_exposed_pipelined_ms": round(exposed, 3),
-            "hidden": round(1 - exposed / total, 3) if total > 0 else None}
+    arms = {"compute": (step_of(models["plain"]), "off"), "blocking": (step_of(models["plain"]), "blocking")}
+    for name in models:
+        if name != "plain":
+            arms[name + ":overlap"] = (step_of(models[name]), "overlap")
+            arms[name + ":off"] = (step_of(models[name]), "off")
+    if ARMS:
+        arms = {k: v for k, v in arms.items() if k in ARMS}
+    res = {k: [] for k in arms}
+    comm = 0.0
+    for r in range(a.rounds):
+        for k, (fn, mode) in arms.items():
+            for g in (g1, g2):
+                g.mode = mode
+            fn()
+            for g in (g1, g2):
+                g.reset_stats()
+            res[k].append(_time(fn, a.iters))
+            if k == "blocking":
+                comm = (g1.modelled_s + g2.modelled_s) * 1e3 / a.iters
+    med = {k: round(statistics.median(v), 3) for k, v in res.items()}
+    out = {"config": "gemma_7b_mqa TP=8 local shard (2 q-heads x 256, GeGLU 3072, V/8)", "layers": a.layers,
+           "seq": a.seq, "ms": med, "modelled_comm_ms": round(comm, 3)}
+    if not ARMS:
+        total = med["blocking"] - med["compute"]
+        out["comm_added_blocking_ms"] = round(total, 3)
+        for name in models:
+            if name == "plain":
+                continue
+            exposed = med[name + ":overlap"] - med[name + ":off"]
+            out[f"hidden_{name}"] = round(1 - exposed / total, 3) if total > 0 else None
+            out[f"vs_blocking_{name}"] = round(med["blocking"] / med[name + ":overlap"], 3)
+    return out
 
 
 def ep_moe(a):
@@ -120,7 +125,7 @@ def ep_moe(a):
     g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
     g2 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
     variants = {"plain": dict(ep_chunks=1), "interleaved2": dict(ep_chunks=2), "interleaved4": dict(ep_chunks=4),
-                "two_stream": dict(ep_group2=g2)}
+                "two_stream": dict(ep_group2=g2, ep_schedule="two_stream")}
     if a.variants:
         variants = {k: v for k, v in variants.items() if k in a.variants.split(",") or k == "plain"}
     mods = {}
@@ -185,8 +190,9 @@ def main():
     ap.add_argument("--nwg", type=int, default=16)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--arms", default="", help="comma list: compute,blocking,pipelined,pipe_comp (default all)")
-    ap.add_argument("--variants", default="", help="EP: subset of interleaved2,interleaved4,two_stream")
+    ap.add_argument("--arms", default="", help="comma list of arm names (default all), e.g. interleave:overlap")
+    ap.add_argument("--variants", default="", help="EP: subset of interleaved2,interleaved4,two_stream; "
+                                                   "TP: subset of interleave,two_stream")
     a = ap.parse_args()
     global ARMS
     ARMS = [x for x in a.arms.split(",") if x] or None

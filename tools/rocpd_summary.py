@@ -5,6 +5,11 @@ kernel start to the last kernel end and the sum of kernel time (busy union per q
 whether two streams' kernels ran side by side).
 
   python tools/rocpd_summary.py gpurun_out/<dir>/run_results.db [--top 25] [--grep attn]
+      [--timeline START_MS:DUR_MS] [--comm stream_copy]
+
+--timeline prints every kernel of that window (ms from the first kernel) per stream, with the
+idle gaps; --comm NAME reports how much of the time kernels matching NAME (a collective or its
+stand-in) ran with / without a concurrent compute kernel on another stream.
 """
 from __future__ import annotations
 
@@ -70,16 +75,63 @@ def summarise(rows, top=25, grep=None, out=sys.stdout):
         print(f"{t / 1e6:10.3f} {100 * t / total:6.2f} {n:6d}  {k}", file=out)
 
 
+def _short(name):
+    n = name.split("(")[0]
+    for pre in ("void ", "spa::"):
+        n = n.replace(pre, "")
+    return n[:48]
+
+
+def timeline(rows, start_ms, dur_ms, out=sys.stdout):
+    t0 = min(r[0] for r in rows)
+    lo, hi = t0 + start_ms * 1e6, t0 + (start_ms + dur_ms) * 1e6
+    byq = {}
+    for s, e, q, st, disp, name in sorted(rows):
+        if e >= lo and s <= hi:
+            byq.setdefault((q, st), []).append((s, e, disp or name))
+    for key, ks in sorted(byq.items()):
+        print(f"-- queue {key[0]} stream {key[1]}", file=out)
+        prev = None
+        for s, e, n in ks:
+            gap = (s - prev) / 1e3 if prev is not None else 0.0
+            print(f"  {(s - t0) / 1e6:9.3f} ms  +{(e - s) / 1e3:8.1f} us  gap {gap:7.1f} us  {_short(n)}", file=out)
+            prev = e
+
+
+def comm_overlap(rows, pat, out=sys.stdout):
+    comm = [(s, e, st) for s, e, q, st, d, n in rows if pat in (d or n)]
+    comp = [(s, e, st) for s, e, q, st, d, n in rows if pat not in (d or n)]
+    if not comm:
+        print(f"no kernels matching {pat}", file=out)
+        return
+    comp.sort()
+    tot = over = 0
+    for cs, ce, cst in comm:
+        tot += ce - cs
+        iv = [(max(s, cs), min(e, ce)) for s, e, st in comp if e > cs and s < ce and st != cst]
+        over += _union(iv) if iv else 0
+    print(f"comm kernels '{pat}': {len(comm)}, {tot / 1e6:.3f} ms; with concurrent compute {over / 1e6:.3f} ms "
+          f"({100 * over / max(tot, 1):.1f} %)", file=out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db", nargs="+")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--grep", default=None)
+    ap.add_argument("--timeline", default=None, help="START_MS:DUR_MS")
+    ap.add_argument("--comm", default=None, help="kernel-name substring of the collective kernels")
     a = ap.parse_args()
     for pat in a.db:
         for path in sorted(glob.glob(pat)):
             print(f"== {path}")
-            summarise(load(path), a.top, a.grep)
+            rows = load(path)
+            summarise(rows, a.top, a.grep)
+            if a.comm:
+                comm_overlap(rows, a.comm)
+            if a.timeline:
+                st, du = (float(x) for x in a.timeline.split(":"))
+                timeline(rows, st, du)
 
 
 if __name__ == "__main__":
