@@ -82,21 +82,31 @@ __device__ __forceinline__ bf16x8 rd_tr(const bf16* img, int rbase, int c0, int 
 // invariant under the +32-row / +16-row steps of the loops, which become
 // immediate offsets): row reads (row = lane&31, chunk = 2ks + half) and the
 // two halves of each transposed read (k-step rows 0..15, d-tile dt).
+// The swizzle XORs the low 4 bits of the 16-B chunk index, so at HD = 256 the offsets of chunks
+// 16..31 are those of chunks 0..15 plus 128 elements: only the first 8 row / 4 transposed
+// offsets are kept in registers, the rest are immediates (16 fewer VGPRs per image at HD 256).
+template <int N>
+struct LdsOffs {            // operator[k] = v[k % N] + (k / N) * 128 elements (k a constant)
+  int v[N];
+  __device__ __forceinline__ int operator[](int k) const { return v[k % N] + (k / N) * 128; }
+};
 template <int HD>
 struct LdsOff {
-  int row[HD / 16];
-  int tra[HD / 32], trb[HD / 32];
+  static constexpr int NR = HD / 16 > 8 ? 8 : HD / 16, NTR = HD / 32 > 4 ? 4 : HD / 32;
+  LdsOffs<NR> row;
+  LdsOffs<NTR> tra, trb;
   __device__ __forceinline__ void init(int lane) {
+    static_assert(HD <= 256, "LdsOff: the +128 offset rule holds up to 32 chunks per row");
     const int l32 = lane & 31, hh = lane >> 5, g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
 #pragma unroll
-    for (int ks = 0; ks < HD / 16; ++ks) row[ks] = l32 * HD + 8 * ((2 * ks + hh) ^ swz<HD>(l32));
+    for (int ks = 0; ks < NR; ++ks) row.v[ks] = l32 * HD + 8 * ((2 * ks + hh) ^ swz<HD>(l32));
     const int ra = 4 * hh + q, rb = ra + 8;
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt) {
+    for (int dt = 0; dt < NTR; ++dt) {
       const int c = 32 * dt + 16 * (g & 1) + 4 * pp;
       const int ch = c >> 3, within = c & 7;
-      tra[dt] = ra * HD + 8 * (ch ^ swz<HD>(ra)) + within;
-      trb[dt] = rb * HD + 8 * (ch ^ swz<HD>(rb)) + within;
+      tra.v[dt] = ra * HD + 8 * (ch ^ swz<HD>(ra)) + within;
+      trb.v[dt] = rb * HD + 8 * (ch ^ swz<HD>(rb)) + within;
     }
   }
 };

@@ -176,18 +176,24 @@ __global__ __launch_bounds__(256) void dequant_act_blk_kernel(const uint8_t* __r
 }
 
 // Weight-gradient operands (dW_e = dY_e^T X_e, reduction over the expert's tokens): x [T, C] bf16
-// with rows grouped by expert (offsets [E+1]) -> q [C, ldq] e4m3 TRANSPOSED (token-contiguous)
+// with rows grouped by expert (offsets [E+1]) -> qt [C, ldq] e4m3 TRANSPOSED (token-contiguous)
 // with each expert's segment starting at the 128-aligned padded offset poff[e] and zero-filled to
-// it, and s [C, ldq/128] E8M0: one scale per (channel, 128-token block) -- the 128 x 1 tiles of the
-// DeepSeek-V3 recipe for the Wgrad operands. Block (tb, cb): padded tokens [128 tb, +128) x
-// channels [64 cb, +64); tile through LDS in fp32, per-channel amax over the 128 tokens, then
-// 128-byte rows of the transposed image.
+// it, and st [C, ldq/128] E8M0: one scale per (channel, 128-token block) -- the 128 x 1 tiles of
+// the DeepSeek-V3 recipe for the Wgrad operands. Optionally ALSO the row-major 1 x 128 image the
+// forward / dX GEMMs consume (qr [T, C], sr [T, C/128], as quant_act_blk_kernel), from the same
+// read of x. Block (tb, cb): padded tokens [128 tb, +128) x channels [128 cb, +128), 256 threads;
+// thread t holds channels 8 (t & 15) .. +8 of rows (t >> 4) + 16 i: row amax over the 16 lanes of
+// a row group, column amax over the 32 threads of a channel group (shuffles + LDS), values staged
+// once in a padded bf16 LDS tile for the transposed 32-token stores.
 __global__ __launch_bounds__(256) void quant_t_fp8_seg_kernel(const bf16* __restrict__ x, const int* __restrict__ offsets,
                                                               const int* __restrict__ poff, int E, int C,
-                                                              uint8_t* __restrict__ q, uint8_t* __restrict__ s, long ldq) {
-  __shared__ float tile[128][65];
-  __shared__ float inv_s[64];
-  const int tb = blockIdx.x, cb = blockIdx.y, tid = threadIdx.x;
+                                                              uint8_t* __restrict__ qt, uint8_t* __restrict__ st, long ldq,
+                                                              uint8_t* __restrict__ qr, uint8_t* __restrict__ sr) {
+  constexpr int TS = 128 + 8;                           // bf16 row stride of the LDS tile
+  __shared__ __attribute__((aligned(16))) bf16 tile[128 * TS];
+  __shared__ float cm[4][128];
+  __shared__ float cinv[128];
+  const int tb = blockIdx.x, cb = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int p0 = tb * 128;
   if (p0 >= poff[E]) return;
   int lo = 0, hi = E;                                   // expert e: poff[e] <= p0 < poff[e + 1]
@@ -195,35 +201,75 @@ __global__ __launch_bounds__(256) void quant_t_fp8_seg_kernel(const bf16* __rest
     const int mid = (lo + hi) >> 1;
     if (poff[mid] <= p0) lo = mid; else hi = mid;
   }
-  const int e = lo;
-  const long src0 = offsets[e] + (p0 - poff[e]), send = offsets[e + 1];
-  const int c8 = (tid & 7) * 8;
+  const long src0 = offsets[lo] + (p0 - poff[lo]), send = offsets[lo + 1];
+  const int c8 = (tid & 15) * 8, rg = tid >> 4;
+  const int KB = C / 128;
+  float v[8][8];
+  float cmax[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (tid >> 3) + 32 * i;
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (src0 + r < send) load8(x + (src0 + r) * C + cb * 64 + c8, v);
+  for (int i = 0; i < 8; ++i) {
+    const int r = rg + 16 * i;
+    const bool ok = src0 + r < send;
+    if (ok) load8(x + (src0 + r) * C + cb * 128 + c8, v[i]);
+    else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) tile[r][c8 + j] = v[j];
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+    bf16x8 w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      w[j] = (bf16)v[i][j];
+      cmax[j] = fmaxf(cmax[j], fabsf(v[i][j]));
+    }
+    *reinterpret_cast<bf16x8*>(tile + r * TS + c8) = w;
+    if (qr != nullptr && ok) {                          // 1 x 128 row tile = this block's 128 channels
+      float am = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[i][j]));
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 16));
+      const int ex = e8m0_exp(am);
+      *reinterpret_cast<int2*>(qr + (src0 + r) * C + cb * 128 + c8) = q8(v[i], e8m0_inv(ex));
+      if ((tid & 15) == 0) sr[(src0 + r) * KB + cb] = (uint8_t)(ex + 127);
+    }
+  }
+  // column amax: lanes l, l^16, l^32 (same channel group, other row groups) then the 4 waves
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    cmax[j] = fmaxf(cmax[j], __shfl_xor(cmax[j], 16, 64));
+    cmax[j] = fmaxf(cmax[j], __shfl_xor(cmax[j], 32, 64));
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cm[wave][c8 + j] = cmax[j];
   }
   __syncthreads();
-  if (tid < 64) {
-    float amax = 0.f;
-    for (int r = 0; r < 128; ++r) amax = fmaxf(amax, fabsf(tile[r][tid]));
-    const int ex = e8m0_exp(amax);
-    inv_s[tid] = e8m0_inv(ex);
-    s[(long)(cb * 64 + tid) * (ldq / 128) + tb] = (uint8_t)(ex + 127);
+  if (tid < 128) {
+    const float am = fmaxf(fmaxf(cm[0][tid], cm[1][tid]), fmaxf(cm[2][tid], cm[3][tid]));
+    const int ex = e8m0_exp(am);
+    cinv[tid] = e8m0_inv(ex);
+    st[(long)(cb * 128 + tid) * (ldq / 128) + tb] = (uint8_t)(ex + 127);
   }
   __syncthreads();
-  const int c = tid >> 2, seg = tid & 3;               // channel c, tokens [32 seg, +32)
-  const float inv = inv_s[c];
-  uint8_t* qr = q + (long)(cb * 64 + c) * ldq + p0 + 32 * seg;
+  // transposed stores: thread -> channel pair cp (2cp, 2cp+1), tokens [32 qq, +32)
+  const int cp = tid & 63, qq = tid >> 6;
+  const float i0 = cinv[2 * cp], i1 = cinv[2 * cp + 1];
+  float a[32], b2[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const bf16x2 w = *reinterpret_cast<const bf16x2*>(tile + (32 * qq + j) * TS + 2 * cp);
+    a[j] = (float)w[0];
+    b2[j] = (float)w[1];
+  }
+  uint8_t* o0 = qt + (long)(cb * 128 + 2 * cp) * ldq + p0 + 32 * qq;
+  uint8_t* o1 = o0 + ldq;
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
-    float v[8];
+    float t0[8], t1[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tile[32 * seg + 8 * h + j][c];
-    *reinterpret_cast<int2*>(qr + 8 * h) = q8(v, inv);
+    for (int j = 0; j < 8; ++j) { t0[j] = a[8 * h + j]; t1[j] = b2[8 * h + j]; }
+    *reinterpret_cast<int2*>(o0 + 8 * h) = q8(t0, i0);
+    *reinterpret_cast<int2*>(o1 + 8 * h) = q8(t1, i1);
   }
 }
 
@@ -586,24 +632,34 @@ at::Tensor grouped_gemm_fp8_blk(const at::Tensor& xq, const at::Tensor& sx, cons
 }
 
 // x [T, C] bf16 (rows grouped by offsets [E+1]), poff [E+1] (128-aligned padded segment starts,
-// poff[E] <= ldq) -> (q [C, ldq] e4m3, s [C, ldq/128] E8M0): transposed Wgrad operand
+// poff[E] <= ldq) -> (qt [C, ldq] e4m3, st [C, ldq/128] E8M0): transposed Wgrad operand; with
+// ``rows``, also (qr [T, C] e4m3, sr [T, C/128]) = quant_act_fp8_blk(x) from the same read
 std::vector<at::Tensor> quant_t_fp8_seg(const at::Tensor& x_, const at::Tensor& offsets, const at::Tensor& poff,
-                                        int64_t ldq) {
+                                        int64_t ldq, bool rows) {
   SPA_CHECK_CUDA(x_);
   auto x = x_.contiguous();
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "quant_t_fp8_seg: bf16 [T, C]");
   TORCH_CHECK(offsets.scalar_type() == at::kInt && poff.scalar_type() == at::kInt && offsets.numel() == poff.numel(),
               "quant_t_fp8_seg: int32 offsets / padded offsets [E+1]");
+  const long T = x.size(0);
   const int C = x.size(1), E = offsets.numel() - 1;
-  TORCH_CHECK(C % 64 == 0 && ldq % 128 == 0 && ldq >= x.size(0), "quant_t_fp8_seg: C % 64, ldq % 128");
+  TORCH_CHECK(C % 128 == 0 && ldq % 128 == 0 && ldq >= T, "quant_t_fp8_seg: C % 128, ldq % 128");
   DeviceGuard g(x.device());
-  auto q = at::empty({C, ldq}, x.options().dtype(at::kFloat8_e4m3fn));
+  auto o8 = x.options().dtype(at::kFloat8_e4m3fn);
+  auto q = at::empty({C, ldq}, o8);
   auto s = at::empty({C, ldq / 128}, x.options().dtype(at::kByte));
-  if (ldq == 0 || C == 0) return {q, s};
-  quant_t_fp8_seg_kernel<<<dim3((unsigned)(ldq / 128), C / 64), 256, 0, stream()>>>(
-      (const bf16*)x.data_ptr(), offsets.data_ptr<int>(), poff.data_ptr<int>(), E, C, (uint8_t*)q.data_ptr(),
-      s.data_ptr<uint8_t>(), ldq);
-  SPA_LAUNCH_CHECK();
+  at::Tensor qr, sr;
+  if (rows) {
+    qr = at::empty({T, C}, o8);
+    sr = at::empty({T, C / 128}, x.options().dtype(at::kByte));
+  }
+  if (ldq > 0 && C > 0) {
+    quant_t_fp8_seg_kernel<<<dim3((unsigned)(ldq / 128), C / 128), 256, 0, stream()>>>(
+        (const bf16*)x.data_ptr(), offsets.data_ptr<int>(), poff.data_ptr<int>(), E, C, (uint8_t*)q.data_ptr(),
+        s.data_ptr<uint8_t>(), ldq, rows ? (uint8_t*)qr.data_ptr() : nullptr, rows ? sr.data_ptr<uint8_t>() : nullptr);
+    SPA_LAUNCH_CHECK();
+  }
+  if (rows) return {q, s, qr, sr};
   return {q, s};
 }
 
@@ -646,7 +702,7 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("dequant_act_fp8_blk(Tensor q, Tensor s) -> Tensor");
   m.def("quant_weight_fp8_blk(Tensor w) -> Tensor[]");
   m.def("grouped_gemm_fp8_blk(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor offsets) -> Tensor");
-  m.def("quant_t_fp8_seg(Tensor x, Tensor offsets, Tensor poff, int ldq) -> Tensor[]");
+  m.def("quant_t_fp8_seg(Tensor x, Tensor offsets, Tensor poff, int ldq, bool rows) -> Tensor[]");
   m.def("wgrad_fp8_blk(Tensor aq, Tensor sa, Tensor bq, Tensor sb, Tensor poff, Tensor(a!)? out, bool accumulate) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {

@@ -403,9 +403,13 @@ class Gemma(tnn.Module):
         self.tp_rank, self.tp = tp_rank_size(tp_group)
         self.sp = bool(sequence_parallel) and self.tp > 1
         self.tp_group2 = tp_group2 if (self.tp > 1 and not self.sp) else None
-        # "interleave": one-stream staged schedule (_hidden_interleaved); "two_stream": half B on
-        # a second compute stream (_hidden_pipelined). SPA_TP_SCHEDULE overrides the default.
-        self.tp_schedule = tp_schedule or os.environ.get("SPA_TP_SCHEDULE", "interleave")
+        # "two_stream": half B on a second compute stream (_hidden_pipelined); "interleave": the
+        # one-stream staged schedule (_hidden_interleaved). 1-GPU proxy, TP=8 Gemma-7B layers
+        # (profiles/r3_overlap_proxy_tp_schedules.jsonl): two_stream hides 0.28-0.35 of the
+        # collective time, interleave 0.19 at +17 % compute (its per-layer stages are two tiny
+        # norms and two large blocks, so half of the collectives can only bracket a norm; and
+        # every host-side stall of the one stream idles the GPU). SPA_TP_SCHEDULE overrides.
+        self.tp_schedule = tp_schedule or os.environ.get("SPA_TP_SCHEDULE", "two_stream")
         assert self.tp_schedule in ("interleave", "two_stream"), self.tp_schedule
         self._side = None
         if self.tp_group2 is not None and self.tp_schedule == "two_stream":

@@ -265,7 +265,8 @@ class _LinearFP8Fn(torch.autograd.Function):
     """fp8 Linear for the dense projections of the DeepSeek-V3 recipe (arXiv 2412.19437 sec. 3.3):
     forward and dX are e4m3 GEMMs on hipBLASLt (torch._scaled_mm, row-wise fp32 scales: one per
     token row of X / dY, one per output channel of W for the forward and per input channel for
-    dX), dW stays bf16 through the fused-accumulation path. Weight images (W and W^T, e4m3 +
+    dX); dW runs in fp8 too (dims % 128) on the block-scaled Wgrad kernel with 128 x 1 token
+    tiles (ops/moe.py FP8_WGRAD), else bf16 through the fused-accumulation path. Weight images (W and W^T, e4m3 +
     scales) are quantized once per optimizer step (ops/moe.py weight cache). Measured on MI355X
     (tools/probe_scaled_mm.py): 1.7-2.7 PF vs 0.9-1.5 PF bf16 at V3 projection shapes. The
     routed experts use the 1 x 128 / 128 x 128 block-scaled grouped kernel instead."""
@@ -294,13 +295,33 @@ class _LinearFP8Fn(torch.autograd.Function):
             _, _, wtq, swt = quant_weight_fp8_rows(w)
             dx = torch._scaled_mm(dq, wtq.t(), sd[:, None], swt[None, :], out_dtype=dy.dtype).view(x.shape)
         gw = gb = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and _dense_wgrad_fp8_ok(dy2, x2, w):
+            gw = _dense_wgrad_fp8(w, dy2, x2)
+        elif ctx.needs_input_grad[1]:
             def _w(out, acc):
                 return wgrad(dy2, x2, out, acc)
             gw = commit(w, _w)
         if b is not None and ctx.needs_input_grad[2]:
             gb = _commit_bias(b, bias_grad(dy2))
         return dx, gw, gb
+
+
+def _dense_wgrad_fp8_ok(dy2, x2, w):
+    from .moe import FP8_WGRAD
+    return (FP8_WGRAD and dy2.is_cuda and w.dim() == 2 and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0
+            and dy2.shape[0] > 0)
+
+
+def _dense_wgrad_fp8(w, dy2, x2):
+    """fp8 dW = dY^T X of an fp8 Linear on the block-scaled Wgrad kernel (one group): dY and X
+    quantized in 128 x 1 token tiles (transposed images), as the routed experts' dW."""
+    from .moe import commit_weight_grad_fp8, padded_offsets, quant_t_fp8_seg
+    T = dy2.shape[0]
+    off = _one_group(T, dy2.device)
+    poff, ld = padded_offsets(off), (T + 127) // 128 * 128
+    aq, sa = quant_t_fp8_seg(dy2, off, poff, ld)
+    bq, sb = quant_t_fp8_seg(x2, off, poff, ld)
+    return commit_weight_grad_fp8(w, aq, sa, bq, sb, poff)
 
 
 _GROUP1: dict = {}

@@ -113,18 +113,27 @@ class _Fp8DispatchW13(torch.autograd.Function):
     def backward(ctx, dh):
         xq_l, sx_l, rc, offsets = ctx.saved_tensors
         W, (send_splits, recv_splits) = ctx.W, ctx.splits
+        from ..ops import moe as _m
         dh = dh.contiguous()
         lplan = SimpleNamespace(offsets=offsets)
         dxp = None
+        wg8 = ctx.needs_input_grad[1] and _m._wgrad_fp8_ok(dh, xq_l, W)
+        if wg8:   # fp8 dW (128 x 1 token tiles): dh's transposed image + its dX row image, one read
+            poff, ld = _m.padded_offsets(offsets), _m.wgrad_ld(dh.shape[0], W.shape[0])
+            dtq, dts, dq, sd = _m.quant_t_fp8_seg(dh, offsets, poff, ld, rows=True)
         if ctx.needs_input_grad[0]:
-            dq, sd = quant_act_fp8_blk(dh)
+            if not wg8:
+                dq, sd = quant_act_fp8_blk(dh)
             _, wtq, _, swt = quant_weight_fp8_blk(W)
             dxl = grouped_gemm_fp8_blk(dq, sd, wtq, swt, offsets).to(dh.dtype)
             dxr = regroup_rows(dxl, rc, False)
             dxp = dxr.new_empty((sum(send_splits), dxr.shape[1]))
             comm.all_to_all_single(dxp, dxr, send_splits, recv_splits, ctx.group)
         gw = None
-        if ctx.needs_input_grad[1]:
+        if wg8:   # the received rows are 1 x 128 tiles: dequantize, re-tile along tokens
+            xtq, xts = _m.quant_t_fp8_seg(dequant_act_fp8_blk(xq_l, sx_l, dh.dtype), offsets, poff, ld)
+            gw = _m.commit_weight_grad_fp8(W, dtq, dts, xtq, xts, poff)
+        elif ctx.needs_input_grad[1]:
             gw = commit_weight_grad(W, dh, dequant_act_fp8_blk(xq_l, sx_l, dh.dtype), lplan)
         return dxp, gw, None, None, None, None, None
 

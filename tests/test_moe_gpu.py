@@ -360,7 +360,8 @@ def test_fp8_weight_cache_follows_optimizer_steps():
 
 
 def test_fp8_linear_close_to_bf16():
-    """ops.linear(fp8=True): e4m3 fwd / dX on hipBLASLt (row-wise scales, cached weight images), bf16 dW."""
+    """ops.linear(fp8=True): e4m3 fwd / dX on hipBLASLt (row-wise scales, cached weight images) and
+    e4m3 dW on the block-scaled Wgrad kernel (128 x 1 token tiles; bf16 with SPA_FP8_WGRAD=0)."""
     from solvingpapers_amd.ops.linear import linear
     g = torch.Generator().manual_seed(4)
     x = torch.randn(3, 96, 512, generator=g).to(dev, torch.bfloat16).requires_grad_(True)
@@ -374,5 +375,5 @@ def test_fp8_linear_close_to_bf16():
     yr.backward(gy.float())
     assert _rel(y, yr) < 4e-2
     assert _rel(x.grad, xr.grad) < 4e-2
-    assert _rel(w.grad, wr.grad) < 1e-2            # dW stays bf16 (hipBLASLt)
+    assert _rel(w.grad, wr.grad) < 4e-2            # fp8 dW (dims % 128)
     assert _rel(b.grad, br.grad) < 1e-2
