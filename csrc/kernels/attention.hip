@@ -458,9 +458,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   // p.dqacc) -> 5 MFMA products per tile instead of 7 for the split dq + dkdv kernels.
   // dS crosses LDS once ([key][q] image, transposed reads), K sits in a [key][d] image.
   constexpr int KIMG = FUSEDQ ? BNK * IK : 8, DSIMG = FUSEDQ ? BNK * 64 : 8;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TB + KIMG + DSIMG];  // [buf][Q|dO] | K | dS
+  // VLDS (head dim 256, one wave per SIMD): the V fragments of the block's 128 keys live in an
+  // LDS image instead of 64 VGPRs, which leaves the registers to request every chain's LDS
+  // operands ahead (chain_sched); without them hipcc re-used one operand quad per chain and
+  // waited out each LDS read before each MFMA (a bare 1-wave SIMD has nothing to overlap it)
+  constexpr bool VLDS = HDK == 256 && HDV == 256 && !FUSEDQ && !DROP;
+  constexpr int VIMG = VLDS ? BNK * IV : 8;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TB + KIMG + DSIMG + VIMG];  // [buf][Q|dO] | K | dS | V
   bf16* kimg = smem + 2 * TB;
   bf16* dsimg = kimg + KIMG;
+  bf16* vimg = dsimg + DSIMG + (long)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 32 * IV;  // this wave's keys
   __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];  // [buf][-lse2 | -delta]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lk = lane & 31, hh = lane >> 5;
@@ -487,7 +494,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
         *reinterpret_cast<bf16x8*>(kimg + img_off<IK>(wave * 32 + lk, 2 * s + hh)) = kf[s];
     }
 #pragma unroll
-    for (int s = 0; s < KSV; ++s) vf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(vp + 16 * s) : zero8();
+    for (int s = 0; s < KSV; ++s) {
+      vf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(vp + 16 * s) : zero8();
+      if constexpr (VLDS) *reinterpret_cast<bf16x8*>(vimg + img_off<IV>(lk, 2 * s + hh)) = vf[s];
+    }
   }
   f32x16 dkt[DTK], dvt[DTV];
 #pragma unroll
@@ -597,8 +607,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
         f32x16 s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[0]), kf[0], splat16(0.f));
 #pragma unroll
         for (int ks = 1; ks < KSK; ++ks) s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[ks]), kf[ks], s);
+        if constexpr (VLDS) chain_sched<KSK, 1, 3, 4>();        // + the 4 delta reads
 #pragma unroll
-        for (int ks = 0; ks < KSV; ++ks) dp = mfma32(ld_row(Ds + 32 * t * IV, offv.row[ks]), vf[ks], dp);
+        for (int ks = 0; ks < KSV; ++ks)
+          dp = mfma32(ld_row(Ds + 32 * t * IV, offv.row[ks]), VLDS ? ld_row(vimg, offv.row[ks]) : vf[ks], dp);
+        if constexpr (VLDS) chain_sched<KSV, 2, 2>();
         const int qt0 = qq0 + 32 * t;
         unsigned keep = 0xffffu;  // bit r: element r kept by dropout
         if constexpr (DROP) {
@@ -638,11 +651,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
           dvt[dt] = mfma32(ld_tr(Ds + 32 * t * IV, offv.tra[dt], offv.trb[dt]), pa, dvt[dt]);
           dvt[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * IV, offv.tra[dt], offv.trb[dt]), pb, dvt[dt]);
         }
+        if constexpr (VLDS) chain_sched<2 * DTV, 2, 2>();
 #pragma unroll
         for (int dt = 0; dt < DTK; ++dt) {
           dkt[dt] = mfma32(ld_tr(Qs + 32 * t * IK, offk.tra[dt], offk.trb[dt]), sa, dkt[dt]);
           dkt[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * IK, offk.tra[dt], offk.trb[dt]), sb, dkt[dt]);
         }
+        if constexpr (VLDS) chain_sched<2 * DTK, 2, 2>();
       }
     } else if constexpr (FUSEDQ) {
       // masked-out wave: its keys contribute nothing to dQ this tile

@@ -441,7 +441,7 @@ class Gemma(tnn.Module):
 
     def _pipelined(self, ids, cache):
         return (self.tp_group2 is not None and cache is None and torch.is_grad_enabled() and self.training
-                and ids.shape[1] % 2 == 0 and ids.shape[1] >= 2)
+                and (ids.shape[0] % 2 == 0 or (ids.shape[1] % 2 == 0 and ids.shape[1] >= 2)))
 
     def _hidden_interleaved(self, ids, targets=None):
         """One-stream two-chunk TP schedule. Each layer is four stages per chunk (GemmaBlock
@@ -459,6 +459,8 @@ class Gemma(tnn.Module):
         into lockstep and their collectives coincide, profiles/r3_overlap_proxy_v2.jsonl)."""
         from ..parallel import comm
         from ..parallel.tensor_parallel import vocab_parallel_cross_entropy, vocab_parallel_embedding
+        if ids.shape[1] % 2:             # an odd length with an even batch: the batch-split form
+            return self._hidden_pipelined(ids, targets)
         c = self.c
         half = ids.shape[1] // 2
         g = (self.tp_group, self.tp_group2 if self.tp_group2 is not None else self.tp_group)
@@ -506,6 +508,10 @@ class Gemma(tnn.Module):
         c = self.c
         T = ids.shape[1]
         half = T // 2
+        # an even batch splits by SEQUENCES: the halves share no K/V and run as two independent
+        # pipelines (B is offset by half a layer: it starts when A's first o-projection is done);
+        # otherwise each sequence splits in halves and B's queries attend to A's K/V
+        by_batch = ids.shape[0] % 2 == 0
         groups = (self.tp_group, self.tp_group2)
         cuda = ids.is_cuda
         main = torch.cuda.current_stream(ids.device) if cuda else None
@@ -521,22 +527,26 @@ class Gemma(tnn.Module):
 
         if side is not None:
             side.wait_stream(main)
-        chunks = (ids[:, :half], ids[:, half:])
+        hb = ids.shape[0] // 2
+        chunks = (ids[:hb], ids[hb:]) if by_batch else (ids[:, :half], ids[:, half:])
         delta = [None, None]
         for i in range(2):
             with on(i):
                 delta[i] = vocab_parallel_embedding(self.embed, chunks[i], groups[i], scale=math.sqrt(c.dim))
         res = [None, None]
-        for l in self.layers:
+        for li, l in enumerate(self.layers):
             with on(0):
                 res[0], delta[0], kv = l(res[0], delta[0], groups[0], None, 0, False, want_kv=True)
-            if side is not None:
+            if side is not None and (not by_batch or li == 0):
                 side.wait_event(kv[2])       # half A's K/V are rope'd: half B may start its layer
                 for t in kv[:2]:
                     t.record_stream(side)
             kv = kv[:2]
             with on(1):
-                res[1], delta[1] = l(res[1], delta[1], groups[1], None, half, False, kv_prefix=kv)
+                if by_batch:
+                    res[1], delta[1] = l(res[1], delta[1], groups[1], None, 0, False)
+                else:
+                    res[1], delta[1] = l(res[1], delta[1], groups[1], None, half, False, kv_prefix=kv)
         outs = [None, None]
         for i in range(2):
             with on(i):
@@ -546,7 +556,7 @@ class Gemma(tnn.Module):
             # [T/2, D] hidden-gradient all-reduce of one chunk's head backward overlaps the other
             # chunk's head GEMMs (one [T, D] all-reduce here was the longest exposed collective)
             from ..parallel.tensor_parallel import vocab_parallel_cross_entropy
-            tg = (targets[:, :half], targets[:, half:])
+            tg = (targets[:hb], targets[hb:]) if by_batch else (targets[:, :half], targets[:, half:])
             ls, nv = [None, None], [None, None]
             for i in range(2):
                 with on(i):
@@ -559,11 +569,12 @@ class Gemma(tnn.Module):
                 nv[1].record_stream(main)
             loss = (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
             return _JoinStreams.apply(loss, side) if side is not None else loss
+        cat_dim = 0 if by_batch else 1
         if side is not None:
             main.wait_stream(side)
             outs[1].record_stream(main)
-            return _JoinStreams.apply(torch.cat(outs, 1), side)
-        return torch.cat(outs, 1)
+            return _JoinStreams.apply(torch.cat(outs, cat_dim), side)
+        return torch.cat(outs, cat_dim)
 
     def hidden(self, ids, cache=None, pos=0):
         """Final-norm hidden states; a [B, T/tp, D] sequence shard under sequence parallelism."""

@@ -10,8 +10,8 @@ from solvingpapers_amd.parallel.comm import ProxyGroup, group_rank_size
 import pytest
 
 
-@pytest.mark.parametrize("schedule", ["interleave", "two_stream"])
-def test_proxy_group_tp_gemma_pipelined_matches_plain(schedule):
+@pytest.mark.parametrize("schedule,nb", [("interleave", 2), ("two_stream", 2), ("two_stream", 1)])
+def test_proxy_group_tp_gemma_pipelined_matches_plain(schedule, nb):
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.utils.flat import FlatParams
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=8, head_dim=16, ffn_hidden=128)
@@ -20,7 +20,7 @@ def test_proxy_group_tp_gemma_pipelined_matches_plain(schedule):
     plain = gemma.Gemma(c, tp_group=g1, seed=3)
     pipe = gemma.Gemma(c, tp_group=g1, tp_group2=g2, seed=3, tp_schedule=schedule)
     assert plain.layers[0].hl == 1 and plain.embed.shape[0] == 8     # TP=8 local shard shapes
-    ids = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(0))
+    ids = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(0))[:nb]   # nb 2: batch split
     grads = []
     for m in (plain, pipe):
         FlatParams(m)

@@ -135,9 +135,11 @@ def test_zero1_matches_dp():
 
 
 def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
-    schedule = None
-    if isinstance(pipelined, str):                # "interleave" / "two_stream"
+    schedule, nb = None, 2
+    if isinstance(pipelined, str):                # "interleave" / "two_stream" / "two_stream_b1"
         schedule, pipelined = pipelined, True
+        if schedule == "two_stream_b1":           # batch 1: the sequence-split form
+            schedule, nb = "two_stream", 1
     _init(rank, world, port)
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.parallel.tensor_parallel import shard_gemma_from_full
@@ -150,7 +152,7 @@ def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
     assert not pipelined or local.tp_group2 is not None
     shard_gemma_from_full(full, local, rank, world)
     flat = FlatParams(local)
-    ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
+    ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))[:nb]
     even = sp or pipelined                       # SP shards T; the pipeline splits T in halves
     loss = local(ids[:, :-1], ids[:, 1:]) if not even else local(ids[:, :-2], ids[:, 1:-1])
     if pipelined:
@@ -165,7 +167,7 @@ def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
 
 
 @pytest.mark.parametrize("sp,pipelined", [(False, False), (True, False), (False, "interleave"),
-                                          (False, "two_stream")])
+                                          (False, "two_stream"), (False, "two_stream_b1")])
 def test_tensor_parallel_gemma_matches_unsharded(sp, pipelined):
     """TP=2 (and TP=2 with Megatron sequence parallelism: reduce-scatter / all-gather over T,
     norms on sequence shards, norm-weight grads summed over TP; and the two-chunk pipeline on a
@@ -176,6 +178,8 @@ def test_tensor_parallel_gemma_matches_unsharded(sp, pipelined):
     full = gemma.Gemma(c, seed=5)
     FlatParams(full)
     ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
+    if pipelined == "two_stream_b1":
+        ids = ids[:1]
     even = sp or pipelined
     loss = full(ids[:, :-1], ids[:, 1:]) if not even else full(ids[:, :-2], ids[:, 1:-1])  # SP / pipeline: T even
     loss.backward()

@@ -73,7 +73,7 @@ def tp_gemma(a):
         m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=g1, seed=1, **kw)
         FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
         models[name] = m
-    ids = torch.randint(0, c.vocab_size, (1, a.seq + 1), device=dev)
+    ids = torch.randint(0, c.vocab_size, (a.batch, a.seq + 1), device=dev)
 
     def step_of(m):
         def step():
@@ -103,7 +103,8 @@ def tp_gemma(a):
                 comm = (g1.modelled_s + g2.modelled_s) * 1e3 / a.iters
     med = {k: round(statistics.median(v), 3) for k, v in res.items()}
     out = {"config": "gemma_7b_mqa TP=8 local shard (2 q-heads x 256, GeGLU 3072, V/8)", "layers": a.layers,
-           "seq": a.seq, "ms": med, "modelled_comm_ms": round(comm, 3)}
+           "batch": a.batch, "seq": a.seq, "split": "batch" if a.batch % 2 == 0 else "sequence",
+           "ms": med, "modelled_comm_ms": round(comm, 3)}
     if not ARMS:
         total = med["blocking"] - med["compute"]
         out["comm_added_blocking_ms"] = round(total, 3)
@@ -183,6 +184,7 @@ def main():
     ap.add_argument("--which", default="tp,ep")
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--batch", type=int, default=1, help="TP: sequences per step (even: the pipeline splits by batch)")
     ap.add_argument("--tokens", type=int, default=4096)
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--ar-gbps", type=float, default=300.0)
