@@ -108,6 +108,9 @@ __device__ __forceinline__ void q_block_map(const AttnParams& p, int nqb, bool c
 // ---------------------------------------------------------------------------
 template <int HDK, int HDV> constexpr int attn_bn() { return (HDK >= 256 || HDV >= 256) ? 32 : 64; }
 
+#ifndef FWD_PV_SCHED
+#define FWD_PV_SCHED 1
+#endif
 template <int HDK, int HDV, int NW, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   constexpr int BN = attn_bn<HDK, HDV>(), NSUB = BN / 32, BM = 32 * NW, KS = HDK / 16, DT = HDV / 32;
@@ -245,6 +248,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
           o[dt] = mfma32(ld_tr(Vs + 32 * t * IV, offv.tra[dt], offv.trb[dt]), pa, o[dt]);
           o[dt] = mfma32(ld_tr(Vs + (32 * t + 16) * IV, offv.tra[dt], offv.trb[dt]), pb, o[dt]);
         }
+        if (FWD_PV_SCHED) chain_sched<2 * DT, 2, 3>();
       }
     }
     __syncthreads();
@@ -417,6 +421,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
           acc[dt] = mfma32(ld_tr(Ks + 32 * t * IK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
           acc[dt] = mfma32(ld_tr(Ks + (32 * t + 16) * IK, offk.tra[dt], offk.trb[dt]), sb, acc[dt]);
         }
+        if (FWD_PV_SCHED) chain_sched<2 * DT, 2, 3>();
       }
     }
     __syncthreads();
