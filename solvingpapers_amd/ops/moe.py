@@ -415,8 +415,19 @@ def quant_weight_fp8_rows(W):
     return out
 
 
+# Block-scaled fp8 GEMMs: the register-staged 32x32x64 kernel (moe_fp8.hip) or the 8-phase
+# LDS-DMA kernel (csrc/kernels/gemm8_fp8.hip, v_mfma_scale_f32_16x16x128_f8f6f4). Same-process A/B
+# at DeepSeek-V3 widths (tools/bench_fp8_g8.py, profiles/r3_fp8_g8_kernel_ab.txt): forward / dX
+# within +-5 % of each other (the register kernel ahead at K <= 2048), the token-segment Wgrad 31-37 %
+# faster on the 8-phase kernel (1.46-1.59 PF vs 1.07-1.21). SPA_FP8_G8: 1 (default) = 8-phase
+# Wgrad, register forward / dX; 2 = 8-phase everywhere; 0 = register kernels everywhere.
+FP8_G8 = int(os.environ.get("SPA_FP8_G8", "1"))
+
+
 def grouped_gemm_fp8_blk(xq, sx, wq, sw, offsets):
     if xq.is_cuda:
+        if FP8_G8 >= 2 and xq.shape[1] % 128 == 0:
+            return ops().gemm8_fp8_blk(xq, sx, wq, sw, offsets)
         return ops().grouped_gemm_fp8_blk(xq, sx, wq, sw, offsets)
     x = xq.float().view(xq.shape[0], -1, 128) * torch.exp2(sx.float() - 127)[..., None]
     E, N, K = wq.shape
@@ -461,6 +472,8 @@ def quant_t_fp8_seg(x, offsets, poff, ld, rows=False):
 def wgrad_fp8_blk(aq, sa, bq, sb, poff, out=None, accumulate=False):
     """dW_e [M, N] (+)= aq[:, seg_e] bq[:, seg_e]^T on the images of :func:`quant_t_fp8_seg`."""
     if aq.is_cuda:
+        if FP8_G8 >= 1:
+            return ops().wgrad8_fp8_blk(aq, sa, bq, sb, poff, out, accumulate)
         return ops().wgrad_fp8_blk(aq, sa, bq, sb, poff, out, accumulate)
     M, ld = aq.shape
     a = (aq.float().view(M, ld // 128, 128) * torch.exp2(sa.float() - 127)[..., None]).view(M, ld)

@@ -347,6 +347,58 @@ def test_fp8_wgrad_exact_on_dequantized_and_close_to_fp32(counts):
     assert _rel(out.cpu() - 1, ref_dq.cpu()) < 1e-4
 
 
+@pytest.mark.parametrize("K,N,counts", [(128, 264, [300, 0, 129, 1]), (256, 512, [513, 7]),
+                                         (1024, 640, [300, 0, 129, 1, 64, 700, 0, 33])])
+def test_gemm8_fp8_matches_dequantized_and_register_kernel(K, N, counts):
+    """8-phase LDS-DMA fp8 kernel (gemm8_fp8.hip, 16x16x128 scaled MFMA): forward / dX == fp32 GEMM
+    of the dequantized operands and == the register-staged 32x32x64 kernel, for 1, 2 and 8 K-tiles
+    (prologue-only, one steady step, the full pipeline), ragged / empty experts, N % 256 != 0."""
+    g = torch.Generator().manual_seed(7)
+    E, M_ = len(counts), sum(counts)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    x = (torch.randn(M_, K, generator=g) * torch.logspace(-2, 1, K)).to(dev, torch.bfloat16)
+    W = (torch.randn(E, (N + 127) // 128 * 128, K, generator=g) * 0.05)[:, :N].contiguous().to(dev, torch.bfloat16)
+    xq, sx = M.quant_act_fp8_blk(x)
+    Wp = torch.nn.functional.pad(W, (0, 0, 0, (N + 127) // 128 * 128 - N))
+    wq, _, sw, _ = M.quant_weight_fp8_blk(Wp)
+    wq = wq[:, :N].contiguous()
+    y = M.ops().gemm8_fp8_blk(xq, sx, wq, sw, off)
+    y_old = M.ops().grouped_gemm_fp8_blk(xq, sx, wq, sw, off)
+    xd = (xq.float().view(M_, -1, 128) * torch.exp2(sx.float() - 127)[..., None]).view(M_, K)
+    wd = (wq.float().cpu().view(E, N, K // 128, 128) * torch.exp2(sw.float().cpu() - 127)
+          .repeat_interleave(128, 1)[:, :N, :, None]).view(E, N, K)
+    ref = _oracle(xd.cpu(), wd, off.cpu(), 0)
+    assert torch.isfinite(y).all()
+    assert _rel(y.cpu(), ref) < 5e-3
+    assert _rel(y.cpu(), y_old.cpu()) < 5e-3
+
+
+@pytest.mark.parametrize("counts", [[300, 0, 129, 1, 64, 700, 0, 33], [1100, 5]])
+def test_wgrad8_fp8_matches_register_kernel(counts):
+    """8-phase fp8 Wgrad (token segments of 1..9 K-tiles) == the register-staged kernel, bf16 and
+    fp32 (accumulating) outputs, M and N not multiples of 256."""
+    g = torch.Generator().manual_seed(8)
+    E, Nr, Kr = len(counts), 384, 264
+    T = sum(counts)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    dy = (torch.randn(T, Nr, generator=g) * torch.logspace(-2, 1, Nr)).to(dev, torch.bfloat16)
+    x = torch.randn(T, Kr + 120, generator=g)[:, :Kr].contiguous().to(dev, torch.bfloat16)
+    poff = M.padded_offsets(off)
+    ld = (T + E * 127 + 127) // 128 * 128
+    aq, sa = M.quant_t_fp8_seg(dy, off, poff, ld)
+    bq, sb = M.quant_t_fp8_seg(torch.nn.functional.pad(x, (0, 384 - Kr)), off, poff, ld)
+    bq, sb = bq[:Kr].contiguous(), sb[:Kr].contiguous()
+    new = M.ops().wgrad8_fp8_blk(aq, sa, bq, sb, poff, None, False)
+    old = M.ops().wgrad_fp8_blk(aq, sa, bq, sb, poff, None, False)
+    assert torch.isfinite(new).all()
+    assert _rel(new.cpu(), old.cpu()) < 5e-3
+    o1 = torch.ones(E, Nr, Kr, device=dev)
+    o2 = torch.ones(E, Nr, Kr, device=dev)
+    M.ops().wgrad8_fp8_blk(aq, sa, bq, sb, poff, o1, True)
+    M.ops().wgrad_fp8_blk(aq, sa, bq, sb, poff, o2, True)
+    assert _rel(o1.cpu() - 1, o2.cpu() - 1) < 1e-4
+
+
 def test_fp8_weight_cache_follows_optimizer_steps():
     W = torch.randn(2, 256, 256, device=dev, dtype=torch.bfloat16) * 0.02
     a = M.quant_weight_fp8_blk(W)
