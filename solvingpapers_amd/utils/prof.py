@@ -7,7 +7,7 @@
 * :class:`PhaseTimer` -- device-side phase timing with HIP events (no host sync until
   :meth:`PhaseTimer.summary`), averaged over steps.
 * Kernel counters (MFMA utilisation, LDS bank conflicts, HBM bytes) come from
-  ``rocprofv3 --pmc`` runs: tools/gpu_pmc_*.sh, summarised by tools/prof_summary.py.
+  ``rocprofv3 --pmc`` runs: tools/gpu_tasks.sh (headline-pmc, kernels-pmc), summarised by tools/prof_summary.py.
 """
 from __future__ import annotations
 

@@ -1,0 +1,96 @@
+#!/bin/bash
+# GPU-box task runner: one named task per gpurun call, e.g.
+#   gpurun --timeout 1200 -- 'bash tools/gpu_tasks.sh validate'
+# Every GPU step runs under its own time limit and the steps are chained: the first failing step
+# ends the call (no retries). Logs and summaries go to gpurun_out/<task>_*; copy the ones worth
+# keeping into profiles/.
+#
+# tasks:
+#   start          attention micro-bench at the LLaMA shape + a short headline bench
+#   validate       every GPU test, smoke(), headline bench, ViT / dsv3_style / Gemma-7B benches, B8
+#   headline-prof  rocprofv3 kernel trace of 3 headline optimizer steps + per-kernel summary
+#   headline-pmc   two counter passes over a 4-layer headline step (MFMA busy, HBM bytes)
+#   kernels-pmc    memory-bound kernel bandwidths + LDS / VALU counter passes
+#   attn-ab ENV    bench_attn.py A/B of an SPA_* switch (LLaMA, ViT and Gemma shapes), ABBA
+#   parity         fp32 reference-loop parity rows B1/B3/B5/B7 and B8 end to end
+#   overlap        TP / EP collective-overlap proxy (tools/overlap_proxy.py)
+#   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+task=${1:?task}; shift
+O=gpurun_out/$task
+
+run() {  # run <seconds> <log> <cmd...>: one GPU step under its own limit; stop the call on failure
+  local t=$1 log=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "[$rc] $*"
+  if [ $rc -ne 0 ]; then tail -20 "$log"; exit $rc; fi
+}
+jsonl() { grep -h '^{' "$@" | cut -c1-600; }
+
+case $task in
+start)
+  run 300 ${O}_attn.log python -u tools/bench_attn.py
+  grep -i 'attn B' ${O}_attn.log | cut -c1-300
+  run 400 ${O}_bench.log python -u bench.py --steps 8 --warmup 2
+  jsonl ${O}_bench.log ;;
+validate)
+  run 900 ${O}_pytest.log python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 180 ${O}_smoke.log python -c "import __graft_entry__ as g; g.smoke()"
+  tail -1 ${O}_smoke.log
+  run 600 ${O}_bench.log python -u bench.py --steps 6 --warmup 2
+  run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
+  run 300 ${O}_dsv3s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
+  run 400 ${O}_gemma.log python -u bench/gemma_tp.py --layers 28 --steps 3 --warmup 1
+  jsonl ${O}_bench.log ${O}_vit.log ${O}_dsv3s.log ${O}_gemma.log ;;
+headline-prof)
+  run 400 ${O}.log rocprofv3 --kernel-trace --stats -d ${O}_db -o run -- python3 bench.py --steps 2 --warmup 1
+  jsonl ${O}.log
+  for db in $(find ${O}_db -name "*.db"); do python tools/rocpd_summary.py "$db" --top 40 > ${O}_summary.txt 2>&1; done
+  head -50 ${O}_summary.txt | cut -c1-160 ;;
+headline-pmc)
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
+    -d ${O}_a -o run --output-format csv -- python3 bench.py --layers 4 --steps 1 --warmup 1 > ${O}_a.log 2>&1 || exit 1
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE \
+    -d ${O}_b -o run --output-format csv -- python3 bench.py --layers 4 --steps 1 --warmup 1 > ${O}_b.log 2>&1 || exit 2
+  python tools/pmc_step_summary.py "$(find ${O}_a -name '*counter_collection.csv' | head -1)" \
+    "$(find ${O}_b -name '*counter_collection.csv' | head -1)" > ${O}.txt
+  rm -rf ${O}_a ${O}_b
+  cat ${O}.txt ;;
+kernels-pmc)
+  run 180 ${O}_bw.jsonl python -u tools/bench_kernels.py --iters 20
+  timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT FETCH_SIZE \
+    -d ${O}_a -o run --output-format csv -- python3 tools/bench_kernels.py --iters 2 > ${O}_a.log 2>&1 || exit 1
+  timeout -s KILL 150 rocprofv3 --kernel-trace --pmc WRITE_SIZE GRBM_GPU_ACTIVE \
+    -d ${O}_b -o run --output-format csv -- python3 tools/bench_kernels.py --iters 2 > ${O}_b.log 2>&1 || exit 2
+  for d in ${O}_a ${O}_b; do python tools/pmc_summary.py "$(find $d -name '*counter_collection.csv' | head -1)"; done > ${O}.txt 2>&1
+  cat ${O}.txt ;;
+attn-ab)
+  ab=${1:?SPA_X=v[,SPA_Y=w]}
+  for i in 1 2; do
+    run 150 ${O}_llama_$i.log python -u tools/bench_attn.py --iters 20 --ab "$ab"
+    run 150 ${O}_vit_$i.log python -u tools/bench_attn.py --iters 20 --T 197 --B 256 --H 12 --Hkv 12 --hd 64 --noncausal --ab "$ab"
+    run 150 ${O}_gemma_$i.log python -u tools/bench_attn.py --iters 10 --T 8192 --H 16 --Hkv 1 --hd 256 --ab "$ab"
+  done
+  grep -h 'attn B' ${O}_*.log | cut -c1-300 ;;
+parity)
+  run 900 ${O}_fp32.log python -u bench/parity.py --which B1,B3,B5,B7 --dtype fp32 --ref-loop --graph
+  run 600 ${O}_b8.log python -u bench/parity.py --which B8 --ref-loop --graph
+  jsonl ${O}_fp32.log ${O}_b8.log ;;
+overlap)
+  run 400 ${O}.log python -u tools/overlap_proxy.py --layers 2
+  grep -v amdgpu.ids ${O}.log | cut -c1-900 ;;
+secondary)
+  run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
+  run 300 ${O}_dsv3s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
+  run 300 ${O}_v3.log python -u bench/dsv3_train.py --preset dsv3_v3 --steps 4 --warmup 2
+  run 300 ${O}_v3fp8.log python -u bench/dsv3_train.py --preset dsv3_v3 --fp8 --steps 4 --warmup 2
+  run 400 ${O}_gemma.log python -u bench/gemma_tp.py --layers 28 --steps 3 --warmup 1
+  jsonl ${O}_*.log ;;
+*)
+  echo "unknown task $task"; exit 2 ;;
+esac
