@@ -14,6 +14,8 @@
 #   attn-ab ENV    bench_attn.py A/B of an SPA_* switch (LLaMA, ViT and Gemma shapes), ABBA
 #   parity         fp32 reference-loop parity rows B1/B3/B5/B7 and B8 end to end
 #   overlap        TP / EP collective-overlap proxy (tools/overlap_proxy.py)
+#   dsv3-prof      dsv3_style at accum 1 and 4, kernel trace at accum 4
+#   gemm-pmc       gemm8 vs hipBLASLt on a dense 8192^3 + one counter pass
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -91,6 +93,20 @@ secondary)
   run 300 ${O}_v3fp8.log python -u bench/dsv3_train.py --preset dsv3_v3 --fp8 --steps 4 --warmup 2
   run 400 ${O}_gemma.log python -u bench/gemma_tp.py --layers 28 --steps 3 --warmup 1
   jsonl ${O}_*.log ;;
+dsv3-prof)
+  run 300 ${O}_a1.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
+  run 300 ${O}_a4.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4
+  jsonl ${O}_a1.log ${O}_a4.log
+  run 400 ${O}_prof.log rocprofv3 --kernel-trace --stats -d ${O}_db -o run -- python3 bench/dsv3_train.py --preset dsv3_style --steps 2 --warmup 1 --accum 4
+  for db in $(find ${O}_db -name "*.db"); do python tools/rocpd_summary.py "$db" --top 45 > ${O}_summary.txt 2>&1; done
+  head -60 ${O}_summary.txt | cut -c1-170 ;;
+gemm-pmc)
+  run 120 ${O}_bench.log python -u tools/bench_gemm8_dense.py 8192 --iters 20
+  cat ${O}_bench.log | grep -v amdgpu.ids
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
+    -d ${O}_a -o run --output-format csv -- python3 tools/bench_gemm8_dense.py 8192 --iters 3 > ${O}_a.log 2>&1 || { tail -5 ${O}_a.log; exit 1; }
+  python tools/pmc_summary.py "$(find ${O}_a -name '*counter_collection.csv' | head -1)" > ${O}.txt 2>&1
+  cat ${O}.txt | cut -c1-400 ;;
 *)
   echo "unknown task $task"; exit 2 ;;
 esac
