@@ -11,10 +11,11 @@
 // 128-row A halves and two 128-col B halves; wave (wm, wn) owns rows {h*128 + wm*64 + [0,64)} and
 // cols {h*128 + wn*32 + [0,32)} of both halves, so each of its four quadrants (mh, nh) reads one
 // A half and one B half. Per K-tile the wave computes its quadrants in the order
-// (0,0) (0,1) (1,1) (1,0) -- 16 v_mfma_f32_16x16x32_bf16 each -- while the block stages one half
-// (2 DMA per thread) per phase, up to two K-tiles ahead (schedule at the main loop):
+// (0,0) (0,1) (1,1) (1,0) -- 16 v_mfma_f32_16x16x32_bf16 each -- while the block stages the
+// four halves of a K-tile up to two K-tiles ahead (schedule at the main loop: none in the phase
+// that reads 12 fragments, one each in phases 2 and 3, two in phase 4):
 //
-//   phase: ds_read this quadrant's new fragments | DMA one half | [vmcnt] | s_barrier |
+//   phase: ds_read this quadrant's new fragments | DMA 0-2 halves | [vmcnt] | s_barrier |
 //          lgkmcnt(0) | 16 MFMA | s_barrier
 //
 // Waves 4-7 run one barrier behind waves 0-3 (an extra s_barrier before the loop), so on every
@@ -23,8 +24,8 @@
 // both groups, and every restage is >= 2 phases after the last read (one barrier of slack for
 // the stagger).
 //
-// The counted waits (vmcnt 8 after phases 1, 2 and 4) retire exactly the half the next phase
-// reads (B1, A1, then A0 + B0 of the next tile); every half is restaged >= 2 phases after
+// The counted waits (vmcnt 8 / 8 / 10 after phases 1, 2 and 4) retire exactly the half the next
+// phase reads (B1, A1, then A0 + B0 of the next tile); every half is restaged >= 2 phases after
 // its last read. All LDS is one array and every barrier is a bare s_barrier, so no implicit
 // vmcnt(0) drains the DMA queue inside the loop.
 //
@@ -115,8 +116,8 @@ __device__ __forceinline__ bf16x8 rd_ks(const char* half, int col0, int s, int l
   } while (0)
 
 // ABL: ablation switch for profiling only (tools/bench_moe.py --ablate): 0 normal, 1 no DMA
-// (compute on whatever LDS holds), 2 no LDS fragment reads, 3 no vmcnt waits; env value 4
-// selects the ILV schedule (DMA pieces issued between the MFMAs of each cluster). Measured at
+// (compute on whatever LDS holds), 2 no LDS fragment reads, 3 no vmcnt waits (1-3 on the
+// round-2 schedule), 8 the round-2 schedule itself (A/B reference); env value 4 selects the ILV schedule (DMA pieces issued between the MFMAs of each cluster). Measured at
 // 8192^3 (tools/bench_moe.py, profiles/r2_gemm8_ablation.txt): ILV 764 TF vs 1113 TF for the
 // shipped schedule -- a DMA piece's issue stalls the issuing wave's own MFMA stream. 1-3 give wrong
 // results by construction and are never selected by the op unless SPA_GG8_ABLATE is set.
@@ -339,6 +340,56 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       __builtin_amdgcn_s_barrier();
       mfma_qs(1, 0, b0f, n2 ? t + 2 : -1, 2);
       if (n1) { if (n2) { G8_WAIT_VM(6); } else { G8_WAIT_VM(2); } }        // retire B1(t+1)
+      __builtin_amdgcn_s_barrier();
+    }
+  } else if (ABL == 0) {
+    // Shipped schedule ("schedule 2"): no DMA in the phase that reads 12 fragments (P1: A0 + B0).
+    // B1(t+2) moves from P1(t+1) to P4(t) next to B0(t+2) (B1(t) was last read in P2(t): 2
+    // phases, the minimum that A0's restage already uses), so the phases carry reads / DMA halves
+    // 12/0, 4/1, 8/1, 0/2 instead of 12/1, 4/1, 8/1, 0/1, and up to 5 halves stay in flight.
+    // ABBA vs the previous schedule (tools/bench_gemm8_dense.py --ab 8,
+    // profiles/r3_gemm8_schedule2_ab.txt): dense 8192^3 +3-8 %, grouped dX +10-11 %, fwd and dW
+    // +1-3 %. Rejected in the same A/B: A0(t+2) also in P4 (12/0 4/1 8/0 0/3: -2..-5 %) and a
+    // second A fragment set with A0(t+1) read in P4 (4/1 4/1 8/1 8/1: -3..-14 %).
+    //   P1 -        P2 A1(t+1)   P3 A0(t+2)   P4 B0(t+2) B1(t+2)
+    // Waits: end of P1 retires B1(t) (younger: A1(t) + A0 B0 B1(t+1)), end of P2 A1(t) (younger:
+    // A0 B0 B1 A1(t+1)), end of P4 A0, B0(t+1) (younger: B1 A1(t+1) + A0 B0 B1(t+2)).
+    if (ktiles > 0) {
+      stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+      if (ktiles > 1) { stage(1, 0); stage(1, 2); stage(1, 3); G8_WAIT_VM(10); } else { G8_WAIT_VM(4); }  // A0, B0 (0)
+      __builtin_amdgcn_s_barrier();
+      if (late) __builtin_amdgcn_s_barrier();
+    }
+    for (int t = 0; t < ktiles; ++t) {
+      const int s = t & 1;
+      const bool n1 = t + 1 < ktiles, n2 = t + 2 < ktiles;
+      // ---- phase 1: quadrant (0,0), no DMA
+      read_a(half(s, 0));
+      read_b(half(s, 2), b0f);
+      if (n1) { G8_WAIT_VM(8); } else { G8_WAIT_VM(2); }                       // retire B1(t)
+      __builtin_amdgcn_s_barrier();
+      G8_WAIT_LGKM0();
+      mfma_q(0, 0, b0f);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 2: quadrant (0,1)
+      read_b(half(s, 3), b1f);
+      if (n1) { stage(t + 1, 1); G8_WAIT_VM(8); } else { G8_WAIT_VM(0); }      // retire A1(t)
+      __builtin_amdgcn_s_barrier();
+      G8_WAIT_LGKM0();
+      mfma_q(0, 1, b1f);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 3: quadrant (1,1)
+      read_a(half(s, 1));
+      if (n2) stage(t + 2, 0);
+      __builtin_amdgcn_s_barrier();
+      G8_WAIT_LGKM0();
+      mfma_q(1, 1, b1f);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 4: quadrant (1,0) -- no LDS reads
+      if (n2) { stage(t + 2, 2); stage(t + 2, 3); G8_WAIT_VM(10); }             // retire A0, B0(t+1)
+      else if (n1) { G8_WAIT_VM(4); }
+      __builtin_amdgcn_s_barrier();
+      mfma_q(1, 0, b0f);
       __builtin_amdgcn_s_barrier();
     }
   } else {
@@ -616,9 +667,9 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
                                                      Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{})
     const int abl = ablation();
     if (mode == 0) {
-      if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else { G8_L(0, 0); }
+      if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else if (abl == 8) { G8_L(0, 8); } else { G8_L(0, 0); }
     } else {
-      if (abl == 1) { G8_L(1, 1); } else if (abl == 2) { G8_L(1, 2); } else if (abl == 3) { G8_L(1, 3); } else { G8_L(1, 0); }
+      if (abl == 1) { G8_L(1, 1); } else if (abl == 2) { G8_L(1, 2); } else if (abl == 3) { G8_L(1, 3); } else if (abl == 8) { G8_L(1, 8); } else { G8_L(1, 0); }
     }
 #undef G8_L
     SPA_LAUNCH_CHECK();
@@ -640,7 +691,7 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
                                                     (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, \
                                                     K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{})
   const int abl = ablation();
-  if (abl == 1) { G8_L2(1); } else if (abl == 2) { G8_L2(2); } else if (abl == 3) { G8_L2(3); } else { G8_L2(0); }
+  if (abl == 1) { G8_L2(1); } else if (abl == 2) { G8_L2(2); } else if (abl == 3) { G8_L2(3); } else if (abl == 8) { G8_L2(8); } else { G8_L2(0); }
 #undef G8_L2
   SPA_LAUNCH_CHECK();
   return out;

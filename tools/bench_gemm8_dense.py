@@ -16,6 +16,8 @@ ap.add_argument("S", type=int, nargs="?", default=8192)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--modes", default="0,1,2")
 ap.add_argument("--no-blas", action="store_true")
+ap.add_argument("--ab", type=int, default=None, help="also run SPA_GG8_ABLATE=<v> (ABBA, same process) and "
+                "the dsv3_style grouped shapes")
 a = ap.parse_args()
 ops = _ext.ops()
 S = a.S
@@ -41,6 +43,47 @@ def tm(fn):
 
 
 ref = torch.mm(xa, wb[0].t()).float()
+
+
+def arm(v):
+    os.environ["SPA_GG8_ABLATE"] = str(v)
+
+
+if a.ab is not None:
+    from solvingpapers_amd.ops import moe as M
+    torch.manual_seed(0)
+    T, E, k, D, F = 8192, 64, 6, 2048, 1408
+    idx, _ = M.route(torch.randn(T, E, device=dev), k)
+    plan = M.permute(idx, E)
+    A = T * k
+    x = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
+    W13 = torch.randn(E, 2 * F, D, device=dev, dtype=torch.bfloat16) * 0.02
+    W2 = torch.randn(E, D, F, device=dev, dtype=torch.bfloat16) * 0.02
+    h = torch.randn(A, F, device=dev, dtype=torch.bfloat16)
+    dy13 = torch.randn(A, 2 * F, device=dev, dtype=torch.bfloat16)
+    dy2 = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
+    cases = {"dense mode0": (lambda: ops.grouped_gemm8(xa, wb, off1, 0, None, False), fl),
+             "dense mode1": (lambda: ops.grouped_gemm8(xa, wb, off1, 1, None, False), fl),
+             "dense mode2": (lambda: ops.grouped_gemm8(xa, xa, off1, 2, None, False), fl),
+             "fwd W13": (lambda: ops.grouped_gemm8(x, W13, plan.offsets, 0, None, False), 2 * A * 2 * F * D),
+             "fwd W2": (lambda: ops.grouped_gemm8(h, W2, plan.offsets, 0, None, False), 2 * A * D * F),
+             "dX W13": (lambda: ops.grouped_gemm8(dy13, W13, plan.offsets, 1, None, False), 2 * A * 2 * F * D),
+             "dX W2": (lambda: ops.grouped_gemm8(dy2, W2, plan.offsets, 1, None, False), 2 * A * D * F),
+             "dW W13": (lambda: ops.grouped_gemm8(dy13, x, plan.offsets, 2, None, False), 2 * A * 2 * F * D),
+             "dW W2": (lambda: ops.grouped_gemm8(dy2, h, plan.offsets, 2, None, False), 2 * A * D * F)}
+    for name, (fn, f) in cases.items():
+        arm(0); r0 = fn().float()
+        arm(a.ab); r1 = fn().float()
+        same = torch.equal(r0, r1)
+        t = {0: [], a.ab: []}
+        for v in (0, a.ab, a.ab, 0):
+            arm(v)
+            t[v].append(tm(fn))
+        m0, m1 = sum(t[0]) / 2, sum(t[a.ab]) / 2
+        print(f"{name:12s} default {f / m0 / 1e9:6.0f} TF | sched {a.ab} {f / m1 / 1e9:6.0f} TF "
+              f"({m0 / m1:.3f}x) bitwise-equal {same}", flush=True)
+    arm(0)
+    sys.exit(0)
 for mode in [int(m) for m in a.modes.split(",")]:
     bb = wb if mode < 2 else xa
     out = ops.grouped_gemm8(xa, bb, off1, mode, None, False)

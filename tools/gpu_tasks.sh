@@ -15,6 +15,8 @@
 #   parity         fp32 reference-loop parity rows B1/B3/B5/B7 and B8 end to end
 #   overlap        TP / EP collective-overlap proxy (tools/overlap_proxy.py)
 #   dsv3-prof      dsv3_style at accum 1 and 4, kernel trace at accum 4
+#   gemm-ab V..    gemm8 default vs SPA_GG8_ABLATE=V (dense 8192^3 + dsv3_style grouped), ABBA
+#   gemm-validate  GEMM/MoE GPU tests, schedule A/B vs the round-2 one, dsv3_style + ViT benches
 #   gemm-pmc       gemm8 vs hipBLASLt on a dense 8192^3 + one counter pass
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 set -o pipefail
@@ -100,6 +102,20 @@ dsv3-prof)
   run 400 ${O}_prof.log rocprofv3 --kernel-trace --stats -d ${O}_db -o run -- python3 bench/dsv3_train.py --preset dsv3_style --steps 2 --warmup 1 --accum 4
   for db in $(find ${O}_db -name "*.db"); do python tools/rocpd_summary.py "$db" --top 45 > ${O}_summary.txt 2>&1; done
   head -60 ${O}_summary.txt | cut -c1-170 ;;
+gemm-ab)
+  for v in "${@:?schedule}"; do
+    run 300 ${O}_$v.log python -u tools/bench_gemm8_dense.py 8192 --iters 10 --ab $v
+    grep -v amdgpu.ids ${O}_$v.log
+  done ;;
+gemm-validate)
+  run 400 ${O}_pytest.log python -u -m pytest tests/test_moe_gpu.py tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 300 ${O}_ab.log python -u tools/bench_gemm8_dense.py 8192 --iters 10 --ab 8
+  grep -v amdgpu.ids ${O}_ab.log
+  run 300 ${O}_dsv3a1.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
+  run 300 ${O}_dsv3a4.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4
+  run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
+  jsonl ${O}_dsv3a1.log ${O}_dsv3a4.log ${O}_vit.log ;;
 gemm-pmc)
   run 120 ${O}_bench.log python -u tools/bench_gemm8_dense.py 8192 --iters 20
   cat ${O}_bench.log | grep -v amdgpu.ids
