@@ -12,6 +12,7 @@ import torch
 
 from common import PEAK_BF16, report, sdist, timed
 from solvingpapers_amd.models import deepseekv3 as ds
+from solvingpapers_amd.ops.moe import defer_expert_wgrad
 from solvingpapers_amd.parallel.data_parallel import DataParallel
 from solvingpapers_amd.train.optim import FlatAdamW
 from solvingpapers_amd.utils.flat import FlatParams
@@ -38,6 +39,10 @@ def main():
                     help="AdamW moments in bf16 (DeepSeek-V3 sec. 3.3.2; fp32 master weights kept; default)")
     ap.add_argument("--fp32-moments", dest="bf16_moments", action="store_false", help="AdamW moments in fp32")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
+    ap.add_argument("--defer-wgrad", dest="defer", action="store_true",
+                    help="with --accum > 1: defer the routed experts' weight gradients to the last micro-batch "
+                         "(one long-K grouped GEMM per weight, ops/moe.py defer_expert_wgrad)")
+    ap.add_argument("--no-defer-wgrad", dest="defer", action="store_false")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="no two-chunk EP pipeline (default: token halves on two streams / communicators)")
     a = ap.parse_args()
@@ -75,7 +80,8 @@ def main():
         for i in range(a.accum):
             t = torch.randint(0, c.vocab_size, (B, T + 1), device=dev, generator=gen)
             inner = dp is not None and i < a.accum - 1
-            with (dp.no_sync() if inner else contextlib.nullcontext()):
+            with (dp.no_sync() if inner else contextlib.nullcontext()), \
+                    defer_expert_wgrad(a.defer and i < a.accum - 1):
                 loss = m(t[:, :-1], t[:, 1:]) / a.accum
                 loss.backward()
         if dp is not None:
@@ -89,7 +95,7 @@ def main():
     report("training tokens/sec, DeepSeek-V3-style MLA+MoE " + ("fp8 (e4m3 block-scaled GEMMs)" if a.fp8 else "bf16"),
            tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
-            + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum, "adam_moments": "bf16" if a.bf16_moments else "fp32",
+            + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum, "deferred_expert_wgrad": a.defer and a.accum > 1, "adam_moments": "bf16" if a.bf16_moments else "fp32",
             "parallelism": (f"ep{world}-dp{world}" + ("-pipe2" if ep2 is not None else "")) if world > 1 else "1gpu",
             "params": m.num_params(),
             "active_params": m.num_params(active=True)},

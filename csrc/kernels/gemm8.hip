@@ -134,13 +134,25 @@ struct G8Epi {
   float* part;
   float alpha;
 };
+// Mode 2 over several token sources (gradient-accumulation micro-batches whose weight gradients
+// were deferred, ops/moe.py defer_expert_wgrad): expert e's reduction range is the concatenation
+// of [off_s[e], off_s[e+1]) of every source s, each read from its own (dY_s, X_s) pair; every
+// source's last K-tile is zero-filled past its end by the buffer range check. n == 0: the
+// kernel's own (A, B, offsets).
+constexpr int G8_MAXSEG = 8;
+struct G8Segs {
+  const bf16* a[G8_MAXSEG];
+  const bf16* b[G8_MAXSEG];
+  const int* off[G8_MAXSEG];
+  int n;
+};
 
-template <int MODE, int ABL = 0, bool ILV = false, bool PART = false, int EPI = 0, int KIND = 0>
+template <int MODE, int ABL = 0, bool ILV = false, bool PART = false, int EPI = 0, int KIND = 0, bool SEGS = false>
 __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                                bf16* __restrict__ C, const int* __restrict__ offsets,
                                                                int E, int M, int N, int K, long lda, long ldb, long ldc,
                                                                long strideB, long strideC, int accumulate, long a_rows,
-                                                               long b_rows, G8Epi ep) {
+                                                               long b_rows, G8Epi ep, G8Segs sg) {
   using namespace g8;
   constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
   // ONE LDS array (a second __shared__ object can make hipcc drain the DMA queue before ds_reads);
@@ -186,12 +198,36 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     mt = mt % nmt;
     if (e >= E) return;
     m0 = (long)mt * BM;
-    k0 = __builtin_amdgcn_readfirstlane(offsets[e]);
-    kend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
     Cp = C + e * strideC;
   }
+  // mode 2 reduction sources: (A, B, [k0, kend)) per source, its K-tiles in sequence
+  int nseg = 1, sk0[G8_MAXSEG], skend[G8_MAXSEG], skt[G8_MAXSEG];
+  if (MODE == 2 && !SEGS) {
+    k0 = __builtin_amdgcn_readfirstlane(offsets[e]);
+    kend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
+  }
+  if (MODE == 2 && SEGS) {
+    nseg = sg.n > 0 ? sg.n : 1;
+#pragma unroll
+    for (int q = 0; q < G8_MAXSEG; ++q) {
+      sk0[q] = skend[q] = skt[q] = 0;
+      if (q < nseg) {
+        const int* o = sg.n > 0 ? sg.off[q] : offsets;
+        sk0[q] = __builtin_amdgcn_readfirstlane(o[e]);
+        skend[q] = __builtin_amdgcn_readfirstlane(o[e + 1]);
+        skt[q] = skend[q] > sk0[q] ? (skend[q] - sk0[q] + BK - 1) / BK : 0;
+      }
+    }
+    k0 = sk0[0];
+    kend = skend[0];
+  }
   const int n0 = nt * BN;
-  const int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
+  int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
+  if (MODE == 2 && SEGS) {
+    ktiles = 0;
+#pragma unroll
+    for (int q = 0; q < G8_MAXSEG; ++q) ktiles += skt[q];
+  }
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   unsigned voA[2], voB[2];
 #pragma unroll
@@ -208,6 +244,40 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   auto stage = [&](int t, int which) {       // which: 0 A0, 1 A1, 2 B0, 3 B1
     if (ABL == 1) return;
     char* dst = half(t & 1, which) + wave_u * 1024;
+    if (MODE == 2 && SEGS) {
+      // K-tile t of the concatenated sources: its source q and local tile tt by scalar selects
+      // (no array indexed at run time), then every selected value through readfirstlane so the
+      // buffer descriptor is provably wave-uniform (a VGPR descriptor makes hipcc emit a
+      // waterfall loop around each DMA: cdna_hip_programming.md T20)
+      int q = 0, tt = t;
+#pragma unroll
+      for (int j = 0; j < G8_MAXSEG - 1; ++j) {
+        const bool adv = q == j && j + 1 < nseg && tt >= skt[j];
+        tt = adv ? tt - skt[j] : tt;
+        q = adv ? j + 1 : q;
+      }
+      uint64_t pa = (uint64_t)sg.a[0], pb = (uint64_t)sg.b[0];
+      int kb = sk0[0], ke = skend[0];
+#pragma unroll
+      for (int j = 1; j < G8_MAXSEG; ++j) {
+        const bool h = q == j;
+        pa = h ? (uint64_t)sg.a[j] : pa;
+        pb = h ? (uint64_t)sg.b[j] : pb;
+        kb = h ? sk0[j] : kb;
+        ke = h ? skend[j] : ke;
+      }
+      const bf16* sa = (const bf16*)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(pa >> 32)) << 32) |
+                                     (unsigned)__builtin_amdgcn_readfirstlane((int)pa));
+      const bf16* sb = (const bf16*)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(pb >> 32)) << 32) |
+                                     (unsigned)__builtin_amdgcn_readfirstlane((int)pb));
+      kb = __builtin_amdgcn_readfirstlane(kb);
+      ke = __builtin_amdgcn_readfirstlane(ke);
+      tt = __builtin_amdgcn_readfirstlane(tt);
+      const long kk = (long)kb + (long)tt * BK;
+      if (which < 2) stage_half(sa, kk * lda + m0 + 128 * which, (long)ke * lda, dst, voA);
+      else stage_half(sb, kk * ldb + n0 + 128 * (which - 2), (long)ke * ldb, dst, voB);
+      return;
+    }
     const long kk = k0 + (long)t * BK;       // absolute reduction index of the tile
     if (which < 2) {
       const long r = m0 + 128 * which;
@@ -616,7 +686,7 @@ at::Tensor wgrad8(const at::Tensor& dy, const at::Tensor& x, const c10::optional
   auto part = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
   grouped_gemm8_kernel<2, 0, false, true><<<S * tiles, 512, 0, st>>>(
       (const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(), reinterpret_cast<bf16*>(part.data_ptr<float>()),
-      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T, G8Epi{});
+      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T, G8Epi{}, G8Segs{});
   SPA_LAUNCH_CHECK();
   const long n = (long)N * K;
   const int rb = (int)std::min<long>((n / 4 + 255) / 256, 4096);
@@ -661,10 +731,10 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 #define G8_L(MD, AB)                                                                                          \
   if (abl == 4) grouped_gemm8_kernel<MD, 0, true><<<grid, 512, 0, st>>>(                                     \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,  \
-      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{});                                  \
+      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{}, G8Segs{});                                  \
   else grouped_gemm8_kernel<MD, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),     \
                                                      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
-                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{})
+                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{}, G8Segs{})
     const int abl = ablation();
     if (mode == 0) {
       if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else if (abl == 8) { G8_L(0, 8); } else { G8_L(0, 0); }
@@ -686,13 +756,51 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 #define G8_L2(AB)                                                                                             \
   if (abl == 4) grouped_gemm8_kernel<2, 0, true><<<grid, 512, 0, st>>>(                                      \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N,  \
-      K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{});                                     \
+      K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{}, G8Segs{});                                     \
   else grouped_gemm8_kernel<2, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),      \
                                                     (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, \
-                                                    K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{})
+                                                    K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{}, G8Segs{})
   const int abl = ablation();
   if (abl == 1) { G8_L2(1); } else if (abl == 2) { G8_L2(2); } else if (abl == 3) { G8_L2(3); } else if (abl == 8) { G8_L2(8); } else { G8_L2(0); }
 #undef G8_L2
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+// Mode 2 over several (dY_s [T_s, N], X_s [T_s, K], offsets_s [E+1]) sources in ONE launch:
+// out[e] (+)= sum_s dY_s[rows_e]^T X_s[rows_e] -- the deferred expert weight gradient of several
+// gradient-accumulation micro-batches (G8Segs).
+at::Tensor grouped_gemm8_wgrad_multi(const std::vector<at::Tensor>& dys, const std::vector<at::Tensor>& xs,
+                                     const std::vector<at::Tensor>& offs, at::Tensor out, bool accumulate) {
+  const int S = (int)dys.size();
+  TORCH_CHECK(S >= 1 && S <= G8_MAXSEG && (int)xs.size() == S && (int)offs.size() == S,
+              "grouped_gemm8_wgrad_multi: 1..8 sources, equal list lengths");
+  const int N = dys[0].size(1), K = xs[0].size(1), E = offs[0].numel() - 1;
+  TORCH_CHECK(E >= 1 && E <= 512 && N % 8 == 0 && K % 8 == 0, "grouped_gemm8_wgrad_multi: shapes");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == (long)E * N * K,
+              "grouped_gemm8_wgrad_multi: out bf16 [E, N, K]");
+  G8Segs sg{};
+  sg.n = S;
+  for (int q = 0; q < S; ++q) {
+    const auto &a = dys[q], &x = xs[q], &o = offs[q];
+    TORCH_CHECK(a.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && a.is_contiguous() &&
+                    x.is_contiguous() && a.dim() == 2 && x.dim() == 2, "grouped_gemm8_wgrad_multi: bf16 2-D");
+    TORCH_CHECK(a.size(1) == N && x.size(1) == K && a.size(0) == x.size(0), "grouped_gemm8_wgrad_multi: source shapes");
+    TORCH_CHECK(o.scalar_type() == at::kInt && o.numel() == E + 1 && o.is_contiguous() && o.is_cuda(),
+                "grouped_gemm8_wgrad_multi: offsets int32 [E+1] on the device");
+    TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)x.data_ptr() % 16 == 0, "16-B aligned");
+    const long T = a.size(0);
+    TORCH_CHECK((T + 64) * (N + 256) * 2 < (1L << 32) && (T + 64) * (K + 256) * 2 < (1L << 32),
+                "grouped_gemm8_wgrad_multi: operands < 4 GiB");
+    sg.a[q] = (const bf16*)a.data_ptr();
+    sg.b[q] = (const bf16*)x.data_ptr();
+    sg.off[q] = o.data_ptr<int>();
+  }
+  DeviceGuard g(out.device());
+  auto st = stream();
+  const int grid = E * cdiv(N, 256) * cdiv(K, 256);
+  grouped_gemm8_kernel<2, 0, false, false, 0, 0, true><<<grid, 512, 0, st>>>(sg.a[0], sg.b[0], (bf16*)out.data_ptr(), sg.off[0], E, N, K, 0, N,
+                                                    K, K, 0, (long)N * K, accumulate ? 1 : 0, 0, 0, G8Epi{}, sg);
   SPA_LAUNCH_CHECK();
   return out;
 }
@@ -740,7 +848,7 @@ std::vector<at::Tensor> gemm8_epi(const at::Tensor& a, const at::Tensor& w, cons
 #define G8E(MD, EP, KD)                                                                                      \
   grouped_gemm8_kernel<MD, 0, false, false, EP, KD><<<grid, 512, 0, st>>>(                                   \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), 1, M, \
-      N, K, K, Kw, N, (long)Nw * Kw, 0, 0, M, Nw, ep)
+      N, K, K, Kw, N, (long)Nw * Kw, 0, 0, M, Nw, ep, G8Segs{})
 #define G8E_KIND(MD, EP)                                  \
   switch (kind) {                                         \
     case GELU_ERF: G8E(MD, EP, GELU_ERF); break;          \
@@ -761,10 +869,12 @@ std::vector<at::Tensor> gemm8_epi(const at::Tensor& a, const at::Tensor& w, cons
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("grouped_gemm8(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def("wgrad8(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate, int splits) -> Tensor");
+  m.def("grouped_gemm8_wgrad_multi(Tensor[] dy, Tensor[] x, Tensor[] offsets, Tensor(a!) out, bool accumulate) -> Tensor");
   m.def("gemm8_epi(Tensor a, Tensor w, Tensor offsets, int epi, Tensor aux, int kind, float alpha) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("grouped_gemm8", &spa::grouped_gemm8);
   m.impl("wgrad8", &spa::wgrad8);
   m.impl("gemm8_epi", &spa::gemm8_epi);
+  m.impl("grouped_gemm8_wgrad_multi", &spa::grouped_gemm8_wgrad_multi);
 }

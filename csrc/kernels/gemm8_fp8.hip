@@ -212,13 +212,22 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
   };
 
   // Schedule (gemm8.hip): K-tile t lives in stage t & 1. Reads: P1 A0 + B0 + the tile's scales,
-  // P2 B1, P3 A1, P4 none. Stages: P1 B1(t+1), P2 A1(t+1), P3 A0(t+2) (+ scales), P4 B0(t+2).
-  // Waits (end of P1, P2, P4) retire exactly the next reader's half; waves 4-7 run one barrier
-  // behind waves 0-3.
+  // P2 B1, P3 A1, P4 none. Stages, S2 (forward / dX: gemm8.hip's shipped schedule): P1 none, P2
+  // A1(t+1), P3 A0(t+2) (+ scales), P4 B0(t+2) and B1(t+2), waits vmcnt 8 / 8 / 10; otherwise (Wgrad:
+  // the round-2 schedule, 3 % faster there, profiles/r3_gemm8_schedule2_ab.txt) P1 B1(t+1), P2
+  // A1(t+1), P3 A0(t+2), P4 B0(t+2), waits 8 / 8 / 8. Waits (end of P1, P2, P4) retire exactly the
+  // next reader's half (waves 0 / 1 count one scale piece more per A0 half, so their waits are one
+  // piece stricter); waves 4-7 run one barrier behind waves 0-3.
+  constexpr bool S2 = !WG;
   const bool late = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (ktiles > 0) {
     stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
-    if (ktiles > 1) { stage(1, 0); stage(1, 2); G8F_WAIT_VM(8); } else { G8F_WAIT_VM(4); }   // A0, B0 (0)
+    if (ktiles > 1) {
+      stage(1, 0); stage(1, 2);
+      if (S2) { stage(1, 3); G8F_WAIT_VM(10); } else { G8F_WAIT_VM(8); }                    // A0, B0 (0)
+    } else {
+      G8F_WAIT_VM(4);
+    }
     __builtin_amdgcn_s_barrier();
     if (late) __builtin_amdgcn_s_barrier();
   }
@@ -229,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
     read_a(half(s, 0));
     read_b(half(s, 2), b0f);
     read_scales(s);
-    if (n1) { stage(t + 1, 3); G8F_WAIT_VM(8); } else { G8F_WAIT_VM(2); }      // retire B1(t)
+    if (n1) { if (!S2) stage(t + 1, 3); G8F_WAIT_VM(8); } else { G8F_WAIT_VM(2); }   // retire B1(t)
     __builtin_amdgcn_s_barrier();
     G8F_WAIT_LGKM0();
     mfma_q(0, 0, b0f);
@@ -249,8 +258,12 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
     mfma_q(1, 1, b1f);
     __builtin_amdgcn_s_barrier();
     // ---- phase 4: quadrant (1,0) -- no LDS reads
-    if (n2) { stage(t + 2, 2); G8F_WAIT_VM(8); }                              // retire A0, B0(t+1)
-    else if (n1) { G8F_WAIT_VM(0); }
+    if (n2) {                                                                  // retire A0, B0(t+1)
+      stage(t + 2, 2);
+      if (S2) { stage(t + 2, 3); G8F_WAIT_VM(10); } else { G8F_WAIT_VM(8); }
+    } else if (n1) {
+      if (S2) { G8F_WAIT_VM(4); } else { G8F_WAIT_VM(0); }
+    }
     __builtin_amdgcn_s_barrier();
     mfma_q(1, 0, b0f);
     __builtin_amdgcn_s_barrier();

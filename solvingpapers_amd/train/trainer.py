@@ -29,6 +29,7 @@ from ..parallel.data_parallel import DataParallel
 from ..utils.flat import FlatParams
 from ..utils.prof import annotate
 from . import checkpoint as ckpt
+from ..ops.moe import defer_expert_wgrad, flush_expert_wgrad
 from .optim import FlatAdamW, FlatSGD, cosine_lr
 
 
@@ -36,6 +37,9 @@ from .optim import FlatAdamW, FlatSGD, cosine_lr
 class TrainConfig:
     steps: int = 1000
     grad_accum: int = 1
+    # routed-expert weight gradients of the inner micro-batches deferred to the last one (one
+    # long-K grouped GEMM per weight, ops/moe.py defer_expert_wgrad); costs the kept activations
+    defer_expert_wgrad: bool = False
     optimizer: str = "adamw"            # adamw | adam | sgd
     lr: float = 3e-4
     min_lr: Optional[float] = None       # None -> constant LR
@@ -207,12 +211,13 @@ class Trainer:
             ntok += c.tokens_per_sample * x.shape[0] if c.tokens_per_sample else x.numel()
             last = mi == c.grad_accum - 1
             ctx = self.dp.no_sync() if (self.dp is not None and not last) else _null()
-            with ctx:
+            with ctx, defer_expert_wgrad(c.defer_expert_wgrad and not last):
                 with annotate("forward"):
                     loss = self.model(x, y)
                 with annotate("backward"):
                     (loss / c.grad_accum).backward()
             tot = loss.detach() if tot is None else tot + loss.detach()
+        flush_expert_wgrad()                 # no-op unless a kept weight missed the last micro-batch
         if self.dp is not None:
             with annotate("grad_sync"):
                 self.dp.finish_grad_sync()

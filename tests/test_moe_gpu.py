@@ -429,3 +429,61 @@ def test_fp8_linear_close_to_bf16():
     assert _rel(x.grad, xr.grad) < 4e-2
     assert _rel(w.grad, wr.grad) < 4e-2            # fp8 dW (dims % 128)
     assert _rel(b.grad, br.grad) < 1e-2
+
+
+def _counts_offsets(counts):
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    return off, int(sum(counts))
+
+
+def test_grouped_gemm8_wgrad_multi_sources():
+    """dW over several (dY_s, X_s, offsets_s) sources in one launch (deferred micro-batches) vs the
+    fp32 sum of per-source per-expert products; ragged tails, empty experts, accumulate."""
+    torch.manual_seed(11)
+    E, N, K = 5, 264, 200
+    srcs = []
+    for counts in ([70, 0, 130, 3, 65], [0, 0, 300, 1, 1], [64, 64, 0, 129, 7]):
+        off, T = _counts_offsets(counts)
+        srcs.append((torch.randn(T, N, device=dev).bfloat16(), torch.randn(T, K, device=dev).bfloat16(), off))
+    ref = torch.zeros(E, N, K)
+    for dy, x, off in srcs:
+        o = off.tolist()
+        for e in range(E):
+            ref[e] += dy[o[e]:o[e + 1]].float().cpu().t() @ x[o[e]:o[e + 1]].float().cpu()
+    out = torch.empty(E, N, K, device=dev, dtype=torch.bfloat16)
+    M.ops().grouped_gemm8_wgrad_multi([s[0] for s in srcs], [s[1] for s in srcs], [s[2] for s in srcs], out, False)
+    assert _rel(out.cpu(), ref) < 1e-2
+    M.ops().grouped_gemm8_wgrad_multi([s[0] for s in srcs], [s[1] for s in srcs], [s[2] for s in srcs], out, True)
+    assert _rel(out.cpu(), 2 * ref) < 1e-2
+    # one source == the single-source kernel, bitwise
+    one = torch.empty_like(out)
+    M.ops().grouped_gemm8_wgrad_multi([srcs[0][0]], [srcs[0][1]], [srcs[0][2]], one, False)
+    assert torch.equal(one, M.grouped_gemm(srcs[0][0], srcs[0][1], srcs[0][2], 2))
+
+
+def test_deferred_expert_wgrad_matches_per_microbatch():
+    """An accumulation loop with the inner micro-batches under defer_expert_wgrad() gives the same
+    expert weight gradients as committing each micro-batch (fp32 oracle for both), and the other
+    parameters' gradients are unchanged."""
+    from solvingpapers_amd.models import deepseekv3 as ds
+    from solvingpapers_amd.utils.flat import FlatParams
+    from solvingpapers_amd.utils.grad import next_generation
+    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0, mtp_heads=0)
+    grads = []
+    for defer in (False, True):
+        m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=0)
+        flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.float32)
+        flat.grad.zero_()
+        next_generation()
+        gen = torch.Generator().manual_seed(3)
+        for i in range(3):
+            ids = torch.randint(0, c.vocab_size, (2, 65), generator=gen).to(dev)
+            with M.defer_expert_wgrad(defer and i < 2):
+                (m(ids[:, :-1], ids[:, 1:]) / 3).backward()
+        assert not M._Defer.pending
+        grads.append({n: p.main_grad.float().clone() for n, p in m.named_parameters()})
+    for n, g0 in grads[0].items():
+        g1 = grads[1][n]
+        if g0.abs().max() == 0:
+            continue
+        assert _rel(g1, g0) < (2e-2 if g0.dim() == 3 else 1e-5), n      # routed experts: [E, out, in]

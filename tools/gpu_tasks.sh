@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU-box task runner: one named task per gpurun call, e.g.
 #   gpurun --timeout 1200 -- 'bash tools/gpu_tasks.sh validate'
-# Every GPU step runs under its own time limit and the steps are chained: the first failing step
+# Profiler databases go to /tmp on the box (gpurun copies back at most 64 MiB); only summaries
+# land in gpurun_out. Every GPU step runs under its own time limit and the steps are chained: the first failing step
 # ends the call (no retries). Logs and summaries go to gpurun_out/<task>_*; copy the ones worth
 # keeping into profiles/.
 #
@@ -17,6 +18,7 @@
 #   dsv3-prof      dsv3_style at accum 1 and 4, kernel trace at accum 4
 #   gemm-ab V..    gemm8 default vs SPA_GG8_ABLATE=V (dense 8192^3 + dsv3_style grouped), ABBA
 #   gemm-validate  GEMM/MoE GPU tests, schedule A/B vs the round-2 one, dsv3_style + ViT benches
+#   defer-ab       MoE GPU tests; dsv3_style accum 4 with / without deferred expert Wgrad, ABBA
 #   gemm-pmc       gemm8 vs hipBLASLt on a dense 8192^3 + one counter pass
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 set -o pipefail
@@ -52,9 +54,9 @@ validate)
   run 400 ${O}_gemma.log python -u bench/gemma_tp.py --layers 28 --steps 3 --warmup 1
   jsonl ${O}_bench.log ${O}_vit.log ${O}_dsv3s.log ${O}_gemma.log ;;
 headline-prof)
-  run 400 ${O}.log rocprofv3 --kernel-trace --stats -d ${O}_db -o run -- python3 bench.py --steps 2 --warmup 1
+  run 400 ${O}.log rocprofv3 --kernel-trace --stats -d /tmp/$task -o run -- python3 bench.py --steps 2 --warmup 1
   jsonl ${O}.log
-  for db in $(find ${O}_db -name "*.db"); do python tools/rocpd_summary.py "$db" --top 40 > ${O}_summary.txt 2>&1; done
+  python tools/rocpd_summary.py /tmp/$task/run_results.db --last-step adamw --top 40 > ${O}_summary.txt 2>&1
   head -50 ${O}_summary.txt | cut -c1-160 ;;
 headline-pmc)
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
@@ -99,8 +101,8 @@ dsv3-prof)
   run 300 ${O}_a1.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
   run 300 ${O}_a4.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4
   jsonl ${O}_a1.log ${O}_a4.log
-  run 400 ${O}_prof.log rocprofv3 --kernel-trace --stats -d ${O}_db -o run -- python3 bench/dsv3_train.py --preset dsv3_style --steps 2 --warmup 1 --accum 4
-  for db in $(find ${O}_db -name "*.db"); do python tools/rocpd_summary.py "$db" --top 45 > ${O}_summary.txt 2>&1; done
+  run 400 ${O}_prof.log rocprofv3 --kernel-trace --stats -d /tmp/$task -o run -- python3 bench/dsv3_train.py --preset dsv3_style --steps 2 --warmup 1 --accum 4
+  python tools/rocpd_summary.py /tmp/$task/run_results.db --last-step adamw --top 45 > ${O}_summary.txt 2>&1
   head -60 ${O}_summary.txt | cut -c1-170 ;;
 gemm-ab)
   for v in "${@:?schedule}"; do
@@ -116,6 +118,21 @@ gemm-validate)
   run 300 ${O}_dsv3a4.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4
   run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
   jsonl ${O}_dsv3a1.log ${O}_dsv3a4.log ${O}_vit.log ;;
+defer-ab)
+  run 300 ${O}_pytest.log python -u -m pytest tests/test_moe_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  for arm in on off off on; do
+    flag="--defer-wgrad"; [ $arm = off ] && flag="--no-defer-wgrad"
+    run 300 ${O}_$arm.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4 $flag
+    echo "$arm $(grep -h '^{' ${O}_$arm.log | cut -c1-200)"
+  done ;;
+defer-prof)
+  for arm in on off; do
+    flag="--defer-wgrad"; [ $arm = off ] && flag="--no-defer-wgrad"
+    run 400 ${O}_$arm.log rocprofv3 --kernel-trace --stats -d /tmp/${task}_$arm -o run -- python3 bench/dsv3_train.py --preset dsv3_style --steps 2 --warmup 1 --accum 4 $flag
+    python tools/rocpd_summary.py /tmp/${task}_$arm/run_results.db --last-step adamw --top 30 > ${O}_$arm.txt 2>&1
+    head -24 ${O}_$arm.txt | cut -c1-150
+  done ;;
 gemm-pmc)
   run 120 ${O}_bench.log python -u tools/bench_gemm8_dense.py 8192 --iters 20
   cat ${O}_bench.log | grep -v amdgpu.ids

@@ -5,7 +5,7 @@ kernel start to the last kernel end and the sum of kernel time (busy union per q
 whether two streams' kernels ran side by side).
 
   python tools/rocpd_summary.py gpurun_out/<dir>/run_results.db [--top 25] [--grep attn]
-      [--timeline START_MS:DUR_MS] [--comm stream_copy]
+      [--timeline START_MS:DUR_MS] [--comm stream_copy] [--last-step adamw]
 
 --timeline prints every kernel of that window (ms from the first kernel) per stream, with the
 idle gaps; --comm NAME reports how much of the time kernels matching NAME (a collective or its
@@ -114,6 +114,20 @@ def comm_overlap(rows, pat, out=sys.stdout):
           f"({100 * over / max(tot, 1):.1f} %)", file=out)
 
 
+def last_step(rows, pat):
+    marks = sorted(r for r in rows if pat in (r[4] or r[5]))
+    ends, prev = [], None
+    for r in marks:
+        if prev is not None and r[0] - prev > 50e6:
+            ends.append(prev)
+        prev = r[1]
+    ends.append(prev)
+    if len(ends) < 2:
+        return rows
+    lo, hi = ends[-2], ends[-1]
+    return [r for r in rows if r[0] >= lo and r[1] <= hi]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db", nargs="+")
@@ -121,11 +135,16 @@ def main():
     ap.add_argument("--grep", default=None)
     ap.add_argument("--timeline", default=None, help="START_MS:DUR_MS")
     ap.add_argument("--comm", default=None, help="kernel-name substring of the collective kernels")
+    ap.add_argument("--last-step", default=None, metavar="KERNEL",
+                    help="summarise only the last training step: the window between the last two "
+                         "bursts of KERNEL (e.g. adamw), bursts split at gaps > 50 ms")
     a = ap.parse_args()
     for pat in a.db:
         for path in sorted(glob.glob(pat)):
             print(f"== {path}")
             rows = load(path)
+            if a.last_step:
+                rows = last_step(rows, a.last_step)
             summarise(rows, a.top, a.grep)
             if a.comm:
                 comm_overlap(rows, a.comm)
