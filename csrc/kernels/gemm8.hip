@@ -163,7 +163,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   const int wm = wave >> 2, wn = wave & 3;
   const int nnt = (N + BN - 1) / BN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = lid % nnt;
+  int nt = lid % nnt;
   int mt = lid / nnt;
   int e = 0;
   long m0 = 0, mend = M, k0 = 0, kend = K;
@@ -197,6 +197,61 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     e = mt / nmt;
     mt = mt % nmt;
     if (e >= E) return;
+    if constexpr (!PART && ABL != 8) {   // (ABL 8 = the round-2 kernel: expert-major order)
+      // Heavy experts first. Every expert owns the same number of output tiles but a tile's work
+      // is its expert's token count, and routing is rarely balanced: the expert-major order ran a
+      // dsv3_style step's dW at 507 TF (750 on balanced routing) and 400-440 TF at a 9x hot expert
+      // (profiles/r3_gemm8_dw_order_ab.txt). Position pos takes the expert of count rank pos
+      // (descending, ties by index). Block -> pos: with E % 8 == 0 and no expert above twice the
+      // mean, each XCD (block i runs on XCD i % 8) owns E / 8 whole experts -- their tiles share
+      // dY_e / X_e in its L2 -- dealt from the ranking in snake order (ranks 0-7 to XCDs 0-7, 8-15
+      // to 7-0, ...), heaviest first on each; otherwise (a hot expert would pin its XCD) plain
+      // dispatch order, which spreads every expert's tiles over all XCDs. Counts are staged in the
+      // not yet used stage area; the choice is the same in every block.
+      int* cnt = reinterpret_cast<int*>(smem);
+      if (tid < E) {
+        int c = 0;
+        if (SEGS) {
+#pragma unroll
+          for (int q = 0; q < G8_MAXSEG; ++q)
+            if (q < sg.n) c += sg.off[q][tid + 1] - sg.off[q][tid];
+        } else {
+          c = offsets[tid + 1] - offsets[tid];
+        }
+        cnt[tid] = c;
+      }
+      __syncthreads();
+      long tot = 0;
+      int mx = 0;
+      for (int j = 0; j < E; ++j) {
+        tot += cnt[j];
+        mx = max(mx, cnt[j]);
+      }
+      const bool snake = E % 8 == 0 && (long)mx * E <= 2 * tot;
+      const int per_e = nmt * nnt;
+      int pos, r;
+      if (snake) {
+        const int x = blockIdx.x % 8, j = blockIdx.x / 8, u = j / per_e;
+        r = j % per_e;
+        pos = u * 8 + ((u & 1) ? 7 - x : x);
+      } else {
+        pos = blockIdx.x / per_e;
+        r = blockIdx.x % per_e;
+      }
+      nt = r % nnt;
+      mt = r / nnt;
+      if (tid < E) {
+        const int c = cnt[tid];
+        int rank = 0;
+        for (int j = 0; j < E; ++j) {
+          const int cj = cnt[j];
+          rank += (cj > c) || (cj == c && j < tid);
+        }
+        if (rank == pos) scratch[0] = tid;
+      }
+      __syncthreads();
+      e = __builtin_amdgcn_readfirstlane(scratch[0]);
+    }
     m0 = (long)mt * BM;
     Cp = C + e * strideC;
   }

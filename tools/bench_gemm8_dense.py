@@ -62,6 +62,11 @@ if a.ab is not None:
     h = torch.randn(A, F, device=dev, dtype=torch.bfloat16)
     dy13 = torch.randn(A, 2 * F, device=dev, dtype=torch.bfloat16)
     dy2 = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
+    # skewed routing (per-expert logit offsets, as an untrained router produces): a few hot experts
+    idx_s, _ = M.route(torch.randn(T, E, device=dev) + 1.5 * torch.randn(E, device=dev), k)
+    plan_s = M.permute(idx_s, E)
+    cnt = plan_s.counts.float()
+    print(f"skewed routing: max/mean tokens per expert {cnt.max().item() / cnt.mean().item():.2f}", flush=True)
     cases = {"dense mode0": (lambda: ops.grouped_gemm8(xa, wb, off1, 0, None, False), fl),
              "dense mode1": (lambda: ops.grouped_gemm8(xa, wb, off1, 1, None, False), fl),
              "dense mode2": (lambda: ops.grouped_gemm8(xa, xa, off1, 2, None, False), fl),
@@ -70,7 +75,10 @@ if a.ab is not None:
              "dX W13": (lambda: ops.grouped_gemm8(dy13, W13, plan.offsets, 1, None, False), 2 * A * 2 * F * D),
              "dX W2": (lambda: ops.grouped_gemm8(dy2, W2, plan.offsets, 1, None, False), 2 * A * D * F),
              "dW W13": (lambda: ops.grouped_gemm8(dy13, x, plan.offsets, 2, None, False), 2 * A * 2 * F * D),
-             "dW W2": (lambda: ops.grouped_gemm8(dy2, h, plan.offsets, 2, None, False), 2 * A * D * F)}
+             "dW W2": (lambda: ops.grouped_gemm8(dy2, h, plan.offsets, 2, None, False), 2 * A * D * F),
+             "dW W13 skew": (lambda: ops.grouped_gemm8(dy13, x, plan_s.offsets, 2, None, False), 2 * A * 2 * F * D),
+             "dW W2 skew": (lambda: ops.grouped_gemm8(dy2, h, plan_s.offsets, 2, None, False), 2 * A * D * F),
+             "dX W13 skew": (lambda: ops.grouped_gemm8(dy13, W13, plan_s.offsets, 1, None, False), 2 * A * 2 * F * D)}
     for name, (fn, f) in cases.items():
         arm(0); r0 = fn().float()
         arm(a.ab); r1 = fn().float()

@@ -19,6 +19,7 @@
 #   gemm-ab V..    gemm8 default vs SPA_GG8_ABLATE=V (dense 8192^3 + dsv3_style grouped), ABBA
 #   gemm-validate  GEMM/MoE GPU tests, schedule A/B vs the round-2 one, dsv3_style + ViT benches
 #   defer-ab       MoE GPU tests; dsv3_style accum 4 with / without deferred expert Wgrad, ABBA
+#   g8-e2e         dsv3_style (accum 4) and ViT-B/16 with the shipped gemm8 vs the round-2 one, ABBA
 #   gemm-pmc       gemm8 vs hipBLASLt on a dense 8192^3 + one counter pass
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 set -o pipefail
@@ -118,6 +119,22 @@ gemm-validate)
   run 300 ${O}_dsv3a4.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4
   run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
   jsonl ${O}_dsv3a1.log ${O}_dsv3a4.log ${O}_vit.log ;;
+g8-e2e)
+  for arm in new old old new; do
+    if [ $arm = old ]; then export SPA_GG8_ABLATE=8; else unset SPA_GG8_ABLATE; fi
+    run 300 ${O}_d_$arm.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4
+    run 300 ${O}_v_$arm.log python -u bench/vit_train.py --steps 20 --warmup 5
+    echo "$arm $(grep -ho '"value": [0-9.]*' ${O}_d_$arm.log ${O}_v_$arm.log | tr '\n' ' ')"
+  done
+  unset SPA_GG8_ABLATE ;;
+lpt)
+  run 300 ${O}_pytest.log python -u -m pytest tests/test_moe_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 300 ${O}_ab.log python -u tools/bench_gemm8_dense.py 8192 --iters 10 --ab 8
+  grep -v amdgpu.ids ${O}_ab.log
+  run 300 ${O}_a4.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4
+  run 300 ${O}_a1.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
+  jsonl ${O}_a4.log ${O}_a1.log ;;
 defer-ab)
   run 300 ${O}_pytest.log python -u -m pytest tests/test_moe_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
   tail -2 ${O}_pytest.log
