@@ -475,7 +475,9 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     // ABBA vs the previous schedule (tools/bench_gemm8_dense.py --ab 8,
     // profiles/r3_gemm8_schedule2_ab.txt): dense 8192^3 +3-8 %, grouped dX +10-11 %, fwd and dW
     // +1-3 %. Rejected in the same A/B: A0(t+2) also in P4 (12/0 4/1 8/0 0/3: -2..-5 %) and a
-    // second A fragment set with A0(t+1) read in P4 (4/1 4/1 8/1 8/1: -3..-14 %).
+    // second A fragment set with A0(t+1) read in P4 (4/1 4/1 8/1 8/1: -3..-14 %); later A/Bs: the
+    // MFMA clusters without s_setprio(1) -13..-19 %, P1 reading B0 before A0 with an lgkmcnt(8)
+    // before its barrier -1..-2 % (profiles/r3_gemm8_schedule2_ab.txt).
     //   P1 -        P2 A1(t+1)   P3 A0(t+2)   P4 B0(t+2) B1(t+2)
     // Waits: end of P1 retires B1(t) (younger: A1(t) + A0 B0 B1(t+1)), end of P2 A1(t) (younger:
     // A0 B0 B1 A1(t+1)), end of P4 A0, B0(t+1) (younger: B1 A1(t+1) + A0 B0 B1(t+2)).
