@@ -241,3 +241,23 @@ def test_moe_ops_match_dense_loop():
     gr = torch.autograd.grad(ref, [x, logits, W13, W2], gy)
     for a, b in zip(ga, gr):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)
+
+
+def test_defer_expert_wgrad_is_exact_noop_off_gpu():
+    """defer_expert_wgrad() only engages on the GPU kernels (ops/moe.py): on CPU an accumulation
+    loop under it gives bitwise the gradients of the plain loop and leaves nothing pending."""
+    from solvingpapers_amd.ops import moe as M
+    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0, mtp_heads=0)
+    grads = []
+    for defer in (False, True):
+        m = ds.DeepSeekV3(c, seed=0)
+        gen = torch.Generator().manual_seed(1)
+        for i in range(2):
+            ids = torch.randint(0, c.vocab_size, (2, 33), generator=gen)
+            with M.defer_expert_wgrad(defer and i == 0):
+                (m(ids[:, :-1], ids[:, 1:]) / 2).backward()
+        assert not M._Defer.pending and M._Defer.depth == 0
+        grads.append([p.grad.clone() for p in m.parameters() if p.grad is not None])
+    assert len(grads[0]) == len(grads[1])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
