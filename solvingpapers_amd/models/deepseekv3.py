@@ -648,9 +648,24 @@ class DeepSeekV3(tnn.Module):
         pe = None if self.pe is None else self.pe[0, pos:pos + T]
         return embedding(self.embed, ids, pe)
 
+    def _expert_buckets(self):
+        """layer index (main layers, then MTP layers) -> index of its expert bucket in
+        param_groups(); the overlapped optimizer updates those after every dense bucket, so each
+        MoE layer waits for its own before it reads its experts."""
+        eb = getattr(self, "_ebk", None)
+        if eb is None:
+            eb, k = {}, len(self.layers) + 2
+            for j, l in enumerate(list(self.layers) + list(self.mtp_layers)):
+                if l.expert_params():
+                    eb[j] = k
+                    k += 1
+            self._ebk = eb
+        return eb
+
     def hidden(self, ids, caches=None, pos=0):
         c = self.c
         wait = self.param_wait_cb or (lambda i: None)
+        eb = self._expert_buckets() if self.param_wait_cb is not None else {}
         wait(0)
         x = self._embed(ids, pos)
         x0 = x
@@ -659,6 +674,8 @@ class DeepSeekV3(tnn.Module):
         res, delta = None, x
         for i, layer in enumerate(self.layers):
             wait(i + 1)
+            if i in eb:
+                wait(eb[i])
             delta = mark_ready(delta, cb, i + 1)
             if c.attention == "ref":
                 res, delta, L0 = layer.forward_split(res, delta, L0, None if caches is None else caches[0], pos)
@@ -694,9 +711,13 @@ class DeepSeekV3(tnn.Module):
         c = self.c
         B, T, D = h.shape
         tot = 0.0
+        wait = self.param_wait_cb or (lambda i: None)
+        eb = self._expert_buckets() if self.param_wait_cb is not None else {}
         for k, layer in enumerate(self.mtp_layers, start=1):
             if T - k <= 0:
                 break
+            if len(self.layers) + k - 1 in eb:
+                wait(eb[len(self.layers) + k - 1])
             e = layer_norm(emb[:, k:], self.mtp_norm1_w, self.mtp_norm1_b, 1e-6)
             hp = layer_norm(h[:, :T - k], self.mtp_norm2_w, self.mtp_norm2_b, 1e-6)
             hk = linear(torch.cat([e, hp], dim=-1), self.mtp_proj)

@@ -118,6 +118,12 @@ class Trainer:
             raise ValueError(cfg.optimizer)
         for m in getattr(model, "moe_layers", lambda: [])():
             m.balance_group = dp_group
+        # overlapped optimizer: a model that waits for each bucket's update before reading it
+        # (param_wait_cb: LLaMA3, DeepSeek-V3) overlaps it with its next forward; any other model
+        # waits for the whole update right after the step (train_step), never reading stale weights
+        self._overlap_waits = bool(cfg.opt_overlap and hasattr(model, "param_wait_cb"))
+        if self._overlap_waits:
+            model.param_wait_cb = self.flat.wait_bucket
         self.step = 0
         self.bad_steps = 0
         self.history = []
@@ -228,6 +234,8 @@ class Trainer:
         epoch = _WEIGHT_EPOCH[0]
         with annotate("optimizer"):
             self.opt.step(lr=self.lr_at(step), overlap=c.opt_overlap)
+        if c.opt_overlap and not self._overlap_waits:
+            self.flat.wait_all()
         # cached W^T / fp8 weight images are keyed on this epoch (ops/linear.py CONTRACT)
         assert _WEIGHT_EPOCH[0] != epoch, "optimizer step did not invalidate the cached weight images"
         if self.dp is not None:

@@ -261,3 +261,24 @@ def test_defer_expert_wgrad_is_exact_noop_off_gpu():
     assert len(grads[0]) == len(grads[1])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("which", ["dsv3", "llama3"])
+def test_forward_waits_for_every_optimizer_bucket(which):
+    """An overlapped optimizer updates bucket i on a side stream and the model must wait for it
+    (param_wait_cb) before reading bucket i's parameters: one training forward waits for EVERY
+    bucket of param_groups() -- DeepSeek-V3's expert buckets included."""
+    from solvingpapers_amd.models import llama3
+    if which == "dsv3":
+        c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0)
+        m = ds.DeepSeekV3(c, seed=0)
+        V = c.vocab_size
+    else:
+        c = llama3.config("llama3_tiny")
+        m = llama3.Llama3(c)
+        V = c.vocab_size
+    seen = []
+    m.param_wait_cb = seen.append
+    ids = torch.randint(0, V, (2, 17))
+    m(ids[:, :-1], ids[:, 1:])
+    assert sorted(set(seen)) == list(range(len(m.param_groups())))
