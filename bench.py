@@ -128,7 +128,7 @@ def run(a):
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0, shard=shard)
     overlap = cuda and not a.no_opt_overlap and not a.zero1
     if overlap:
-        model.param_wait_cb = flat.wait_bucket
+        model.param_wait_cb = flat.group_waiter(model.param_groups())
 
     gen = torch.Generator(device=dev).manual_seed(1000 + info.rank)
     V, T, B = cfg.vocab_size, a.seq, a.mb

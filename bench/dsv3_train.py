@@ -68,7 +68,7 @@ def main():
                     moment_dtype=torch.bfloat16 if a.bf16_moments else torch.float32)
     overlap = not a.no_opt_overlap and torch.cuda.is_available()
     if overlap:   # AdamW per bucket on a side stream, each layer's forward waits for its bucket
-        m.param_wait_cb = flat.wait_bucket
+        m.param_wait_cb = flat.group_waiter(m.param_groups())
     for l in m.moe_layers():
         l.balance_group = None
     gen = torch.Generator(device=dev).manual_seed(7 + info.rank)

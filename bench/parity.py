@@ -209,8 +209,27 @@ def run_b8(a, dev, dt, name):
     eval_every, warm = max(1, total // 20), max(1, total * 400 // 10000)
     B, T, V = 16, 256, c.vocab_size
     g = torch.Generator(device=dev).manual_seed(0)
-    x = torch.randint(0, V, (B, T), device=dev, generator=g)
-    y = torch.randint(0, V, (B, T), device=dev, generator=g)
+    # a synthetic corpus with a next-token signal (the reference streams TinyStories windows,
+    # deepseekv3.ipynb:715-794); every step takes B fresh windows, x = corpus[i : i+T],
+    # y = corpus[i+1 : i+T+1]
+    n_corpus = 1 << 22
+    noise = torch.rand(n_corpus, device=dev, generator=g) < 0.1
+    draw = torch.randint(0, V, (n_corpus,), device=dev, generator=g)
+    # 1024-token runs of the chain, each from a random start: next = (tok + 48271) mod V (a fixed
+    # bigram map to learn) plus 10 % noise
+    starts = torch.randint(0, V, (n_corpus // 1024, 1), device=dev, generator=g)
+    corpus = ((torch.arange(1024, device=dev) * 48271 + starts) % V).reshape(-1)
+    corpus = torch.where(noise, draw, corpus)
+    del noise, draw, starts
+    x = torch.empty(B, T, dtype=torch.long, device=dev)
+    y = torch.empty(B, T, dtype=torch.long, device=dev)
+    ar = torch.arange(T, device=dev)
+
+    def next_batch():                                      # in place: HIP-graph replays read x / y
+        i = torch.randint(0, n_corpus - T - 1, (B, 1), device=dev, generator=g) + ar
+        x.copy_(corpus[i])
+        y.copy_(corpus[i + 1])
+    next_batch()
     prompt = torch.randint(0, V, (1, 14), device=dev, generator=g)   # the reference prompt's length
     out = {}
 
@@ -231,7 +250,9 @@ def run_b8(a, dev, dt, name):
     for _ in range(a.warmup):
         run()
     ck = tempfile.mkdtemp(prefix="b8_")
-    n_eval = n_tok_gen = 0
+    from solvingpapers_amd.train.checkpoint import save_reference_dsv3
+    n_eval = n_tok_gen = n_ckpt = 0
+    loss0 = None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for it in range(total):
@@ -240,17 +261,22 @@ def run_b8(a, dev, dt, name):
                 m.eval()
                 vl = torch.zeros((), device=dev)
                 for _ in range(100):
-                    x.random_(0, V, generator=g)
+                    next_batch()
                     vl += m(x, y).float()
                 gen = api.topk_sampling(m, prompt, max_length=T, top_k=100, temperature=0.9, generator=g)
                 n_tok_gen += gen.shape[1] - prompt.shape[1]
                 m.train()
             n_eval += 1
         if it % (eval_every * 2) == 0 and it != 0:
-            torch.save({"step": it, "model_state_dict": m.state_dict()}, os.path.join(ck, "ckpt.pt"))
+            # the reference's checkpoint dict (deepseekv3.ipynb:2167-2178): model AND optimizer
+            # state (fp32 master + both moments) and the loss, written to disk every 1,000 steps
+            save_reference_dsv3(os.path.join(ck, "ckpt.pt"), m, it, float(out["loss"]), opt.state_dict())
+            n_ckpt += 1
         opt.set_lr(lr_at(it))
-        x.random_(0, V, generator=g)
+        next_batch()
         run()
+        if it == 0:
+            loss0 = out["loss"].detach().clone()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     tok_s = B * T * total / el
@@ -259,7 +285,9 @@ def run_b8(a, dev, dt, name):
                       "vs_reference": round(tok_s / REF["B8"], 2), "dtype": name, "steps": total,
                       "wall_s": round(el, 2), "evals": f"{n_eval} x 100 val batches + top-k sample",
                       "generated_tokens": n_tok_gen, "hip_graph": a.graph, "n_gpus": 1,
-                      "loss": round(float(out["loss"].detach()), 4), "data": "synthetic ids"}), flush=True)
+                      "checkpoints": f"{n_ckpt} x {{step, model_state_dict, optimizer_state_dict, loss}}",
+                      "first_loss": round(float(loss0), 4), "loss": round(float(out["loss"].detach()), 4),
+                      "data": "synthetic corpus (noisy affine token chain, fresh windows every step)"}), flush=True)
 
 
 def run_b13(a, dev, dt, name):

@@ -138,6 +138,20 @@ __device__ __forceinline__ void chain_sched() {
   __builtin_amdgcn_sched_group_barrier(0x008, AHEAD, 0);
 }
 
+// 32-bit LDS address of a pointer into __shared__ memory (a generic pointer to LDS carries the
+// LDS offset in its low 32 bits), made provably wave-uniform for an "s" asm operand
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)p);
+}
+// 16 B per lane of a buffer straight into LDS (lane i -> lds + 16 i) as inline asm: hipcc neither
+// counts it (the caller's own s_waitcnt vmcnt(N) retires it) nor makes later ds_reads wait vmcnt(0)
+// for it. M0 carries the LDS base and is restored.
+__device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+
 // Register-staged tile loader: ROWS x HDC bf16 tile of a strided tensor -> regs -> LDS image
 // with IW-element rows (IW = img_w<HDC>, >= HDC).
 // Global side: one buffer descriptor per tile (scalar work), its range ending at the

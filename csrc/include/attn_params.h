@@ -27,7 +27,25 @@ struct AttnParams {
   // profiling only (SPA_ATTN_STAMP): per-wave s_memtime segment sums of the dK/dV loop, or null
   long long* stamp;
   int xcd;  // query-parallel kernels: XCD-aware block order (q_block_map)
+  // dS-materialising backward (attn_bwd_dkdv3_kernel<.., DSOUT> -> attn_bwd_dq_ds_kernel): the
+  // bf16 dS of every live 32-query x 32-key block, ds_hstride elements per (b, q-head), block
+  // (qt, kt) at ds_block(); ds_nqt / ds_nkt = 32-row tiles of Tq / Tk
+  bf16* dsbuf;
+  long ds_hstride;
+  int ds_nqt, ds_nkt;
 };
+
+// dS block index inside one (b, q-head): causal (Tq == Tk) keeps the lower triangle incl. the
+// diagonal (kt <= qt), row-major over qt; non-causal every block
+__device__ __forceinline__ long ds_block(int qt, int kt, int nkt, bool causal) {
+  return causal ? (long)qt * (qt + 1) / 2 + kt : (long)qt * nkt + kt;
+}
+// 16-B chunk slot of (producer half s, lane half h, key k) in a 2 KiB dS block: the 8 bf16 of a
+// chunk are the dS of key k for queries 16s + 8(j>>2) + 4h + (j&3), j = 0..7 (the dK/dV kernel's
+// packed-accumulator order). Slot = (k>>2)*16 + (2s+h)*4 + (k&3): every 32-lane half of the
+// consumer's transposed reads (4 keys k>>2-aligned x all (s, h)) then covers 16 distinct slots
+// mod 16 = one whole bank row, conflict-free.
+__device__ __forceinline__ int ds_slot(int s, int h, int k) { return (k >> 2) * 16 + (2 * s + h) * 4 + (k & 3); }
 
 // dK^T / dV^T accumulator (rows d = 32dt + (r&3) + 8(r>>2) + 4hh, column = key) -> global:
 // bf16 (dk scaled) when the block owns all q-heads of its kv-head, else fp32 partials.

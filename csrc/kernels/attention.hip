@@ -960,7 +960,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
 #ifndef DKDV3_SCHED
 #define DKDV3_SCHED 0   // 1: chain_sched hints (no effect at 256 VGPRs: one operand register quad; kept for experiments)
 #endif
-template <int HD, bool CAUSAL>
+// DSOUT: role B also stores the bf16 dS of each live 32 x 32 block to p.dsbuf (ds_slot layout),
+// the operand of the separate dQ = dS K pass (attn_bwd_dq_ds_kernel) that replaces the dq
+// kernel's recomputation of S and dP.
+template <int HD, bool CAUSAL, bool DSOUT = false>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 512, IW = img_w<HD>();
   constexpr int TQ = BMQ * IW, TB = 2 * TQ, PSLOT = 4 * MT * 2 * 64 * 8;
@@ -1112,6 +1115,13 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
       // tile k-1: dP, dS, dK^T
       const bf16* Dpr = Dp;
       const float* rc = rowc[SP];
+      // DSOUT: one scalar buffer descriptor per (b, q-head) and scalar block offsets; the only
+      // per-lane part (the chunk slot) is recomputed at the store (this kernel is at 256 VGPRs)
+      int qtp = 0, hp = 0;
+      if constexpr (DSOUT) {
+        hp = h0 + (k - 1) / nper;
+        qtp = (t0 + (k - 1) % nper) * (BMQ / 32);
+      }
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         f32x16 dp;
@@ -1133,6 +1143,18 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           ds[8 + r] = (float)pb[r] * dp[8 + r];
         }
         const bf16x8 sa = pack_acc(ds, 0), sb = pack_acc(ds, 1);
+        if constexpr (DSOUT) {
+          const int qt = qtp + t, kt = kw0 >> 5;
+          if ((!CAUSAL || kt <= qt) && qt < p.ds_nqt && kt < p.ds_nkt) {
+            const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(p.dsbuf + ((long)b * p.H + hp) * p.ds_hstride), 0, (int)(p.ds_hstride * 2), 0x00020000);
+            const int bo = (int)(ds_block(qt, kt, p.ds_nkt, CAUSAL) * 2048);              // bytes, scalar
+            const int vo = 16 * ds_slot(0, (int)(__lane_id() >> 5), (int)(__lane_id() & 31));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sa), dsr, vo, bo, 0);        // s = 0
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sb), dsr, vo + 128, bo, 0);  // s = 1: slot + 8
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
           acc[dt] = mfma32(ld_tr(Qp + 32 * t * IW, off.tra[dt], off.trb[dt]), sa, acc[dt]);
@@ -1159,6 +1181,157 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
     }
   }
   store_kv_grad<HD>(p, acc, role == 1, b, hk, key, split, hh);
+}
+
+// ---------------------------------------------------------------------------
+// Backward dQ from the materialised dS (after attn_bwd_dkdv3_kernel<HD, CAUSAL, true>):
+//   dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q]
+// One product instead of the dq kernel's three (S = Q K^T, dP = dO V^T recomputed, then dS K), at
+// the price of writing and reading dS once (bf16, 2 KiB per live 32 x 32 block: 2.2 GB at the
+// LLaMA3-8B shape) -- so this pass streams HBM rather than the matrix pipe.
+// Block = 4 waves = 4 (q-head, 64-query) units of one (batch, kv-head): with GQA group G the units
+// run heads fastest (G = 4: the four q-heads of one 64-query block), so the K tile of each 32-key
+// step is staged once for all of them. Per step every wave DMAs its two 2 KiB dS blocks (its
+// 64 queries) and a quarter of the K tile straight into LDS (buffer_load ... lds): 3 slots, two
+// steps in flight, one counted vmcnt + one barrier per step; no vmcnt(0) of hipcc's own (the DMA is inline asm: hipcc's waitcnt pass, which cannot tell the DMA's
+// LDS bytes from the ds_reads', would otherwise drain it before every step's reads). dS^T fragments come out of the ds_slot image with ds_read_b64_tr_b16
+// (conflict-free), K^T fragments out of the swizzled K image (same reads as the dq kernel).
+// Non-live blocks (above the causal diagonal, or a missing unit) are loaded through a zero-range
+// descriptor (zeros, same DMA count per step) and skipped by the MFMAs.
+// ---------------------------------------------------------------------------
+template <int HD, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
+  static_assert(HD == 128, "dq_ds: head dim 128 (K tile = 4 KiB-row images of 256 B)");
+  constexpr int DT = HD / 32, KIMG = 32 * HD, WSLOT = 2 * 1024, SLOT = KIMG + 4 * WSLOT, NSLOT = 3;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSLOT * SLOT];   // [slot][K | 4 waves x 2 dS blocks]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5;
+  const int G = p.H / p.Hkv;
+  const int nq64 = cdiv(p.Tq, 64);
+  const int upkv = nq64 * G;
+  const int wgpkv = cdiv(upkv, 4);
+  const int nbkv = p.B * p.Hkv;
+  const int bkv = blockIdx.x % nbkv;                            // = XCD group when B*Hkv == 8
+  const int w = CAUSAL ? wgpkv - 1 - (int)(blockIdx.x / nbkv) : (int)(blockIdx.x / nbkv);  // heaviest first
+  const int b = bkv / p.Hkv, hk = bkv % p.Hkv;
+  const int u = 4 * w + wave;
+  const bool uvalid = u < upkv;
+  const int qb = uvalid ? u / G : 0;
+  const int h = hk * G + (uvalid ? u % G : 0);
+  // key steps (32 keys) of this wave and of the block (the block's last valid unit is its largest)
+  auto unit_steps = [&](int uu) {
+    const int qbb = uu / G;
+    return CAUSAL ? cdiv(min(p.Tk, qbb * 64 + 64 + p.causal_off), 32) : cdiv(p.Tk, 32);
+  };
+  const int nsteps_w = uvalid ? unit_steps(u) : 0;
+  const int nsteps = unit_steps(min(4 * w + 3, upkv - 1));
+
+  // K tile DMA: wave `wave` fills rows 8*wave .. +7 (two 1 KiB pieces of 4 rows); lane -> row
+  // r = 8*wave + 4j + lane/16, image chunk lane%16 holding source chunk (lane%16) ^ swz(r)
+  const bf16* kbase = p.k + b * p.skb + hk * p.skh;
+  unsigned kvo[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = 8 * wave + 4 * j + (lane >> 4);
+    kvo[j] = (unsigned)(((long)r * p.skt + 8 * ((lane & 15) ^ swz<HD>(r))) * 2);
+  }
+  const bf16* dshead = p.dsbuf + ((long)b * p.H + h) * p.ds_hstride;
+  auto live = [&](int qt, int kt) { return uvalid && qt < p.ds_nqt && (!CAUSAL || kt <= qt); };
+  auto issue = [&](int j, int slot) {
+    bf16* sl = smem + slot * SLOT;
+    const int key0 = 32 * j;
+    const long kbytes = key0 < p.Tk ? ((long)(p.Tk - key0 - 1) * p.skt + HD) * 2 : 0;
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(kbase + (long)key0 * p.skt), 0, (int)min(kbytes, 0x7fffffffL), 0x00020000);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) dma16_asm(rk, kvo[jj], lds_addr(sl + (8 * wave + 4 * jj) * HD));
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int qt = 2 * qb + t;
+      const bool lv = live(qt, j);
+      const bf16* src = lv ? dshead + ds_block(qt, j, p.ds_nkt, CAUSAL) * 1024 : p.dsbuf;
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, lv ? 2048 : 0, 0x00020000);
+      bf16* dst = sl + KIMG + wave * WSLOT + t * 1024;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) dma16_asm(rd, (unsigned)(lane * 16 + jj * 1024), lds_addr(dst + jj * 512));
+    }
+  };
+  LdsOff<HD> off;
+  off.init(lane);
+  // dS^T operand reads (per 16-key k-step s): lane 4q+p of 16-lane group g addresses key
+  // 16s + 4hh + q (+8 for the second read), queries 16(g&1) + 4p .. +3 = half p>>1 of the chunk
+  // (s_p = g&1, h_p = p&1, key)
+  int dso[2];
+  {
+    const int g = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int ab = 0; ab < 2; ++ab) {
+      const int key = 4 * hh + q + 8 * ab;
+      dso[ab] = 8 * ds_slot(g, pp & 1, key) + 4 * (pp >> 1);   // elements; +512 per 16-key step
+    }
+  }
+  f32x16 acc[2][DT];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < DT; ++i) acc[t][i] = splat16(0.f);
+
+  auto compute = [&](int j, const bf16* sl) {
+    if (j >= nsteps_w) return;
+    const bf16* Ks = sl;
+    const bf16* Dw = sl + KIMG + wave * WSLOT;
+    const bool l0 = live(2 * qb, j), l1 = live(2 * qb + 1, j);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 kt[DT];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) kt[dt] = ld_tr(Ks + 16 * s * HD, off.tra[dt], off.trb[dt]);
+      const bf16x8 d0 = ld_tr(Dw + 512 * s, dso[0], dso[1]);          // keys 16s.. = slots 64s..
+      const bf16x8 d1 = ld_tr(Dw + 1024 + 512 * s, dso[0], dso[1]);
+      if (l0) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) acc[0][dt] = mfma32(kt[dt], d0, acc[0][dt]);
+      }
+      if (l1) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) acc[1][dt] = mfma32(kt[dt], d1, acc[1][dt]);
+      }
+    }
+  };
+  if (nsteps > 0) issue(0, 0);
+  if (nsteps > 1) issue(1, 1);
+  for (int j = 0; j < nsteps; j += 3) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int jj = j + r;
+      if (jj < nsteps) {
+        if (jj + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // step jj landed, jj+1 in flight
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step jj-1's LDS reads done before its slot is restaged
+        __builtin_amdgcn_s_barrier();
+        // slot (jj+2)%3 was last read in step jj-1, which every wave finished before this barrier
+        if (jj + 2 < nsteps) issue(jj + 2, (r + 2) % 3);
+        compute(jj, smem + r * SLOT);
+      }
+    }
+  }
+  if (!uvalid) return;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int q = qb * 64 + 32 * t + (lane & 31);
+    if (q >= p.Tq) continue;
+    bf16* op = p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 wv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wv[i] = (bf16)(acc[t][dt][4 * g + i] * p.scale);
+        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * hh) = wv;
+      }
+  }
 }
 
 // sum the q-head-split fp32 partials of ONE tensor (dK with HD = HDK, or dV with HD = HDV)
@@ -1528,7 +1701,8 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
 }
 
 template <int HDK, int HDV, bool DROP>
-static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, int nkv, hipStream_t st) {
+static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, int nkv, hipStream_t st,
+                       const at::TensorOptions& bf16_opts) {
   constexpr int NW = dq_waves<HDK, HDV>();
   constexpr int MT = (HDK <= 128 && HDV <= 128) ? 2 : 1;
   // paired-wave dK/dV keeps half the state per wave at 2 waves/SIMD: spill-free for square
@@ -1544,6 +1718,29 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
       else attn_bwd_dkdv_kernel<HDK, HDV, false, MT, true, false><<<g2, 256, 0, st>>>(p);
       const long n = rows * (HDK / 8);
       attn_dq_store_kernel<HDK><<<(int)std::min<long>((n + 255) / 256, 65536), 256, 0, st>>>(p);
+      return;
+    }
+  }
+  if constexpr (HDK == 128 && HDV == 128 && !DROP) {
+    // dS-materialising backward (default for head dim 128 without a q-head split): delta pass,
+    // dK/dV kernel that also stores dS, then dQ = dS K in one streaming product. SPA_ATTN_DQ_DS=0
+    // (read per call) keeps the dq kernel that recomputes S and dP.
+    const char* de = getenv("SPA_ATTN_DQ_DS");
+    const bool want = !(de && atoi(de) == 0);
+    if (want && p.hsplit == 1 && p.Tk > 0 && dkdv_mode == 0 && (!causal || p.causal_off == 0)) {
+      const long rows = (long)p.B * p.Tq * p.H;
+      attn_delta_kernel<HDK><<<(int)cdiv(rows, 256 / (HDK / 8)), 256, 0, st>>>(p);
+      p.ds_nqt = cdiv(p.Tq, 32);
+      p.ds_nkt = cdiv(p.Tk, 32);
+      p.ds_hstride = 1024L * (causal ? (long)p.ds_nqt * (p.ds_nqt + 1) / 2 : (long)p.ds_nqt * p.ds_nkt);
+      at::Tensor dsb = at::empty({(long)p.B * p.H * p.ds_hstride}, bf16_opts);   // freed (stream-ordered) on return
+      p.dsbuf = (bf16*)dsb.data_ptr();
+      if (causal) attn_bwd_dkdv3_kernel<HDK, true, true><<<nkv, 512, 0, st>>>(p);
+      else attn_bwd_dkdv3_kernel<HDK, false, true><<<nkv, 512, 0, st>>>(p);
+      const int G = p.H / p.Hkv;
+      const int wg = cdiv(cdiv(p.Tq, 64) * G, 4) * p.B * p.Hkv;
+      if (causal) attn_bwd_dq_ds_kernel<HDK, true><<<wg, 256, 0, st>>>(p);
+      else attn_bwd_dq_ds_kernel<HDK, false><<<wg, 256, 0, st>>>(p);
       return;
     }
   }
@@ -1682,9 +1879,9 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   }
   HDKV_SWITCH(HDK, HDV, {
     if (drop) {
-      if constexpr (HDK_ == HDV_) launch_bwd<HDK_, HDV_, true>(p, causal, false, dkdv_mode, nkv, st);
+      if constexpr (HDK_ == HDV_) launch_bwd<HDK_, HDV_, true>(p, causal, false, dkdv_mode, nkv, st, q.options());
     } else {
-      launch_bwd<HDK_, HDV_, false>(p, causal, fused, dkdv_mode, nkv, st);
+      launch_bwd<HDK_, HDV_, false>(p, causal, fused, dkdv_mode, nkv, st, q.options());
     }
   });
   SPA_LAUNCH_CHECK();

@@ -114,6 +114,10 @@ class DSV3Config:
 
 PRESETS = {
     "dsv3_ref": DSV3Config(),
+    # the notebook's stale checkpoint copy (SURVEY D23,
+    # deepseekv3/.ipynb_checkpoints/deepseekv3-checkpoint.ipynb:53-80): block 512, batch 32 and one
+    # MTP head, everything else as dsv3_ref
+    "dsv3_ref_stale": DSV3Config(block_size=512, batch_size=32, mtp_heads=1),
     "dsv3_tiny": DSV3Config(vocab_size=512, block_size=128, dim=256, n_layers=2, n_heads=4, attention="mla",
                             kv_lora_rank=64, qk_nope_dim=32, qk_rope_dim=32, v_head_dim=64, n_experts=8, top_k=2,
                             n_shared=1, expert_hidden=128, n_dense_layers=1, dense_hidden=512, pos_emb="none",
@@ -364,9 +368,6 @@ class MoE(tnn.Module):
         self.ep_group2 = ep_group2 if (self.ep > 1 and sched == "two_stream") else None
         self.ep_chunks = int(ep_chunks) if self.ep > 1 else 1
         self._side = None
-        if self.ep_group2 is not None:
-            from ..utils.grad import set_multi_stream
-            set_multi_stream(True)        # weight-grad commits come from two streams
         assert c.n_experts % self.ep == 0
         El = c.n_experts // self.ep
         D, F = c.dim, c.ffn_hidden
@@ -383,6 +384,9 @@ class MoE(tnn.Module):
         self.register_buffer("routing_bias", torch.zeros(c.n_experts, device=fk.get("device")))
         self.balance_group = None      # DP group for the counts all-reduce (set by the trainer)
         self.last_counts = None
+        if self.ep_group2 is not None:
+            from ..utils.grad import mark_multi_stream
+            mark_multi_stream(self.parameters())     # weight-grad commits come from two streams
 
     @torch.no_grad()
     def reset_parameters(self, std, g):
@@ -649,9 +653,10 @@ class DeepSeekV3(tnn.Module):
         return embedding(self.embed, ids, pe)
 
     def _expert_buckets(self):
-        """layer index (main layers, then MTP layers) -> index of its expert bucket in
-        param_groups(); the overlapped optimizer updates those after every dense bucket, so each
-        MoE layer waits for its own before it reads its experts."""
+        """layer index (main layers, then MTP layers) -> index of its expert group in
+        param_groups() (the index param_wait_cb receives; FlatParams.group_waiter maps it to the
+        bucket that group landed in). The overlapped optimizer updates the expert buckets after
+        every dense bucket, so each MoE layer waits for its own before it reads its experts."""
         eb = getattr(self, "_ebk", None)
         if eb is None:
             eb, k = {}, len(self.layers) + 2

@@ -412,9 +412,6 @@ class Gemma(tnn.Module):
         self.tp_schedule = tp_schedule or os.environ.get("SPA_TP_SCHEDULE", "two_stream")
         assert self.tp_schedule in ("interleave", "two_stream"), self.tp_schedule
         self._side = None
-        if self.tp_group2 is not None and self.tp_schedule == "two_stream":
-            from ..utils.grad import set_multi_stream
-            set_multi_stream(True)        # weight-grad commits come from two streams
         assert c.vocab_size % self.tp == 0
         fk = dict(device=device, dtype=dtype)
         self.embed = tnn.Parameter(torch.empty(c.vocab_size // self.tp, c.dim, **fk))   # vocab-parallel, tied head
@@ -435,6 +432,9 @@ class Gemma(tnn.Module):
             gl = torch.Generator(device=self.embed.device).manual_seed(seed)
             for l in self.layers:
                 l.reset_parameters(gl, self.tp_rank)
+        if self.tp_group2 is not None and self.tp_schedule == "two_stream":
+            from ..utils.grad import mark_multi_stream
+            mark_multi_stream(self.parameters())     # weight-grad commits come from two streams
 
     def param_groups(self):
         return [[self.embed]] + [list(l.parameters()) for l in self.layers] + [[self.norm_f]]

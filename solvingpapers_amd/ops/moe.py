@@ -398,10 +398,10 @@ def defer_expert_wgrad(enabled: bool = True):
 
 
 def _defer_ok(W, dy, xp):
-    from ..utils.grad import _Gen
+    from ..utils.grad import is_multi_stream
     return (DEFER_WGRAD and _gpu(dy) and GG8 and dy.dtype == torch.bfloat16 and xp.dtype == torch.bfloat16
             and W.dtype == torch.bfloat16 and dy.shape[1] % 8 == 0 and xp.shape[1] % 8 == 0
-            and not _Gen.multi_stream and not torch.cuda.is_current_stream_capturing())
+            and not is_multi_stream(W) and not torch.cuda.is_current_stream_capturing())
 
 
 DEFER_WGRAD = os.environ.get("SPA_DEFER_WGRAD", "1") != "0"

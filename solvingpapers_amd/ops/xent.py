@@ -228,12 +228,11 @@ class _ChunkedLinearXent(torch.autograd.Function):
             del lc, G
         if need_h:
             from ..parallel import comm
-            # h is replicated over TP: sum the vocab partials -- in h's dtype (bf16 on the wire,
-            # half the bytes of the fp32 accumulator; each partial is already fp32-accumulated)
-            dh = dh.to(h2.dtype)
+            # h is replicated over TP: sum the fp32 vocab partials, then round once (a bf16 sum
+            # would round every rank's partial before adding them)
             if ctx.reduce_dh and comm.group_rank_size(group)[1] > 1:
                 comm.all_reduce(dh, group)
-            dh = dh.view(ctx.hshape)
+            dh = dh.to(h2.dtype).view(ctx.hshape)
         if need_b:
             gb = commit_tensor(b, gb.to(b.dtype))
         return dh, gw, gb, None, None, None, None, None, None

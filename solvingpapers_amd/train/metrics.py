@@ -3,7 +3,7 @@
 The DeepSeek notebook logs ``{train_loss, train_perplexity, lr, grad_norm, tokens, step}``
 per step and ``{val_loss, val_perplexity}`` per eval to Weights & Biases
 (deepseekv3/deepseekv3.ipynb:2323-2336, 2380, 2451-2458). The Trainer's records are
-``{step, loss, lr, grad_norm, tok_per_s, ...}`` / ``{step, val_loss}``; ``reference_names``
+``{step, loss, lr, grad_norm, tok_per_s, tokens, mfu, mem_gb, ...}`` / ``{step, val_loss}``; ``reference_names``
 maps one to the other. ``WandbHook`` forwards them to wandb when that package exists
 (it is not installed here: constructing the hook then raises, nothing is silently dropped);
 ``JsonlHook`` writes the same renamed records to a file, for offline dashboards.
@@ -24,11 +24,13 @@ def reference_names(rec: dict, tokens_per_step: Optional[int] = None) -> dict:
     if rec.get("val_loss") is not None:
         out["val_loss"] = float(rec["val_loss"])
         out["val_perplexity"] = math.exp(min(float(rec["val_loss"]), 80.0))
-    for k in ("lr", "grad_norm", "tok_per_s"):
+    for k in ("lr", "grad_norm", "tok_per_s", "mfu", "mem_gb"):
         if rec.get(k) is not None:
             out[k] = float(rec[k])
     if tokens_per_step is not None:
         out["tokens"] = (rec["step"] + 1) * tokens_per_step
+    elif rec.get("tokens") is not None:            # the Trainer's own cumulative count
+        out["tokens"] = int(rec["tokens"])
     return out
 
 

@@ -63,6 +63,10 @@ class TrainConfig:
     zero1: bool = False
     opt_overlap: bool = False
     tokens_per_sample: int = 0           # for tok/s (0 -> x.numel())
+    # MFU in the metrics record: model FLOPs per token (0 -> model.flops_per_token(seq_len) when the
+    # model has it) against this per-GPU peak (MI355X dense bf16)
+    flops_per_token: float = 0.0
+    peak_flops: float = 2.5e15
     profile_steps: tuple = ()            # (start, stop) -> torch.profiler trace into ckpt_dir/log dir
     grad_dtype: Optional[torch.dtype] = None
     param_dtype: Optional[torch.dtype] = None
@@ -123,18 +127,31 @@ class Trainer:
         # waits for the whole update right after the step (train_step), never reading stale weights
         self._overlap_waits = bool(cfg.opt_overlap and hasattr(model, "param_wait_cb"))
         if self._overlap_waits:
-            model.param_wait_cb = self.flat.wait_bucket
+            model.param_wait_cb = self.flat.group_waiter(pgroups) if pgroups else self.flat.wait_bucket
         self.step = 0
+        self.tokens_seen = 0     # cumulative training tokens over all DP ranks (the reference logs "tokens")
         self.bad_steps = 0
         self.history = []
         self.hooks = list(hooks)
         self._pending = []      # per-step device values awaiting one batched host read
+        self._last_seq = 0
         self._log = None
         if cfg.log_path and self.rank == 0:
             os.makedirs(os.path.dirname(os.path.abspath(cfg.log_path)), exist_ok=True)
             self._log = open(cfg.log_path, "a")
 
     # ------------------------------------------------------------------ utils
+    def _flops_per_token(self, seq):
+        if self.cfg.flops_per_token:
+            return self.cfg.flops_per_token
+        f = getattr(self.model, "flops_per_token", None)
+        if f is None or not seq:
+            return 0.0
+        try:
+            return float(f(seq))
+        except TypeError:
+            return 0.0
+
     def lr_at(self, step):
         c = self.cfg
         if c.min_lr is None:
@@ -158,7 +175,7 @@ class Trainer:
             return None
         self.flat.wait_all()
         # saved step = index of the last completed step; resume continues at step + 1
-        extra = {"loss": loss, "config": {k: str(v) for k, v in asdict(self.cfg).items()}}
+        extra = {"loss": loss, "tokens": self.tokens_seen, "config": {k: str(v) for k, v in asdict(self.cfg).items()}}
         if self.groups is not None:
             extra["layout"] = self.groups.layout()
         return ckpt.save(self.cfg.ckpt_dir, self.step - 1, self.flat, self.opt, self.buffers(), extra=extra,
@@ -176,6 +193,8 @@ class Trainer:
         if self.groups is not None and saved is not None and saved != self.groups.layout():
             raise RuntimeError(f"checkpoint layout {saved} != running layout {self.groups.layout()}")
         self.step = info["step"] + 1
+        if isinstance(info.get("extra"), dict):
+            self.tokens_seen = int(info["extra"].get("tokens") or 0)
         return True
 
     # ------------------------------------------------------------------ eval
@@ -215,6 +234,7 @@ class Trainer:
         for mi in range(c.grad_accum):
             x, y = self.train_batch(step * c.grad_accum + mi)
             ntok += c.tokens_per_sample * x.shape[0] if c.tokens_per_sample else x.numel()
+            self._last_seq = x.shape[1] if x.dim() > 1 else 1
             last = mi == c.grad_accum - 1
             ctx = self.dp.no_sync() if (self.dp is not None and not last) else _null()
             with ctx, defer_expert_wgrad(c.defer_expert_wgrad and not last):
@@ -234,7 +254,9 @@ class Trainer:
         epoch = _WEIGHT_EPOCH[0]
         with annotate("optimizer"):
             self.opt.step(lr=self.lr_at(step), overlap=c.opt_overlap)
-        if c.opt_overlap and not self._overlap_waits:
+        if c.opt_overlap and (not self._overlap_waits or (self.dp is not None and c.zero1)):
+            # models without per-bucket waits, and ZeRO-1: gather_params() below clones this rank's
+            # shard on the main stream, so the side-stream update of that shard must be complete
             self.flat.wait_all()
         # cached W^T / fp8 weight images are keyed on this epoch (ops/linear.py CONTRACT)
         assert _WEIGHT_EPOCH[0] != epoch, "optimizer step did not invalidate the cached weight images"
@@ -263,9 +285,17 @@ class Trainer:
                 else:
                     dt = r["dt"]
                 gn = r["gn"]
+                tps = r["ntok"] * self.dp_size / max(dt, 1e-9)
                 rec = {"step": r["step"], "loss": float(r["loss"]) if ok else float("nan"), "lr": r["lr"],
-                       "ok": ok, "dt": dt, "tok_per_s": r["ntok"] * self.dp_size / max(dt, 1e-9),
+                       "ok": ok, "dt": dt, "tok_per_s": tps, "tokens": r["tokens"],
                        "grad_norm": float(gn) if gn is not None else None}
+                fpt = self._flops_per_token(r["seq"])
+                if fpt:
+                    # per-GPU model FLOP/s over the peak; tok/s is over the DP ranks, each of which
+                    # holds 1/(tp*ep...) of the model work for its tokens: divide by the world size
+                    rec["mfu"] = tps * fpt / max(1, self.world) / self.cfg.peak_flops
+                if dev.type == "cuda":
+                    rec["mem_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9
                 self.log(rec)
             if self.bad_steps >= self.cfg.max_bad_steps:
                 self._pending.clear()
@@ -299,7 +329,9 @@ class Trainer:
                 prof.stop()
                 prof = None
             gn = self.opt.last_grad_norm
+            self.tokens_seen += ntok * self.dp_size
             self._pending.append({"step": s, "loss": loss, "ok": ok, "gn": gn, "lr": self.lr_at(s), "ntok": ntok,
+                                  "tokens": self.tokens_seen, "seq": self._last_seq,
                                   "ev0": ev0, "ev": ev, "dt": time.perf_counter() - t0,
                                   "log": s % c.log_every == 0 or s == c.steps - 1})
             evals = c.eval_every and ((s % c.eval_every == 0 and s) or s == c.steps - 1)

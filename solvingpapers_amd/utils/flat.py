@@ -127,6 +127,23 @@ class FlatParams:
             for idx in list(r):
                 self.wait_bucket(idx)
 
+    def group_waiter(self, groups: Sequence[Sequence[torch.nn.Parameter]]) -> Callable[[int], None]:
+        """``wait(i)`` for a model that numbers its waits by its param_groups() index i: waits for
+        the bucket that holds group i's parameters. FlatParams drops empty / frozen groups and
+        appends a trailing bucket for unlisted params, so group index != bucket index in general;
+        the map is taken from where each group's parameters actually landed."""
+        table = []
+        for g in groups:
+            bs = sorted({self.bucket_of(p).index for p in g if id(p) in self.offsets})
+            table.append(bs)
+
+        def wait(i: int):
+            if 0 <= i < len(table):
+                for b in table[i]:
+                    self.wait_bucket(b)
+        wait.table = table
+        return wait
+
     def bucket_of(self, p) -> Bucket:
         o = self.offsets[id(p)]
         for b in self.buckets:

@@ -16,9 +16,6 @@ import torch
 
 class _Gen:
     value = 0
-    # > 0 while a model runs its backward on more than one compute stream (tensor-parallel
-    # chunk pipelining, models/gemma.py): weight-gradient commits are then ordered across streams
-    multi_stream = 0
 
 
 def next_generation():
@@ -26,13 +23,20 @@ def next_generation():
     _Gen.value += 1
 
 
-def set_multi_stream(on: bool):
-    """Enter / leave multi-stream mode: every commit to a param waits for the previous commit
-    to it (an event recorded on the stream that made it) when that came from another stream,
-    so the first-writer-overwrites / later-writers-accumulate order decided on the host is the
-    order the device applies. The direct-write shortcuts (direct_out, claim_main_grad) are off
-    in this mode: their writes happen after they return, outside the ordering."""
-    _Gen.multi_stream += 1 if on else -1
+def mark_multi_stream(params):
+    """Put these parameters in multi-stream mode: their model runs its backward on more than one
+    compute stream (tensor- / expert-parallel chunk pipelining), so every commit to one of them
+    waits for the previous commit to it (an event recorded on the stream that made it) when that
+    came from another stream -- the first-writer-overwrites / later-writers-accumulate order
+    decided on the host is the order the device applies. The direct-write shortcuts (direct_out,
+    claim_main_grad, deferred expert Wgrad) are off for them: their writes happen after they
+    return, outside the ordering. Per parameter, so other models in the process keep them."""
+    for p in params:
+        p._spa_multi = True
+
+
+def is_multi_stream(p) -> bool:
+    return getattr(p, "_spa_multi", False)
 
 
 _SIDE_STREAMS: list = []
@@ -54,7 +58,7 @@ def wait_side_streams():
 
 
 def _order_before(p, t):
-    if not _Gen.multi_stream or not t.is_cuda:
+    if not is_multi_stream(p) or not t.is_cuda:
         return None
     cur = torch.cuda.current_stream(t.device)
     ev = getattr(p, "_spa_ev", None)
@@ -97,7 +101,7 @@ def direct_out(p: torch.Tensor):
     straight into it (no temporary + copy). Returns None otherwise."""
     mg = getattr(p, "main_grad", None)
     if mg is None or getattr(p, "_spa_gen", -1) == _Gen.value or mg.dtype != p.dtype or not mg.is_contiguous() \
-            or _Gen.multi_stream:
+            or is_multi_stream(p):
         return None
     p._spa_gen = _Gen.value
     return mg
@@ -108,7 +112,7 @@ def claim_main_grad(p: torch.Tensor):
     ``(main_grad, accumulate)`` -- accumulate is False on the first commit of this iteration --
     and marks the commit, or None when ``p`` has no contiguous main_grad of its own dtype."""
     mg = getattr(p, "main_grad", None)
-    if mg is None or mg.dtype != p.dtype or not mg.is_contiguous() or _Gen.multi_stream:
+    if mg is None or mg.dtype != p.dtype or not mg.is_contiguous() or is_multi_stream(p):
         return None
     accumulate = getattr(p, "_spa_gen", -1) == _Gen.value
     p._spa_gen = _Gen.value

@@ -282,3 +282,33 @@ def test_forward_waits_for_every_optimizer_bucket(which):
     ids = torch.randint(0, V, (2, 17))
     m(ids[:, :-1], ids[:, 1:])
     assert sorted(set(seen)) == list(range(len(m.param_groups())))
+    # ...and through FlatParams.group_waiter every BUCKET is waited for, also when a frozen group
+    # vanishes from the buckets (group index != bucket index)
+    from solvingpapers_amd.utils.flat import FlatParams
+    groups = m.param_groups()
+    for p in groups[1]:
+        p.requires_grad_(False)
+    flat = FlatParams(m, groups=groups, hook_autograd=False)
+    waited = []
+    flat.wait_bucket = waited.append
+    m.param_wait_cb = flat.group_waiter(groups)
+    m(ids[:, :-1], ids[:, 1:])
+    assert sorted(set(waited)) == [b.index for b in flat.buckets]
+
+
+def test_stale_checkpoint_preset():
+    """dsv3_ref_stale = the notebook's .ipynb_checkpoints copy (block 512, batch 32, one MTP head;
+    deepseekv3/.ipynb_checkpoints/deepseekv3-checkpoint.ipynb:53-80); a shrunken copy trains one
+    step through the MTP path."""
+    c = ds.config("dsv3_ref_stale")
+    ref = ds.config("dsv3_ref")
+    assert (c.block_size, c.batch_size, c.mtp_heads) == (512, 32, 1)
+    assert (c.dim, c.n_layers, c.n_heads, c.n_experts, c.top_k, c.latent_dim) == \
+        (ref.dim, ref.n_layers, ref.n_heads, ref.n_experts, ref.top_k, ref.latent_dim)
+    m = ds.DeepSeekV3(ds.config("dsv3_ref_stale", vocab_size=97, block_size=24, dim=64, n_layers=2, n_heads=4,
+                                latent_dim=16, n_experts=4), seed=0)
+    ids = torch.randint(0, 97, (2, 25))
+    loss = m(ids[:, :-1], ids[:, 1:])
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert m.mtp_proj.grad is not None and torch.isfinite(m.mtp_proj.grad).all()   # the MTP head trained

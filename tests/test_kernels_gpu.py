@@ -374,6 +374,44 @@ def test_flash_attention(B, Tq, Tk, H, Hkv, hd, causal):
     assert rel(v.grad, vf.grad) < 3e-2, rel(v.grad, vf.grad)
 
 
+@pytest.mark.parametrize("B,T,H,Hkv,causal", [
+    (1, 1024, 8, 8, True),     # MHA: 4 q-blocks per dq_ds block
+    (2, 200, 8, 2, True),      # GQA 4, ragged tail (not a multiple of 32 / 64)
+    (1, 300, 4, 4, False),     # non-causal, ragged
+    (1, 512, 16, 2, True),     # GQA 8: two blocks per 64-query block
+    (1, 96, 6, 3, True),       # GQA 2
+    (1, 2048, 32, 8, True),    # LLaMA3-8B head layout
+])
+def test_attn_bwd_ds_path(B, T, H, Hkv, causal, monkeypatch):
+    """Head dim 128 backward through the materialised dS (dK/dV kernel stores dS, dQ = dS K in a
+    separate streaming pass; the default) == the dq kernel that recomputes S and dP
+    (SPA_ATTN_DQ_DS=0), and both track the fp32 reference."""
+    from solvingpapers_amd.ops import _ext
+    torch.manual_seed(3)
+    hd = 128
+    q = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, T, Hkv, hd, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, T, Hkv, hd, device=DEV, dtype=torch.bfloat16)
+    sc = 1 / math.sqrt(hd)
+    out, lse = _ext.ops().attn_fwd(q, k, v, sc, causal)
+    do = torch.randn_like(out)
+    grads = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SPA_ATTN_DQ_DS", mode)
+        dq, dk, dv = torch.full_like(q, float("nan")), torch.empty_like(k), torch.empty_like(v)
+        _ext.ops().attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal)
+        torch.cuda.synchronize()
+        grads[mode] = (dq, dk, dv)
+    for a, b in zip(grads["1"], grads["0"]):
+        assert torch.isfinite(a).all()
+        assert rel(a, b) < 1e-2, rel(a, b)     # same bf16 dS and fp32 sums, different order
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention(qf, kf, vf, causal)
+    of.backward(do.float())
+    for a, r in zip(grads["1"], (qf.grad, kf.grad, vf.grad)):
+        assert rel(a, r) < 3e-2, rel(a, r)
+
+
 @pytest.mark.parametrize("Hkv,dqk,dv", [(4, 192, 128), (1, 96, 64), (2, 128, 64)])
 def test_flash_attention_mixed_head_dims(Hkv, dqk, dv):
     """Mixed q/k vs v head dims: (192, 128) is the MLA shape (q/k 128 nope + 64 rope, v 128) and

@@ -72,7 +72,7 @@ def test_optimizer_overlap_bitwise_equal():
         flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
         opt = FlatAdamW(flat, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
         if overlap:
-            m.param_wait_cb = flat.wait_bucket
+            m.param_wait_cb = flat.group_waiter(m.param_groups())
         g = torch.Generator(device="cuda").manual_seed(5)
         for _ in range(4):
             ids = torch.randint(0, c.vocab_size, (2, 129), device="cuda", generator=g)

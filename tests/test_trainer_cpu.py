@@ -34,6 +34,22 @@ def test_trainer_reduces_loss_and_logs(tmp_path):
     assert losses[-1] < losses[0] * 0.6
     recs = [json.loads(l) for l in open(log)]
     assert any("val_loss" in r for r in recs) and all("lr" in r for r in recs if "loss" in r)
+    steps = [r for r in recs if "loss" in r]
+    # cumulative tokens (B 4 x T 16 per step), as the reference logs them
+    assert [r["tokens"] for r in steps] == [64 * (r["step"] + 1) for r in steps]
+
+
+def test_trainer_logs_mfu_from_model_flops(tmp_path):
+    """A model with flops_per_token(T) gets an MFU figure per record (per-GPU model FLOP/s over
+    TrainConfig.peak_flops); an explicit flops_per_token overrides it."""
+    m = _gpt()
+    m.flops_per_token = lambda T: 1e6 * T
+    tr = Trainer(m, TrainConfig(steps=2, lr=1e-3, peak_flops=1e9), _batches())
+    hist = tr.fit()
+    for r in hist:
+        assert r["mfu"] == pytest.approx(r["tok_per_s"] * 16e6 / 1e9)
+    tr2 = Trainer(_gpt(), TrainConfig(steps=1, lr=1e-3, peak_flops=1e9, flops_per_token=5e5), _batches())
+    assert tr2.fit()[0]["mfu"] == pytest.approx(tr2.history[0]["tok_per_s"] * 5e5 / 1e9)
 
 
 def test_resume_is_bit_exact(tmp_path):
@@ -49,6 +65,7 @@ def test_resume_is_bit_exact(tmp_path):
     second = Trainer(_gpt(), TrainConfig(**cfg), _batches())
     second.fit()
     assert second.history[0]["step"] == 3
+    assert second.history[-1]["tokens"] == straight.history[-1]["tokens"]    # restored from the checkpoint
     assert torch.equal(second.flat.param, straight.flat.param)
     assert torch.equal(second.opt.m, straight.opt.m)
 

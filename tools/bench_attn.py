@@ -17,20 +17,29 @@ ap.add_argument("--hdv", type=int, default=0, help="v head dim (default = hd); 1
 ap.add_argument("--pad", type=int, default=0, help="also time the same problem zero-padded to this head dim")
 ap.add_argument("--dropout", type=float, default=0.0)
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--packed", action="store_true", help="q/k/v as views of one fused qkv buffer (the model's layout)")
 ap.add_argument("--ab", default="")
+ap.add_argument("--interleave", action="store_true",
+                help="also time each pass right after a LLaMA-8B w13-sized GEMM (the in-step order: "
+                     "the GEMM's power draw sets the clock the attention kernel starts at)")
 a = ap.parse_args()
 ops = _ext.ops()
 B, T, H, Hkv, hd = a.B, a.T, a.H, a.Hkv, a.hd
 hdv = a.hdv or hd
 causal = not a.noncausal
-q = torch.randn(B, T, H, hd, device="cuda", dtype=torch.bfloat16)
-k = torch.randn(B, T, Hkv, hd, device="cuda", dtype=torch.bfloat16)
-v = torch.randn(B, T, Hkv, hdv, device="cuda", dtype=torch.bfloat16)
+if a.packed:      # the model's layout: q / k / v are head slices of one fused [B, T, H + 2 Hkv, hd] buffer
+    assert hdv == hd
+    qkv = torch.randn(B, T, H + 2 * Hkv, hd, device="cuda", dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, :H], qkv[:, :, H:H + Hkv], qkv[:, :, H + Hkv:]
+else:
+    q = torch.randn(B, T, H, hd, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, T, Hkv, hd, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, T, Hkv, hdv, device="cuda", dtype=torch.bfloat16)
 sc = 1 / math.sqrt(hd)
 P, SEED = a.dropout, 1234
 out, lse = ops.attn_fwd(q, k, v, sc, causal, P, SEED)
 do = torch.randn_like(out)
-dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+dq, dk, dv = (torch.empty(t.shape, device="cuda", dtype=t.dtype) for t in (q, k, v))
 def t(fn):
     # warm for >= 0.3 s first: the clock ramps over the first ~0.1 s of load, and a short warmup
     # made the first reading of a process ~15 % slow (0.62 vs 0.52 ms fwd at the LLaMA shape)
@@ -49,6 +58,23 @@ tf = t(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
 tb = t(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
 print(f"attn B{B} T{T} H{H}/{Hkv} hd{hd}/{hdv} causal={causal} p={P}: fwd {tf*1e3:.3f} ms {fl/tf/1e12:.0f} TF | "
       f"bwd {tb*1e3:.3f} ms {flb/tb/1e12:.0f} TF", flush=True)
+if a.interleave:
+    xg = torch.randn(B * T, 4096, device="cuda", dtype=torch.bfloat16)
+    wg = torch.randn(4096, 14336, device="cuda", dtype=torch.bfloat16)
+    def ti(fn):
+        """mean time of fn alone when each call follows a GEMM on the same stream (events bracket fn only)"""
+        e0 = [torch.cuda.Event(enable_timing=True) for _ in range(a.iters)]
+        e1 = [torch.cuda.Event(enable_timing=True) for _ in range(a.iters)]
+        for _ in range(8): xg @ wg; fn()
+        for i in range(a.iters):
+            xg @ wg
+            e0[i].record(); fn(); e1[i].record()
+        torch.cuda.synchronize()
+        return sum(x.elapsed_time(y) for x, y in zip(e0, e1)) / a.iters / 1e3
+    tfi = ti(lambda: ops.attn_fwd(q, k, v, sc, causal, P, SEED))
+    tbi = ti(lambda: ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal, P, SEED))
+    print(f"   after a GEMM each: fwd {tfi*1e3:.3f} ms {fl/tfi/1e12:.0f} TF | bwd {tbi*1e3:.3f} ms {flb/tbi/1e12:.0f} TF",
+          flush=True)
 if a.pad:
     pad = lambda x: torch.nn.functional.pad(x, (0, a.pad - x.shape[-1]))
     qp, kp, vp = pad(q), pad(k), pad(v)

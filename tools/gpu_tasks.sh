@@ -21,6 +21,9 @@
 #   defer-ab       MoE GPU tests; dsv3_style accum 4 with / without deferred expert Wgrad, ABBA
 #   g8-e2e         dsv3_style (accum 4) and ViT-B/16 with the shipped gemm8 vs the round-2 one, ABBA
 #   gemm-pmc       gemm8 vs hipBLASLt on a dense 8192^3 + one counter pass
+#   attn-ds        dS-materialising backward: GPU tests, attention ABBA vs the dq kernel, headline bench
+#   headline-ab ENV  bench.py default vs ENV=VAL, separate processes in ABBA order
+#   attn-pmc       attention counters + clocks in the headline step (4 layers) and in isolation; GEMM-interleaved timing
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -91,6 +94,31 @@ parity)
 overlap)
   run 400 ${O}.log python -u tools/overlap_proxy.py --layers 2
   grep -v amdgpu.ids ${O}.log | cut -c1-900 ;;
+attn-ds)
+  run 300 ${O}_pytest.log python -u -m pytest tests/test_kernels_gpu.py -k "ds_path or flash" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 200 ${O}_ab.log python -u tools/bench_attn.py --iters 20 --interleave --ab SPA_ATTN_DQ_DS=0
+  grep -h 'attn B\|after a GEMM\|with SPA' ${O}_ab.log | cut -c1-300
+  run 400 ${O}_bench.log python -u bench.py --steps 6 --warmup 2
+  jsonl ${O}_bench.log ;;
+headline-ab)
+  # headline bench.py A/B of one env switch, separate processes in ABBA order: headline-ab SPA_X=v
+  ab=${1:?SPA_X=v}
+  for arm in base var var base; do
+    if [ $arm = var ]; then run 400 ${O}_$arm.log env $ab python -u bench.py --steps 6 --warmup 2
+    else run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2; fi
+    echo "$arm $ab $(grep -ho '"value": [0-9.]*' ${O}_$arm.log)"
+  done ;;
+attn-pmc)
+  run 200 ${O}_il.log python -u tools/bench_attn.py --iters 20 --interleave
+  grep -h 'attn B\|after a GEMM' ${O}_il.log
+  C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY GRBM_GUI_ACTIVE"
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $C -d ${O}_a -o run --output-format csv -- python3 bench.py --layers 4 --steps 1 --warmup 1 > ${O}_a.log 2>&1 || { tail -5 ${O}_a.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $C -d ${O}_b -o run --output-format csv -- python3 tools/bench_attn.py --iters 3 > ${O}_b.log 2>&1 || { tail -5 ${O}_b.log; exit 2; }
+  { echo "== in situ (bench.py --layers 4)"; python tools/pmc_summary.py "$(find ${O}_a -name '*counter_collection.csv' | head -1)" attn Cijk;
+    echo "== isolated (tools/bench_attn.py)"; python tools/pmc_summary.py "$(find ${O}_b -name '*counter_collection.csv' | head -1)" attn; } > ${O}.txt 2>&1
+  rm -rf ${O}_a ${O}_b
+  cut -c1-250 ${O}.txt ;;
 secondary)
   run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
   run 300 ${O}_dsv3s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2

@@ -10,6 +10,7 @@ def main():
     path, keys = sys.argv[1], sys.argv[2:]
     acc = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
+    dur = defaultdict(dict)   # name -> dispatch -> ns (counter rows carry the dispatch's timestamps)
     for r in csv.DictReader(open(path)):
         name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
         if keys and not any(k in name for k in keys):
@@ -17,6 +18,8 @@ def main():
         cid = r.get("Dispatch_Id") or r.get("Correlation_Id") or ""
         acc[name][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[name].add(cid)
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            dur[name][cid] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     for name, c in sorted(acc.items(), key=lambda x: -x[1].get("SQ_WAVE_CYCLES", 0)):
         n = max(1, len(disp[name]))
         m = {k: v / n for k, v in c.items()}
@@ -29,6 +32,11 @@ def main():
                 # SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed over SIMDs; SQ_BUSY_CYCLES per SE
                 extra += f"  MFMA-busy/SQ-busy {m.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / m['SQ_BUSY_CYCLES']:.2f}"
             print(extra)
+        if dur[name] and m.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: /8 / duration = the clock the dispatch ran at
+            # (meaningful for dispatches >> launch overhead, e.g. the 8192^3 hipBLASLt GEMM: 1.87 GHz)
+            t = sum(dur[name].values()) / len(dur[name])
+            print(f"   mean duration {t / 1e3:.1f} us  clock {m['GRBM_GUI_ACTIVE'] / 8 / t:.2f} GHz")
 
 
 if __name__ == "__main__":
