@@ -12,7 +12,6 @@ import torch
 
 from common import PEAK_BF16, report, sdist, timed
 from solvingpapers_amd.models import deepseekv3 as ds
-from solvingpapers_amd.ops.moe import defer_expert_wgrad
 from solvingpapers_amd.parallel.data_parallel import DataParallel
 from solvingpapers_amd.train.optim import FlatAdamW
 from solvingpapers_amd.utils.flat import FlatParams
@@ -39,12 +38,9 @@ def main():
                     help="AdamW moments in bf16 (DeepSeek-V3 sec. 3.3.2; fp32 master weights kept; default)")
     ap.add_argument("--fp32-moments", dest="bf16_moments", action="store_false", help="AdamW moments in fp32")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
-    ap.add_argument("--defer-wgrad", dest="defer", action="store_true",
-                    help="with --accum > 1: defer the routed experts' weight gradients to the last micro-batch "
-                         "(one long-K grouped GEMM per weight, ops/moe.py defer_expert_wgrad)")
-    ap.add_argument("--no-defer-wgrad", dest="defer", action="store_false")
-    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="no two-chunk EP pipeline (default: token halves on two streams / communicators)")
+    ap.add_argument("--no-pair", dest="pair", action="store_false",
+                    help="with --accum even: run the micro-batches one by one instead of in layer-interleaved "
+                         "pairs (DeepSeekV3.forward_pair: each EP all-to-all overlaps the other micro-batch)")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
@@ -60,8 +56,8 @@ def main():
         kw["fp8_linears"] = not a.fp8_experts_only
     c = ds.config(a.preset, **kw)
     ep = torch.distributed.group.WORLD if world > 1 else None
-    ep2 = torch.distributed.new_group(list(range(world))) if (world > 1 and a.pipeline) else None
-    m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep, ep_group2=ep2)
+    m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep)
+    pair = a.pair and a.accum % 2 == 0
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16, align=64 * world)
     dp = DataParallel(m, flat) if world > 1 else None
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, ep_group=ep,
@@ -77,17 +73,20 @@ def main():
 
     def step():
         opt.zero_grad()
-        for i in range(a.accum):
-            t = torch.randint(0, c.vocab_size, (B, T + 1), device=dev, generator=gen)
-            inner = dp is not None and i < a.accum - 1
-            with (dp.no_sync() if inner else contextlib.nullcontext()), \
-                    defer_expert_wgrad(a.defer and i < a.accum - 1):
-                loss = m(t[:, :-1], t[:, 1:]) / a.accum
+        n = 2 if pair else 1
+        for i in range(0, a.accum, n):
+            t = [torch.randint(0, c.vocab_size, (B, T + 1), device=dev, generator=gen) for _ in range(n)]
+            inner = dp is not None and i + n < a.accum
+            with dp.no_sync() if inner else contextlib.nullcontext():
+                if pair:
+                    loss = m.forward_pair(t[0][:, :-1], t[0][:, 1:], t[1][:, :-1], t[1][:, 1:]) / a.accum
+                else:
+                    loss = m(t[0][:, :-1], t[0][:, 1:]) / a.accum
                 loss.backward()
         if dp is not None:
             dp.finish_grad_sync()
         opt.step(overlap=overlap)
-        last[0] = loss * a.accum
+        last[0] = loss * a.accum / (2 if pair else 1)
 
     el = timed(step, a.steps, a.warmup)
     tok_s = world * B * T * a.accum * a.steps / el
@@ -95,8 +94,8 @@ def main():
     report("training tokens/sec, DeepSeek-V3-style MLA+MoE " + ("fp8 (e4m3 block-scaled GEMMs)" if a.fp8 else "bf16"),
            tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
-            + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum, "deferred_expert_wgrad": a.defer and a.accum > 1, "adam_moments": "bf16" if a.bf16_moments else "fp32",
-            "parallelism": (f"ep{world}-dp{world}" + ("-pipe2" if ep2 is not None else "")) if world > 1 else "1gpu",
+            + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum, "microbatch_pairs": pair, "adam_moments": "bf16" if a.bf16_moments else "fp32",
+            "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu",
             "params": m.num_params(),
             "active_params": m.num_params(active=True)},
            tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4))

@@ -146,10 +146,16 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 // 16 B per lane of a buffer straight into LDS (lane i -> lds + 16 i) as inline asm: hipcc neither
 // counts it (the caller's own s_waitcnt vmcnt(N) retires it) nor makes later ds_reads wait vmcnt(0)
 // for it. M0 carries the LDS base and is restored.
+// NT: non-temporal (streamed once; keeps the L2 for data that is re-read, e.g. a shared K tile)
+template <bool NT = false>
 __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
   unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
 }
 
 // Register-staged tile loader: ROWS x HDC bf16 tile of a strided tensor -> regs -> LDS image

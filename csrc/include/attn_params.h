@@ -28,17 +28,26 @@ struct AttnParams {
   long long* stamp;
   int xcd;  // query-parallel kernels: XCD-aware block order (q_block_map)
   // dS-materialising backward (attn_bwd_dkdv3_kernel<.., DSOUT> -> attn_bwd_dq_ds_kernel): the
-  // bf16 dS of every live 32-query x 32-key block, ds_hstride elements per (b, q-head), block
-  // (qt, kt) at ds_block(); ds_nqt / ds_nkt = 32-row tiles of Tq / Tk
+  // bf16 dS of every 32-query x 32-key block in consumer order, ds_kvstride elements per (b, kv-head),
+  // block (qt, kt) of q-head g at ds_index(); ds_nqt / ds_nkt = 32-row tiles of Tq / Tk
   bf16* dsbuf;
-  long ds_hstride;
+  long ds_kvstride;
   int ds_nqt, ds_nkt;
 };
 
-// dS block index inside one (b, q-head): causal (Tq == Tk) keeps the lower triangle incl. the
-// diagonal (kt <= qt), row-major over qt; non-causal every block
-__device__ __forceinline__ long ds_block(int qt, int kt, int nkt, bool causal) {
-  return causal ? (long)qt * (qt + 1) / 2 + kt : (long)qt * nkt + kt;
+// 2 KiB dS block index inside one (b, kv-head) region, in the order the dQ pass streams it: per
+// 64-query block qb its key steps kt (causal Tq == Tk: kt <= 2qb + 1, non-causal: all nkt), per
+// step the G q-heads of the group, per head the two 32-query halves t. A dQ block (4 waves = 4 heads
+// of one qb at G = 4) then reads one contiguous 16 KiB piece per key step. The t = 0 block of the
+// causal last step (kt = 2qb + 1 > qt) is a hole: never written, never used.
+__device__ __forceinline__ long ds_index(int qt, int kt, int g, int G, int nkt, bool causal) {
+  const int qb = qt >> 1, t = qt & 1;
+  const long step = causal ? (long)qb * (qb + 1) + kt : (long)qb * nkt + kt;
+  return (step * G + g) * 2 + t;
+}
+// elements per (b, kv-head) region
+inline long ds_kv_elems(int nq64, int nkt, int G, bool causal) {
+  return 1024L * 2 * G * (causal ? (long)nq64 * (nq64 + 1) : (long)nq64 * nkt);
 }
 // 16-B chunk slot of (producer half s, lane half h, key k) in a 2 KiB dS block: the 8 bf16 of a
 // chunk are the dS of key k for queries 16s + 8(j>>2) + 4h + (j&3), j = 0..7 (the dK/dV kernel's

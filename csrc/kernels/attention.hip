@@ -1147,8 +1147,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           const int qt = qtp + t, kt = kw0 >> 5;
           if ((!CAUSAL || kt <= qt) && qt < p.ds_nqt && kt < p.ds_nkt) {
             const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(p.dsbuf + ((long)b * p.H + hp) * p.ds_hstride), 0, (int)(p.ds_hstride * 2), 0x00020000);
-            const int bo = (int)(ds_block(qt, kt, p.ds_nkt, CAUSAL) * 2048);              // bytes, scalar
+                (void*)(p.dsbuf + ((long)b * p.Hkv + hk) * p.ds_kvstride), 0, (int)(p.ds_kvstride * 2), 0x00020000);
+            const int bo = (int)(ds_index(qt, kt, hp - hk * (p.H / p.Hkv), p.H / p.Hkv, p.ds_nkt, CAUSAL) * 2048);
             const int vo = 16 * ds_slot(0, (int)(__lane_id() >> 5), (int)(__lane_id() & 31));
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sa), dsr, vo, bo, 0);        // s = 0
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sb), dsr, vo + 128, bo, 0);  // s = 1: slot + 8
@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
 // Non-live blocks (above the causal diagonal, or a missing unit) are loaded through a zero-range
 // descriptor (zeros, same DMA count per step) and skipped by the MFMAs.
 // ---------------------------------------------------------------------------
-template <int HD, bool CAUSAL>
+template <int HD, bool CAUSAL, bool NT>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   static_assert(HD == 128, "dq_ds: head dim 128 (K tile = 4 KiB-row images of 256 B)");
   constexpr int DT = HD / 32, KIMG = 32 * HD, WSLOT = 2 * 1024, SLOT = KIMG + 4 * WSLOT, NSLOT = 3;
@@ -1236,7 +1236,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
     const int r = 8 * wave + 4 * j + (lane >> 4);
     kvo[j] = (unsigned)(((long)r * p.skt + 8 * ((lane & 15) ^ swz<HD>(r))) * 2);
   }
-  const bf16* dshead = p.dsbuf + ((long)b * p.H + h) * p.ds_hstride;
+  const bf16* dskv = p.dsbuf + ((long)b * p.Hkv + hk) * p.ds_kvstride;
+  const int g = h - hk * G;
   auto live = [&](int qt, int kt) { return uvalid && qt < p.ds_nqt && (!CAUSAL || kt <= qt); };
   auto issue = [&](int j, int slot) {
     bf16* sl = smem + slot * SLOT;
@@ -1246,16 +1247,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
         (void*)(kbase + (long)key0 * p.skt), 0, (int)min(kbytes, 0x7fffffffL), 0x00020000);
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) dma16_asm(rk, kvo[jj], lds_addr(sl + (8 * wave + 4 * jj) * HD));
+    // this wave's two blocks of the step (t = 0, 1) are one contiguous 4 KiB piece; a step past the
+    // unit's range, or a missing unit, reads zeros (same DMA count in every wave and step)
+    const bool lv = live(2 * qb + 1, j) || live(2 * qb, j);
+    const bf16* src = lv ? dskv + ds_index(2 * qb, j, g, G, p.ds_nkt, CAUSAL) * 1024 : p.dsbuf;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, lv ? 4096 : 0, 0x00020000);
+    bf16* dst = sl + KIMG + wave * WSLOT;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int qt = 2 * qb + t;
-      const bool lv = live(qt, j);
-      const bf16* src = lv ? dshead + ds_block(qt, j, p.ds_nkt, CAUSAL) * 1024 : p.dsbuf;
-      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, lv ? 2048 : 0, 0x00020000);
-      bf16* dst = sl + KIMG + wave * WSLOT + t * 1024;
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) dma16_asm(rd, (unsigned)(lane * 16 + jj * 1024), lds_addr(dst + jj * 512));
-    }
+    for (int jj = 0; jj < 4; ++jj) dma16_asm<NT>(rd, (unsigned)(lane * 16 + jj * 1024), lds_addr(dst + jj * 512));
   };
   LdsOff<HD> off;
   off.init(lane);
@@ -1727,20 +1726,32 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
     // (read per call) keeps the dq kernel that recomputes S and dP.
     const char* de = getenv("SPA_ATTN_DQ_DS");
     const bool want = !(de && atoi(de) == 0);
-    if (want && p.hsplit == 1 && p.Tk > 0 && dkdv_mode == 0 && (!causal || p.causal_off == 0)) {
+    // (the per-(b, kv-head) dS region is addressed by a buffer descriptor: < 2 GiB, T <= ~22K causal)
+    const long kv_bytes = 2 * ds_kv_elems(cdiv(p.Tq, 64), cdiv(p.Tk, 32), p.H / p.Hkv, causal);
+    if (want && p.hsplit == 1 && p.Tk > 0 && dkdv_mode == 0 && (!causal || p.causal_off == 0) &&
+        kv_bytes < 0x7fffffffL) {
       const long rows = (long)p.B * p.Tq * p.H;
       attn_delta_kernel<HDK><<<(int)cdiv(rows, 256 / (HDK / 8)), 256, 0, st>>>(p);
       p.ds_nqt = cdiv(p.Tq, 32);
       p.ds_nkt = cdiv(p.Tk, 32);
-      p.ds_hstride = 1024L * (causal ? (long)p.ds_nqt * (p.ds_nqt + 1) / 2 : (long)p.ds_nqt * p.ds_nkt);
-      at::Tensor dsb = at::empty({(long)p.B * p.H * p.ds_hstride}, bf16_opts);   // freed (stream-ordered) on return
+      p.ds_kvstride = ds_kv_elems(cdiv(p.Tq, 64), p.ds_nkt, p.H / p.Hkv, causal);
+      at::Tensor dsb = at::empty({(long)p.B * p.Hkv * p.ds_kvstride}, bf16_opts);   // freed (stream-ordered) on return
       p.dsbuf = (bf16*)dsb.data_ptr();
       if (causal) attn_bwd_dkdv3_kernel<HDK, true, true><<<nkv, 512, 0, st>>>(p);
       else attn_bwd_dkdv3_kernel<HDK, false, true><<<nkv, 512, 0, st>>>(p);
       const int G = p.H / p.Hkv;
       const int wg = cdiv(cdiv(p.Tq, 64) * G, 4) * p.B * p.Hkv;
-      if (causal) attn_bwd_dq_ds_kernel<HDK, true><<<wg, 256, 0, st>>>(p);
-      else attn_bwd_dq_ds_kernel<HDK, false><<<wg, 256, 0, st>>>(p);
+      // SPA_ATTN_DS_NT (read per call, default 1): dS streamed with non-temporal loads, so the
+      // once-read 2 KiB blocks do not evict the K tiles every block of the XCD re-reads
+      const char* ne = getenv("SPA_ATTN_DS_NT");
+      const bool nt = !(ne && atoi(ne) == 0);
+      if (nt) {
+        if (causal) attn_bwd_dq_ds_kernel<HDK, true, true><<<wg, 256, 0, st>>>(p);
+        else attn_bwd_dq_ds_kernel<HDK, false, true><<<wg, 256, 0, st>>>(p);
+      } else {
+        if (causal) attn_bwd_dq_ds_kernel<HDK, true, false><<<wg, 256, 0, st>>>(p);
+        else attn_bwd_dq_ds_kernel<HDK, false, false><<<wg, 256, 0, st>>>(p);
+      }
       return;
     }
   }

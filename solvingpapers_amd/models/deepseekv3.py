@@ -320,54 +320,40 @@ class DenseFFN(tnn.Module):
         return linear(glu(linear(x, self.w13, fp8=self.fp8), "silu"), self.w2, fp8=self.fp8)
 
 
-class _NullCtx:
-    def __enter__(self):
-        return self
+class _PairReady:
+    """grad_ready_cb for two micro-batches in one backward: a layer's gradients are complete
+    (the DP bucket may launch) only when BOTH micro-batches' backward passed its marker."""
 
-    def __exit__(self, *a):
-        return False
+    def __init__(self, cb):
+        self.cb, self.seen = cb, {}
 
-
-class _JoinSide(torch.autograd.Function):
-    """Identity joining the side stream back; its backward queues an end-of-backward wait of the
-    caller's stream on the side stream (weight gradients committed there are then complete)."""
-
-    @staticmethod
-    def forward(ctx, x, side):
-        ctx.side = side
-        return x.view_as(x)
-
-    @staticmethod
-    def backward(ctx, g):
-        side, main = ctx.side, torch.cuda.current_stream()
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
-        return g, None
+    def __call__(self, key):
+        n = self.seen.get(key, 0) + 1
+        if n == 2:
+            self.seen.pop(key, None)
+            self.cb(key)
+        else:
+            self.seen[key] = n
 
 
 class MoE(tnn.Module):
     """DeepSeekMoE: shared experts + top-k routed experts with aux-free load balancing.
     Under EP (``ep_group`` of size P) this rank holds experts [r*E/P, (r+1)*E/P)."""
 
-    def __init__(self, c: DSV3Config, ep_group=None, ep_group2=None, ep_chunks=2, ep_schedule=None, **fk):
-        """Under EP (P > 1) the layer's tokens run as ``ep_chunks`` chunks whose dispatch /
-        combine all-to-alls overlap the other chunks' expert GEMMs and the shared expert on
-        ONE stream (expert_parallel.ep_run_interleaved; ``ep_chunks=1``: no overlap) -- the
-        default ``ep_schedule="interleave"``. ``ep_schedule="two_stream"`` with ``ep_group2`` (a
-        second communicator over the same EP ranks): two chunks on two compute streams (chunk A
-        with ``ep_group``, chunk B on a side stream with ``ep_group2``); see _forward_pipelined.
-        1-GPU proxy (profiles/r3_overlap_proxy_streamk_dp.jsonl): interleave hides 0.47-0.55 of
-        the all-to-all time, two_stream 0.42-0.48 (its chunks share the CUs). SPA_EP_SCHEDULE
-        overrides the default."""
+    def __init__(self, c: DSV3Config, ep_group=None, ep_chunks=1, **fk):
+        """One forward is four stages (expert_parallel.EPStage): prepare (routing, count exchange,
+        fp8 payload) -> shared expert -> dispatch (the one host sync; the all-to-all starts right
+        after the payload, so the shared expert queued before the sync runs beside it) -> experts +
+        combine. DeepSeekV3.forward_pair interleaves the stages of two micro-batches so every
+        exchange also overlaps the other micro-batch's attention / experts. ``ep_chunks > 1``
+        instead splits this layer's tokens into chunks whose exchanges overlap each other's experts
+        (fewer rows per expert: measured slower, kept for comparison)."""
         super().__init__()
         from ..parallel.expert_parallel import ep_rank_size
         self.c = c
         self.ep_group = ep_group
         self.ep_rank, self.ep = ep_rank_size(ep_group)
-        sched = ep_schedule or os.environ.get("SPA_EP_SCHEDULE", "interleave")
-        assert sched in ("interleave", "two_stream"), sched
-        self.ep_group2 = ep_group2 if (self.ep > 1 and sched == "two_stream") else None
         self.ep_chunks = int(ep_chunks) if self.ep > 1 else 1
-        self._side = None
         assert c.n_experts % self.ep == 0
         El = c.n_experts // self.ep
         D, F = c.dim, c.ffn_hidden
@@ -384,9 +370,7 @@ class MoE(tnn.Module):
         self.register_buffer("routing_bias", torch.zeros(c.n_experts, device=fk.get("device")))
         self.balance_group = None      # DP group for the counts all-reduce (set by the trainer)
         self.last_counts = None
-        if self.ep_group2 is not None:
-            from ..utils.grad import mark_multi_stream
-            mark_multi_stream(self.parameters())     # weight-grad commits come from two streams
+        self._pending_bias = []        # (work, load): bias updates whose counts all-reduce is in flight
 
     @torch.no_grad()
     def reset_parameters(self, std, g):
@@ -423,125 +407,109 @@ class MoE(tnn.Module):
             logits = logits + torch.nn.functional.softplus(router_logits(x2, self.noise)) * torch.randn_like(logits)
         return logits
 
-    def forward(self, x):
-        from ..parallel.expert_parallel import ep_moe_ffn
+    def _fp8(self, x2):
+        return self.c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0
+
+    # ---- stages (expert_parallel.EPStage); forward() runs them in order, forward_pair interleaves
+    def stage_prepare(self, x2):
+        from ..parallel.expert_parallel import ep_stage_prepare
         c = self.c
+        self.finish_pending()                   # last step's bias updates before this routing
+        idx, w = route(self._logits(x2), c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
+        st = ep_stage_prepare(x2, idx, w, c.n_experts, self.ep_group, self._fp8(x2), self.w13)
+        st.x2, st.idx, st.sh = x2, idx, None
+        return st
+
+    def stage_shared(self, st):
+        if self.shared is not None:
+            st.sh = self.shared(st.x2)
+
+    def stage_dispatch(self, st):
+        from ..parallel.expert_parallel import ep_stage_dispatch
+        ep_stage_dispatch(st)
+
+    def stage_experts(self, st):
+        from ..parallel.expert_parallel import ep_stage_experts
+        ep_stage_experts(st, self.w13, self.w2)
+
+    def stage_finish(self, st):
+        from ..parallel.expert_parallel import ep_stage_finish
+        plan, idx, w = st.prep.plan, st.idx, st.w
+        y = ep_stage_finish(st)
+        if st.sh is not None:
+            y = y + st.sh
+        self.last_counts = plan.counts
+        if self.c.aux_free and self.training:
+            self._update_bias(idx, w, plan)
+        st.x2 = st.sh = None
+        return y
+
+    def forward(self, x):
         B, T, D = x.shape
         x2 = x.reshape(-1, D)
-        if self.ep_group2 is not None and x2.shape[0] >= 2:
-            return self._forward_pipelined(x2).view(B, T, D)
         if self.ep_chunks > 1 and x2.shape[0] >= self.ep_chunks:
-            return self._forward_interleaved(x2).view(B, T, D)
-        logits = self._logits(x2)
-        idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
-        y, plan = ep_moe_ffn(x2, idx, w, self.w13, self.w2, c.n_experts, self.ep_group,
-                             fp8=c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0)
-        if self.shared is not None:
-            y = y + self.shared(x2)
-        self.last_counts = plan.counts
-        if c.aux_free and self.training:
-            self._update_bias(idx, w, plan)
-        return y.view(B, T, D)
+            return self._forward_chunked(x2).view(B, T, D)
+        st = self.stage_prepare(x2)
+        self.stage_shared(st)                   # queued before the dispatch's host sync
+        self.stage_dispatch(st)
+        self.stage_experts(st)
+        return self.stage_finish(st).view(B, T, D)
 
-    def _forward_interleaved(self, x2):
-        """``ep_chunks`` token chunks, one stream (expert_parallel.ep_run_interleaved): routing,
-        permutation and count exchange of every chunk first (one host sync per chunk, all
-        issued before the first dispatch), then the interleaved dispatch / experts / combine."""
-        from ..parallel.expert_parallel import ep_prepare, ep_run_interleaved
+    def _forward_chunked(self, x2):
+        """``ep_chunks`` token chunks of this layer, one stream (expert_parallel.ep_run_interleaved)."""
+        from ..parallel.expert_parallel import ep_run_interleaved
         c = self.c
-        n = self.ep_chunks
-        parts = torch.tensor_split(x2, n)
-        idxs, ws, preps = [], [], []
+        self.finish_pending()
+        parts = torch.tensor_split(x2, self.ep_chunks)
+        idxs, ws = [], []
         for xp in parts:
             idx, w = route(self._logits(xp), c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
             idxs.append(idx)
             ws.append(w)
-            preps.append(ep_prepare(idx, c.n_experts, self.ep_group))
-        fp8 = c.moe_fp8 and x2.is_cuda and self.Fp % 16 == 0
-        ys = ep_run_interleaved(parts, ws, preps, self.w13, self.w2, c.n_experts, self.ep_group, fp8=fp8,
+        ys = ep_run_interleaved(parts, idxs, ws, self.w13, self.w2, c.n_experts, self.ep_group, fp8=self._fp8(x2),
                                 shared=self.shared)
-        counts = preps[0].plan.counts
-        for p_ in preps[1:]:
-            counts = counts + p_.plan.counts
-        self.last_counts = counts
+        self.last_counts = None
         if c.aux_free and self.training:
-            self._update_bias(torch.cat(idxs), torch.cat(ws), SimpleNamespace(counts=counts))
+            for idx, w in zip(idxs, ws):
+                self._update_bias(idx, w, None)
         return torch.cat(ys)
-
-    def _forward_pipelined(self, x2):
-        """Two token chunks on two streams / two EP communicators (see __init__). Host order:
-        route + permute + count exchange + shared expert of BOTH chunks, then one host sync per
-        chunk for its split sizes (the GPU is busy with the shared experts meanwhile), then each
-        chunk's dispatch -> experts -> combine on its own stream. A stream waits only for its own
-        chunk's all-to-alls, so the other chunk's grouped GEMMs fill those gaps; autograd runs
-        each backward op on its forward's stream, so the backward overlaps the same way."""
-        from ..parallel.expert_parallel import ep_prepare, ep_run
-        c = self.c
-        N = x2.shape[0]
-        half = N // 2
-        groups = (self.ep_group, self.ep_group2)
-        cuda = x2.is_cuda
-        main = torch.cuda.current_stream(x2.device) if cuda else None
-        if cuda and self._side is None:
-            from ..parallel.comm import side_stream
-            self._side = side_stream(x2.device)
-            from ..utils.grad import register_side_stream
-            register_side_stream(self._side)
-        side = self._side if cuda else None
-
-        def on(i):
-            return torch.cuda.stream(side) if (i == 1 and side is not None) else _NullCtx()
-
-        if side is not None:
-            side.wait_stream(main)
-        parts = (x2[:half], x2[half:])
-        fp8 = c.moe_fp8 and cuda and self.Fp % 16 == 0
-        st = []
-        for i in range(2):
-            with on(i):
-                logits = self._logits(parts[i])
-                idx, w = route(logits, c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
-                prep = ep_prepare(idx, c.n_experts, groups[i])
-                ys = self.shared(parts[i]) if self.shared is not None else None
-                st.append((idx, w, prep, ys))
-        outs = []
-        for i in range(2):
-            idx, w, prep, ys = st[i]
-            with on(i):
-                y, _ = ep_run(parts[i], w, prep, self.w13, self.w2, c.n_experts, groups[i], fp8=fp8)
-                outs.append(y + ys if ys is not None else y)
-        idx = torch.cat([st[0][0], st[1][0]])
-        w = torch.cat([st[0][1], st[1][1]])
-        counts = st[0][2].plan.counts + st[1][2].plan.counts
-        if side is not None:
-            main.wait_stream(side)
-            for t in (outs[1], st[1][0], st[1][1], st[1][2].plan.counts):
-                t.record_stream(main)
-        y = torch.cat(outs)
-        if side is not None:
-            y = _JoinSide.apply(y, side)
-        self.last_counts = counts
-        if c.aux_free and self.training:
-            self._update_bias(idx, w, SimpleNamespace(counts=counts))
-        return y
 
     @torch.no_grad()
     def _update_bias(self, idx, w, plan):
+        """Aux-loss-free balancing (deepseekv3.ipynb:1082-1086): bias += rate * sign(mean - load).
+        "counts": the load is summed over the DP group with an ASYNC all-reduce, applied by
+        finish_pending() -- at the layer's next routing, or before a checkpoint / eval -- so the
+        forward never blocks on it; the update still lands before the next use of the bias."""
         c = self.c
         if c.balance_stat == "soft":            # deepseekv3.ipynb:1082-1086
             load = torch.zeros(idx.shape[0], c.n_experts, device=w.device).scatter_(1, idx.long(), w).sum(0)
+            self._apply_bias(load)
+            return
+        load = (plan.counts if plan is not None else
+                torch.bincount(idx.reshape(-1).long(), minlength=c.n_experts)).float()
+        grp = self.balance_group
+        if grp is not None or (dist.is_initialized() and dist.get_world_size() > 1):
+            self._pending_bias.append((dist.all_reduce(load, group=grp, async_op=True), load))
         else:
-            load = plan.counts.float()
-            grp = self.balance_group
-            if grp is not None or (dist.is_initialized() and dist.get_world_size() > 1):
-                dist.all_reduce(load, group=grp)
+            self._apply_bias(load)
+
+    @torch.no_grad()
+    def _apply_bias(self, load):
         err = load.mean() - load
-        self.routing_bias.add_(c.bias_update_rate * torch.sign(err))
+        self.routing_bias.add_(self.c.bias_update_rate * torch.sign(err))
+
+    @torch.no_grad()
+    def finish_pending(self):
+        """Apply the bias updates whose load all-reduce was in flight (in issue order)."""
+        while self._pending_bias:
+            work, load = self._pending_bias.pop(0)
+            work.wait()
+            self._apply_bias(load)
 
 
 # =============================================================================== layers
 class DSV3Layer(tnn.Module):
-    def __init__(self, c: DSV3Config, dense: bool, ep_group=None, ep_group2=None, **fk):
+    def __init__(self, c: DSV3Config, dense: bool, ep_group=None, **fk):
         super().__init__()
         self.c = c
         self.attn_norm = tnn.Parameter(torch.ones(c.dim, **fk))
@@ -550,7 +518,7 @@ class DSV3Layer(tnn.Module):
         if dense:
             self.ffn = DenseFFN(c.dim, c.dense_hidden or c.ffn_hidden, fp8=c.fp8_linears, **fk)
         else:
-            self.ffn = MoE(c, ep_group, ep_group2, **fk)
+            self.ffn = MoE(c, ep_group, **fk)
 
     @torch.no_grad()
     def reset_parameters(self, g):
@@ -571,10 +539,8 @@ class DSV3Layer(tnn.Module):
     def expert_params(self):
         return self.ffn.expert_params() if isinstance(self.ffn, MoE) else []
 
-    def forward_split(self, res, delta, L0=None, cache=None, pos=0):
-        """Pre-norm layer on a split residual stream (as LlamaBlock): the input is res + delta and
-        the output (h, f) means h + f; both residual adds happen inside the fused RMSNorms, so
-        neither the forward nor the backward launches a separate add."""
+    def attn_part(self, res, delta, L0=None, cache=None, pos=0):
+        """norm -> attention -> residual -> FFN norm: returns (h2, n2, L0), the FFN's input n2."""
         c = self.c
         if res is None:
             xn, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
@@ -586,6 +552,13 @@ class DSV3Layer(tnn.Module):
                 cache[:, pos:pos + xn.shape[1]] = L0.to(cache.dtype)
         a = self.attn(xn, L0, cache, pos)
         n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
+        return h2, n2, L0
+
+    def forward_split(self, res, delta, L0=None, cache=None, pos=0):
+        """Pre-norm layer on a split residual stream (as LlamaBlock): the input is res + delta and
+        the output (h, f) means h + f; both residual adds happen inside the fused RMSNorms, so
+        neither the forward nor the backward launches a separate add."""
+        h2, n2, L0 = self.attn_part(res, delta, L0, cache, pos)
         return h2, self.ffn(n2), L0
 
     def forward(self, x, L0=None, cache=None, pos=0):
@@ -594,13 +567,12 @@ class DSV3Layer(tnn.Module):
 
 
 class DeepSeekV3(tnn.Module):
-    def __init__(self, c: DSV3Config, device=None, dtype=torch.float32, seed: int = 0, ep_group=None,
-                 ep_group2=None):
+    def __init__(self, c: DSV3Config, device=None, dtype=torch.float32, seed: int = 0, ep_group=None):
         super().__init__()
         self.c = c
         fk = dict(device=device, dtype=dtype)
         self.embed = tnn.Parameter(torch.empty(c.vocab_size, c.dim, **fk))     # tied LM head
-        self.layers = tnn.ModuleList([DSV3Layer(c, i < c.n_dense_layers, ep_group, ep_group2, **fk)
+        self.layers = tnn.ModuleList([DSV3Layer(c, i < c.n_dense_layers, ep_group, **fk)
                                       for i in range(c.n_layers)])
         self.norm_f = tnn.Parameter(torch.ones(c.dim, **fk))
         # MTP (deepseekv3.ipynb:1466-1485): norm1 on the shifted-token embedding, norm2 on the
@@ -612,7 +584,7 @@ class DeepSeekV3(tnn.Module):
         self.mtp_norm2_b = tnn.Parameter(torch.zeros(D, **fk))
         self.mtp_proj = tnn.Parameter(torch.empty(D, 2 * D, **fk))
         self.mtp_heads = tnn.ParameterList([tnn.Parameter(torch.empty(D, D, **fk)) for _ in range(c.mtp_heads)])
-        self.mtp_layers = tnn.ModuleList([DSV3Layer(c, False, ep_group, ep_group2, **fk) for _ in range(c.mtp_heads)])
+        self.mtp_layers = tnn.ModuleList([DSV3Layer(c, False, ep_group, **fk) for _ in range(c.mtp_heads)])
         if c.pos_emb == "sinusoidal":
             self.register_buffer("pe", sinusoidal_pe(c.block_size, c.dim, device=device).to(dtype))
         else:
@@ -688,14 +660,104 @@ class DeepSeekV3(tnn.Module):
                 res, delta, _ = layer.forward_split(res, delta, None, None if caches is None else caches[i], pos)
         wait(len(self.layers) + 1)
         delta = mark_ready(delta, cb, len(self.layers) + 1)
+        return self._final(res, delta), x0
+
+    def hidden_pair(self, ids0, ids1):
+        """Two micro-batches through the main layers, interleaved so every expert-parallel
+        all-to-all of one runs under the other's compute (DualPipe-style micro-batch overlap; no
+        layer's tokens are split, so every grouped GEMM keeps its full rows per expert). Per MoE
+        layer l, host order (each exchange is issued right after its producer, expert_parallel
+        EPStage):
+
+            finish combine_0(l-1) | attn_0 | prepare_0 | shared_0 | dispatch_0 (host sync)
+            finish combine_1(l-1) | attn_1 | prepare_1 | shared_1 | dispatch_1 (host sync)
+            experts_0 + combine_0 | experts_1 + combine_1
+
+        so dispatch_0 overlaps shared_0 and attn_1, dispatch_1 overlaps shared_1 and experts_0,
+        combine_0 overlaps experts_1 and combine_1 overlaps the next layer's attn_0; autograd
+        replays the nodes in reverse creation order, which interleaves the backward the same way.
+        Returns ([n_0, n_1], [x0_0, x0_1]) as hidden() does per micro-batch."""
+        c = self.c
+        wait = self.param_wait_cb or (lambda i: None)
+        eb = self._expert_buckets() if self.param_wait_cb is not None else {}
+        wait(0)
+        xs = [self._embed(ids0), self._embed(ids1)]
+        x0s = list(xs)
+        cb = _PairReady(self.grad_ready_cb) if self.grad_ready_cb is not None else None
+        S = [{"res": None, "delta": xs[0], "L0": None}, {"res": None, "delta": xs[1], "L0": None}]
+        pend = [None, None]
+
+        def settle(m):
+            if pend[m] is not None:
+                moe, st = pend[m]
+                S[m]["delta"] = moe.stage_finish(st).view(st.shape)
+                pend[m] = None
+
+        for i, layer in enumerate(self.layers):
+            wait(i + 1)
+            if i in eb:
+                wait(eb[i])
+            is_moe = isinstance(layer.ffn, MoE)
+            sts = [None, None]
+            for m in (0, 1):
+                settle(m)
+                sm = S[m]
+                sm["delta"] = mark_ready(sm["delta"], cb, i + 1)
+                h2, n2, L0 = layer.attn_part(sm["res"], sm["delta"], sm["L0"] if c.attention == "ref" else None)
+                sm["res"] = h2
+                if c.attention == "ref":
+                    sm["L0"] = L0
+                if not is_moe:
+                    sm["delta"] = layer.ffn(n2)
+                    continue
+                st = layer.ffn.stage_prepare(n2.reshape(-1, n2.shape[-1]))
+                st.shape = n2.shape
+                layer.ffn.stage_shared(st)        # queued before the dispatch's host sync
+                layer.ffn.stage_dispatch(st)
+                sts[m] = st
+            if is_moe:
+                layer.ffn.stage_experts(sts[0])
+                layer.ffn.stage_experts(sts[1])
+                pend = [(layer.ffn, sts[0]), (layer.ffn, sts[1])]
+        for m in (0, 1):
+            settle(m)
+        wait(len(self.layers) + 1)
+        ns = []
+        for m in (0, 1):
+            delta = mark_ready(S[m]["delta"], cb, len(self.layers) + 1)
+            ns.append(self._final(S[m]["res"], delta))
+        return ns, x0s
+
+    def _final(self, res, delta):
+        c = self.c
         if (c.dropout > 0 and self.training) or c.final_scale or res is None:
             x = delta if res is None else res + delta
             x = dropout(x, c.dropout, self.training)
             if c.final_scale:
                 x = x * (2.0 * c.n_layers ** -0.5)
-            return rms_norm(x, self.norm_f, c.norm_eps), x0
+            return rms_norm(x, self.norm_f, c.norm_eps)
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
-        return n, x0
+        return n
+
+    def forward_pair(self, ids0, targets0, ids1, targets1):
+        """loss(micro-batch 0) + loss(micro-batch 1) with the two run layer-interleaved
+        (hidden_pair): the same values and gradients as two forward() calls, with each MoE
+        layer's all-to-alls overlapped by the other micro-batch's compute. Training only."""
+        ns, x0s = self.hidden_pair(ids0, ids1)
+        D = self.c.dim
+        loss = None
+        for n, x0, t in zip(ns, x0s, (targets0, targets1)):
+            l = linear_cross_entropy(n.reshape(-1, D), self.embed, t.reshape(-1))
+            if self.c.mtp_heads and self.training:
+                l = l + self.mtp_loss(n, x0, t)
+            loss = l if loss is None else loss + l
+        return loss
+
+    def finish_pending_updates(self):
+        """Apply routing-bias updates whose DP all-reduce is still in flight (before a checkpoint,
+        an evaluation, or reading the buffers)."""
+        for m in self.moe_layers():
+            m.finish_pending()
 
     def logits(self, n):
         return linear(n, self.embed)

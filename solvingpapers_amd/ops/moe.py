@@ -367,97 +367,8 @@ def dequant_act_fp8_blk(q, s, dtype=torch.bfloat16):
     return (q.float().view(R, -1, 128) * torch.exp2(s[:, :K // 128].float() - 127)[..., None]).view(R, K).to(dtype)
 
 
-# ---- deferred expert weight gradients (gradient accumulation)
-# A micro-batch routes only ~tokens*k/E rows to each expert (768 at dsv3_style widths), so its
-# dW_e = dY_e^T X_e GEMMs reduce over ~12 K-tiles: the 256 x 256 tile's prologue / epilogue and
-# the bf16 read-modify-write of the accumulated gradient cost a third of the kernel (563 TF in
-# situ at accum 4, profiles/r3_dsv3_style_accum4_step_kernels.txt). Inside
-# ``defer_expert_wgrad()`` (the inner micro-batches of an accumulation loop) the routed experts'
-# bf16 weight-gradient products are not run: (dY, X, offsets) are kept, and the next commit
-# outside the context -- the last micro-batch's backward -- computes dW over every kept
-# micro-batch's tokens plus its own in ONE grouped launch per weight (K = all micro-batches'
-# tokens of the expert, gemm8.hip G8Segs), written once. All FLOPs still run inside the step;
-# the kept activations cost memory (dsv3_style accum 4: ~0.8 GB per MoE layer per kept
-# micro-batch). The fp8 Wgrad path and multi-stream (pipelined EP) backward are not deferred.
-class _Defer:
-    depth = 0
-    pending: dict = {}      # id(W) -> (W, [(dy, xp, offsets), ...])
-
-
-@contextlib.contextmanager
-def defer_expert_wgrad(enabled: bool = True):
-    """Context for the inner micro-batches of a gradient-accumulation loop (see _Defer)."""
-    if not enabled:
-        yield
-        return
-    _Defer.depth += 1
-    try:
-        yield
-    finally:
-        _Defer.depth -= 1
-
-
-def _defer_ok(W, dy, xp):
-    from ..utils.grad import is_multi_stream
-    return (DEFER_WGRAD and _gpu(dy) and GG8 and dy.dtype == torch.bfloat16 and xp.dtype == torch.bfloat16
-            and W.dtype == torch.bfloat16 and dy.shape[1] % 8 == 0 and xp.shape[1] % 8 == 0
-            and not is_multi_stream(W) and not torch.cuda.is_current_stream_capturing())
-
-
-DEFER_WGRAD = os.environ.get("SPA_DEFER_WGRAD", "1") != "0"
-
-
-def _wgrad_multi(W, srcs, out, acc):
-    """out (+)= sum over srcs of the grouped dY^T X, at most 8 sources per launch."""
-    for i in range(0, len(srcs), 8):
-        ch = srcs[i:i + 8]
-        ops().grouped_gemm8_wgrad_multi([c[0] for c in ch], [c[1] for c in ch], [c[2] for c in ch],
-                                        out, acc or i > 0)
-    return out
-
-
-def flush_expert_wgrad():
-    """Commit every kept expert weight gradient (a loop whose last micro-batch did not reach a
-    deferred weight, e.g. an early exit). No-op when nothing is pending."""
-    for key in list(_Defer.pending):
-        W, srcs = _Defer.pending.pop(key)
-        g = commit(W, lambda out, acc: _commit_multi(W, srcs, out, acc))
-        if g is not None:
-            W.grad = g if W.grad is None else W.grad + g
-
-
-def _commit_multi(W, srcs, out, acc):
-    if out is None:
-        return _wgrad_multi(W, srcs, torch.empty(W.shape, device=W.device, dtype=W.dtype), False)
-    if out.dtype == W.dtype and out.is_contiguous():
-        _wgrad_multi(W, srcs, out.view(W.shape), acc)
-        return None
-    g = _wgrad_multi(W, srcs, torch.empty(W.shape, device=W.device, dtype=W.dtype), False)
-    if acc:
-        out.add_(g.view_as(out))
-    else:
-        out.copy_(g.view_as(out))
-    return None
-
-
 def commit_weight_grad(W, dy, xp, plan):
-    """bf16 dW_e = dy_e^T xp_e (grouped), committed into W's gradient storage; kept for later
-    inside ``defer_expert_wgrad()``, and summed with the kept micro-batches on the next commit."""
-    if _gpu(dy) and (_Defer.depth > 0 or id(W) in _Defer.pending) and _defer_ok(W, dy, xp):
-        dy, xp = dy.contiguous(), xp.contiguous()
-        ent = _Defer.pending.get(id(W))
-        if ent is None or ent[0] is not W:
-            ent = (W, [])
-            _Defer.pending[id(W)] = ent
-        ent[1].append((dy, xp, plan.offsets))
-        if _Defer.depth > 0:
-            return None
-        del _Defer.pending[id(W)]
-        return commit(W, lambda out, acc: _commit_multi(W, ent[1], out, acc))
-    kept = None
-    if id(W) in _Defer.pending:              # kept sources this commit cannot join: theirs first
-        Wk, srcs = _Defer.pending.pop(id(W))
-        kept = commit(W, lambda out, acc: _commit_multi(W, srcs, out, acc))
+    """bf16 dW_e = dy_e^T xp_e (grouped), committed into W's gradient storage."""
 
     def _w(out, acc):
         if out is None:
@@ -470,8 +381,7 @@ def commit_weight_grad(W, dy, xp, plan):
                 out.add_(g.view_as(out))
             else:
                 out.copy_(g.view_as(out))
-    g = commit(W, _w)
-    return g if kept is None else (kept if g is None else kept + g)
+    return commit(W, _w)
 
 
 def quant_weight_fp8_rows(W):

@@ -168,16 +168,53 @@ def all_reduce(t: torch.Tensor, group, async_op: bool = False, op=None):
     return dist.all_reduce(t, op=op, group=group, async_op=async_op)
 
 
+_LAUNCH = {}
+
+
+def launch_stream(device):
+    """Per-device stream that collectives are ISSUED from when they must start right after an
+    earlier point of the compute stream (``after`` event) instead of after everything queued on it
+    by the time the host knows the split sizes (work queued meanwhile then overlaps the exchange)."""
+    d = torch.device(device)
+    key = d.index if d.index is not None else torch.cuda.current_device()
+    if key not in _LAUNCH:
+        _LAUNCH[key] = torch.cuda.Stream(d)
+    return _LAUNCH[key]
+
+
 def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group,
-                      async_op: bool = False):
+                      async_op: bool = False, after=None):
     """Variable-split all-to-all into ``out``. The proxy copies ``inp`` across (sizes must
-    match: a balanced exchange) while modelling the time of the bytes that leave the rank."""
+    match: a balanced exchange) while modelling the time of the bytes that leave the rank.
+    ``after`` (a CUDA event recorded when ``inp`` was complete; async only): the exchange is issued
+    from :func:`launch_stream` waiting on that event alone, so compute queued on the current stream
+    after the event runs beside it. ``out`` must then have been allocated on the launch stream (or
+    before the event) -- see :func:`alloc_for_launch`."""
+    if after is not None and async_op and inp.is_cuda:
+        ls = launch_stream(inp.device)
+        ls.wait_event(after)
+        with torch.cuda.stream(ls):
+            w = all_to_all_single(out, inp, out_splits, in_splits, group, async_op=True)
+        return w
     if is_proxy(group):
         assert out.shape == inp.shape, "proxy all-to-all models a balanced exchange"
         out.copy_(inp)
         w = group._occupy(group.a2a_seconds(inp.numel() * inp.element_size()))
         return w if async_op else w.wait()
     return dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=group, async_op=async_op)
+
+
+def alloc_for_launch(shape, like: torch.Tensor):
+    """An output buffer for an ``after=`` collective: allocated from the launch stream's pool (a
+    block freed by compute-stream work queued after the event can never be handed out here) and
+    marked as used by the current stream, where its consumer runs."""
+    if not like.is_cuda:
+        return like.new_empty(shape)
+    ls = launch_stream(like.device)
+    with torch.cuda.stream(ls):
+        out = like.new_empty(shape)
+    out.record_stream(torch.cuda.current_stream(like.device))
+    return out
 
 
 def all_to_all_counts(recv: torch.Tensor, counts: torch.Tensor, group):
@@ -192,10 +229,10 @@ def all_to_all_counts(recv: torch.Tensor, counts: torch.Tensor, group):
 # ----------------------------------------------------------------- autograd pieces
 class _Box:
     """Hand-off between a collective's start and finish nodes (forward and backward)."""
-    __slots__ = ("work", "bwork", "splits", "group", "dx", "gkeep")
+    __slots__ = ("work", "bwork", "splits", "group", "dx", "gkeep", "ev", "pay", "recv", "D", "dtype")
 
     def __init__(self):
-        self.work = self.bwork = self.dx = self.gkeep = None
+        self.work = self.bwork = self.dx = self.gkeep = self.ev = self.pay = self.recv = None
 
 
 class _A2AStart(torch.autograd.Function):
@@ -206,8 +243,10 @@ class _A2AStart(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, box):
         out_splits, in_splits = box.splits
-        out = x.new_empty((sum(out_splits),) + tuple(x.shape[1:]))
-        box.work = all_to_all_single(out, x.contiguous(), out_splits, in_splits, box.group, async_op=True)
+        shape = (sum(out_splits),) + tuple(x.shape[1:])
+        out = alloc_for_launch(shape, x) if box.ev is not None else x.new_empty(shape)
+        box.work = all_to_all_single(out, x.contiguous(), out_splits, in_splits, box.group, async_op=True,
+                                     after=box.ev)
         ctx.box = box
         return out
 
@@ -240,14 +279,16 @@ class _A2AFinish(torch.autograd.Function):
         return gc, None
 
 
-def a2a_start(x, out_splits, in_splits, group):
+def a2a_start(x, out_splits, in_splits, group, after=None):
     """Start an overlappable all-to-all. Returns a handle for :func:`a2a_finish`; ops issued
     between the two (forward) -- and, in reverse, between their backward nodes -- run while
     the rows are on the wire. Autograd runs backward nodes in reverse creation order, so
     work created between start and finish in the forward lands between the reverse
-    all-to-all's launch and its wait in the backward."""
+    all-to-all's launch and its wait in the backward. ``after``: an event recorded when ``x``
+    was complete -- the exchange then starts there, not behind work queued since
+    (see :func:`all_to_all_single`)."""
     box = _Box()
-    box.splits, box.group = (list(out_splits), list(in_splits)), group
+    box.splits, box.group, box.ev = (list(out_splits), list(in_splits)), group, after
     return _A2AStart.apply(x, box), box
 
 
@@ -348,5 +389,5 @@ def grad_ar_finish(handle):
     return _GradARFinish.apply(y, box)
 
 
-__all__ = ["grad_ar_start", "grad_ar_finish", "ProxyGroup", "side_stream", "SIDE_PRIORITY", "COMM_PRIORITY", "is_proxy", "group_rank_size", "backend", "all_reduce", "all_to_all_single",
+__all__ = ["launch_stream", "alloc_for_launch", "grad_ar_start", "grad_ar_finish", "ProxyGroup", "side_stream", "SIDE_PRIORITY", "COMM_PRIORITY", "is_proxy", "group_rank_size", "backend", "all_reduce", "all_to_all_single",
            "all_to_all_counts", "a2a_start", "a2a_finish", "a2a", "ar_start", "ar_finish"]

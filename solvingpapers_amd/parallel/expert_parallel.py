@@ -11,8 +11,8 @@ The reference keeps all 8 experts on every replica and runs them in a Python loo
 3. token rows exchanged (``all_to_all_single`` with uneven splits) — they arrive
    ordered by (source rank, local expert) and are regrouped to (local expert, source)
    by one device kernel (``regroup_rows``, csrc/kernels/ep.hip; no host loop). With fp8
-   experts the payload is e4m3 rows + 1 x 128 E8M0 scales (``_Fp8DispatchW13``);
-   the combine stays bf16;
+   experts the payload is e4m3 rows + 1 x 128 E8M0 scales (``_Fp8DispatchStart`` /
+   ``_Fp8DispatchFinish``, on every path); the combine stays bf16;
 4. the local experts run as ONE grouped GEMM per projection (csrc/kernels/moe.hip);
 5. the inverse regroup + all-to-all return the rows; ``combine`` applies the gate
    weights in the original token order.
@@ -84,63 +84,83 @@ class _Regroup(torch.autograd.Function):
         return regroup_rows(g.contiguous(), ctx.rc, not ctx.to_em), None, None
 
 
-class _Fp8DispatchW13(torch.autograd.Function):
-    """fp8 dispatch fused with the first expert projection (DeepSeek-V3 sec. 3.3: dispatch in fp8,
-    combine in bf16). The sender quantizes its expert-sorted rows once (1 x 128 E8M0 tiles); the
-    all-to-all carries e4m3 bytes + scales (~0.52x the bf16 payload); the receiver regroups the
-    packed rows and feeds them straight to the block-scaled grouped GEMM. Backward: dX in fp8 on
-    the cached W^T bytes, returned in bf16 through the inverse regroup + all-to-all; dW in bf16
-    on the dequantized received rows (the same values the forward consumed)."""
+class _Fp8DispatchStart(torch.autograd.Function):
+    """fp8 dispatch, first half (DeepSeek-V3 sec. 3.3: dispatch in fp8, combine in bf16). Forward:
+    issue the all-to-all of the e4m3 + E8M0 payload the caller quantized from the expert-sorted rows
+    (``box.pay``, ~0.52x the bf16 bytes) -- from the launch stream after ``box.ev`` when given -- and
+    return an empty token carrying the autograd edge to those rows. Backward: wait for the bf16
+    reverse exchange that _Fp8DispatchFinish.backward issued and return it (the rows' gradient)."""
 
     @staticmethod
-    def forward(ctx, xp, W13, rc, send_splits, recv_splits, offsets, group):
-        D = xp.shape[1]
+    def forward(ctx, xp, box):
+        out_splits, in_splits = box.splits
+        pay = box.pay
+        box.recv = comm.alloc_for_launch((sum(out_splits), pay.shape[1]), pay) if box.ev is not None else \
+            pay.new_empty((sum(out_splits), pay.shape[1]))
+        box.work = comm.all_to_all_single(box.recv, pay, out_splits, in_splits, box.group, async_op=True, after=box.ev)
+        ctx.box = box
+        return xp.new_empty(0)
+
+    @staticmethod
+    def backward(ctx, g):
+        box = ctx.box
+        box.bwork.wait()
+        dx, box.dx, box.gkeep = box.dx, None, None
+        return dx, None
+
+
+class _Fp8DispatchFinish(torch.autograd.Function):
+    """fp8 dispatch, second half, fused with the first expert projection. Forward: wait for the
+    payload, regroup the received rows to (local expert, source) order and run the block-scaled W13
+    grouped GEMM on them. Backward: dX in fp8 on the cached W^T bytes, regrouped back and sent home
+    in bf16 (issued here, waited in _Fp8DispatchStart.backward), then dW13 while it is on the wire
+    (fp8 128 x 1 token tiles of dh and of the received rows, or bf16 on the dequantized rows)."""
+
+    @staticmethod
+    def forward(ctx, token, W13, rc, offsets, box):
+        box.work.wait()
+        D = box.D
         KB = D // 128
-        q, sx = quant_act_fp8_blk(xp)
-        pad = (-KB) % 16
-        pay = torch.cat([q.view(torch.uint8), torch.nn.functional.pad(sx, (0, pad))], 1).contiguous()
-        pr = pay.new_empty((sum(recv_splits), pay.shape[1]))
-        comm.all_to_all_single(pr, pay, recv_splits, send_splits, group)
-        pl = regroup_rows(pr, rc, True)
+        pl = regroup_rows(box.recv, rc, True)
+        box.recv = box.pay = None
         xq_l = pl[:, :D].contiguous().view(torch.float8_e4m3fn)
         sx_l = pl[:, D:D + KB].contiguous()
         wq, _, sw, _ = quant_weight_fp8_blk(W13)
         ctx.save_for_backward(xq_l, sx_l, rc, offsets)
-        ctx.W, ctx.splits, ctx.group = W13, (send_splits, recv_splits), group
-        return grouped_gemm_fp8_blk(xq_l, sx_l, wq, sw, offsets).to(xp.dtype)
+        ctx.W, ctx.box = W13, box
+        return grouped_gemm_fp8_blk(xq_l, sx_l, wq, sw, offsets).to(box.dtype)
 
     @staticmethod
     def backward(ctx, dh):
         xq_l, sx_l, rc, offsets = ctx.saved_tensors
-        W, (send_splits, recv_splits) = ctx.W, ctx.splits
+        W, box = ctx.W, ctx.box
+        out_splits, in_splits = box.splits
         from ..ops import moe as _m
         dh = dh.contiguous()
-        lplan = SimpleNamespace(offsets=offsets)
-        dxp = None
         wg8 = ctx.needs_input_grad[1] and _m._wgrad_fp8_ok(dh, xq_l, W)
         if wg8:   # fp8 dW (128 x 1 token tiles): dh's transposed image + its dX row image, one read
             poff, ld = _m.padded_offsets(offsets), _m.wgrad_ld(dh.shape[0], W.shape[0])
             dtq, dts, dq, sd = _m.quant_t_fp8_seg(dh, offsets, poff, ld, rows=True)
-        if ctx.needs_input_grad[0]:
-            if not wg8:
-                dq, sd = quant_act_fp8_blk(dh)
-            _, wtq, _, swt = quant_weight_fp8_blk(W)
-            dxl = grouped_gemm_fp8_blk(dq, sd, wtq, swt, offsets).to(dh.dtype)
-            dxr = regroup_rows(dxl, rc, False)
-            dxp = dxr.new_empty((sum(send_splits), dxr.shape[1]))
-            comm.all_to_all_single(dxp, dxr, send_splits, recv_splits, ctx.group)
+        else:
+            dq, sd = quant_act_fp8_blk(dh)
+        _, wtq, _, swt = quant_weight_fp8_blk(W)
+        dxl = grouped_gemm_fp8_blk(dq, sd, wtq, swt, offsets).to(dh.dtype)
+        dxr = regroup_rows(dxl, rc, False)
+        box.dx = dxr.new_empty((sum(in_splits), dxr.shape[1]))
+        box.gkeep = dxr                       # the source must live until the exchange is done
+        box.bwork = comm.all_to_all_single(box.dx, dxr, in_splits, out_splits, box.group, async_op=True)
         gw = None
         if wg8:   # the received rows are 1 x 128 tiles: dequantize, re-tile along tokens
             xtq, xts = _m.quant_t_fp8_seg(dequant_act_fp8_blk(xq_l, sx_l, dh.dtype), offsets, poff, ld)
             gw = _m.commit_weight_grad_fp8(W, dtq, dts, xtq, xts, poff)
         elif ctx.needs_input_grad[1]:
-            gw = commit_weight_grad(W, dh, dequant_act_fp8_blk(xq_l, sx_l, dh.dtype), lplan)
-        return dxp, gw, None, None, None, None, None
+            gw = commit_weight_grad(W, dh, dequant_act_fp8_blk(xq_l, sx_l, dh.dtype), SimpleNamespace(offsets=offsets))
+        return dh.new_empty(0), gw, None, None, None
 
 
 class EPPrep:
     """Routing plan of one token chunk, with its per-(rank, expert) counts on their way to the
-    host (``ep_prepare``); ``ep_run`` reads them after one host sync."""
+    host (``ep_prepare``); the dispatch reads them after one host sync."""
 
     def __init__(self, plan, counts=None, recv=None, host=None, ev=None):
         self.plan, self.counts, self.recv, self.host, self.ev = plan, counts, recv, host, ev
@@ -155,9 +175,7 @@ class EPPrep:
 
 def ep_prepare(idx, n_experts, group):
     """Local permutation + the count exchange of a chunk, all on the device; the counts are
-    copied to (pinned) host memory asynchronously. Issue the prepare of every chunk, plus any
-    independent work (the shared expert), before the first ``ep_run``: its host sync then
-    waits while the GPU is busy."""
+    copied to (pinned) host memory asynchronously."""
     plan = permute(idx, n_experts)
     rank, P = ep_rank_size(group)
     if P == 1:
@@ -175,81 +193,132 @@ def ep_prepare(idx, n_experts, group):
     return EPPrep(plan, counts, recv, both.clone())
 
 
-def ep_run(x, w, prep, W13, W2, n_experts, group, act="silu", fp8=False):
-    """Dispatch -> local grouped experts -> combine for a chunk prepared by ``ep_prepare``."""
-    plan = prep.plan
+class EPStage:
+    """One token chunk (e.g. one micro-batch) through an expert-parallel MoE layer, in four calls
+    that a caller interleaves with other work (models/deepseekv3.py hidden_pair):
+
+      ep_stage_prepare   routing plan, count exchange (its D2H starts), the expert-sorted rows and,
+                         fp8, their e4m3 + E8M0 payload -- all queued on the compute stream; an
+                         event marks the payload complete
+      ep_stage_dispatch  the ONE host sync of the chunk (split sizes), then the exchange, issued from
+                         the launch stream after that event: compute queued after the prepare (the
+                         shared expert, another micro-batch's attention) runs while it is on the wire
+      ep_stage_experts   wait, regroup, local grouped experts (W13 fused with the fp8 receive), and
+                         the combine exchange issued right behind them
+      ep_stage_finish    wait, weighted combine in the original token order
+
+    fp8 (default for D, 2F multiples of 128): the dispatch payload is e4m3 + 1 x 128 E8M0 scales,
+    the combine bf16. P == 1: no exchange, the same stages run the local experts."""
+
+    def __init__(self):
+        self.prep = self.xp = self.w = self.box = self.handle = self.chandle = None
+
+
+def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None):
+    st = EPStage()
+    st.prep = ep_prepare(idx, n_experts, group)
+    st.w = w
+    st.group = group
+    st.n_experts = n_experts
+    st.xp = gather(x, st.prep.plan)                          # [A, D] sorted by global expert
+    D = x.shape[-1]
+    st.fp8 = bool(fp8)
     rank, P = ep_rank_size(group)
+    st.fp8_dispatch = st.fp8 and P > 1 and D % 128 == 0 and (W13 is None or W13.shape[1] % 128 == 0)
+    if st.fp8_dispatch:
+        box = comm._Box()
+        KB = D // 128
+        q, sx = quant_act_fp8_blk(st.xp.detach())
+        pad = (-KB) % 16
+        box.pay = torch.cat([q.view(torch.uint8), torch.nn.functional.pad(sx, (0, pad))], 1).contiguous()
+        box.D, box.dtype, box.group = D, x.dtype, group
+        st.box = box
+    st.ev = None
+    if P > 1 and x.is_cuda:
+        st.ev = torch.cuda.Event()
+        st.ev.record()
+    return st
+
+
+def ep_stage_dispatch(st):
+    rank, P = ep_rank_size(st.group)
     if P == 1:
-        xp = gather(x, plan)
-        h = glu(grouped_linear(xp, W13, plan, fp8), act)
-        return combine(grouped_linear(h, W2, plan, fp8), w, plan), plan
-    El = n_experts // P
-    assert El * P == n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
-    send_splits, rc = prep.splits(P, El)                     # the single host sync of the chunk
+        return st
+    El = st.n_experts // P
+    send_splits, rc = st.prep.splits(P, El)                  # the single host sync of the chunk
     recv_splits = rc.sum(1).tolist()
-    xp = gather(x, plan)                                      # [A, D] sorted by global expert
     per_e = rc.sum(0)
     loff = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
-    dev = x.device
-    rc_dev = prep.recv.view(P, El)                           # device copy of the counts
-    lplan = SimpleNamespace(offsets=loff.to(device=dev, dtype=torch.int32))
-    D = x.shape[-1]
-    if fp8 and D % 128 == 0 and W13.shape[1] % 128 == 0:
-        # fp8 dispatch payload (e4m3 rows + E8M0 tile scales), fused with the W13 projection
-        h13 = _Fp8DispatchW13.apply(xp, W13, rc_dev, send_splits, recv_splits, lplan.offsets, group)
+    st.splits = (send_splits, recv_splits)
+    st.rc_dev = st.prep.recv.view(P, El)                     # device copy of the counts
+    st.lplan = SimpleNamespace(offsets=loff.to(device=st.xp.device, dtype=torch.int32))
+    if st.fp8_dispatch:
+        st.box.splits = (recv_splits, send_splits)
+        st.box.ev = st.ev
+        st.token = _Fp8DispatchStart.apply(st.xp, st.box)
     else:
-        xr = all_to_all(xp, recv_splits, send_splits, group)  # [R, D] (src, e_local) order
-        xl = _Regroup.apply(xr, rc_dev, True)                 # (src, e) -> (e, src) rows
-        h13 = grouped_linear(xl, W13, lplan, fp8)
+        st.handle = comm.a2a_start(st.xp, recv_splits, send_splits, st.group, after=st.ev)
+    return st
+
+
+def ep_stage_experts(st, W13, W2, act="silu"):
+    rank, P = ep_rank_size(st.group)
+    if P == 1:
+        plan = st.prep.plan
+        h = glu(grouped_linear(st.xp, W13, plan, st.fp8), act)
+        st.yp = grouped_linear(h, W2, plan, st.fp8)
+        return st
+    El = st.n_experts // P
+    assert El * P == st.n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
+    send_splits, recv_splits = st.splits
+    if st.fp8_dispatch:
+        h13 = _Fp8DispatchFinish.apply(st.token, W13, st.rc_dev, st.lplan.offsets, st.box)
+    else:
+        xl = _Regroup.apply(comm.a2a_finish(st.handle), st.rc_dev, True)   # (src, e) -> (e, src) rows
+        h13 = grouped_linear(xl, W13, st.lplan, st.fp8)
     h = glu(h13, act)
-    yl = grouped_linear(h, W2, lplan, fp8)
-    yr = _Regroup.apply(yl, rc_dev, False)
-    yp = all_to_all(yr, send_splits, recv_splits, group)
-    return combine(yp, w, plan), plan
+    yr = _Regroup.apply(grouped_linear(h, W2, st.lplan, st.fp8), st.rc_dev, False)
+    st.chandle = comm.a2a_start(yr, send_splits, recv_splits, st.group)
+    return st
 
 
-def ep_run_interleaved(parts, ws, preps, W13, W2, n_experts, group, act="silu", fp8=False, shared=None):
-    """Token chunks of ONE MoE layer on ONE compute stream, their all-to-alls interleaved so
-    that each exchange is on the wire while another chunk's experts compute:
+def ep_stage_finish(st):
+    rank, P = ep_rank_size(st.group)
+    yp = st.yp if P == 1 else comm.a2a_finish(st.chandle)
+    y = combine(yp, st.w, st.prep.plan)
+    st.xp = st.yp = st.handle = st.chandle = st.box = st.token = None
+    return y
 
-        start dispatch(0..n-1), shared(first half) | for c: finish dispatch(c), experts(c),
-        start combine(c) | shared(second half) | for c: finish combine(c), combine(c)
 
-    (comm.a2a_start / a2a_finish; autograd replays the same interleave in reverse, each
-    reverse exchange launched before the other chunks' backward and waited after it). One
-    stream, so chunks never compete for the CUs the way two concurrent grouped GEMMs do.
-    ``shared(x_part)`` (the shared expert) covers the first dispatch and the last combine.
-    Returns the per-chunk outputs (shared expert added)."""
-    from . import comm as _c
-    rank, P = ep_rank_size(group)
-    El = n_experts // P
-    assert El * P == n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
+def ep_run(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
+    """Dispatch -> local grouped experts -> combine of one chunk, stage after stage (blocking).
+    Returns (y, plan)."""
+    st = ep_stage_prepare(x, idx, w, n_experts, group, fp8, W13)
+    ep_stage_experts(ep_stage_dispatch(st), W13, W2, act)
+    plan = st.prep.plan
+    return ep_stage_finish(st), plan
+
+
+def ep_run_interleaved(parts, idxs, ws, W13, W2, n_experts, group, act="silu", fp8=False, shared=None):
+    """Token chunks of ONE MoE layer, their exchanges interleaved on one compute stream:
+    prepare all | shared(chunk 0) | dispatch all | for c: experts(c) | shared(others) | finish all.
+    Splitting a layer's tokens costs grouped-GEMM efficiency (fewer rows per expert), so the model
+    overlaps micro-batches instead (DeepSeekV3.forward_pair); kept for ``ep_chunks > 1``."""
     n = len(parts)
-    meta, hd = [], []
-    for i in range(n):
-        send_splits, rc = preps[i].splits(P, El)
-        recv_splits = rc.sum(1).tolist()
-        per_e = rc.sum(0)
-        loff = torch.cat([per_e.new_zeros(1), per_e.cumsum(0)])
-        lplan = SimpleNamespace(offsets=loff.to(device=parts[i].device, dtype=torch.int32))
-        meta.append((send_splits, recv_splits, preps[i].recv.view(P, El), lplan))
-        hd.append(_c.a2a_start(gather(parts[i], preps[i].plan), recv_splits, send_splits, group))
+    sts = [ep_stage_prepare(parts[i], idxs[i], ws[i], n_experts, group, fp8, W13) for i in range(n)]
     sh = [None] * n
-    if shared is not None:                                   # under the first dispatch
-        sh[0] = shared(parts[0])
-    hc = []
-    for i in range(n):
-        send_splits, recv_splits, rc_dev, lplan = meta[i]
-        xl = _Regroup.apply(_c.a2a_finish(hd[i]), rc_dev, True)
-        h = glu(grouped_linear(xl, W13, lplan, fp8), act)
-        yr = _Regroup.apply(grouped_linear(h, W2, lplan, fp8), rc_dev, False)
-        hc.append(_c.a2a_start(yr, send_splits, recv_splits, group))
-    if shared is not None:                                   # under the last combines
+    if shared is not None:
+        sh[0] = shared(parts[0])                             # queued before the first host sync
+    for st in sts:
+        ep_stage_dispatch(st)
+    for st in sts:
+        ep_stage_experts(st, W13, W2, act)
+    if shared is not None:
         for i in range(1, n):
             sh[i] = shared(parts[i])
     out = []
-    for i in range(n):
-        y = combine(_c.a2a_finish(hc[i]), ws[i], preps[i].plan)
+    for i, st in enumerate(sts):
+        y = ep_stage_finish(st)
         out.append(y + sh[i] if sh[i] is not None else y)
     return out
 
@@ -258,7 +327,7 @@ def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
     [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
     ``W2`` [E/P, D, F] are this rank's experts. Returns (y [N, D], local plan)."""
-    return ep_run(x, w, ep_prepare(idx, n_experts, group), W13, W2, n_experts, group, act, fp8)
+    return ep_run(x, idx, w, W13, W2, n_experts, group, act, fp8)
 
 
 def shard_experts(full_w, rank, P):

@@ -41,10 +41,9 @@ class ProcessGroups:
     dp_group: Optional[object] = None
     ep_group: Optional[object] = None
     expert_dp_group: Optional[object] = None
-    # second communicators over the same TP / EP ranks (two-chunk comm/compute pipelines:
-    # models/gemma.py tp_group2, models/deepseekv3.py ep_group2); None unless requested
+    # second communicator over the same TP ranks (two-chunk comm/compute pipeline,
+    # models/gemma.py tp_group2); None unless requested
     tp_group2: Optional[object] = None
-    ep_group2: Optional[object] = None
     tp_ranks: Optional[List[int]] = None
     dp_ranks: Optional[List[int]] = None
     ep_ranks: Optional[List[int]] = None
@@ -90,14 +89,14 @@ def _hp_options(kind):
 
 
 def build_groups(tp: int = 1, ep: int = 1, pipeline: bool = False) -> ProcessGroups:
-    """``pipeline``: also build a second communicator for every TP and EP group (each chunk of
-    the two-chunk pipelines runs its collectives on its own RCCL communicator / stream)."""
+    """``pipeline``: also build a second communicator for every TP group (each chunk of the
+    two-chunk TP pipeline runs its collectives on its own RCCL communicator / stream)."""
     initialized = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size() if initialized else 1
     rank = dist.get_rank() if initialized else 0
     lay = layout_ranks(world, tp, ep)
     mine = {}
-    kinds = ("tp", "dp", "ep", "expert_dp") + (("tp2", "ep2") if pipeline else ())
+    kinds = ("tp", "dp", "ep", "expert_dp") + (("tp2",) if pipeline else ())
     for kind in kinds:
         for ranks in lay[kind.rstrip("2")]:
             # new_group is collective over the WORLD: create every group on every rank, in order
@@ -110,5 +109,5 @@ def build_groups(tp: int = 1, ep: int = 1, pipeline: bool = False) -> ProcessGro
         tp_rank=tp_ranks.index(rank), dp_rank=dp_ranks.index(rank), ep_rank=ep_ranks.index(rank),
         tp_group=mine["tp"][0], dp_group=mine["dp"][0], ep_group=mine["ep"][0],
         expert_dp_group=mine["expert_dp"][0],
-        tp_group2=mine["tp2"][0] if pipeline else None, ep_group2=mine["ep2"][0] if pipeline else None,
+        tp_group2=mine["tp2"][0] if pipeline else None,
         tp_ranks=tp_ranks, dp_ranks=dp_ranks, ep_ranks=ep_ranks, expert_dp_ranks=mine["expert_dp"][1])

@@ -104,8 +104,7 @@ def _lm(args, info):
             V, T, B = c.vocab_size, args.seq or c.max_seq_len, c.batch_size
     elif fam == "dsv3":
         c = deepseekv3.config(args.preset or "dsv3_ref", **sets)
-        model = deepseekv3.DeepSeekV3(c, device=dev, dtype=dtype, seed=args.seed, ep_group=pg.ep_group,
-                                      ep_group2=pg.ep_group2)
+        model = deepseekv3.DeepSeekV3(c, device=dev, dtype=dtype, seed=args.seed, ep_group=pg.ep_group)
         V, T, B = c.vocab_size, c.block_size, c.batch_size
     else:
         raise SystemExit(f"unknown model {fam}")

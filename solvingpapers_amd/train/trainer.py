@@ -29,7 +29,6 @@ from ..parallel.data_parallel import DataParallel
 from ..utils.flat import FlatParams
 from ..utils.prof import annotate
 from . import checkpoint as ckpt
-from ..ops.moe import defer_expert_wgrad, flush_expert_wgrad
 from .optim import FlatAdamW, FlatSGD, cosine_lr
 
 
@@ -37,9 +36,9 @@ from .optim import FlatAdamW, FlatSGD, cosine_lr
 class TrainConfig:
     steps: int = 1000
     grad_accum: int = 1
-    # routed-expert weight gradients of the inner micro-batches deferred to the last one (one
-    # long-K grouped GEMM per weight, ops/moe.py defer_expert_wgrad); costs the kept activations
-    defer_expert_wgrad: bool = False
+    # models with forward_pair (DeepSeek-V3): micro-batches run in layer-interleaved pairs so each
+    # expert-parallel all-to-all overlaps the other micro-batch's compute (even grad_accum only)
+    pair_microbatches: bool = True
     optimizer: str = "adamw"            # adamw | adam | sgd
     lr: float = 3e-4
     min_lr: Optional[float] = None       # None -> constant LR
@@ -159,6 +158,9 @@ class Trainer:
         return cosine_lr(step, c.lr, c.warmup, c.steps, c.min_lr)
 
     def buffers(self):
+        fin = getattr(self.model, "finish_pending_updates", None)
+        if fin is not None:
+            fin()                             # in-flight routing-bias updates land first
         return {n: b for n, b in self.model.named_buffers() if n.endswith("routing_bias")}
 
     def log(self, rec):
@@ -204,6 +206,9 @@ class Trainer:
         if self.eval_batch is None:
             return None
         self.flat.wait_all()
+        fin = getattr(self.model, "finish_pending_updates", None)
+        if fin is not None:
+            fin()
         was = self.model.training
         self.model.eval()
         tot = 0.0
@@ -231,19 +236,22 @@ class Trainer:
         self.opt.zero_grad()
         tot = None
         ntok = 0
-        for mi in range(c.grad_accum):
-            x, y = self.train_batch(step * c.grad_accum + mi)
-            ntok += c.tokens_per_sample * x.shape[0] if c.tokens_per_sample else x.numel()
-            self._last_seq = x.shape[1] if x.dim() > 1 else 1
-            last = mi == c.grad_accum - 1
+        pair = (c.pair_microbatches and c.grad_accum % 2 == 0 and hasattr(self.model, "forward_pair")
+                and self.model.training)
+        n = 2 if pair else 1
+        for mi in range(0, c.grad_accum, n):
+            xs = [self.train_batch(step * c.grad_accum + mi + j) for j in range(n)]
+            for x, _ in xs:
+                ntok += c.tokens_per_sample * x.shape[0] if c.tokens_per_sample else x.numel()
+                self._last_seq = x.shape[1] if x.dim() > 1 else 1
+            last = mi + n == c.grad_accum
             ctx = self.dp.no_sync() if (self.dp is not None and not last) else _null()
-            with ctx, defer_expert_wgrad(c.defer_expert_wgrad and not last):
+            with ctx:
                 with annotate("forward"):
-                    loss = self.model(x, y)
+                    loss = self.model.forward_pair(*xs[0], *xs[1]) if pair else self.model(*xs[0])
                 with annotate("backward"):
                     (loss / c.grad_accum).backward()
             tot = loss.detach() if tot is None else tot + loss.detach()
-        flush_expert_wgrad()                 # no-op unless a kept weight missed the last micro-batch
         if self.dp is not None:
             with annotate("grad_sync"):
                 self.dp.finish_grad_sync()

@@ -34,18 +34,26 @@ def test_proxy_group_tp_gemma_pipelined_matches_plain(schedule, nb):
     assert g1.calls > 0 and g2.calls > 0                              # both chunks' collectives ran
 
 
-def test_proxy_group_ep_moe_pipelined_matches_plain():
+def test_proxy_group_ep_forward_pair_matches_plain():
+    """EP=8 on the stand-in group: DeepSeekV3.forward_pair (micro-batches interleaved) == two
+    plain forward() calls -- loss and expert / dense gradients -- and the exchanges ran."""
     from solvingpapers_amd.models import deepseekv3 as ds
-    c = ds.config("dsv3_tiny", dim=32, n_experts=16, top_k=2, n_shared=1, expert_hidden=24, aux_free=False)
-    g1, g2 = ProxyGroup(8, "cpu"), ProxyGroup(8, "cpu")
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = ds.config("dsv3_tiny", vocab_size=64, dim=32, n_heads=2, kv_lora_rank=16, qk_nope_dim=8, qk_rope_dim=8,
+                  v_head_dim=16, n_experts=16, top_k=2, n_shared=1, expert_hidden=24, dense_hidden=48, n_layers=2,
+                  n_dense_layers=1, aux_free=False, mtp_heads=0)
+    g1 = ProxyGroup(8, "cpu")
+    ids = torch.randint(0, 64, (2, 2, 13), generator=torch.Generator().manual_seed(1))
     outs = []
-    for pipe in (False, True):
-        m = ds.MoE(c, ep_group=g1, ep_group2=g2 if pipe else None, ep_schedule="two_stream" if pipe else None)
-        m.reset_parameters(0.1, torch.Generator().manual_seed(3))
-        assert m.w13.shape[0] == 2                                    # 16 experts / EP 8
-        x = torch.randn(2, 6, 32, generator=torch.Generator().manual_seed(1)).requires_grad_()
-        y = m(x)
-        y.square().sum().backward()
-        outs.append((y.detach(), x.grad, m.w13.grad.clone(), m.gate.grad.clone()))
-    for a, b in zip(*outs):
-        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
+    for pair in (False, True):
+        m = ds.DeepSeekV3(c, seed=3, ep_group=g1)
+        assert m.layers[1].ffn.w13.shape[0] == 2                       # 16 experts / EP 8
+        FlatParams(m)
+        x0, y0, x1, y1 = ids[0, :, :-1], ids[0, :, 1:], ids[1, :, :-1], ids[1, :, 1:]
+        loss = m.forward_pair(x0, y0, x1, y1) if pair else m(x0, y0) + m(x1, y1)
+        loss.backward()
+        outs.append((loss.item(), {n: p.main_grad.clone() for n, p in m.named_parameters()}))
+    assert abs(outs[0][0] - outs[1][0]) < 1e-5
+    for n, g in outs[0][1].items():
+        assert torch.allclose(g, outs[1][1][n], atol=1e-5, rtol=1e-4), n
+    assert g1.calls > 0

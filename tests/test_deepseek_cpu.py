@@ -243,24 +243,21 @@ def test_moe_ops_match_dense_loop():
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)
 
 
-def test_defer_expert_wgrad_is_exact_noop_off_gpu():
-    """defer_expert_wgrad() only engages on the GPU kernels (ops/moe.py): on CPU an accumulation
-    loop under it gives bitwise the gradients of the plain loop and leaves nothing pending."""
-    from solvingpapers_amd.ops import moe as M
-    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0, mtp_heads=0)
-    grads = []
-    for defer in (False, True):
+def test_trainer_pairs_microbatches_like_one_by_one():
+    """Trainer.pair_microbatches (DeepSeekV3.forward_pair on each two micro-batches of an even
+    grad_accum) trains to the same parameters as the one-by-one loop."""
+    from solvingpapers_amd.train.trainer import TrainConfig, Trainer
+    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0, aux_free=False)
+    gen = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, c.vocab_size, (8, 2, 33), generator=gen)
+    params = []
+    for pair in (False, True):
         m = ds.DeepSeekV3(c, seed=0)
-        gen = torch.Generator().manual_seed(1)
-        for i in range(2):
-            ids = torch.randint(0, c.vocab_size, (2, 33), generator=gen)
-            with M.defer_expert_wgrad(defer and i == 0):
-                (m(ids[:, :-1], ids[:, 1:]) / 2).backward()
-        assert not M._Defer.pending and M._Defer.depth == 0
-        grads.append([p.grad.clone() for p in m.parameters() if p.grad is not None])
-    assert len(grads[0]) == len(grads[1])
-    for a, b in zip(*grads):
-        assert torch.equal(a, b)
+        tr = Trainer(m, TrainConfig(steps=2, grad_accum=4, lr=1e-3, pair_microbatches=pair),
+                     lambda i: (ids[i, :, :-1], ids[i, :, 1:]))
+        tr.fit()
+        params.append(tr.flat.param.clone())
+    assert torch.allclose(params[0], params[1], atol=1e-6)
 
 
 @pytest.mark.parametrize("which", ["dsv3", "llama3"])

@@ -461,29 +461,47 @@ def test_grouped_gemm8_wgrad_multi_sources():
     assert torch.equal(one, M.grouped_gemm(srcs[0][0], srcs[0][1], srcs[0][2], 2))
 
 
-def test_deferred_expert_wgrad_matches_per_microbatch():
-    """An accumulation loop with the inner micro-batches under defer_expert_wgrad() gives the same
-    expert weight gradients as committing each micro-batch (fp32 oracle for both), and the other
-    parameters' gradients are unchanged."""
+@pytest.mark.parametrize("ep,fp8", [(1, False), (8, False), (8, True)])
+def test_forward_pair_matches_two_forwards_gpu(ep, fp8):
+    """DeepSeekV3.forward_pair on the GPU kernels == two forward() calls: loss and every gradient.
+    ep=8 runs one rank's share on the one-GPU stand-in group (parallel/comm.ProxyGroup, modelled
+    collectives on a comm stream): the dispatch is issued from the launch stream after the payload
+    event, the combine from the compute stream -- overlap paths, identical values. fp8: the
+    dispatch payload is e4m3 + E8M0 (checked by dtype)."""
     from solvingpapers_amd.models import deepseekv3 as ds
+    from solvingpapers_amd.parallel import comm
     from solvingpapers_amd.utils.flat import FlatParams
     from solvingpapers_amd.utils.grad import next_generation
-    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0, mtp_heads=0)
-    grads = []
-    for defer in (False, True):
-        m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=0)
-        flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.float32)
-        flat.grad.zero_()
-        next_generation()
-        gen = torch.Generator().manual_seed(3)
-        for i in range(3):
-            ids = torch.randint(0, c.vocab_size, (2, 65), generator=gen).to(dev)
-            with M.defer_expert_wgrad(defer and i < 2):
-                (m(ids[:, :-1], ids[:, 1:]) / 3).backward()
-        assert not M._Defer.pending
-        grads.append({n: p.main_grad.float().clone() for n, p in m.named_parameters()})
-    for n, g0 in grads[0].items():
-        g1 = grads[1][n]
-        if g0.abs().max() == 0:
-            continue
-        assert _rel(g1, g0) < (2e-2 if g0.dim() == 3 else 1e-5), n      # routed experts: [E, out, in]
+    c = ds.config("dsv3_tiny", dim=256, n_heads=4, n_experts=16, top_k=2, expert_hidden=256, dense_hidden=512,
+                  n_layers=3, n_dense_layers=1, dropout=0.0, attn_dropout=0.0, aux_free=False, moe_fp8=fp8,
+                  mtp_heads=1)
+    grp = comm.ProxyGroup(ep, dev) if ep > 1 else None
+    seen = []
+    real = comm.all_to_all_single
+
+    def spy(out, inp, out_splits, in_splits, group, async_op=False, after=None):
+        seen.append(inp.dtype)
+        return real(out, inp, out_splits, in_splits, group, async_op=async_op, after=after)
+    comm.all_to_all_single = spy
+    try:
+        gen = torch.Generator().manual_seed(4)
+        ids = torch.randint(0, c.vocab_size, (2, 2, 129), generator=gen).to(dev)
+        res = []
+        for pair in (False, True):
+            m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=2, ep_group=grp)
+            flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.float32)
+            flat.grad.zero_()
+            next_generation()
+            x0, y0, x1, y1 = ids[0, :, :-1], ids[0, :, 1:], ids[1, :, :-1], ids[1, :, 1:]
+            loss = m.forward_pair(x0, y0, x1, y1) if pair else m(x0, y0) + m(x1, y1)
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append((float(loss), flat.grad.clone()))
+    finally:
+        comm.all_to_all_single = real
+    assert abs(res[0][0] - res[1][0]) < 1e-2 * abs(res[0][0])
+    assert _rel(res[1][1], res[0][1]) < 2e-2
+    if ep > 1:
+        assert (torch.uint8 in seen) == fp8                   # fp8 payload on the default path
+
+

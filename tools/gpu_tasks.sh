@@ -22,6 +22,8 @@
 #   g8-e2e         dsv3_style (accum 4) and ViT-B/16 with the shipped gemm8 vs the round-2 one, ABBA
 #   gemm-pmc       gemm8 vs hipBLASLt on a dense 8192^3 + one counter pass
 #   attn-ds        dS-materialising backward: GPU tests, attention ABBA vs the dq kernel, headline bench
+#   attn-quick     attention GPU tests, packed-layout ABBA vs the dq kernel, per-kernel times
+#   ep-pair        micro-batch-pair EP overlap: MoE GPU tests, EP=8 proxy, dsv3_style pairs vs one-by-one ABBA
 #   headline-ab ENV  bench.py default vs ENV=VAL, separate processes in ABBA order
 #   attn-pmc       attention counters + clocks in the headline step (4 layers) and in isolation; GEMM-interleaved timing
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
@@ -101,6 +103,26 @@ attn-ds)
   grep -h 'attn B\|after a GEMM\|with SPA' ${O}_ab.log | cut -c1-300
   run 400 ${O}_bench.log python -u bench.py --steps 6 --warmup 2
   jsonl ${O}_bench.log ;;
+attn-quick)
+  # attention GPU tests + packed-layout ABBA vs the dq kernel + per-kernel times
+  run 300 ${O}_pytest.log python -u -m pytest tests/test_kernels_gpu.py -k "ds_path or flash" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 200 ${O}_ab.log python -u tools/bench_attn.py --iters 20 --packed --ab SPA_ATTN_DQ_DS=0
+  grep -h 'attn B\|with SPA' ${O}_ab.log | cut -c1-300
+  run 200 ${O}_prof.log rocprofv3 --kernel-trace --stats -d /tmp/$task -o run -- python3 tools/bench_attn.py --iters 10 --packed
+  python tools/rocpd_summary.py /tmp/$task/run_results.db --top 8 > ${O}_summary.txt 2>&1
+  head -14 ${O}_summary.txt | cut -c1-150 ;;
+ep-pair)
+  # micro-batch-pair EP overlap: GPU tests, the 1-GPU EP=8 proxy, dsv3_style accum 4 pairs vs one by one (ABBA)
+  run 400 ${O}_pytest.log python -u -m pytest tests/test_moe_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 500 ${O}_proxy.log python -u tools/overlap_proxy.py --which ep --layers 2
+  grep -v amdgpu.ids ${O}_proxy.log | cut -c1-900
+  for arm in pair one one pair; do
+    flag=""; [ $arm = one ] && flag="--no-pair"
+    run 300 ${O}_$arm.log python -u bench/dsv3_train.py --preset dsv3_style --steps 3 --warmup 1 --accum 4 $flag
+    echo "$arm $(grep -ho '"value": [0-9.]*' ${O}_$arm.log)"
+  done ;;
 headline-ab)
   # headline bench.py A/B of one env switch, separate processes in ABBA order: headline-ab SPA_X=v
   ab=${1:?SPA_X=v}

@@ -9,14 +9,15 @@ xGMI at the modelled bandwidth (``--ar-gbps`` RCCL all-reduce bus bandwidth,
 ``--a2a-gbps`` all-to-all bytes leaving a rank per second -- inputs, not measurements).
 
 Arms (fwd + bwd, same process, interleaved rounds):
-  compute       plain layer, collectives skipped                      (proxy mode "off")
-  blocking      plain layer, collectives modelled, each one waited    (= compute + comm)
-  <form>:overlap  a two-chunk form, collectives modelled and overlapped (models/gemma.py,
-                models/deepseekv3.py: TP interleave / two_stream; EP interleaved2/4 / two_stream)
-  <form>:off    the same form with collectives skipped                (chunking's own cost)
+  compute / off   plain layers, collectives skipped                     (proxy mode "off")
+  blocking        plain layers, collectives modelled, each one waited   (= compute + comm)
+  <form>:overlap  an overlapping form, collectives modelled and overlapped (TP: models/gemma.py
+                  interleave / two_stream; EP: DeepSeekV3.forward_pair, two micro-batches)
+  <form>:off      the same form with collectives skipped                (the form's own cost)
 
 hidden = 1 - (overlap - off) / (blocking - compute): the fraction of the collective time that
-no longer adds to the layer time. One JSON line per config.
+no longer adds to the layer time; vs_blocking / pair_vs_blocking: overlapped time over blocking
+time, the headline figure. One JSON line per config.
 
   python tools/overlap_proxy.py [--which tp,ep] [--layers 2] [--seq 8192]
 """
@@ -118,64 +119,57 @@ def tp_gemma(a):
 
 
 def ep_moe(a):
-    """Variants: plain (one exchange per layer), one-stream interleaved chunks (2 and 4), and two
-    chunks on two streams / communicators; each timed with collectives modelled and skipped."""
+    """EP=8 DeepSeek-V3 widths, one rank's share: ``--layers`` decoder layers (MLA attention +
+    MoE with 32 of 256 routed experts, top-8, 1 shared; --fp8: e4m3 dispatch payload and expert
+    GEMMs), two micro-batches of ``--tokens`` tokens per step, fwd + bwd. Arms:
+      off / blocking   the micro-batches one after the other (forward()), collectives skipped /
+                       modelled and waited at once
+      pair:off / pair:overlap   DeepSeekV3.forward_pair (layer-interleaved micro-batches)"""
     from solvingpapers_amd.models import deepseekv3 as ds
     dev = torch.device("cuda")
-    c = ds.config("dsv3_v3", moe_fp8=a.fp8)
+    c = ds.config("dsv3_v3", moe_fp8=a.fp8, n_layers=a.layers, n_dense_layers=0, mtp_heads=0,
+                  vocab_size=1024, block_size=a.tokens)
     g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
-    g2 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
-    variants = {"plain": dict(ep_chunks=1), "interleaved2": dict(ep_chunks=2), "interleaved4": dict(ep_chunks=4),
-                "two_stream": dict(ep_group2=g2, ep_schedule="two_stream")}
-    if a.variants:
-        variants = {k: v for k, v in variants.items() if k in a.variants.split(",") or k == "plain"}
-    mods = {}
-    for name, kw in variants.items():
-        m = ds.MoE(c, ep_group=g1, device=dev, dtype=torch.bfloat16, **kw)
-        m.reset_parameters(0.02, torch.Generator(device=dev).manual_seed(3))
-        FlatParams(m, grad_dtype=torch.bfloat16)
-        mods[name] = m.train()
-    x = (torch.randn(1, a.tokens, c.dim, device=dev) * 0.5).bfloat16().requires_grad_()
-    gy = torch.randn_like(x)
+    m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=3, ep_group=g1).train()
+    FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
+    ids = torch.randint(0, c.vocab_size, (2, 1, a.tokens + 1), device=dev)
+    x0, y0, x1, y1 = ids[0, :, :-1], ids[0, :, 1:], ids[1, :, :-1], ids[1, :, 1:]
 
-    def step_of(m):
+    def step_of(pair):
         def step():
             from solvingpapers_amd.utils.grad import next_generation
             next_generation()
-            x.grad = None
-            m(x).backward(gy)
+            if pair:
+                m.forward_pair(x0, y0, x1, y1).backward()
+            else:
+                m(x0, y0).backward()
+                m(x1, y1).backward()
         return step
 
-    arms = {}
-    for name, m in mods.items():
-        arms[name + ":off"] = (step_of(m), "off")
-        arms[name + ":overlap" if name != "plain" else "plain:blocking"] = (step_of(m), "overlap" if name != "plain" else "blocking")
+    arms = {"off": (step_of(False), "off"), "blocking": (step_of(False), "blocking"),
+            "pair:off": (step_of(True), "off"), "pair:overlap": (step_of(True), "overlap")}
     if ARMS:
         arms = {k: v for k, v in arms.items() if k in ARMS}
     res = {k: [] for k in arms}
     comm = 0.0
     for r in range(a.rounds):
         for k, (fn, mode) in arms.items():
-            for g in (g1, g2):
-                g.mode = mode
+            g1.mode = mode
             fn()
-            for g in (g1, g2):
-                g.reset_stats()
+            g1.reset_stats()
             res[k].append(_time(fn, a.iters))
-            if k == "plain:blocking":
-                comm = (g1.modelled_s + g2.modelled_s) * 1e3 / a.iters
+            if k == "blocking":
+                comm = g1.modelled_s * 1e3 / a.iters
     med = {k: round(statistics.median(v), 3) for k, v in res.items()}
-    out = {"config": f"dsv3_v3 MoE layer EP=8 local shard (32 of 256 experts, top-8, D 7168, F 2048, 1 shared)"
-                     f"{' fp8' if a.fp8 else ''}", "tokens": a.tokens, "ms": med, "modelled_comm_ms": round(comm, 3)}
+    out = {"config": f"dsv3_v3 widths EP=8 local shard, {a.layers} MLA+MoE layers (32 of 256 experts, top-8, D 7168, "
+                     f"F 2048, 1 shared){' fp8' if a.fp8 else ''}, 2 micro-batches x {a.tokens} tokens",
+           "ms": med, "modelled_comm_ms": round(comm, 3)}
     if not ARMS:
-        total = med["plain:blocking"] - med["plain:off"]
+        total = med["blocking"] - med["off"]
         out["comm_added_blocking_ms"] = round(total, 3)
-        for name in variants:
-            if name == "plain":
-                continue
-            exposed = med[name + ":overlap"] - med[name + ":off"]
-            out[f"hidden_{name}"] = round(1 - exposed / total, 3) if total > 0 else None
-            out[f"vs_blocking_{name}"] = round(med["plain:blocking"] / med[name + ":overlap"], 3)
+        out["pair_compute_cost_ms"] = round(med["pair:off"] - med["off"], 3)
+        out["hidden_pair"] = round(1 - (med["pair:overlap"] - med["pair:off"]) / total, 3) if total > 0 else None
+        out["pair_vs_blocking"] = round(med["pair:overlap"] / med["blocking"], 3)
     return out
 
 
@@ -186,15 +180,15 @@ def main():
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--batch", type=int, default=1, help="TP: sequences per step (even: the pipeline splits by batch)")
     ap.add_argument("--tokens", type=int, default=4096)
-    ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--fp8", action="store_true", default=True, help="EP: fp8 experts + dispatch (config #5)")
+    ap.add_argument("--bf16", dest="fp8", action="store_false")
     ap.add_argument("--ar-gbps", type=float, default=300.0)
     ap.add_argument("--a2a-gbps", type=float, default=300.0)
     ap.add_argument("--nwg", type=int, default=16)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--arms", default="", help="comma list of arm names (default all), e.g. interleave:overlap")
-    ap.add_argument("--variants", default="", help="EP: subset of interleaved2,interleaved4,two_stream; "
-                                                   "TP: subset of interleave,two_stream")
+    ap.add_argument("--variants", default="", help="TP: subset of interleave,two_stream")
     a = ap.parse_args()
     global ARMS
     ARMS = [x for x in a.arms.split(",") if x] or None
