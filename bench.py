@@ -82,6 +82,9 @@ def main(argv=None):
     ap.add_argument("--zero1", action="store_true")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (NOT for headline runs)")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the main stream")
+    ap.add_argument("--grad-fp32", action="store_true", default=os.environ.get("SPA_GRAD_FP32") == "1",
+                    help="fp32 main gradients (accumulated and all-reduced in fp32) instead of bf16 "
+                         "(env SPA_GRAD_FP32=1)")
     ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (default tuning/tunableop_llama8b.csv; "
                     "SPA_GEMM_TUNING=0 disables)")
     a = ap.parse_args(argv)
@@ -120,7 +123,8 @@ def run(a):
     cfg = llama3.config(a.model, max_seq_len=a.seq, **kw)
     dtype = torch.bfloat16 if cuda else torch.float32
     model = llama3.Llama3(cfg, device=dev, dtype=dtype, seed=1234)
-    flat = FlatParams(model, groups=model.param_groups(), grad_dtype=dtype, align=64 * world)
+    gdt = torch.float32 if a.grad_fp32 else dtype
+    flat = FlatParams(model, groups=model.param_groups(), grad_dtype=gdt, align=64 * world)
     dp = DataParallel(model, flat, zero1=a.zero1) if world > 1 else None
     if dp is not None:
         dp.broadcast_params(0)
@@ -206,7 +210,12 @@ def run(a):
             "world_size": world,
             "backend": tdist.get_backend() if tdist.is_initialized() else "none",
             "device_count": torch.cuda.device_count() if cuda else 0,
+            "grad_dtype": str(gdt).replace("torch.", ""),
             "streamk_data_parallel": os.environ.get("TENSILE_STREAMK_DATA_PARALLEL"),
+            # the communication / runtime knobs of this run (RCCL, HIP IPC, hipBLASLt, torch c10d)
+            "env": {k: v for k, v in sorted(os.environ.items())
+                    if k.startswith(("NCCL_", "RCCL_", "TORCH_NCCL_", "TENSILE_", "HSA_ENABLE_IPC", "GPU_MAX_HW_QUEUES",
+                                     "PYTORCH_TUNABLEOP", "SPA_"))},
             "launcher": "bench.py self-launch" if os.environ.get("SPA_BENCH_SELF") else
                         ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "direct"),
         }

@@ -1,5 +1,4 @@
-// Flash-attention kernel parameters shared by attention.hip and attention_bwd4.hip (the dK/dV
-// kernel built with the max-ILP machine scheduler in its own translation unit).
+// Flash-attention kernel parameters and device helpers shared by the attention kernels.
 #pragma once
 #include "attn_common.h"
 
@@ -91,8 +90,5 @@ __device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 
   }
 }
 
-
-// attention_bwd4.hip: one-wave-per-SIMD dK/dV for head dim 128
-void launch_dkdv4_128(const AttnParams& p, bool causal, int grid, hipStream_t st);
 
 }  // namespace spa

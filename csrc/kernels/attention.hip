@@ -1760,11 +1760,8 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
   else attn_bwd_dq_kernel<HDK, HDV, NW, false, DROP><<<grid, NW * 64, 0, st>>>(p);
   if (p.Tk == 0) return;
   const bool paired = PAIRED_OK && dkdv_mode == 2;
-  const bool single4 = PAIRED_OK && HDK == 128 && dkdv_mode == 4;
   const bool piped = PAIRED_OK && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
-  if (single4) {
-    if constexpr (PAIRED_OK && HDK == 128) launch_dkdv4_128(p, causal, g2, st);   // attention_bwd4.hip
-  } else if (piped) {
+  if (piped) {
     if constexpr (PAIRED_OK) {
       if (causal) attn_bwd_dkdv3_kernel<HDK, true><<<g2, 512, 0, st>>>(p);
       else attn_bwd_dkdv3_kernel<HDK, false><<<g2, 512, 0, st>>>(p);

@@ -25,10 +25,8 @@ CSRC = ROOT / "csrc"
 BUILD = ROOT / "build"
 OUT = PKG / "_C.so"
 ARCH = os.environ.get("SPA_OFFLOAD_ARCH", "gfx950")
-# per-file device flags. attention_bwd4.hip (one-wave-per-SIMD dK/dV): the max-ILP machine
-# scheduler issues a chain's LDS operand reads ahead of its MFMAs; the default (occupancy-
-# driven) scheduler re-uses one register quad and waits out every LDS round trip there.
-EXTRA_FLAGS = {"attention_bwd4.hip": "-mllvm -amdgpu-sched-strategy=max-ilp"}
+# per-file device flags (none at present; a translation unit can get its own scheduler flags here)
+EXTRA_FLAGS = {}
 
 
 def _torch_paths():

@@ -676,7 +676,9 @@ class DeepSeekV3(tnn.Module):
         so dispatch_0 overlaps shared_0 and attn_1, dispatch_1 overlaps shared_1 and experts_0,
         combine_0 overlaps experts_1 and combine_1 overlaps the next layer's attn_0; autograd
         replays the nodes in reverse creation order, which interleaves the backward the same way.
-        Returns ([n_0, n_1], [x0_0, x0_1]) as hidden() does per micro-batch."""
+        Returns (final, [x0_0, x0_1]): final(m) finishes micro-batch m (its last combine, final
+        norm) and returns its hidden state; call final(0), use it, then final(1), so micro-batch
+        1's last combine overlaps micro-batch 0's head."""
         c = self.c
         wait = self.param_wait_cb or (lambda i: None)
         eb = self._expert_buckets() if self.param_wait_cb is not None else {}
@@ -719,14 +721,15 @@ class DeepSeekV3(tnn.Module):
                 layer.ffn.stage_experts(sts[0])
                 layer.ffn.stage_experts(sts[1])
                 pend = [(layer.ffn, sts[0]), (layer.ffn, sts[1])]
-        for m in (0, 1):
-            settle(m)
         wait(len(self.layers) + 1)
-        ns = []
-        for m in (0, 1):
+
+        def final(m):
+            """micro-batch m's last combine, then its final norm: called for m = 0 before m = 1,
+            with micro-batch 0's head in between, micro-batch 1's last combine overlaps it"""
+            settle(m)
             delta = mark_ready(S[m]["delta"], cb, len(self.layers) + 1)
-            ns.append(self._final(S[m]["res"], delta))
-        return ns, x0s
+            return self._final(S[m]["res"], delta)
+        return final, x0s
 
     def _final(self, res, delta):
         c = self.c
@@ -743,10 +746,11 @@ class DeepSeekV3(tnn.Module):
         """loss(micro-batch 0) + loss(micro-batch 1) with the two run layer-interleaved
         (hidden_pair): the same values and gradients as two forward() calls, with each MoE
         layer's all-to-alls overlapped by the other micro-batch's compute. Training only."""
-        ns, x0s = self.hidden_pair(ids0, ids1)
+        final, x0s = self.hidden_pair(ids0, ids1)
         D = self.c.dim
         loss = None
-        for n, x0, t in zip(ns, x0s, (targets0, targets1)):
+        for m, (x0, t) in enumerate(zip(x0s, (targets0, targets1))):
+            n = final(m)
             l = linear_cross_entropy(n.reshape(-1, D), self.embed, t.reshape(-1))
             if self.c.mtp_heads and self.training:
                 l = l + self.mtp_loss(n, x0, t)

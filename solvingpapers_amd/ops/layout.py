@@ -65,7 +65,9 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False, x2t=N
     when both are wide and T is large (x2t: x2 already transposed)."""
     if wgrad8_ok(dy2, x2, out):
         return _ext.ops().wgrad8(dy2, x2, out, accumulate, 0)
-    if out is not None and out.dtype != dy2.dtype:
+    f32out = (out is not None and out.dtype == torch.float32 and dy2.dtype == torch.bfloat16 and dy2.is_cuda
+              and out.is_contiguous() and _MM_F32[0] is not False)
+    if out is not None and out.dtype != dy2.dtype and not f32out:
         g = wgrad(dy2, x2, x2t=x2t)
         out.add_(g) if accumulate else out.copy_(g)
         return out
@@ -79,11 +81,29 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False, x2t=N
         a, b = dy2.t(), x2
     if out is None:
         return torch.mm(a, b)
+    if f32out:
+        # fp32 main gradient: hipBLASLt accumulates in fp32 and writes / adds fp32 directly
+        # (aten::mm.dtype / addmm.dtype), no bf16 temporary and no separate add pass
+        try:
+            if accumulate:
+                torch.addmm(out, a, b, out_dtype=torch.float32, out=out)
+            else:
+                torch.mm(a, b, out_dtype=torch.float32, out=out)
+            _MM_F32[0] = True
+            return out
+        except (RuntimeError, TypeError):
+            _MM_F32[0] = False
+            g = torch.mm(a, b)
+            out.add_(g) if accumulate else out.copy_(g)
+            return out
     if accumulate:
         out.addmm_(a, b)
     else:
         torch.mm(a, b, out=out)
     return out
+
+
+_MM_F32 = [None]     # aten::mm.dtype_out / addmm.dtype_out usable (probed on first use)
 
 
 def bias_grad(dy2: torch.Tensor) -> torch.Tensor:

@@ -558,7 +558,7 @@ def test_attention_short_bwd(B, Tq, Tk, H, causal, monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{"SPA_ATTN_BWD_FUSED": "1"}, {"SPA_ATTN_DKDV": "0"}, {"SPA_ATTN_DKDV": "2"},
-                                 {"SPA_ATTN_DKDV": "3"}, {"SPA_ATTN_DKDV": "4"}])
+                                 {"SPA_ATTN_DKDV": "3"}])
 def test_attention_bwd_variants_match_default(env):
     """The optional backward variants -- fused (dQ via fp32 atomics inside the dK/dV kernel)
     and the paired-wave dK/dV kernel -- against the default kernels, each run in a subprocess
