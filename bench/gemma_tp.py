@@ -1,7 +1,9 @@
 #!/usr/bin/env python
 """Gemma-7B-shape (MQA, 1 KV head) bf16 training tokens/s with tensor parallelism over all
-ranks (BASELINE.json config #4: TP=8 on one node). Column-parallel q / GeGLU, row-parallel
-o / down with RCCL all-reduces, replicated K/V, vocab-parallel embedding + CE.
+ranks (BASELINE.json config #4: TP=8 on one node). Sequence parallel by default: column-parallel
+q / GeGLU open with an all-gather over T, row-parallel o / down close with a reduce-scatter,
+the K/V projection runs on the sequence shard, vocab-parallel embedding + CE; the two sequence
+halves overlap each other's collectives (models/gemma.py _forward_sp_pair).
 ``[torchrun --nproc-per-node N ...] python bench/gemma_tp.py --steps K --warmup W [--layers L]``"""
 from __future__ import annotations
 
@@ -22,9 +24,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--layers", type=int, default=None)
-    ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")
+    ap.add_argument("--no-sp", dest="sp", action="store_false",
+                    help="plain Megatron TP (default: sequence parallelism inside the TP group)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="no two-chunk TP pipeline (default: halves on two streams / communicators)")
+                    help="no overlapped chunk pair (default under SP: sequence halves whose collectives "
+                         "run on a side stream under the other half's GEMMs)")
     ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (tuning/*.csv) to look up")
     a = ap.parse_args()
     info = sdist.init_distributed()
@@ -37,8 +41,8 @@ def main():
         kw["n_layers"] = a.layers
     c = gemma.config("gemma_7b_mqa", **kw)
     tp = dist.group.WORLD if world > 1 else None
-    tp2 = dist.new_group(list(range(world))) if (world > 1 and a.pipeline and not a.sp) else None
-    m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=tp, seed=1, sequence_parallel=a.sp, tp_group2=tp2)
+    m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=tp, seed=1, sequence_parallel=a.sp,
+                    tp_pipeline=a.pipeline)
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     # global grad norm: TP-sharded squares summed over the group, replicated params counted once
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, tp_group=tp)
@@ -59,7 +63,7 @@ def main():
     tf = tok_s * m.flops_per_token(a.seq) / world / 1e12
     report("training tokens/sec, Gemma-7B-shape MQA bf16 (TP)", tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": "gemma_7b_mqa" + (f"-L{a.layers}" if a.layers else ""), "global_batch": 1, "seq_len": a.seq,
-            "parallelism": f"tp{world}" + ("-sp" if a.sp and world > 1 else "") + ("-pipe2" if tp2 is not None else "")}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
+            "parallelism": f"tp{world}" + ("-sp" if m.sp else "") + ("-pair" if m.sp and m.tp_pipeline else "")}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
            loss=round(float(last[0].detach()), 4))
     sdist.cleanup()
 

@@ -243,32 +243,25 @@ class GemmaBlock(tnn.Module):
         self.w13.copy_(torch.cat([full["w13"][r * fl:(r + 1) * fl], full["w13"][F + r * fl:F + (r + 1) * fl]]))
         self.w2.copy_(full["w2"][:, r * fl:(r + 1) * fl])
 
-    def forward(self, res, delta, tp_group=None, cache=None, pos=0, sp=False, kv_prefix=None, want_kv=False):
-        """``sp``: sequence parallel -- res/delta are [B, T/tp, D] shards; the TP regions
-        open with an all-gather over T and close with a reduce-scatter over T.
-        ``kv_prefix`` / ``want_kv`` (training, TP chunk pipelining in Gemma.hidden): this call
-        holds tokens [pos, pos+T) of the sequence; its queries also attend to the (RoPE'd) K/V
-        of the earlier tokens ``kv_prefix`` = (k, v), and ``want_kv`` returns this chunk's own
-        (k, v) for the next chunk."""
-        from ..parallel.tensor_parallel import (copy_to_tp, gather_seq, reduce_from_tp, reduce_grad_tp,
-                                                reduce_scatter_seq, scale_grad)
+    def forward(self, res, delta, tp_group=None, cache=None, pos=0, sp=False):
+        """``sp``: sequence parallel -- res/delta are [B, T/tp, D] shards; the layer is the
+        four pieces sp_in -> sp_attn -> sp_mlp_in -> sp_mlp + reduce-scatter (see sp_in)."""
+        from ..parallel.tensor_parallel import copy_to_tp, reduce_from_tp, reduce_grad_tp, reduce_scatter_seq
         c = self.c
+        if sp:
+            assert cache is None, "sequence parallelism is a training layout"
+            h, xf = self.sp_in(res, delta, tp_group)
+            part, _ = self.sp_attn(xf, pos)
+            h2, n2f = self.sp_mlp_in(part, h, tp_group)
+            return h2, reduce_scatter_seq(self.sp_mlp(n2f), tp_group)
         if res is None:
             n1, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
         else:
             n1, h = rms_norm(delta, self.attn_norm, c.norm_eps, residual=res)
         hd, KV = c.head_dim, c.n_kv_heads
-        if sp:
-            assert cache is None, "sequence parallelism is a training layout"
-            n1f = gather_seq(n1, tp_group)                               # [B, T, D]
-            q = linear(n1f, self.wq)
-            # the K/V activation grad is summed over TP below, so its input grad is complete on
-            # every rank: scale by 1/tp before gather_seq's reduce-scatter sums the copies
-            kv = reduce_grad_tp(linear(scale_grad(n1f, 1.0 / self.tp), self.wkv), tp_group)
-        else:
-            n1p = copy_to_tp(n1, tp_group)
-            q = linear(n1p, self.wq)                                     # [B, T, hl*hd]
-            kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)          # replicated K/V, grads summed over TP
+        n1p = copy_to_tp(n1, tp_group)
+        q = linear(n1p, self.wq)                                         # [B, T, hl*hd]
+        kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)              # replicated K/V, grads summed over TP
         B, T = q.shape[0], q.shape[1]
         qkv = torch.cat([q, kv], dim=-1)
         if isinstance(pos, DecodeState):  # graph-capturable decode step: positions on the device
@@ -283,20 +276,7 @@ class GemmaBlock(tnn.Module):
             f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
             return h2, reduce_from_tp(linear(f, self.w2), tp_group)
         qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, pos, interleaved=False, head_dim=hd)
-        kv_out = None
-        if cache is None and (kv_prefix is not None or want_kv):
-            x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
-            k4, v4 = x4[:, :, self.hl:self.hl + KV], x4[:, :, self.hl + KV:]
-            ev = None
-            if want_kv and qkv.is_cuda:      # the next chunk waits for THIS point only, not for the
-                ev = torch.cuda.Event()      # rest of the layer (its all-reduces) on this stream
-                ev.record()
-            kv_out = (k4, v4, ev)
-            if kv_prefix is not None:     # causal with offset: query i sees keys <= prefix + i
-                k4 = torch.cat([kv_prefix[0], k4], 1)
-                v4 = torch.cat([kv_prefix[1], v4], 1)
-            o = flash_attention(x4[:, :, :self.hl], k4, v4, causal=True).reshape(B, T, self.hl * hd)
-        elif cache is None:
+        if cache is None:
             o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
         else:  # KV-cached inference: write this step's K/V, attend over the cache
             x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
@@ -305,74 +285,70 @@ class GemmaBlock(tnn.Module):
             vc[:, pos:pos + T] = x4[:, :, self.hl + KV:]
             o = decode_attention(x4[:, :, :self.hl], kc[:, :pos + T], vc[:, :pos + T], causal=True)
             o = o.reshape(B, T, self.hl * hd)
-        close = reduce_scatter_seq if sp else reduce_from_tp
-        a = close(linear(o, self.wo), tp_group)
+        a = reduce_from_tp(linear(o, self.wo), tp_group)
         n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
-        f = glu(linear(gather_seq(n2, tp_group) if sp else copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
-        out = close(linear(f, self.w2), tp_group)
-        return (h2, out, kv_out) if want_kv else (h2, out)
+        f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
+        return h2, reduce_from_tp(linear(f, self.w2), tp_group)
 
-
-    # ---- one-stream interleaved TP schedule (Gemma._hidden_interleaved): the layer in four
-    # stages, each ending where a collective would block; the caller runs the other chunk's
-    # stage between two stages of one chunk, so every collective has a stage to hide behind.
-    def stage1(self, st, g):
-        """norm1 on (res, delta | pending all-reduce of the previous layer's output)."""
-        from ..parallel import comm
+    # ---- sequence-parallel pieces. Between the TP regions the residual stream is a [B, T/tp, D]
+    # sequence shard; each piece ends where a collective starts, so Gemma._forward_sp_pair can
+    # run the collectives (and the shard-local norms between them) of one chunk on a side stream
+    # while the other chunk's GEMMs / attention run on the compute stream.
+    def sp_in(self, res, delta, g):
+        """Attention input: norm1 (+ residual) on the shard, the K/V projection on the shard
+        (MQA: K/V are replicated, so computing them once per token and gathering them is 8x
+        less GEMM than projecting the gathered input on every rank, and their activation
+        gradient needs no all-reduce of its own -- the gather's reduce-scatter sums it), then
+        ONE all-gather over T of [n1 | kv]. Returns (h, gathered [B, T, D + 2 KV hd])."""
+        from ..parallel.tensor_parallel import gather_seq
         c = self.c
-        x = comm.ar_finish(st["out"]) if st.get("out") is not None else st["delta"]
-        st["out"] = None
-        if st["res"] is None:
-            n1, h = rms_norm(x, self.attn_norm, c.norm_eps), x
+        if res is None:
+            n1, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
         else:
-            n1, h = rms_norm(x, self.attn_norm, c.norm_eps, residual=st["res"])
-        st["n1"], st["h"] = n1, h
-        st["sq"] = comm.grad_ar_start(n1, g)            # q path: gradient all-reduce (bwd)
+            n1, h = rms_norm(delta, self.attn_norm, c.norm_eps, residual=res)
+        return h, gather_seq(torch.cat([n1, linear(n1, self.wkv)], dim=-1), g)
 
-    def stage2(self, st, g, pos, kv_prefix=None):
-        """q / kv projections, RoPE, attention (queries of this chunk over kv_prefix + own K/V),
-        o projection; starts its all-reduce. Returns this chunk's (k, v)."""
-        from ..parallel import comm
-        from ..parallel.tensor_parallel import reduce_grad_tp
+    def sp_attn(self, xf, pos=0, kv_prefix=None, want_kv=False):
+        """q projection of the gathered input, RoPE, attention (queries over ``kv_prefix`` + own
+        K/V when given: a later chunk of the same sequences), o projection. Returns the o
+        projection's TP-partial [B, T, D] and, with ``want_kv``, this chunk's RoPE'd (k, v)."""
         c = self.c
         hd, KV = c.head_dim, c.n_kv_heads
-        q = linear(comm.grad_ar_finish(st.pop("sq")), self.wq)
-        kv = reduce_grad_tp(linear(st.pop("n1"), self.wkv), g)
+        n1f, kv = xf.split([c.dim, xf.shape[-1] - c.dim], dim=-1)
+        q = linear(n1f, self.wq)
         B, T = q.shape[0], q.shape[1]
         qkv = rope_packed_(torch.cat([q, kv], dim=-1), self.hl + KV, c.rope_theta, pos, interleaved=False,
                            head_dim=hd)
-        x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
-        k4, v4 = x4[:, :, self.hl:self.hl + KV], x4[:, :, self.hl + KV:]
-        kk, vv = (k4, v4) if kv_prefix is None else (torch.cat([kv_prefix[0], k4], 1), torch.cat([kv_prefix[1], v4], 1))
-        o = flash_attention(x4[:, :, :self.hl], kk, vv, causal=True).reshape(B, T, self.hl * hd)
-        st["sa"] = comm.ar_start(linear(o, self.wo), g)
-        return k4, v4
+        kv_out = None
+        if kv_prefix is None and not want_kv:
+            o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
+        else:
+            x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
+            k4, v4 = x4[:, :, self.hl:self.hl + KV], x4[:, :, self.hl + KV:]
+            kv_out = (k4, v4)
+            if kv_prefix is not None:     # causal with offset: query i sees keys <= prefix + i
+                k4 = torch.cat([kv_prefix[0], k4], 1)
+                v4 = torch.cat([kv_prefix[1], v4], 1)
+            o = flash_attention(x4[:, :, :self.hl], k4, v4, causal=True).reshape(B, T, self.hl * hd)
+        return linear(o.reshape(B, T, self.hl * hd), self.wo), kv_out
 
-    def stage3(self, st, g):
-        from ..parallel import comm
-        n2, h2 = rms_norm(comm.ar_finish(st.pop("sa")), self.ffn_norm, self.c.norm_eps, residual=st.pop("h"))
-        st["res"] = h2
-        st["sm"] = comm.grad_ar_start(n2, g)
+    def sp_mlp_in(self, part, h, g):
+        """Reduce-scatter of the o projection, norm2 + residual on the shard, all-gather of the
+        MLP input. Returns (h2, gathered n2)."""
+        from ..parallel.tensor_parallel import gather_seq, reduce_scatter_seq
+        n2, h2 = rms_norm(reduce_scatter_seq(part, g), self.ffn_norm, self.c.norm_eps, residual=h)
+        return h2, gather_seq(n2, g)
 
-    def stage4(self, st, g):
-        from ..parallel import comm
-        f = glu(linear(comm.grad_ar_finish(st.pop("sm")), self.w13), "gelu_tanh")
-        st["out"] = comm.ar_start(linear(f, self.w2), g)
-
-
-class _Null:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False
+    def sp_mlp(self, n2f):
+        """GeGLU on the gathered input; returns the down projection's TP-partial [B, T, D]."""
+        return linear(glu(linear(n2f, self.w13), "gelu_tanh"), self.w2)
 
 
 class _JoinStreams(torch.autograd.Function):
     """Identity at the end of the two-stream forward. Its backward runs first in the backward
     pass and queues an end-of-backward callback that makes the caller's stream wait for the
-    side stream: weight gradients committed from it (utils/grad.py) are complete before the
-    optimizer (or a DP bucket launched after backward) reads them."""
+    side stream: gradients committed from it (norm weights, K/V projections) are complete
+    before the optimizer (or a DP bucket launched after backward) reads them."""
 
     @staticmethod
     def forward(ctx, x, side):
@@ -386,31 +362,52 @@ class _JoinStreams(torch.autograd.Function):
         return g, None
 
 
+class _Side:
+    """Runs pieces on the side stream after the compute stream's current point and hands their
+    results back (``join``); inline when there is no GPU."""
+
+    def __init__(self, main, side):
+        self.main, self.side = main, side
+
+    def run(self, fn, *args):
+        if self.side is None:
+            return fn(*args), None
+        self.side.wait_stream(self.main)
+        for a in args:
+            if isinstance(a, torch.Tensor):
+                a.record_stream(self.side)       # produced on the compute stream, read here
+        with torch.cuda.stream(self.side):
+            out = fn(*args)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        return out, ev
+
+    def join(self, ev, *ts):
+        if ev is None:
+            return
+        self.main.wait_event(ev)
+        for t in ts:
+            if isinstance(t, torch.Tensor):
+                t.record_stream(self.main)
+
+
 class Gemma(tnn.Module):
     def __init__(self, c: GemmaConfig, device=None, dtype=torch.float32, tp_group=None, seed=0,
-                 sequence_parallel=False, tp_group2=None, tp_schedule=None):
-        """``tp_group2``: a second communicator over the SAME TP ranks. Given (TP > 1, no
-        sequence parallelism), training splits each sequence into two halves that run as two
-        pipelines -- half A on the current stream with ``tp_group``, half B on a second compute
-        stream with ``tp_group2`` -- so every TP all-reduce of one half overlaps the other
-        half's GEMMs / attention, forward AND backward (autograd runs each backward op on its
-        forward's stream). Half B's queries attend to half A's K/V (causal with offset), so
-        the result equals the unsplit model; see hidden()."""
+                 sequence_parallel=None, tp_pipeline=None):
+        """``sequence_parallel`` (default: on when TP > 1): Megatron sequence parallelism for
+        training -- the residual stream between TP regions is a [B, T/tp, D] shard, each TP
+        region opens with an all-gather over T and closes with a reduce-scatter.
+        ``tp_pipeline`` (default on; env SPA_TP_PIPE=0 turns it off): under sequence parallelism a
+        training forward with targets runs as two chunks (the batch halves, or the sequence
+        halves when the batch is odd) whose collectives overlap each other's compute -- see
+        _forward_sp_pair."""
         super().__init__()
         from ..parallel.tensor_parallel import tp_rank_size
         self.c = c
         self.tp_group = tp_group
         self.tp_rank, self.tp = tp_rank_size(tp_group)
-        self.sp = bool(sequence_parallel) and self.tp > 1
-        self.tp_group2 = tp_group2 if (self.tp > 1 and not self.sp) else None
-        # "two_stream": half B on a second compute stream (_hidden_pipelined); "interleave": the
-        # one-stream staged schedule (_hidden_interleaved). 1-GPU proxy, TP=8 Gemma-7B layers
-        # (profiles/r3_overlap_proxy_tp_schedules.jsonl): two_stream hides 0.28-0.35 of the
-        # collective time, interleave 0.19 at +17 % compute (its per-layer stages are two tiny
-        # norms and two large blocks, so half of the collectives can only bracket a norm; and
-        # every host-side stall of the one stream idles the GPU). SPA_TP_SCHEDULE overrides.
-        self.tp_schedule = tp_schedule or os.environ.get("SPA_TP_SCHEDULE", "two_stream")
-        assert self.tp_schedule in ("interleave", "two_stream"), self.tp_schedule
+        self.sp = (self.tp > 1) if sequence_parallel is None else (bool(sequence_parallel) and self.tp > 1)
+        self.tp_pipeline = (os.environ.get("SPA_TP_PIPE", "1") != "0") if tp_pipeline is None else bool(tp_pipeline)
         self._side = None
         assert c.vocab_size % self.tp == 0
         fk = dict(device=device, dtype=dtype)
@@ -432,158 +429,99 @@ class Gemma(tnn.Module):
             gl = torch.Generator(device=self.embed.device).manual_seed(seed)
             for l in self.layers:
                 l.reset_parameters(gl, self.tp_rank)
-        if self.tp_group2 is not None and self.tp_schedule == "two_stream":
-            from ..utils.grad import mark_multi_stream
-            mark_multi_stream(self.parameters())     # weight-grad commits come from two streams
 
     def param_groups(self):
         return [[self.embed]] + [list(l.parameters()) for l in self.layers] + [[self.norm_f]]
 
-    def _pipelined(self, ids, cache):
-        return (self.tp_group2 is not None and cache is None and torch.is_grad_enabled() and self.training
-                and (ids.shape[0] % 2 == 0 or (ids.shape[1] % 2 == 0 and ids.shape[1] >= 2)))
+    def _pair_split(self, ids):
+        """'batch' / 'sequence' when a training forward runs as two overlapped chunks, else None."""
+        if not (self.sp and self.tp_pipeline and self.training and torch.is_grad_enabled()):
+            return None
+        B, T = ids.shape
+        if B % 2 == 0 and T % self.tp == 0:
+            return "batch"
+        if T % (2 * self.tp) == 0:
+            return "sequence"
+        return None
 
-    def _hidden_interleaved(self, ids, targets=None):
-        """One-stream two-chunk TP schedule. Each layer is four stages per chunk (GemmaBlock
-        stage1..4, each ending at a collective: the q-path and MLP-input gradient all-reduces of
-        the backward, the o-projection and MLP-output all-reduces of the forward), issued as
+    def _forward_sp_pair(self, ids, targets, split):
+        """Sequence-parallel TP training step as two chunks on one compute stream. Per layer
+        the compute stream runs
 
-            A.s1(l) B.s3(l-1) A.s2(l) B.s4(l-1) A.s3(l) B.s1(l) A.s4(l) B.s2(l) | A.s1(l+1) ...
+            A.attn(l)  B.attn(l)  A.mlp(l)  B.mlp(l)  |  A.attn(l+1) ...
 
-        with every collective started at the end of one stage of its chunk and finished at the
-        start of the next (parallel/comm ar_start / ar_finish, grad_ar_start / grad_ar_finish).
-        Half B runs half a layer behind half A (its attention needs A's K/V of the same layer),
-        so between the two halves of any collective the other chunk's stage runs -- in the
-        forward, and, since autograd replays nodes in reverse creation order, in the backward.
-        One compute stream: the chunks never share the CUs (the two-stream form's chunks fall
-        into lockstep and their collectives coincide, profiles/r3_overlap_proxy_v2.jsonl)."""
-        from ..parallel import comm
-        from ..parallel.tensor_parallel import vocab_parallel_cross_entropy, vocab_parallel_embedding
-        if ids.shape[1] % 2:             # an odd length with an even batch: the batch-split form
-            return self._hidden_pipelined(ids, targets)
-        c = self.c
-        half = ids.shape[1] // 2
-        g = (self.tp_group, self.tp_group2 if self.tp_group2 is not None else self.tp_group)
-        st = [dict(res=None, delta=vocab_parallel_embedding(self.embed, ids[:, i * half:(i + 1) * half], g[i],
-                                                            scale=math.sqrt(c.dim)), out=None) for i in range(2)]
-        L = self.layers
-        for i, l in enumerate(L):
-            l.stage1(st[0], g[0])
-            if i > 0:
-                L[i - 1].stage3(st[1], g[1])
-            kv = l.stage2(st[0], g[0], 0)
-            if i > 0:
-                L[i - 1].stage4(st[1], g[1])
-            l.stage3(st[0], g[0])
-            l.stage1(st[1], g[1])
-            l.stage4(st[0], g[0])
-            l.stage2(st[1], g[1], half, kv_prefix=kv)
-        L[-1].stage3(st[1], g[1])
-        outs, hs = [None, None], [None, None]
-        for i in range(2):
-            if i == 0:
-                x = comm.ar_finish(st[0]["out"])
-            else:
-                L[-1].stage4(st[1], g[1])
-                x = comm.ar_finish(st[1]["out"])
-            outs[i], _ = rms_norm(x, self.norm_f, c.norm_eps, residual=st[i]["res"])
-            if targets is not None:
-                hs[i] = comm.grad_ar_start(outs[i], g[i])   # head input grads: all-reduced async
-        if targets is None:
-            return torch.cat(outs, 1)
-        ls, nv = [None, None], [None, None]
-        for i in range(2):
-            t = targets[:, i * half:(i + 1) * half].reshape(-1)
-            h = comm.grad_ar_finish(hs[i])
-            ls[i] = vocab_parallel_cross_entropy(h.reshape(-1, c.dim), self.embed, t, g[i], reduce_dh=False)
-            nv[i] = (t != -100).sum().clamp_min(1).to(ls[i].dtype)
-        return (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
-
-    def _hidden_pipelined(self, ids, targets=None):
-        """Two-chunk TP pipeline (see __init__): per layer, half A runs on the current stream
-        (``tp_group``), then half B on the side stream (``tp_group2``) once A's K/V exist.
-        Each stream waits only on its own communicator, so while one half's all-reduce is on
-        the wire the other half's kernels run; the backward replays the same two streams."""
-        from ..parallel.tensor_parallel import vocab_parallel_embedding
-        c = self.c
-        T = ids.shape[1]
-        half = T // 2
-        # an even batch splits by SEQUENCES: the halves share no K/V and run as two independent
-        # pipelines (B is offset by half a layer: it starts when A's first o-projection is done);
-        # otherwise each sequence splits in halves and B's queries attend to A's K/V
-        by_batch = ids.shape[0] % 2 == 0
-        groups = (self.tp_group, self.tp_group2)
+        (attn = q projection, attention, o projection of the gathered input; mlp = GeGLU + down
+        projection), and after each piece its chunk's collectives -- reduce-scatter, the
+        shard-local norm (+ K/V projection), all-gather -- run on a side stream, hidden behind
+        the other chunk's next piece. Every weight GEMM stays on the compute stream and every
+        shard-local op (norm weights, K/V projection) on the side stream, so no parameter gets
+        gradient commits from two streams. The backward replays both streams (autograd runs each
+        backward op on its forward's stream), so the gradient collectives overlap the other
+        chunk's backward GEMMs the same way. ``split`` "sequence": chunk B is the second half
+        of every sequence and attends to chunk A's K/V of the same layer (causal with offset),
+        so the result equals the unsplit model."""
+        from ..parallel.tensor_parallel import gather_seq, reduce_scatter_seq, vocab_parallel_cross_entropy, \
+            vocab_parallel_embedding
+        c, g = self.c, self.tp_group
         cuda = ids.is_cuda
         main = torch.cuda.current_stream(ids.device) if cuda else None
         if cuda and self._side is None:
             from ..parallel.comm import side_stream
-            self._side = side_stream(ids.device)
             from ..utils.grad import register_side_stream
+            self._side = side_stream(ids.device)
             register_side_stream(self._side)
-        side = self._side if cuda else None
-
-        def on(i):
-            return torch.cuda.stream(side) if (i == 1 and side is not None) else _Null()
-
-        if side is not None:
-            side.wait_stream(main)
-        hb = ids.shape[0] // 2
-        chunks = (ids[:hb], ids[hb:]) if by_batch else (ids[:, :half], ids[:, half:])
-        delta = [None, None]
-        for i in range(2):
-            with on(i):
-                delta[i] = vocab_parallel_embedding(self.embed, chunks[i], groups[i], scale=math.sqrt(c.dim))
-        res = [None, None]
-        for li, l in enumerate(self.layers):
-            with on(0):
-                res[0], delta[0], kv = l(res[0], delta[0], groups[0], None, 0, False, want_kv=True)
-            if side is not None and (not by_batch or li == 0):
-                side.wait_event(kv[2])       # half A's K/V are rope'd: half B may start its layer
-                for t in kv[:2]:
-                    t.record_stream(side)
-            kv = kv[:2]
-            with on(1):
-                if by_batch:
-                    res[1], delta[1] = l(res[1], delta[1], groups[1], None, 0, False)
-                else:
-                    res[1], delta[1] = l(res[1], delta[1], groups[1], None, half, False, kv_prefix=kv)
-        outs = [None, None]
-        for i in range(2):
-            with on(i):
-                outs[i], _ = rms_norm(delta[i], self.norm_f, c.norm_eps, residual=res[i])
-        if targets is not None:
-            # the vocab-parallel head + CE per chunk, each on its own stream and communicator: the
-            # [T/2, D] hidden-gradient all-reduce of one chunk's head backward overlaps the other
-            # chunk's head GEMMs (one [T, D] all-reduce here was the longest exposed collective)
-            from ..parallel.tensor_parallel import vocab_parallel_cross_entropy
-            tg = (targets[:hb], targets[hb:]) if by_batch else (targets[:, :half], targets[:, half:])
-            ls, nv = [None, None], [None, None]
-            for i in range(2):
-                with on(i):
-                    t = tg[i].reshape(-1)
-                    ls[i] = vocab_parallel_cross_entropy(outs[i].reshape(-1, c.dim), self.embed, t, groups[i])
-                    nv[i] = (t != -100).sum().clamp_min(1).to(ls[i].dtype)
-            if side is not None:
-                main.wait_stream(side)
-                ls[1].record_stream(main)
-                nv[1].record_stream(main)
-            loss = (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
-            return _JoinStreams.apply(loss, side) if side is not None else loss
-        cat_dim = 0 if by_batch else 1
-        if side is not None:
-            main.wait_stream(side)
-            outs[1].record_stream(main)
-            return _JoinStreams.apply(torch.cat(outs, cat_dim), side)
-        return torch.cat(outs, cat_dim)
+        sd = _Side(main, self._side if cuda else None)
+        B, T = ids.shape
+        if split == "batch":
+            parts, tps, pos = (ids[:B // 2], ids[B // 2:]), (targets[:B // 2], targets[B // 2:]), (0, 0)
+        else:
+            parts, tps, pos = (ids[:, :T // 2], ids[:, T // 2:]), (targets[:, :T // 2], targets[:, T // 2:]), (0, T // 2)
+        cb = None
+        if self.grad_ready_cb is not None:
+            from .deepseekv3 import _PairReady
+            cb = _PairReady(self.grad_ready_cb)
+        L = self.layers
+        h, xf, ev = [None, None], [None, None], [None, None]
+        for m in (0, 1):                      # embedding rows on the compute stream (tied head:
+            x = vocab_parallel_embedding(self.embed, parts[m], g, scale=math.sqrt(c.dim),   # one stream
+                                         sequence_parallel=True, reduce=False)              # per param)
+            (h[m], xf[m]), ev[m] = sd.run(
+                lambda x: L[0].sp_in(None, mark_ready(reduce_scatter_seq(x, g), cb, 1), g), x)
+        for li, l in enumerate(L):
+            part, kv = [None, None], None
+            for m in (0, 1):
+                sd.join(ev[m], h[m], xf[m])
+                part[m], kvo = l.sp_attn(xf[m], pos[m], kv_prefix=kv if (m == 1 and split == "sequence") else None,
+                                         want_kv=(m == 0 and split == "sequence"))
+                kv = kvo
+                (h[m], xf[m]), ev[m] = sd.run(lambda p, hh: l.sp_mlp_in(p, hh, g), part[m], h[m])
+            for m in (0, 1):
+                sd.join(ev[m], h[m], xf[m])
+                out = l.sp_mlp(xf[m])
+                if li + 1 < len(L):
+                    nxt = L[li + 1]
+                    (h[m], xf[m]), ev[m] = sd.run(
+                        lambda o, hh: nxt.sp_in(hh, mark_ready(reduce_scatter_seq(o, g), cb, li + 2), g), out, h[m])
+                else:                          # final norm on the shard, gathered for the vocab-parallel head
+                    def fin(o, hh):
+                        d = mark_ready(reduce_scatter_seq(o, g), cb, len(L) + 1)
+                        n, _ = rms_norm(d, self.norm_f, c.norm_eps, residual=hh)
+                        return None, gather_seq(n, g)
+                    (h[m], xf[m]), ev[m] = sd.run(fin, out, h[m])
+        ls, nv = [None, None], [None, None]
+        for m in (0, 1):
+            sd.join(ev[m], xf[m])
+            t = tps[m].reshape(-1)
+            # the head's input gradient stays TP-partial: the gather's reduce-scatter sums it
+            ls[m] = vocab_parallel_cross_entropy(xf[m].reshape(-1, c.dim), self.embed, t, g, reduce_dh=False)
+            nv[m] = (t != -100).sum().clamp_min(1).to(ls[m].dtype)
+        loss = (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
+        return _JoinStreams.apply(loss, sd.side) if sd.side is not None else loss
 
     def hidden(self, ids, cache=None, pos=0):
         """Final-norm hidden states; a [B, T/tp, D] sequence shard under sequence parallelism."""
         from ..parallel.tensor_parallel import vocab_parallel_embedding
         c = self.c
-        if self._pipelined(ids, cache):
-            if self.tp_schedule == "interleave":
-                return self._hidden_interleaved(ids)
-            return self._hidden_pipelined(ids)
         sp = self.sp and cache is None
         x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim), sequence_parallel=sp)
         res, delta = None, x
@@ -595,26 +533,29 @@ class Gemma(tnn.Module):
         return n
 
     def forward(self, ids, targets=None):
-        from ..parallel.tensor_parallel import gather_seq, scale_grad, vocab_parallel_cross_entropy
+        from ..parallel.tensor_parallel import gather_seq, vocab_parallel_cross_entropy
         c = self.c
-        if targets is not None and self._pipelined(ids, None):
-            if self.tp_schedule == "interleave":
-                return self._hidden_interleaved(ids, targets)
-            return self._hidden_pipelined(ids, targets)
+        if targets is not None:
+            split = self._pair_split(ids)
+            if split is not None:
+                return self._forward_sp_pair(ids, targets, split)
         n = self.hidden(ids)
-        if self.sp:  # the vocab-parallel head needs every token on every rank; its input grad is
-            n = scale_grad(gather_seq(n, self.tp_group), 1.0 / self.tp)  # complete on each rank
+        if self.sp:   # the vocab-parallel head needs every token on every rank
+            n = gather_seq(n, self.tp_group)
         if targets is None:
             from ..parallel.tensor_parallel import gather_vocab_logits
             return gather_vocab_logits(linear(n, self.embed), self.tp_group)
-        return vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, targets.reshape(-1), self.tp_group)
+        # under SP the head's input gradient stays TP-partial: the gather's reduce-scatter sums it
+        return vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, targets.reshape(-1), self.tp_group,
+                                            reduce_dh=not self.sp)
 
     def sync_sequence_parallel_grads(self):
-        """Norm weights see only their sequence shard under SP: sum their grads over TP
-        (call after backward, before the optimizer)."""
+        """Parameters used on sequence shards (norm weights, the replicated K/V projection) see
+        only their shard's tokens: sum their grads over TP in one packed all-reduce (call after
+        backward, before the optimizer)."""
         if self.sp:
             from ..parallel.tensor_parallel import sync_sequence_parallel_grads
-            ps = [self.norm_f] + [p for l in self.layers for p in (l.attn_norm, l.ffn_norm)]
+            ps = [self.norm_f] + [p for l in self.layers for p in (l.attn_norm, l.ffn_norm, l.wkv)]
             sync_sequence_parallel_grads(ps, self.tp_group)
 
     # ---------------------------------------------------------------- inference

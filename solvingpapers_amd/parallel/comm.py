@@ -5,8 +5,9 @@ Every TP / EP collective of the framework goes through :func:`all_reduce` /
 
 * a ``torch.distributed`` process group (RCCL on the GPU, gloo on the CPU), and
 * a :class:`ProxyGroup`: ONE GPU standing in for a group of ``size`` ranks. A collective
-  returns its input unchanged (all-reduce) or copies it straight across (all-to-all:
-  every rank sends as much as it receives), and meanwhile a streaming kernel occupies the
+  returns its input unchanged (all-reduce), copies it straight across (all-to-all:
+  every rank sends as much as it receives), or treats every rank's shard as this one
+  (all-gather / reduce-scatter over the sequence, parallel/tensor_parallel.py), and meanwhile a streaming kernel occupies the
   proxy's own "comm stream" for the time the real collective would take on xGMI
   (``bytes on the wire / modelled bandwidth``), with ``nwg`` workgroups -- the CU footprint
   of an RCCL ring kernel with that many channels. Ops on the compute stream that do not
@@ -114,6 +115,12 @@ class ProxyGroup:
     def ar_seconds(self, nbytes: int) -> float:
         n = self.size
         return 2.0 * (n - 1) / n * nbytes / self.ar_bw
+
+    def ag_seconds(self, nbytes_full: int) -> float:
+        """All-gather (or reduce-scatter) whose gathered (unscattered) tensor is nbytes_full:
+        half an all-reduce of it at the same bus bandwidth."""
+        n = self.size
+        return (n - 1) / n * nbytes_full / self.ar_bw
 
     def a2a_seconds(self, nbytes_sent: int) -> float:
         return (self.size - 1) / self.size * nbytes_sent / self.a2a_bw

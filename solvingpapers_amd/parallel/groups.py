@@ -41,9 +41,6 @@ class ProcessGroups:
     dp_group: Optional[object] = None
     ep_group: Optional[object] = None
     expert_dp_group: Optional[object] = None
-    # second communicator over the same TP ranks (two-chunk comm/compute pipeline,
-    # models/gemma.py tp_group2); None unless requested
-    tp_group2: Optional[object] = None
     tp_ranks: Optional[List[int]] = None
     dp_ranks: Optional[List[int]] = None
     ep_ranks: Optional[List[int]] = None
@@ -75,7 +72,7 @@ def layout_ranks(world: int, tp: int = 1, ep: int = 1):
 
 def _hp_options(kind):
     """RCCL options for the TP / EP communicators: their collectives sit between compute on the
-    critical path (or between the two chunks of a pipeline), so their internal stream is high
+    critical path (or between the two chunks of an overlapped pair), so their internal stream is high
     priority (parallel/comm.py COMM_PRIORITY); DP buckets keep the default."""
     from .comm import COMM_PRIORITY
     if kind in ("dp", "expert_dp") or COMM_PRIORITY >= 0 or dist.get_backend() != "nccl":
@@ -88,17 +85,14 @@ def _hp_options(kind):
         return None
 
 
-def build_groups(tp: int = 1, ep: int = 1, pipeline: bool = False) -> ProcessGroups:
-    """``pipeline``: also build a second communicator for every TP group (each chunk of the
-    two-chunk TP pipeline runs its collectives on its own RCCL communicator / stream)."""
+def build_groups(tp: int = 1, ep: int = 1) -> ProcessGroups:
     initialized = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size() if initialized else 1
     rank = dist.get_rank() if initialized else 0
     lay = layout_ranks(world, tp, ep)
     mine = {}
-    kinds = ("tp", "dp", "ep", "expert_dp") + (("tp2",) if pipeline else ())
-    for kind in kinds:
-        for ranks in lay[kind.rstrip("2")]:
+    for kind in ("tp", "dp", "ep", "expert_dp"):
+        for ranks in lay[kind]:
             # new_group is collective over the WORLD: create every group on every rank, in order
             g = dist.new_group(ranks, pg_options=_hp_options(kind)) if (initialized and len(ranks) > 1) else None
             if rank in ranks:
@@ -109,5 +103,4 @@ def build_groups(tp: int = 1, ep: int = 1, pipeline: bool = False) -> ProcessGro
         tp_rank=tp_ranks.index(rank), dp_rank=dp_ranks.index(rank), ep_rank=ep_ranks.index(rank),
         tp_group=mine["tp"][0], dp_group=mine["dp"][0], ep_group=mine["ep"][0],
         expert_dp_group=mine["expert_dp"][0],
-        tp_group2=mine["tp2"][0] if pipeline else None,
         tp_ranks=tp_ranks, dp_ranks=dp_ranks, ep_ranks=ep_ranks, expert_dp_ranks=mine["expert_dp"][1])

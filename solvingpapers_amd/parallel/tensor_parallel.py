@@ -75,8 +75,10 @@ reduce_grad_tp = copy_to_tp  # identity fwd, sum of activation grads over the TP
 
 def _gather_seq_raw(x, group):
     rank, tp = tp_rank_size(group)
-    if comm.is_proxy(group):
-        raise NotImplementedError("sequence parallelism is not modelled by the proxy group")
+    if comm.is_proxy(group):       # stand-in: every rank's shard is this one; wire time modelled
+        out = torch.cat([x] * tp, dim=1)
+        group._occupy(group.ag_seconds(out.numel() * out.element_size())).wait()
+        return out
     if dist.get_backend(group) == "gloo":
         parts = [torch.empty_like(x) for _ in range(tp)]
         dist.all_gather(parts, x.contiguous(), group=group)
@@ -90,8 +92,9 @@ def _gather_seq_raw(x, group):
 def _reduce_scatter_seq_raw(x, group):
     rank, tp = tp_rank_size(group)
     assert x.shape[1] % tp == 0, "sequence parallelism needs T divisible by the TP size"
-    if comm.is_proxy(group):
-        raise NotImplementedError("sequence parallelism is not modelled by the proxy group")
+    if comm.is_proxy(group):       # stand-in: this rank's rows, unsummed; wire time modelled
+        group._occupy(group.ag_seconds(x.numel() * x.element_size())).wait()
+        return x.chunk(tp, dim=1)[0].contiguous()
     if dist.get_backend(group) == "gloo":                               # gloo has no reduce-scatter
         y = x.contiguous().clone()
         dist.all_reduce(y, group=group)
@@ -152,21 +155,28 @@ def scale_grad(x, s):
 
 
 def sync_sequence_parallel_grads(params, group):
-    """Replicated parameters used on sequence shards (norm weights) see only their shard's
-    tokens: sum their gradients over the TP group (main_grad when present, else .grad)."""
+    """Replicated parameters used on sequence shards (norm weights, an MQA K/V projection) see
+    only their shard's tokens: sum their gradients over the TP group (main_grad when present,
+    else .grad) -- packed per dtype into one all-reduce."""
     if tp_rank_size(group)[1] == 1:
         return
+    by_dtype = {}
     for p in params:
         g = getattr(p, "main_grad", None)
         g = g if g is not None else p.grad
         if g is not None:
-            comm.all_reduce(g, group)
+            by_dtype.setdefault(g.dtype, []).append(g)
+    for gs in by_dtype.values():
+        flat = torch.cat([g.reshape(-1) for g in gs])
+        comm.all_reduce(flat, group)
+        torch._foreach_copy_(gs, [f.view_as(g) for f, g in zip(flat.split([g.numel() for g in gs]), gs)])
 
 
-def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=False):
+def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=False, reduce=True):
     """Rows [r*V/tp, (r+1)*V/tp) live on TP rank r; out-of-shard ids contribute zeros.
     With ``sequence_parallel`` the partial rows are reduce-scattered over T (the output is
-    this rank's [B, T/tp, D] shard) instead of all-reduced."""
+    this rank's [B, T/tp, D] shard) instead of all-reduced; ``reduce=False`` returns the
+    TP-partial rows (the caller reduces them, e.g. on another stream)."""
     rank, tp = tp_rank_size(group)
     if tp == 1:
         return embedding(w_local, ids, scale=scale)
@@ -175,6 +185,8 @@ def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=F
     mask = (ids >= lo) & (ids < lo + vl)
     local = torch.where(mask, ids - lo, torch.zeros_like(ids))
     x = embedding(w_local, local, scale=scale) * mask.unsqueeze(-1).to(w_local.dtype)
+    if not reduce:
+        return x
     return reduce_scatter_seq(x, group) if sequence_parallel else reduce_from_tp(x, group)
 
 

@@ -64,7 +64,7 @@ def _lm(args, info):
     dev = info.device if args.device is None else torch.device(args.device)
     # world = tp x data, data = ep x expert-dp (parallel/groups.py); the data loader shards by the
     # DATA coordinate: TP peers read the same batch, DP/EP ranks different ones
-    pg = build_groups(args.tp, args.ep, pipeline=args.pipeline and (args.tp > 1 or args.ep > 1))
+    pg = build_groups(args.tp, args.ep)
     if args.tp > 1 and args.model != "gemma":
         raise SystemExit("--tp is implemented for gemma (Megatron column/row-parallel + vocab-parallel CE)")
     if args.ep > 1 and args.model != "dsv3":
@@ -100,7 +100,7 @@ def _lm(args, info):
             V, T, B = c.vocab_size, c.block_size, c.batch_size
         else:
             model = gemma.Gemma(c, device=dev, dtype=dtype, seed=args.seed, tp_group=pg.tp_group,
-                                sequence_parallel=args.sp, tp_group2=pg.tp_group2)
+                                sequence_parallel=args.sp, tp_pipeline=args.pipeline)
             V, T, B = c.vocab_size, args.seq or c.max_seq_len, c.batch_size
     elif fam == "dsv3":
         c = deepseekv3.config(args.preset or "dsv3_ref", **sets)
@@ -130,7 +130,8 @@ def _lm(args, info):
                      weight_decay=args.weight_decay, clip=args.clip, eval_every=args.eval_every,
                      eval_iters=args.eval_iters, ckpt_dir=args.ckpt_dir, ckpt_every=args.ckpt_every,
                      log_path=args.log, grad_accum=args.accum, zero1=args.zero1, optimizer=args.optimizer,
-                     grad_dtype=dtype, log_every=args.log_every)
+                     grad_dtype=dtype, log_every=args.log_every,
+                     pair_microbatches=args.pipeline)
     hooks = [lambda r: print(json.dumps(r), flush=True)] if info.rank == 0 else []
     if info.rank == 0 and args.wandb:
         from .metrics import WandbHook
@@ -183,10 +184,13 @@ def main(argv=None):
     ap.add_argument("--log", default=None)
     ap.add_argument("--zero1", action="store_true")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (gemma)")
-    ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism with --tp")
+    ap.add_argument("--sp", action="store_true", default=None,
+                    help="Megatron sequence parallelism with --tp (the default; --no-sp: plain TP)")
+    ap.add_argument("--no-sp", dest="sp", action="store_false")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree (dsv3)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="with --tp / --ep: no two-chunk comm/compute pipeline (one communicator)")
+                    help="with --tp / --ep: no two-chunk comm/compute overlap (TP: sequence-parallel chunk "
+                         "pair; EP: micro-batch pairs)")
     ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--device", default=None)
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"])

@@ -1,7 +1,7 @@
 """parallel/comm.py: the one-GPU stand-in group drives the TP / EP code paths unchanged (here on
-the CPU, where it models no time): an 8-rank TP Gemma and an 8-rank EP MoE run forward +
-backward on local shard shapes, with and without the two-chunk pipeline, and the pipelined
-forms give the same result as the plain ones."""
+the CPU, where it models no time): an 8-rank sequence-parallel TP Gemma and an 8-rank EP
+DeepSeek-V3 run forward + backward on local shard shapes, plain and as overlapped pairs, and
+the pairs give the same result as the plain forms."""
 import torch
 
 from solvingpapers_amd.parallel.comm import ProxyGroup, group_rank_size
@@ -10,28 +10,36 @@ from solvingpapers_amd.parallel.comm import ProxyGroup, group_rank_size
 import pytest
 
 
-@pytest.mark.parametrize("schedule,nb", [("interleave", 2), ("two_stream", 2), ("two_stream", 1)])
-def test_proxy_group_tp_gemma_pipelined_matches_plain(schedule, nb):
+@pytest.mark.parametrize("nb", [2, 1])
+def test_proxy_group_tp_gemma_pair_matches_plain(nb):
+    """TP=8 sequence-parallel Gemma on the stand-in group: the overlapped chunk pair (batch
+    halves, or sequence halves) == the plain SP forward, and its all-gathers / reduce-scatters
+    ran. (The stand-in's gather replicates this rank's shard, so the sequence split -- whose
+    halves gather different tokens -- is checked for running, not for equality.)"""
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.utils.flat import FlatParams
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=8, head_dim=16, ffn_hidden=128)
-    g1, g2 = ProxyGroup(8, "cpu"), ProxyGroup(8, "cpu")
+    g1 = ProxyGroup(8, "cpu")
     assert group_rank_size(g1) == (0, 8)
-    plain = gemma.Gemma(c, tp_group=g1, seed=3)
-    pipe = gemma.Gemma(c, tp_group=g1, tp_group2=g2, seed=3, tp_schedule=schedule)
-    assert plain.layers[0].hl == 1 and plain.embed.shape[0] == 8     # TP=8 local shard shapes
-    ids = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(0))[:nb]   # nb 2: batch split
+    plain = gemma.Gemma(c, tp_group=g1, seed=3, tp_pipeline=False)
+    pair = gemma.Gemma(c, tp_group=g1, seed=3)
+    assert plain.sp and pair.sp and plain.layers[0].hl == 1 and plain.embed.shape[0] == 8   # TP=8 local shards
+    ids = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(0))[:nb]
     grads = []
-    for m in (plain, pipe):
+    for m in (plain, pair):
         FlatParams(m)
         m.train()
+        g1.reset_stats()
         loss = m(ids[:, :-1], ids[:, 1:])
         loss.backward()
+        assert g1.calls > 0
         grads.append((loss.item(), {n: p.main_grad.clone() for n, p in m.named_parameters()}))
+    assert pair._pair_split(ids[:, :-1]) == ("batch" if nb == 2 else "sequence")
+    if nb == 1:
+        return
     assert abs(grads[0][0] - grads[1][0]) < 1e-5
     for n, g in grads[0][1].items():
         assert torch.allclose(g, grads[1][1][n], atol=1e-5, rtol=1e-4), n
-    assert g1.calls > 0 and g2.calls > 0                              # both chunks' collectives ran
 
 
 def test_proxy_group_ep_forward_pair_matches_plain():

@@ -60,7 +60,7 @@ def _final(d, nproc):
 
 
 CASES = {
-    "gemma_dp2_tp2": ["gemma", "--preset", "gemma_tiny", "--tp", "2", "--set", "vocab_size=256", "--set", "dim=64",
+    "gemma_dp2_tp2": ["gemma", "--preset", "gemma_tiny", "--tp", "2", "--no-sp", "--set", "vocab_size=256", "--set", "dim=64",
                       "--set", "n_heads=4", "--set", "head_dim=16", "--set", "ffn_hidden=128"],
     "gemma_dp2_tp2_sp": ["gemma", "--preset", "gemma_tiny", "--tp", "2", "--sp", "--set", "vocab_size=256", "--set",
                          "dim=64", "--set", "n_heads=4", "--set", "head_dim=16", "--set", "ffn_hidden=128"],

@@ -134,12 +134,7 @@ def test_zero1_matches_dp():
         assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
 
 
-def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
-    schedule, nb = None, 2
-    if isinstance(pipelined, str):                # "interleave" / "two_stream" / "two_stream_b1"
-        schedule, pipelined = pipelined, True
-        if schedule == "two_stream_b1":           # batch 1: the sequence-split form
-            schedule, nb = "two_stream", 1
+def _tp_worker(rank, world, port, q, mode="plain", nb=2):
     _init(rank, world, port)
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.parallel.tensor_parallel import shard_gemma_from_full
@@ -147,16 +142,14 @@ def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     grp = dist.new_group([0, 1])
-    grp2 = dist.new_group([0, 1]) if pipelined else None
-    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=sp, tp_group2=grp2, tp_schedule=schedule)
-    assert not pipelined or local.tp_group2 is not None
+    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=mode != "plain", tp_pipeline=mode == "pair")
+    assert local.sp == (mode != "plain")
     shard_gemma_from_full(full, local, rank, world)
     flat = FlatParams(local)
-    ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))[:nb]
-    even = sp or pipelined                       # SP shards T; the pipeline splits T in halves
-    loss = local(ids[:, :-1], ids[:, 1:]) if not even else local(ids[:, :-2], ids[:, 1:-1])
-    if pipelined:
-        assert local._pipelined(ids[:, :-2], None)
+    ids = torch.randint(0, 64, (2, 13), generator=torch.Generator().manual_seed(2))[:nb]
+    if mode == "pair":
+        assert local._pair_split(ids[:, :-1]) == ("batch" if nb == 2 else "sequence")
+    loss = local(ids[:, :-1], ids[:, 1:])
     loss.backward()
     local.sync_sequence_parallel_grads()
     grads = {n: p.main_grad.clone().numpy() for n, p in local.named_parameters()}
@@ -166,25 +159,23 @@ def _tp_worker(rank, world, port, q, sp=False, pipelined=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("sp,pipelined", [(False, False), (True, False), (False, "interleave"),
-                                          (False, "two_stream"), (False, "two_stream_b1")])
-def test_tensor_parallel_gemma_matches_unsharded(sp, pipelined):
-    """TP=2 (and TP=2 with Megatron sequence parallelism: reduce-scatter / all-gather over T,
-    norms on sequence shards, norm-weight grads summed over TP; and the two-chunk pipeline on a
-    second communicator, half B attending to half A's K/V) == the unsharded model."""
+@pytest.mark.parametrize("mode,nb", [("plain", 2), ("sp", 2), ("pair", 2), ("pair", 1)])
+def test_tensor_parallel_gemma_matches_unsharded(mode, nb):
+    """TP=2 == the unsharded model: plain Megatron TP ("plain"); sequence parallelism ("sp":
+    reduce-scatter / all-gather over T, norms and the MQA K/V projection on sequence shards,
+    their grads summed over TP); and the overlapped chunk pair under SP ("pair", Gemma.
+    _forward_sp_pair): batch halves (nb 2) or sequence halves with half B attending to half
+    A's K/V (nb 1)."""
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.utils.flat import FlatParams
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     FlatParams(full)
-    ids = torch.randint(0, 64, (2, 12), generator=torch.Generator().manual_seed(2))
-    if pipelined == "two_stream_b1":
-        ids = ids[:1]
-    even = sp or pipelined
-    loss = full(ids[:, :-1], ids[:, 1:]) if not even else full(ids[:, :-2], ids[:, 1:-1])  # SP / pipeline: T even
+    ids = torch.randint(0, 64, (2, 13), generator=torch.Generator().manual_seed(2))[:nb]
+    loss = full(ids[:, :-1], ids[:, 1:])
     loss.backward()
     fg = {n: p.main_grad for n, p in full.named_parameters()}
-    out = _run(_tp_worker, 2, sp, pipelined)
+    out = _run(_tp_worker, 2, mode, nb)
     world = 2
     full_norm = torch.sqrt(sum((g.float() ** 2).sum() for g in fg.values())).item()
     for rank, l, (grads, gn) in out:

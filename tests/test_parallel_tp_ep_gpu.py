@@ -64,7 +64,7 @@ def _gemma_ids():
     return torch.randint(0, 256, (2, 66), generator=torch.Generator().manual_seed(2))
 
 
-def _tp_worker(rank, world, port, q, sp):
+def _tp_worker(rank, world, port, q, mode, nb):
     sdist = _init(rank, world, port)
     import torch.distributed as dist
     from solvingpapers_amd.models import gemma
@@ -73,10 +73,13 @@ def _tp_worker(rank, world, port, q, sp):
     c = _gemma_cfg()
     full = gemma.Gemma(c, device="cuda:0", dtype=torch.bfloat16, seed=5)
     grp = dist.new_group([0, 1])
-    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=sp, device="cuda:0", dtype=torch.bfloat16)
+    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=mode != "plain", tp_pipeline=mode == "pair",
+                        device="cuda:0", dtype=torch.bfloat16)
     shard_gemma_from_full(full, local, rank, world)
     FlatParams(local, grad_dtype=torch.float32)
-    ids = _gemma_ids().cuda()
+    ids = _gemma_ids().cuda()[:nb]
+    if mode == "pair":      # the overlapped chunk pair: side-stream collectives + norms
+        assert local._pair_split(ids[:, :-2]) == ("batch" if nb == 2 else "sequence")
     loss = local(ids[:, :-2], ids[:, 1:-1])
     loss.backward()
     local.sync_sequence_parallel_grads()
@@ -86,8 +89,8 @@ def _tp_worker(rank, world, port, q, sp):
     sdist.cleanup()
 
 
-@pytest.mark.parametrize("sp", [False, True])
-def test_gemma_tp2_on_one_gpu_matches_unsharded(sp):
+@pytest.mark.parametrize("mode,nb", [("plain", 2), ("sp", 2), ("pair", 2), ("pair", 1)])
+def test_gemma_tp2_on_one_gpu_matches_unsharded(mode, nb):
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.ops import _ext
     from solvingpapers_amd.utils.flat import FlatParams
@@ -95,7 +98,7 @@ def test_gemma_tp2_on_one_gpu_matches_unsharded(sp):
     c = _gemma_cfg()
     full = gemma.Gemma(c, device="cuda:0", dtype=torch.bfloat16, seed=5)
     FlatParams(full, grad_dtype=torch.float32)
-    ids = _gemma_ids().cuda()
+    ids = _gemma_ids().cuda()[:nb]
     loss = full(ids[:, :-2], ids[:, 1:-1])
     loss.backward()
     fg = {n: p.main_grad.float().cpu() for n, p in full.named_parameters()}
@@ -103,7 +106,7 @@ def test_gemma_tp2_on_one_gpu_matches_unsharded(sp):
     del full
     torch.cuda.synchronize()
     world = 2
-    for rank, l, grads in _spawn(_tp_worker, world, sp):
+    for rank, l, grads in _spawn(_tp_worker, world, mode, nb):
         assert abs(l - ref_loss) < 2e-2 * abs(ref_loss), (rank, l, ref_loss)
         for n, g in grads.items():
             g = torch.from_numpy(g)

@@ -11,13 +11,13 @@ xGMI at the modelled bandwidth (``--ar-gbps`` RCCL all-reduce bus bandwidth,
 Arms (fwd + bwd, same process, interleaved rounds):
   compute / off   plain layers, collectives skipped                     (proxy mode "off")
   blocking        plain layers, collectives modelled, each one waited   (= compute + comm)
-  <form>:overlap  an overlapping form, collectives modelled and overlapped (TP: models/gemma.py
-                  interleave / two_stream; EP: DeepSeekV3.forward_pair, two micro-batches)
+  <form>:overlap  an overlapping form, collectives modelled and overlapped (TP: Gemma's
+                  sequence-parallel chunk pair; EP: DeepSeekV3.forward_pair, two micro-batches)
   <form>:off      the same form with collectives skipped                (the form's own cost)
 
 hidden = 1 - (overlap - off) / (blocking - compute): the fraction of the collective time that
-no longer adds to the layer time; vs_blocking / pair_vs_blocking: overlapped time over blocking
-time, the headline figure. One JSON line per config.
+no longer adds to the layer time; pair_vs_blocking: overlapped time over blocking time, the
+headline figure. One JSON line per config.
 
   python tools/overlap_proxy.py [--which tp,ep] [--layers 2] [--seq 8192]
 """
@@ -59,62 +59,54 @@ ARMS = None   # --arms: run only these (profiling one arm under rocprofv3)
 
 
 def tp_gemma(a):
-    """Plain layer (compute / blocking arms) and both two-chunk schedules of models/gemma.py:
-    "interleave" (one stream, staged) and "two_stream" (half B on a second compute stream)."""
+    """TP=8 Gemma-7B shapes, sequence parallel (the TP default): one rank's share of ``--layers``
+    layers, fwd + bwd of ``--batch`` sequences of ``--seq`` tokens. Arms:
+      compute / blocking   the plain SP forward, collectives skipped / modelled and waited at once
+      pair:off / pair:overlap   Gemma._forward_sp_pair (two chunks: batch halves when --batch is
+                           even, else sequence halves; collectives + shard-local norms of one
+                           chunk on a side stream under the other chunk's GEMMs)"""
     from solvingpapers_amd.models import gemma
     dev = torch.device("cuda")
     c = gemma.config("gemma_7b_mqa", n_layers=a.layers, max_seq_len=a.seq)
     g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
-    g2 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
-    models = {}
-    for name, kw in (("plain", {}), ("interleave", dict(tp_group2=g2, tp_schedule="interleave")),
-                     ("two_stream", dict(tp_group2=g2, tp_schedule="two_stream"))):
-        if a.variants and name != "plain" and name not in a.variants.split(","):
-            continue
-        m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=g1, seed=1, **kw)
-        FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
-        models[name] = m
+    m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=g1, seed=1).train()
+    FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     ids = torch.randint(0, c.vocab_size, (a.batch, a.seq + 1), device=dev)
+    split = m._pair_split(ids[:, :-1])
+    assert split is not None, "the pair needs T divisible by 2 x TP (or an even batch)"
 
-    def step_of(m):
+    def step_of(pair):
         def step():
             from solvingpapers_amd.utils.grad import next_generation
             next_generation()
+            m.tp_pipeline = pair
             m(ids[:, :-1], ids[:, 1:]).backward()
+            m.sync_sequence_parallel_grads()
         return step
 
-    arms = {"compute": (step_of(models["plain"]), "off"), "blocking": (step_of(models["plain"]), "blocking")}
-    for name in models:
-        if name != "plain":
-            arms[name + ":overlap"] = (step_of(models[name]), "overlap")
-            arms[name + ":off"] = (step_of(models[name]), "off")
+    arms = {"compute": (step_of(False), "off"), "blocking": (step_of(False), "blocking"),
+            "pair:off": (step_of(True), "off"), "pair:overlap": (step_of(True), "overlap")}
     if ARMS:
         arms = {k: v for k, v in arms.items() if k in ARMS}
     res = {k: [] for k in arms}
     comm = 0.0
     for r in range(a.rounds):
         for k, (fn, mode) in arms.items():
-            for g in (g1, g2):
-                g.mode = mode
+            g1.mode = mode
             fn()
-            for g in (g1, g2):
-                g.reset_stats()
+            g1.reset_stats()
             res[k].append(_time(fn, a.iters))
             if k == "blocking":
-                comm = (g1.modelled_s + g2.modelled_s) * 1e3 / a.iters
+                comm = g1.modelled_s * 1e3 / a.iters
     med = {k: round(statistics.median(v), 3) for k, v in res.items()}
-    out = {"config": "gemma_7b_mqa TP=8 local shard (2 q-heads x 256, GeGLU 3072, V/8)", "layers": a.layers,
-           "batch": a.batch, "seq": a.seq, "split": "batch" if a.batch % 2 == 0 else "sequence",
-           "ms": med, "modelled_comm_ms": round(comm, 3)}
+    out = {"config": "gemma_7b_mqa TP=8 SP local shard (2 q-heads x 256, GeGLU 3072, V/8)", "layers": a.layers,
+           "batch": a.batch, "seq": a.seq, "split": split, "ms": med, "modelled_comm_ms": round(comm, 3)}
     if not ARMS:
         total = med["blocking"] - med["compute"]
         out["comm_added_blocking_ms"] = round(total, 3)
-        for name in models:
-            if name == "plain":
-                continue
-            exposed = med[name + ":overlap"] - med[name + ":off"]
-            out[f"hidden_{name}"] = round(1 - exposed / total, 3) if total > 0 else None
-            out[f"vs_blocking_{name}"] = round(med["blocking"] / med[name + ":overlap"], 3)
+        out["pair_compute_cost_ms"] = round(med["pair:off"] - med["compute"], 3)
+        out["hidden_pair"] = round(1 - (med["pair:overlap"] - med["pair:off"]) / total, 3) if total > 0 else None
+        out["pair_vs_blocking"] = round(med["pair:overlap"] / med["blocking"], 3)
     return out
 
 
@@ -187,8 +179,7 @@ def main():
     ap.add_argument("--nwg", type=int, default=16)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--arms", default="", help="comma list of arm names (default all), e.g. interleave:overlap")
-    ap.add_argument("--variants", default="", help="TP: subset of interleave,two_stream")
+    ap.add_argument("--arms", default="", help="comma list of arm names (default all), e.g. pair:overlap")
     a = ap.parse_args()
     global ARMS
     ARMS = [x for x in a.arms.split(",") if x] or None
