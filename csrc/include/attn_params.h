@@ -32,6 +32,17 @@ struct AttnParams {
   bf16* dsbuf;
   long ds_kvstride;
   int ds_nqt, ds_nkt;
+  // key-split query-parallel kernels (few (b, head) pairs, e.g. TP-sharded MQA): ksplit blocks per
+  // query block, each over a contiguous share of its key tiles, writing fp32 partials -- forward:
+  // unnormalised O rows at part [ksplit, B, H, Tq, part_ld] plus (m, l) pairs at mlpart
+  // [ksplit, B, H, Tq, 2], merged by attn_fwd_merge_kernel; dQ: unscaled dQ rows at part
+  // [ksplit, B, Tq, H, part_ld], summed by attn_dq_reduce_kernel. vhalf: the forward's V / O
+  // column offset per blockIdx.y (head dim 256 run as two 128-column halves in one launch).
+  int ksplit;
+  float* part;
+  float* mlpart;
+  int part_ld;
+  int vhalf;
 };
 
 // 2 KiB dS block index inside one (b, kv-head) region, in the order the dQ pass streams it: per

@@ -82,11 +82,12 @@ __device__ __forceinline__ bool drop_keep(unsigned base, int q, int key, unsigne
 // of an order that is (b, kv-head) major: every q-head of a GQA group, and every q-block of it,
 // runs on the XCD whose private L2 already holds that kv-head's K / V (LLaMA3-8B: one kv-head per
 // XCD). Within an XCD the q-blocks still go heaviest first.
-__device__ __forceinline__ void q_block_map(const AttnParams& p, int nqb, bool causal, int& qb, int& b, int& h) {
+__device__ __forceinline__ void q_block_map(const AttnParams& p, int nqb, bool causal, int& qb, int& b, int& h,
+                                            int bi, int nblk) {
   const int G = p.H / p.Hkv;
   if (p.xcd) {
-    const int cpx = gridDim.x / 8;
-    const int L = (blockIdx.x % 8) * cpx + blockIdx.x / 8;
+    const int cpx = nblk / 8;
+    const int L = (bi % 8) * cpx + bi / 8;
     const int per_unit = nqb * G;
     const int u = L / per_unit, rem = L % per_unit;
     const int qr = rem / G, g = rem % G;
@@ -95,8 +96,8 @@ __device__ __forceinline__ void q_block_map(const AttnParams& p, int nqb, bool c
     h = (u % p.Hkv) * G + g;
   } else {
     const int nbh = p.H * p.B;
-    const int bh = blockIdx.x % nbh;
-    qb = blockIdx.x / nbh;
+    const int bh = bi % nbh;
+    qb = bi / nbh;
     if (causal) qb = nqb - 1 - qb;  // heaviest q-blocks first
     h = bh % p.H;
     b = bh / p.H;
@@ -120,13 +121,16 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lq = lane & 31, hh = lane >> 5;
   const int nqb = cdiv(p.Tq, BM);
-  const int nbh = p.H * p.B;
+  // key split (p.ksplit > 1): block -> (query block, split si); si covers a contiguous share of
+  // the query block's key tiles and writes fp32 partials (see AttnParams)
+  const int si = blockIdx.x % p.ksplit;
   int qb, b, h;
-  q_block_map(p, nqb, CAUSAL, qb, b, h);
+  q_block_map(p, nqb, CAUSAL, qb, b, h, blockIdx.x / p.ksplit, gridDim.x / p.ksplit);
   const int hk = h / (p.H / p.Hkv);
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
   const float c = p.scale_log2;
+  const int vcol = blockIdx.y * p.vhalf;   // this launch slice's V / O columns
   unsigned dbase = 0;
   if constexpr (DROP) dbase = drop_base(p, b, h);
 
@@ -146,20 +150,24 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   // a wave past the last query row (T = 197: rows 224..255 of a 256-row block) skips all MFMA
   // work but keeps staging tiles and meeting the block's barriers
   const int wave_kend = q0 >= p.Tq ? 0 : CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
-  const int ntiles = kend > 0 ? cdiv(kend, BN) : 0;
+  const int ntiles_all = kend > 0 ? cdiv(kend, BN) : 0;
+  const int kper = cdiv(ntiles_all, p.ksplit);
+  const int jbeg = min(ntiles_all, si * kper);
+  const int ntiles = min(ntiles_all, jbeg + kper) - jbeg;
+  const int kb0 = jbeg * BN;
 
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
-  const bf16* vbase = p.v + b * p.svb + hk * p.svh;
+  const bf16* vbase = p.v + b * p.svb + hk * p.svh + vcol;
   TileLoader<HDK, BN, NT> lk;
   TileLoader<HDV, BN, NT> lv;
   lk.init(p.skt, tid);
   lv.init(p.svt, tid);
   if (ntiles > 0) {
-    lk.load(kbase, p.skt, 0, p.Tk);
-    lv.load(vbase, p.svt, 0, p.Tk);
+    lk.load(kbase, p.skt, kb0, p.Tk);
+    lv.load(vbase, p.svt, kb0, p.Tk);
     lk.store(smem);
     lv.store(smem + TK);
-    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk); lv.load(vbase, p.svt, BN, p.Tk); }
+    if (ntiles > 1) { lk.load(kbase, p.skt, kb0 + BN, p.Tk); lv.load(vbase, p.svt, kb0 + BN, p.Tk); }
   }
   __syncthreads();
   LdsOff<IK> offk;
@@ -215,7 +223,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   // every LDS address is a precomputed lane offset + an immediate
   auto body = [&](const int j, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    const int k0 = j * BN;
+    const int k0 = kb0 + j * BN;
     const bf16* Ks = smem + BUF * TB;
     const bf16* Vs = Ks + TK;
     if (j + 1 < ntiles) {
@@ -264,9 +272,31 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     if (j + 1 < ntiles) body(j + 1, IC<1>{});
   }
   l = halfsum(l);
+  if (p.ksplit > 1) {      // fp32 partial: unnormalised O and the (m, l) softmax state
+    if (q < p.Tq) {
+      const long row = (((long)si * p.B + b) * p.H + h) * p.Tq + q;
+      float* dst = p.part + row * p.part_ld + vcol;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 w;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = o[dt][4 * g + i];
+          *reinterpret_cast<f32x4*>(dst + 32 * dt + 8 * g + 4 * hh) = w;
+        }
+      if (hh == 0 && blockIdx.y == 0) {
+        float2 ml;
+        ml.x = m;
+        ml.y = l;
+        reinterpret_cast<float2*>(p.mlpart)[row] = ml;
+      }
+    }
+    return;
+  }
   const float inv = l > 0.f ? 1.f / l : 0.f;
   if (q < p.Tq) {
-    bf16* op = p.out + b * p.sob + (long)q * p.sot + h * p.soh;
+    bf16* op = p.out + b * p.sob + (long)q * p.sot + h * p.soh + vcol;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -296,9 +326,9 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lq = lane & 31, hh = lane >> 5;
   const int nqb = cdiv(p.Tq, BM);
-  const int nbh = p.H * p.B;
+  const int si = blockIdx.x % p.ksplit;     // key split: see the forward kernel
   int qb, b, h;
-  q_block_map(p, nqb, CAUSAL, qb, b, h);
+  q_block_map(p, nqb, CAUSAL, qb, b, h, blockIdx.x / p.ksplit, gridDim.x / p.ksplit);
   const int hk = h / (p.H / p.Hkv);
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
@@ -325,7 +355,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     dlt = halfsum(dlt);
   }
   const long srow = ((long)b * p.H + h) * p.Tq + q;
-  if (qvalid && hh == 0) p.delta[srow] = dlt;
+  if (qvalid && hh == 0 && si == 0) p.delta[srow] = dlt;
   const float nlse2 = qvalid ? -p.lse_in[srow] * 1.4426950408889634f : -INFINITY;
   f32x16 acc[DT];
 #pragma unroll
@@ -336,7 +366,11 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   // a wave past the last query row (T = 197: rows 224..255 of a 256-row block) skips all MFMA
   // work but keeps staging tiles and meeting the block's barriers
   const int wave_kend = q0 >= p.Tq ? 0 : CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
-  const int ntiles = kend > 0 ? cdiv(kend, BN) : 0;
+  const int ntiles_all = kend > 0 ? cdiv(kend, BN) : 0;
+  const int kper = cdiv(ntiles_all, p.ksplit);
+  const int jbeg = min(ntiles_all, si * kper);
+  const int ntiles = min(ntiles_all, jbeg + kper) - jbeg;
+  const int kb0 = jbeg * BN;
   const bf16* kbase = p.k + b * p.skb + hk * p.skh;
   const bf16* vbase = p.v + b * p.svb + hk * p.svh;
   TileLoader<HDK, BN, NT> lk;
@@ -344,11 +378,11 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   lk.init(p.skt, tid);
   lv.init(p.svt, tid);
   if (ntiles > 0) {
-    lk.load(kbase, p.skt, 0, p.Tk);
-    lv.load(vbase, p.svt, 0, p.Tk);
+    lk.load(kbase, p.skt, kb0, p.Tk);
+    lv.load(vbase, p.svt, kb0, p.Tk);
     lk.store(smem);
     lv.store(smem + TK);
-    if (ntiles > 1) { lk.load(kbase, p.skt, BN, p.Tk); lv.load(vbase, p.svt, BN, p.Tk); }
+    if (ntiles > 1) { lk.load(kbase, p.skt, kb0 + BN, p.Tk); lv.load(vbase, p.svt, kb0 + BN, p.Tk); }
   }
   __syncthreads();
   LdsOff<IK> offk;
@@ -369,7 +403,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   };
   auto body = [&](const int j, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    const int k0 = j * BN;
+    const int k0 = kb0 + j * BN;
     const bf16* Ks = smem + BUF * TB;
     const bf16* Vs = Ks + TK;
     if (j + 1 < ntiles) {
@@ -430,7 +464,18 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     body(j, IC<0>{});
     if (j + 1 < ntiles) body(j + 1, IC<1>{});
   }
-  if (qvalid) {
+  if (qvalid && p.ksplit > 1) {   // fp32 partial (unscaled), summed by attn_dq_reduce_kernel
+    float* dst = p.part + ((((long)si * p.B + b) * p.Tq + q) * p.H + h) * p.part_ld;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = acc[dt][4 * g + i];
+        *reinterpret_cast<f32x4*>(dst + 32 * dt + 8 * g + 4 * hh) = w;
+      }
+  } else if (qvalid) {
     bf16* op = p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -442,6 +487,80 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
         *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * hh) = w;
       }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Key-split merges. Forward: per row, M = max_s m_s, w_s = 2^(m_s - M), O = sum_s w_s O_s /
+// sum_s w_s l_s (m in the kernel's log2-scaled units), lse = (M + log2 L) ln 2. dQ: sum of the
+// partials times the softmax scale. One thread per 8 columns of a row.
+// ---------------------------------------------------------------------------
+template <int HDV>
+__global__ __launch_bounds__(256) void attn_fwd_merge_kernel(AttnParams p) {
+  constexpr int CPR = HDV / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rows = (long)p.B * p.H * p.Tq;
+  if (idx >= rows * CPR) return;
+  const long row = idx / CPR;                 // (b, h, q)
+  const int c8 = (int)(idx % CPR) * 8;
+  const int q = (int)(row % p.Tq);
+  const int bh = (int)(row / p.Tq), h = bh % p.H, b = bh / p.H;
+  const float2* ml = reinterpret_cast<const float2*>(p.mlpart);
+  float M = -INFINITY;
+  for (int s = 0; s < p.ksplit; ++s) {
+    const float2 v = ml[(long)s * rows + row];
+    if (v.y > 0.f) M = fmaxf(M, v.x);
+  }
+  float L = 0.f, acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int s = 0; s < p.ksplit; ++s) {
+    const float2 v = ml[(long)s * rows + row];
+    if (!(v.y > 0.f)) continue;
+    const float w = exp2f(v.x - M);
+    L += w * v.y;
+    const float* src = p.part + ((long)s * rows + row) * p.part_ld + c8;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(src), bq = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] += w * a[i];
+      acc[4 + i] += w * bq[i];
+    }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  bf16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (bf16)(acc[i] * inv);
+  *reinterpret_cast<bf16x8*>(p.out + b * p.sob + (long)q * p.sot + h * p.soh + c8) = o;
+  if (c8 == 0 && p.lse) p.lse[row] = L > 0.f ? (M + __log2f(L)) * 0.69314718055994531f : INFINITY;
+}
+
+template <int HDK>
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnParams p) {
+  constexpr int CPR = HDK / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rows = (long)p.B * p.Tq * p.H;
+  if (idx >= rows * CPR) return;
+  const long row = idx / CPR;                 // (b, q, h)
+  const int c8 = (int)(idx % CPR) * 8;
+  const int h = (int)(row % p.H);
+  const long bq = row / p.H;
+  const int q = (int)(bq % p.Tq), b = (int)(bq / p.Tq);
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int s = 0; s < p.ksplit; ++s) {
+    const float* src = p.part + ((long)s * rows + row) * p.part_ld + c8;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(src), bb = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] += a[i];
+      acc[4 + i] += bb[i];
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (bf16)(acc[i] * p.scale);
+  *reinterpret_cast<bf16x8*>(p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh + c8) = o;
 }
 
 // ---------------------------------------------------------------------------
@@ -481,8 +600,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int rest = blockIdx.x / nbh;  // causal: low key blocks are heaviest, launched first
   const int split = rest % p.hsplit, kb = rest / p.hsplit;
   const int hk = bh % p.Hkv, b = bh / p.Hkv;
-  const int G = p.H / p.Hkv / p.hsplit;  // q-heads handled by this block
-  const int h0 = hk * (p.H / p.Hkv) + split * G;
+  const int G = p.H / p.Hkv;             // q-heads sharing this kv-head
+  const int h0 = hk * G;
   const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + wave * 32);
   const int key = kw0 + lk;
   const bool kvalid = key < p.Tk;
@@ -518,7 +637,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int t0 = qstart / BMQ;
   const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
   const int nper = ntq - t0 > 0 ? ntq - t0 : 0;  // q-tiles per head
-  const int total = nper * G;                      // (head, q-tile) iterations
+  // (head, q-tile) iterations of the whole group, in hsplit contiguous shares (whole heads when
+  // hsplit divides G); this block runs [ib, ib + total) into its own fp32 partial
+  const int tot_all = nper * G;
+  const int iper = cdiv(tot_all, p.hsplit);
+  const int ib = min(tot_all, split * iper);
+  const int total = min(tot_all, ib + iper) - ib;
   TileLoader<HDK, BMQ, NT> lq_;
   TileLoader<HDV, BMQ, NT> ld_;
   lq_.init(p.sqt, tid);
@@ -529,6 +653,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   float rl = 0.f, rd = 0.f;
   bool rv = false;
   auto fetch = [&](int it) {
+    it += ib;
     const int hg = it / nper, tq = t0 + it % nper;
     const int h = h0 + hg;
     const int qq0 = tq * BMQ;
@@ -585,7 +710,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   };
   auto body = [&](const int it, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    const int tq = t0 + it % nper;
+    const int tq = t0 + (it + ib) % nper;
     const int qq0 = tq * BMQ;
     const bf16* Qs = smem + BUF * TB;
     const bf16* Ds = Qs + TQ;
@@ -597,7 +722,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
     if (active) {
       unsigned dbase = 0;
-      if constexpr (DROP) dbase = drop_base(p, b, h0 + it / nper);
+      if constexpr (DROP) dbase = drop_base(p, b, h0 + (it + ib) / nper);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         // dP accumulator starts at -delta of each row (register r <-> query row 8g+4hh+i);
@@ -677,7 +802,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     }
     if constexpr (FUSEDQ) {
       __syncthreads();  // dS image complete
-      const int h = h0 + it / nper;
+      const int h = h0 + (it + ib) / nper;
 #pragma unroll
       for (int tile = wave; tile < MT * DTK; tile += 4) {
         const int tq = tile / DTK, td = tile % DTK;
@@ -1635,6 +1760,19 @@ static void fill_dropout(AttnParams& p, double dropout_p, int64_t seed, const c1
   p.drop_scale = (float)(1.0 / (1.0 - dropout_p));
 }
 
+// Key split of the query-parallel kernels: with few (b, head) pairs (TP-sharded MQA: 2 q-heads
+// per rank) the grid is a fraction of the chip -- T 8192 at head dim 256 is 128 blocks of 8 waves
+// for 256 CUs, and the longest causal block runs all 256 key tiles alone. Split each query block's
+// key tiles into ksplit shares (fp32 partials + a merge pass) until there are >= 512 blocks,
+// keeping >= 4 key tiles per share. SPA_ATTN_KSPLIT (read per call): 0/1 off, N forces N.
+static int attn_ksplit(long blocks, int ntk) {
+  const char* e = getenv("SPA_ATTN_KSPLIT");
+  if (e) return std::max(1, std::min(atoi(e), std::max(1, ntk)));
+  int ks = 1;
+  while (blocks * ks < 512 && ks < 8 && ntk / (2 * ks) >= 4) ks *= 2;
+  return ks;
+}
+
 // q [B,Tq,H,dk], k [B,Tk,Hkv,dk], v [B,Tk,Hkv,dv] (strided views allowed).
 // Returns (out [B,Tq,H,dv], lse [B,H,Tq]). dropout_p > 0: fused dropout on P (seeded hash).
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
@@ -1661,40 +1799,52 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal_off = Tk - Tq;
   p.hsplit = 1;
+  p.ksplit = 1;
   p.xcd = xcd_order(B, Hkv);
   if (B * Tq * H == 0) return {out, lse};
   auto st = stream();
-  // head dim 256 (Gemma MQA) as two launches of the (256, 128) kernel, each producing half of the
-  // output columns: the 128-wide O accumulator lets 8 waves (2 per SIMD) share a CU, where the
-  // full 256-wide one holds a wave per SIMD, at the price of computing S twice (1.5x the MFMA
-  // work). SPA_ATTN_SPLITV=0 (read per call) keeps the single 4-wave launch.
+  // head dim 256 (Gemma MQA) as the (256, 128) kernel over two column halves (blockIdx.y), each
+  // producing half of the output columns: the 128-wide O accumulator lets 8 waves (2 per SIMD)
+  // share a CU, where the full 256-wide one holds a wave per SIMD, at the price of computing S
+  // twice (1.5x the MFMA work). SPA_ATTN_SPLITV=0 (read per call) keeps the single 4-wave kernel.
   const char* sve = getenv("SPA_ATTN_SPLITV");
-  if (!(sve && atoi(sve) == 0) && HDK == 256 && HDV == 256 && !drop) {
-    const int grid = cdiv(Tq, 32 * 8) * H * B;
-    for (int half = 0; half < 2; ++half) {
-      AttnParams ph = p;
-      ph.v = p.v + 128 * half;
-      ph.out = p.out + 128 * half;
-      if (causal) attn_fwd_kernel<256, 128, 8, true, false><<<grid, 512, 0, st>>>(ph);
-      else attn_fwd_kernel<256, 128, 8, false, false><<<grid, 512, 0, st>>>(ph);
-    }
-    SPA_LAUNCH_CHECK();
-    return {out, lse};
+  const bool splitv = !(sve && atoi(sve) == 0) && HDK == 256 && HDV == 256 && !drop;
+  const int nw = splitv ? 8 : (HDK <= 192 && HDV <= 192) || (HDK == 256 && HDV == 128) ? 8 : 4;
+  const int blocks = cdiv(Tq, 32 * nw) * H * B * (splitv ? 2 : 1);
+  const int ntk = cdiv(Tk, (HDK >= 256 || HDV >= 256) ? 32 : 64);
+  p.ksplit = attn_ksplit(blocks, ntk);
+  at::Tensor part;
+  if (p.ksplit > 1) {
+    const long rows = (long)B * H * Tq;
+    part = at::empty({(long)p.ksplit * rows * (HDV + 2)}, q.options().dtype(at::kFloat));
+    p.part = part.data_ptr<float>();
+    p.part_ld = HDV;
+    p.mlpart = p.part + (long)p.ksplit * rows * HDV;
   }
-  HDKV_SWITCH(HDK, HDV, {
-    constexpr int NW = fwd_waves<HDK_, HDV_>();
-    constexpr bool SQ = HDK_ == HDV_;
-    const int grid = cdiv(Tq, 32 * NW) * H * B;
-    if (drop) {
-      if constexpr (SQ) {
-        if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, true><<<grid, NW * 64, 0, st>>>(p);
-        else attn_fwd_kernel<HDK_, HDV_, NW, false, true><<<grid, NW * 64, 0, st>>>(p);
+  const int gx = blocks / (splitv ? 2 : 1) * p.ksplit;
+  if (splitv) {
+    p.vhalf = 128;
+    if (causal) attn_fwd_kernel<256, 128, 8, true, false><<<dim3(gx, 2), 512, 0, st>>>(p);
+    else attn_fwd_kernel<256, 128, 8, false, false><<<dim3(gx, 2), 512, 0, st>>>(p);
+  } else {
+    HDKV_SWITCH(HDK, HDV, {
+      constexpr int NW = fwd_waves<HDK_, HDV_>();
+      constexpr bool SQ = HDK_ == HDV_;
+      if (drop) {
+        if constexpr (SQ) {
+          if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, true><<<gx, NW * 64, 0, st>>>(p);
+          else attn_fwd_kernel<HDK_, HDV_, NW, false, true><<<gx, NW * 64, 0, st>>>(p);
+        }
+      } else {
+        if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, false><<<gx, NW * 64, 0, st>>>(p);
+        else attn_fwd_kernel<HDK_, HDV_, NW, false, false><<<gx, NW * 64, 0, st>>>(p);
       }
-    } else {
-      if (causal) attn_fwd_kernel<HDK_, HDV_, NW, true, false><<<grid, NW * 64, 0, st>>>(p);
-      else attn_fwd_kernel<HDK_, HDV_, NW, false, false><<<grid, NW * 64, 0, st>>>(p);
-    }
-  });
+    });
+  }
+  if (p.ksplit > 1) {
+    const long n = (long)B * H * Tq * (HDV / 8);
+    HDKV_SWITCH(HDK, HDV, { attn_fwd_merge_kernel<HDV_><<<(int)cdiv(n, 256L), 256, 0, st>>>(p); });
+  }
   SPA_LAUNCH_CHECK();
   return {out, lse};
 }
@@ -1756,8 +1906,19 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
     }
   }
   const int grid = cdiv(p.Tq, 32 * NW) * p.H * p.B;
-  if (causal) attn_bwd_dq_kernel<HDK, HDV, NW, true, DROP><<<grid, NW * 64, 0, st>>>(p);
-  else attn_bwd_dq_kernel<HDK, HDV, NW, false, DROP><<<grid, NW * 64, 0, st>>>(p);
+  p.ksplit = p.Tk > 0 ? attn_ksplit(grid, cdiv(p.Tk, attn_bn<HDK, HDV>())) : 1;
+  at::Tensor dqpart;
+  if (p.ksplit > 1) {
+    dqpart = at::empty({(long)p.ksplit * p.B * p.Tq * p.H * HDK}, bf16_opts.dtype(at::kFloat));
+    p.part = dqpart.data_ptr<float>();
+    p.part_ld = HDK;
+  }
+  if (causal) attn_bwd_dq_kernel<HDK, HDV, NW, true, DROP><<<grid * p.ksplit, NW * 64, 0, st>>>(p);
+  else attn_bwd_dq_kernel<HDK, HDV, NW, false, DROP><<<grid * p.ksplit, NW * 64, 0, st>>>(p);
+  if (p.ksplit > 1) {
+    const long n = (long)p.B * p.Tq * p.H * (HDK / 8);
+    attn_dq_reduce_kernel<HDK><<<(int)cdiv(n, 256L), 256, 0, st>>>(p);
+  }
   if (p.Tk == 0) return;
   const bool paired = PAIRED_OK && dkdv_mode == 2;
   const bool piped = PAIRED_OK && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
@@ -1822,6 +1983,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   p.scale = (float)scale; p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal_off = Tk - Tq;
   p.xcd = xcd_order(B, Hkv);
+  p.ksplit = 1;
   if (B * H == 0) return;
   auto st = stream();
   if (Tq == 0) { dk.zero_(); dv.zero_(); return; }
@@ -1867,6 +2029,12 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
       while (G % d) ++d;
       hsplit = d;
     }
+  // the single-wave dK/dV kernel splits the (q-head, q-tile) iterations of a kv-head in any
+  // number of shares: past the q-heads (TP-sharded MQA: G = 2), split the q-tiles too
+  const bool pairedk = HDK == HDV && HDK <= 128 && !drop &&
+                       (dkdv_mode == 2 || dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
+  if (!fused && !pairedk)
+    while (nkv * hsplit < 512 && hsplit < 16 && cdiv(Tq, 32) / (2 * hsplit) >= 4) hsplit *= 2;
   p.hsplit = hsplit;
   // SPA_ATTN_STAMP=1: per-wave s_memtime segment sums of the paired dK/dV loop, kept in a
   // process-global buffer the profiling tool reads back (attn_bwd_stamps)

@@ -4,7 +4,8 @@
 // plus the optional additive position table (learned pos_embed gpt/gpt-jax.ipynb:441-472,
 // sinusoidal pe deepseekv3/deepseekv3.ipynb:836-842,867-869) fused into the gather.
 //
-// Forward: one thread per 16-byte vector, rows gathered straight from the table.
+// Forward: one thread per 16-byte vector, rows gathered straight from the table; a negative id
+// gives a zero row and no gradient (vocab-parallel shards pass other ranks' tokens as -1).
 // Backward: fp32 scatter-add with atomics shaped as whole 256-byte row segments per
 // wave instruction (64 lanes x 4 B on one row), the budget-friendly atomic form on
 // MI355X; the fp32 accumulator is then cast to the parameter dtype.
@@ -25,7 +26,13 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const T* __restrict__ W, c
     const long n = i / dv;
     const int c = (i % dv) * 8;
     float v[8];
-    load8(W + idx[n] * D + c, v);
+    const int64_t r = idx[n];
+    if (r >= 0) {
+      load8(W + r * D + c, v);
+    } else {   // negative id (vocab-parallel: a token of another rank's shard): a zero row
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = 0.f;
+    }
     if (scale != 1.f)
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] *= scale;
@@ -52,6 +59,7 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const T* __restrict__ dout
     const int c = (w % nchunk) * 256 + lane * 4;
     if (c >= D) continue;
     const int64_t r = idx[n];
+    if (r < 0) continue;              // zero row of the forward: no gradient
     if (flag && c == 0) flag[r] = 1;  // row touched (every writer stores the same value)
     float* dst = dW + r * D + c;
     const T* src = dout + n * D + c;
@@ -72,6 +80,7 @@ __global__ __launch_bounds__(256) void emb_flush_kernel(float* __restrict__ acc,
   __shared__ int own;
   for (long n = blockIdx.x; n < N; n += gridDim.x) {
     const int64_t r = idx[n];
+    if (r < 0) continue;              // block-uniform: one token per block iteration
     if (threadIdx.x == 0) own = atomicExch(flag + r, 0);
     __syncthreads();
     if (own) {

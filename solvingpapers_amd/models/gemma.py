@@ -309,9 +309,11 @@ class GemmaBlock(tnn.Module):
         return h, gather_seq(torch.cat([n1, linear(n1, self.wkv)], dim=-1), g)
 
     def sp_attn(self, xf, pos=0, kv_prefix=None, want_kv=False):
-        """q projection of the gathered input, RoPE, attention (queries over ``kv_prefix`` + own
-        K/V when given: a later chunk of the same sequences), o projection. Returns the o
-        projection's TP-partial [B, T, D] and, with ``want_kv``, this chunk's RoPE'd (k, v)."""
+        """q projection of the gathered input, RoPE, attention, o projection. ``kv_prefix``: the
+        packed (RoPE'd) qkv buffer of the earlier chunk of the same sequences, whose keys this
+        chunk's queries also see (causal with offset). Returns the o projection's TP-partial
+        [B, T, D] and, with ``want_kv``, this chunk's packed qkv buffer for the next chunk."""
+        from ..ops.attention import attention_packed_prefix
         c = self.c
         hd, KV = c.head_dim, c.n_kv_heads
         n1f, kv = xf.split([c.dim, xf.shape[-1] - c.dim], dim=-1)
@@ -319,18 +321,11 @@ class GemmaBlock(tnn.Module):
         B, T = q.shape[0], q.shape[1]
         qkv = rope_packed_(torch.cat([q, kv], dim=-1), self.hl + KV, c.rope_theta, pos, interleaved=False,
                            head_dim=hd)
-        kv_out = None
-        if kv_prefix is None and not want_kv:
+        if kv_prefix is None:
             o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
         else:
-            x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
-            k4, v4 = x4[:, :, self.hl:self.hl + KV], x4[:, :, self.hl + KV:]
-            kv_out = (k4, v4)
-            if kv_prefix is not None:     # causal with offset: query i sees keys <= prefix + i
-                k4 = torch.cat([kv_prefix[0], k4], 1)
-                v4 = torch.cat([kv_prefix[1], v4], 1)
-            o = flash_attention(x4[:, :, :self.hl], k4, v4, causal=True).reshape(B, T, self.hl * hd)
-        return linear(o.reshape(B, T, self.hl * hd), self.wo), kv_out
+            o = attention_packed_prefix(qkv, kv_prefix, self.hl, KV, hd)
+        return linear(o.reshape(B, T, self.hl * hd), self.wo), (qkv if want_kv else None)
 
     def sp_mlp_in(self, part, h, g):
         """Reduce-scatter of the o projection, norm2 + residual on the shard, all-gather of the

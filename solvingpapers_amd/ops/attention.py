@@ -299,6 +299,59 @@ def attention_packed(qkv, H, Hkv, causal=True, scale=None, head_dim=None, dropou
     return flash_attention(q, k, v, causal, scale, dropout_p, seed).reshape(B, T, H * hd)
 
 
+class _PrefixPackedFn(torch.autograd.Function):
+    """Causal attention of a later chunk of the same sequences: queries of ``qkv`` (positions
+    [Ta, Ta + Tb)) over the keys of ``qkv_a`` (positions [0, Ta)) and its own. Both operands are
+    packed [B, T, (H + 2 Hkv) hd] buffers; their K/V columns are gathered into one [B, Ta + Tb,
+    2 Hkv hd] buffer (the kernels read K/V rows at one stride), and the backward hands qkv_a the
+    gradient of its K/V columns (its q columns get none from here)."""
+
+    @staticmethod
+    def forward(ctx, qkv, qkv_a, H, Hkv, hd, scale):
+        B, Tb, Ta = qkv.shape[0], qkv.shape[1], qkv_a.shape[1]
+        c = H * hd
+        kv = torch.cat([qkv_a[..., c:], qkv[..., c:]], dim=1)
+        q4 = qkv.view(B, Tb, H + 2 * Hkv, hd)[:, :, :H]
+        kv4 = kv.view(B, Ta + Tb, 2 * Hkv, hd)
+        out, lse = _ext.ops().attn_fwd(q4, kv4[:, :, :Hkv], kv4[:, :, Hkv:], scale, True, 0.0, 0, None)
+        ctx.save_for_backward(qkv, kv, out, lse)
+        ctx.H, ctx.Hkv, ctx.hd, ctx.scale, ctx.Ta, ctx.shape_a = H, Hkv, hd, scale, Ta, qkv_a.shape
+        return torch.ops.aten._unsafe_view(out, (B, Tb, H * hd))
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, kv, out, lse = ctx.saved_tensors
+        H, Hkv, hd, Ta = ctx.H, ctx.Hkv, ctx.hd, ctx.Ta
+        B, Tb = qkv.shape[0], qkv.shape[1]
+        c = H * hd
+        dqkv = torch.empty_like(qkv)
+        dkv = torch.empty_like(kv)
+        kv4, dkv4 = kv.view(B, Ta + Tb, 2 * Hkv, hd), dkv.view(B, Ta + Tb, 2 * Hkv, hd)
+        _ext.ops().attn_bwd(dout.contiguous().view(B, Tb, H, hd), qkv.view(B, Tb, H + 2 * Hkv, hd)[:, :, :H],
+                            kv4[:, :, :Hkv], kv4[:, :, Hkv:], out, lse,
+                            dqkv.view(B, Tb, H + 2 * Hkv, hd)[:, :, :H], dkv4[:, :, :Hkv], dkv4[:, :, Hkv:],
+                            ctx.scale, True, 0.0, 0, None)
+        dqkv[..., c:] = dkv[:, Ta:]
+        dqkv_a = torch.zeros(ctx.shape_a, device=dqkv.device, dtype=dqkv.dtype)
+        dqkv_a[..., c:] = dkv[:, :Ta]
+        return dqkv, dqkv_a, None, None, None, None
+
+
+def attention_packed_prefix(qkv, qkv_a, H, Hkv, head_dim, scale=None):
+    """Causal attention of chunk B of a sequence split in two (models/gemma.py _forward_sp_pair):
+    qkv / qkv_a [B, Tb / Ta, (H + 2 Hkv) * head_dim] packed buffers of chunks B / A (RoPE applied),
+    chunk B's queries attending to chunk A's keys and its own (causal with offset Ta) -> [B, Tb, H*hd]."""
+    hd = head_dim
+    B, Tb, Ta = qkv.shape[0], qkv.shape[1], qkv_a.shape[1]
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
+    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and hd in FLASH_HD:
+        return _PrefixPackedFn.apply(qkv, qkv_a, H, Hkv, hd, scale)
+    xa, xb = qkv_a.view(B, Ta, H + 2 * Hkv, hd), qkv.view(B, Tb, H + 2 * Hkv, hd)
+    k = torch.cat([xa[:, :, H:H + Hkv], xb[:, :, H:H + Hkv]], 1)
+    v = torch.cat([xa[:, :, H + Hkv:], xb[:, :, H + Hkv:]], 1)
+    return flash_attention(xb[:, :, :H], k, v, True, scale).reshape(B, Tb, H * hd)
+
+
 def attention_dropout(q, k, v, causal=True, scale=None, p=0.0, training=True, neg=float("-inf")):
     """Attention with dropout on the probability matrix (GPT-ref gpt/gpt-jax.ipynb:351,
     Gemma-ref gemma/gemma.ipynb:248, DeepSeek-ref deepseekv3/deepseekv3.ipynb:1186): the fused

@@ -1,7 +1,8 @@
 """Embedding gather / scatter-add (HIP: csrc/kernels/embedding.hip).
 
 Optional fused additive position table (GPT learned pos_embed, DeepSeek
-sinusoidal pe) and multiplicative scale (Gemma sqrt(D)). The table gradient is
+sinusoidal pe) and multiplicative scale (Gemma sqrt(D)). A negative id gives a zero row
+and no table gradient (vocab-parallel embedding: tokens of other ranks' shards). The table gradient is
 committed to ``W.main_grad`` when present: written in place by ``emb_bwd_into``, which
 touches only the rows of the batch's tokens (fp32 scratch + row flags, then a flush of the
 flagged rows) instead of materialising a dense [V, D] gradient per call.

@@ -130,7 +130,12 @@ def cross_entropy(logits, target, ignore_index=-100, smoothing=0.0):
 
 
 def embedding(W, idx, pos=None, scale=1.0):
-    out = W[idx] * scale if scale != 1.0 else W[idx]
+    if bool((idx < 0).any()):       # negative id: a zero row (vocab-parallel foreign tokens)
+        keep = (idx >= 0).unsqueeze(-1).to(W.dtype)
+        out = W[idx.clamp_min(0)] * keep
+        out = out * scale if scale != 1.0 else out
+    else:
+        out = W[idx] * scale if scale != 1.0 else W[idx]
     if pos is not None:
         T = idx.shape[-1]
         out = out + pos.reshape(-1, W.shape[1])[:T]

@@ -183,8 +183,9 @@ def vocab_parallel_embedding(w_local, ids, group, scale=1.0, sequence_parallel=F
     vl = w_local.shape[0]
     lo = rank * vl
     mask = (ids >= lo) & (ids < lo + vl)
-    local = torch.where(mask, ids - lo, torch.zeros_like(ids))
-    x = embedding(w_local, local, scale=scale) * mask.unsqueeze(-1).to(w_local.dtype)
+    # other shards' tokens as -1: zero rows with no gradient (no mask multiply, and the backward's
+    # scatter-add does not pile (tp-1)/tp of the tokens onto one row's atomics)
+    x = embedding(w_local, torch.where(mask, ids - lo, torch.full_like(ids, -1)), scale=scale)
     if not reduce:
         return x
     return reduce_scatter_seq(x, group) if sequence_parallel else reduce_from_tp(x, group)

@@ -189,6 +189,28 @@ def test_embedding():
     assert rel(W.grad, ref) < 1e-2
 
 
+def test_embedding_negative_ids_are_zero_rows():
+    """A negative id (vocab-parallel: another rank's token) reads a zero row and sends no gradient,
+    on the dense-gradient and the main_grad (emb_bwd_into) paths."""
+    from solvingpapers_amd.ops import embedding
+    ops = _ext.ops()
+    V, D = 300, 256
+    W = torch.randn(V, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    idx = torch.randint(0, V, (2, 65), device=DEV)
+    idx[:, ::3] = -1
+    y = embedding(W, idx, scale=2.0)
+    keep = (idx >= 0)
+    assert torch.equal(y[~keep], torch.zeros_like(y[~keep]))
+    assert torch.equal(y[keep], (W.detach()[idx.clamp_min(0)] * 2.0)[keep])
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    ref = torch.zeros(V, D, device=DEV).index_add_(0, idx[keep], 2.0 * g[keep].float())
+    assert rel(W.grad, ref) < 1e-2
+    out = torch.full((V, D), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.emb_bwd_into(g, idx, 2.0, out, False)
+    assert rel(out, ref) < 1e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_embedding_grad_into_main_grad(dtype):
     """emb_bwd_into: sparse row flush into a main_grad view (overwrite, then accumulate), repeated
@@ -458,8 +480,8 @@ def test_mla_attention_fused_matches_composition(pos_off):
 
 @pytest.mark.parametrize("causal,Hkv", [(True, 1), (False, 2)])
 def test_attn_fwd_hd256_splitv_matches(causal, Hkv, monkeypatch):
-    """Head dim 256 forward as two (256, 128) half-V launches (default) == the single 4-wave
-    launch (SPA_ATTN_SPLITV=0), output and lse."""
+    """Head dim 256 forward as two (256, 128) half-V column slices of one launch (default) == the
+    single 4-wave kernel (SPA_ATTN_SPLITV=0), output and lse."""
     ops = _ext.ops()
     torch.manual_seed(4)
     q = torch.randn(2, 333, 4, 256, device=DEV, dtype=torch.bfloat16)
@@ -472,8 +494,76 @@ def test_attn_fwd_hd256_splitv_matches(causal, Hkv, monkeypatch):
     assert rel(o1, o0) < 5e-3 and (l1 - l0).abs().max().item() < 1e-3
 
 
-def test_flash_lse_and_spike():
-    """Force the online-softmax rescale: one key spiked against one query (rule 26)."""
+@pytest.mark.parametrize("B,Tq,Tk,H,Hkv,hd,causal", [
+    (1, 1024, 1024, 2, 1, 256, True),     # TP=8 Gemma-7B rank: 2 q-heads, MQA, head dim 256
+    (1, 700, 700, 2, 1, 256, False),      # ragged, non-causal
+    (1, 256, 900, 4, 2, 128, True),       # Tq < Tk, GQA
+])
+def test_attn_key_split_matches(B, Tq, Tk, H, Hkv, hd, causal, monkeypatch):
+    """Key-split query-parallel kernels (fp32 partials + merge; few (b, head) pairs) and the
+    iteration-split dK/dV kernel == the unsplit kernels (SPA_ATTN_KSPLIT=1): forward output, lse
+    and all three gradients, for the automatic split and a forced odd one; and the fp32 oracle."""
+    ops = _ext.ops()
+    torch.manual_seed(5)
+    q = torch.randn(B, Tq, H, hd, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Tk, Hkv, hd, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Tk, Hkv, hd, device=DEV, dtype=torch.bfloat16)
+    do = torch.randn(B, Tq, H, hd, device=DEV, dtype=torch.bfloat16)
+    sc = 1 / math.sqrt(hd)
+    res = {}
+    for ks in ("1", None, "3"):
+        if ks is None:
+            monkeypatch.delenv("SPA_ATTN_KSPLIT", raising=False)
+        else:
+            monkeypatch.setenv("SPA_ATTN_KSPLIT", ks)
+        out, lse = ops.attn_fwd(q, k, v, sc, causal)
+        dq, dk, dv = torch.full_like(q, float("nan")), torch.empty_like(k), torch.empty_like(v)
+        ops.attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal)
+        torch.cuda.synchronize()
+        res[ks] = (out, lse, dq, dk, dv)
+    for ks in (None, "3"):
+        for i, (a, b) in enumerate(zip(res[ks], res["1"])):
+            assert torch.isfinite(a).all(), (ks, i)
+            if i == 1:
+                assert (a - b).abs().max().item() < 1e-3, (ks, "lse")
+            else:
+                assert rel(a, b) < 1e-2, (ks, i, rel(a, b))
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention(qf, kf, vf, causal)
+    of.backward(do.float())
+    assert rel(res[None][0], of) < 2e-2
+    for a, r in zip(res[None][2:], (qf.grad, kf.grad, vf.grad)):
+        assert rel(a, r) < 3e-2, rel(a, r)
+
+
+@pytest.mark.parametrize("H,Hkv,hd,Ta,Tb", [(2, 1, 256, 512, 512), (4, 2, 128, 300, 200)])
+def test_attention_packed_prefix_matches_whole_sequence(H, Hkv, hd, Ta, Tb):
+    """ops.attention_packed_prefix (chunk B of a sequence split over chunk A's keys + its own, packed
+    buffers) == causal attention of the whole sequence restricted to chunk B's rows, and its
+    gradients into both packed buffers == the whole-sequence gradients."""
+    from solvingpapers_amd.ops import attention_packed
+    from solvingpapers_amd.ops.attention import attention_packed_prefix
+    torch.manual_seed(6)
+    W = (H + 2 * Hkv) * hd
+    full = torch.randn(1, Ta + Tb, W, device=DEV, dtype=torch.bfloat16)
+    a = full[:, :Ta].clone().requires_grad_()
+    b = full[:, Ta:].clone().requires_grad_()
+    o = attention_packed_prefix(b, a, H, Hkv, hd)
+    do = torch.randn_like(o)
+    o.backward(do)
+    f = full.clone().requires_grad_()
+    of = attention_packed(f, H, Hkv, causal=True, head_dim=hd)
+    of[:, Ta:].backward(do)
+    assert rel(o, of[:, Ta:]) < 1e-2
+    assert rel(b.grad, f.grad[:, Ta:]) < 2e-2 and rel(a.grad, f.grad[:, :Ta]) < 2e-2
+
+
+@pytest.mark.parametrize("ksplit", [None, "3"])
+def test_flash_lse_and_spike(ksplit, monkeypatch):
+    """Force the online-softmax rescale: one key spiked against one query (rule 26); with a forced
+    key split the spike sits in one share and the merge rescales the others."""
+    if ksplit:
+        monkeypatch.setenv("SPA_ATTN_KSPLIT", ksplit)
     B, T, H, hd = 1, 300, 2, 128
     q = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16) * 0.1
     k = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16) * 0.1

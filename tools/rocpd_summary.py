@@ -5,7 +5,7 @@ kernel start to the last kernel end and the sum of kernel time (busy union per q
 whether two streams' kernels ran side by side).
 
   python tools/rocpd_summary.py gpurun_out/<dir>/run_results.db [--top 25] [--grep attn]
-      [--timeline START_MS:DUR_MS] [--comm stream_copy] [--last-step adamw]
+      [--timeline START_MS:DUR_MS [--merged]] [--comm stream_copy] [--last-step adamw]
 
 --timeline prints every kernel of that window (ms from the first kernel) per stream, with the
 idle gaps; --comm NAME reports how much of the time kernels matching NAME (a collective or its
@@ -82,13 +82,22 @@ def _short(name):
     return n[:48]
 
 
-def timeline(rows, start_ms, dur_ms, out=sys.stdout):
+def timeline(rows, start_ms, dur_ms, out=sys.stdout, merged=False):
+    """Kernels of the window [start, start + dur) ms from the first kernel (a negative start:
+    from the last kernel's end), per stream with idle gaps, or (merged) all streams in start order."""
     t0 = min(r[0] for r in rows)
+    if start_ms < 0:
+        start_ms += (max(r[1] for r in rows) - t0) / 1e6
     lo, hi = t0 + start_ms * 1e6, t0 + (start_ms + dur_ms) * 1e6
     byq = {}
     for s, e, q, st, disp, name in sorted(rows):
         if e >= lo and s <= hi:
             byq.setdefault((q, st), []).append((s, e, disp or name))
+    if merged:
+        ev = sorted((s, e, key, n) for key, ks in byq.items() for s, e, n in ks)
+        for s, e, key, n in ev:
+            print(f"  {(s - t0) / 1e6:9.3f} ms  +{(e - s) / 1e3:8.1f} us  s{key[1]}  {_short(n)}", file=out)
+        return
     for key, ks in sorted(byq.items()):
         print(f"-- queue {key[0]} stream {key[1]}", file=out)
         prev = None
@@ -133,7 +142,8 @@ def main():
     ap.add_argument("db", nargs="+")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--grep", default=None)
-    ap.add_argument("--timeline", default=None, help="START_MS:DUR_MS")
+    ap.add_argument("--timeline", default=None, help="START_MS:DUR_MS (negative START: from the end)")
+    ap.add_argument("--merged", action="store_true", help="timeline: all streams in one start-ordered list")
     ap.add_argument("--comm", default=None, help="kernel-name substring of the collective kernels")
     ap.add_argument("--last-step", default=None, metavar="KERNEL",
                     help="summarise only the last training step: the window between the last two "
@@ -150,7 +160,7 @@ def main():
                 comm_overlap(rows, a.comm)
             if a.timeline:
                 st, du = (float(x) for x in a.timeline.split(":"))
-                timeline(rows, st, du)
+                timeline(rows, st, du, merged=a.merged)
 
 
 if __name__ == "__main__":
