@@ -571,7 +571,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnParams p) {
 // Loops over the q-heads sharing this kv-head (GQA) so the group sum stays in regs.
 // DROP: dV^T += dO^T (P M / (1-p)); dS = P (M dP / (1-p) - delta), M regenerated by hash.
 // ---------------------------------------------------------------------------
-template <int HDK, int HDV, bool CAUSAL, int MT, bool FUSEDQ, bool DROP>
+template <int HDK, int HDV, bool CAUSAL, int MT, bool FUSEDQ, bool DROP, bool DSOUT = false>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   // MT 32-row q sub-tiles per iteration (more MFMA work per barrier / LDS fill)
   constexpr int BMQ = 32 * MT, BNK = 128, KSK = HDK / 16, KSV = HDV / 16, DTK = HDK / 32, DTV = HDV / 32;
@@ -766,6 +766,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
           for (int r = 0; r < 16; ++r) s[r] = ((keep >> r) & 1) ? s[r] * p.drop_scale : 0.f;
         }
         const bf16x8 pa = pack_acc(s, 0), pb = pack_acc(s, 1), sa = pack_acc(dp, 0), sb = pack_acc(dp, 1);
+        if constexpr (DSOUT) {   // bf16 dS of this 32 x 32 block -> p.dsbuf (ds_slot layout, see dkdv3)
+          const int qt = qt0 >> 5, kt = kw0 >> 5;
+          if ((!CAUSAL || kt <= qt) && qt < p.ds_nqt && kt < p.ds_nkt) {
+            const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(p.dsbuf + ((long)b * p.Hkv + hk) * p.ds_kvstride), 0, (int)(p.ds_kvstride * 2), 0x00020000);
+            const int bo = (int)(ds_index(qt, kt, (it + ib) / nper, G, p.ds_nkt, CAUSAL) * 2048);
+            const int vo = 16 * ds_slot(0, hh, lk);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sa), dsr, vo, bo, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sb), dsr, vo + 128, bo, 0);
+          }
+        }
         if constexpr (FUSEDQ) {
           // dS rows of this wave's 32 keys -> [key][q] image (registers 4g..4g+3 = 4 consecutive q)
 #pragma unroll
@@ -1458,6 +1469,121 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   }
 }
 
+// Head dim 256 form of the above (after attn_bwd_dkdv_kernel<256, 256, .., DSOUT>): a unit is one
+// (q-head, 32-query tile), so a wave's dQ^T accumulator is 32 queries x 256 dims (128 registers,
+// two waves per SIMD); per 32-key step each wave DMAs its one 2 KiB dS block and an eighth of the
+// 16 KiB K tile (4 + 2 pieces: the same vmcnt(6) discipline), 3 slots of 24 KiB.
+template <bool CAUSAL, bool NT>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds256_kernel(AttnParams p) {
+  constexpr int HD = 256, DT = 8, KIMG = 32 * HD, WSLOT = 1024, SLOT = KIMG + 4 * WSLOT, NSLOT = 3;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSLOT * SLOT];   // [slot][K | 4 waves x 1 dS block]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5;
+  const int G = p.H / p.Hkv;
+  const int nqt = cdiv(p.Tq, 32);
+  const int upkv = nqt * G;
+  const int wgpkv = cdiv(upkv, 4);
+  const int nbkv = p.B * p.Hkv;
+  const int bkv = blockIdx.x % nbkv;
+  const int w = CAUSAL ? wgpkv - 1 - (int)(blockIdx.x / nbkv) : (int)(blockIdx.x / nbkv);  // heaviest first
+  const int b = bkv / p.Hkv, hk = bkv % p.Hkv;
+  const int u = 4 * w + wave;
+  const bool uvalid = u < upkv;
+  const int qt = uvalid ? u / G : 0;
+  const int h = hk * G + (uvalid ? u % G : 0);
+  auto unit_steps = [&](int uu) {
+    const int qtt = uu / G;
+    return CAUSAL ? cdiv(min(p.Tk, qtt * 32 + 32 + p.causal_off), 32) : cdiv(p.Tk, 32);
+  };
+  const int nsteps_w = uvalid ? unit_steps(u) : 0;
+  const int nsteps = unit_steps(min(4 * w + 3, upkv - 1));
+
+  // K tile DMA: wave `wave` fills rows 8*wave .. +7 (four 1 KiB pieces of 2 rows); lane -> row
+  // r = 8*wave + 2j + lane/32, image chunk lane%32 holding source chunk (lane%32) ^ swz(r)
+  const bf16* kbase = p.k + b * p.skb + hk * p.skh;
+  unsigned kvo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 8 * wave + 2 * j + (lane >> 5);
+    kvo[j] = (unsigned)(((long)r * p.skt + 8 * ((lane & 31) ^ swz<HD>(r))) * 2);
+  }
+  const bf16* dskv = p.dsbuf + ((long)b * p.Hkv + hk) * p.ds_kvstride;
+  const int g = h - hk * G;
+  auto live = [&](int kt) { return uvalid && qt < p.ds_nqt && (!CAUSAL || kt <= qt); };
+  auto issue = [&](int j, int slot) {
+    bf16* sl = smem + slot * SLOT;
+    const int key0 = 32 * j;
+    const long kbytes = key0 < p.Tk ? ((long)(p.Tk - key0 - 1) * p.skt + HD) * 2 : 0;
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(kbase + (long)key0 * p.skt), 0, (int)min(kbytes, 0x7fffffffL), 0x00020000);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) dma16_asm(rk, kvo[jj], lds_addr(sl + (8 * wave + 2 * jj) * HD));
+    const bool lv = live(j);
+    const bf16* src = lv ? dskv + ds_index(qt, j, g, G, p.ds_nkt, CAUSAL) * 1024 : p.dsbuf;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, lv ? 2048 : 0, 0x00020000);
+    bf16* dst = sl + KIMG + wave * WSLOT;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) dma16_asm<NT>(rd, (unsigned)(lane * 16 + jj * 1024), lds_addr(dst + jj * 512));
+  };
+  LdsOff<HD> off;
+  off.init(lane);
+  int dso[2];
+  {
+    const int gg = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int ab = 0; ab < 2; ++ab) {
+      const int key = 4 * hh + q + 8 * ab;
+      dso[ab] = 8 * ds_slot(gg, pp & 1, key) + 4 * (pp >> 1);   // elements; +512 per 16-key step
+    }
+  }
+  f32x16 acc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) acc[i] = splat16(0.f);
+
+  auto compute = [&](int j, const bf16* sl) {
+    if (j >= nsteps_w || !live(j)) return;
+    const bf16* Ks = sl;
+    const bf16* Dw = sl + KIMG + wave * WSLOT;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 d0 = ld_tr(Dw + 512 * s, dso[0], dso[1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma32(ld_tr(Ks + 16 * s * HD, off.tra[dt], off.trb[dt]), d0, acc[dt]);
+      chain_sched<DT, 1, 2, 1>();
+    }
+  };
+  if (nsteps > 0) issue(0, 0);
+  if (nsteps > 1) issue(1, 1);
+  for (int j = 0; j < nsteps; j += 3) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int jj = j + r;
+      if (jj < nsteps) {
+        if (jj + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // step jj landed, jj+1 in flight
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (jj + 2 < nsteps) issue(jj + 2, (r + 2) % 3);
+        compute(jj, smem + r * SLOT);
+      }
+    }
+  }
+  if (!uvalid) return;
+  const int q = qt * 32 + (lane & 31);
+  if (q >= p.Tq) return;
+  bf16* op = p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      bf16x4 wv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wv[i] = (bf16)(acc[dt][4 * gq + i] * p.scale);
+      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * gq + 4 * hh) = wv;
+    }
+}
+
 // sum the q-head-split fp32 partials of ONE tensor (dK with HD = HDK, or dV with HD = HDV)
 // -> bf16 dK (scaled) / dV
 template <int HD>
@@ -1901,6 +2027,49 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
       } else {
         if (causal) attn_bwd_dq_ds_kernel<HDK, true, false><<<wg, 256, 0, st>>>(p);
         else attn_bwd_dq_ds_kernel<HDK, false, false><<<wg, 256, 0, st>>>(p);
+      }
+      return;
+    }
+  }
+  if constexpr (HDK == 256 && HDV == 256 && !DROP) {
+    // dS-materialising backward at head dim 256: the single-wave dK/dV kernel also stores dS,
+    // then dQ = dS K streams it (attn_bwd_dq_ds256_kernel) -- instead of the dq kernel's three
+    // products (S and dP recomputed over 256-deep contractions). SPA_ATTN_DQ_DS (per call): 0 keeps
+    // the dq kernel, 2 takes this path at any grid size.
+    const char* de = getenv("SPA_ATTN_DQ_DS");
+    const int dsm = de ? atoi(de) : 1;     // 0 off, 1 by grid size, 2 always
+    const bool want = dsm != 0;
+    const int G = p.H / p.Hkv;
+    const long kv_bytes = 2 * ds_kv_elems(cdiv(p.Tq, 64), cdiv(p.Tk, 32), G, causal);
+    // the dQ pass has one block per 4 (q-head, 32-query) units: with few of them (TP-sharded MQA,
+    // 2 q-heads: 128 blocks at T 8192) the key-split dq kernel fills the chip better (measured
+    // 0.364 vs 0.391 ms there; 1.70 vs 2.21 ms for the 16-head layout)
+    const int wg = cdiv(cdiv(p.Tq, 32) * G, 4) * p.B * p.Hkv;
+    if (want && (wg >= 512 || dsm == 2) && p.Tk > 0 && dkdv_mode == 0 && (!causal || p.causal_off == 0) &&
+        kv_bytes < 0x7fffffffL) {
+      const long rows = (long)p.B * p.Tq * p.H;
+      attn_delta_kernel<HDK><<<(int)cdiv(rows, 256 / (HDK / 8)), 256, 0, st>>>(p);
+      p.ds_nqt = cdiv(p.Tq, 32);
+      p.ds_nkt = cdiv(p.Tk, 32);
+      p.ds_kvstride = ds_kv_elems(cdiv(p.Tq, 64), p.ds_nkt, G, causal);
+      at::Tensor dsb = at::empty({(long)p.B * p.Hkv * p.ds_kvstride}, bf16_opts);   // freed (stream-ordered) on return
+      p.dsbuf = (bf16*)dsb.data_ptr();
+      const int g2 = nkv * p.hsplit;
+      if (causal) attn_bwd_dkdv_kernel<256, 256, true, 1, false, false, true><<<g2, 256, 0, st>>>(p);
+      else attn_bwd_dkdv_kernel<256, 256, false, 1, false, false, true><<<g2, 256, 0, st>>>(p);
+      const char* ne = getenv("SPA_ATTN_DS_NT");
+      const bool nt = !(ne && atoi(ne) == 0);
+      if (nt) {
+        if (causal) attn_bwd_dq_ds256_kernel<true, true><<<wg, 256, 0, st>>>(p);
+        else attn_bwd_dq_ds256_kernel<false, true><<<wg, 256, 0, st>>>(p);
+      } else {
+        if (causal) attn_bwd_dq_ds256_kernel<true, false><<<wg, 256, 0, st>>>(p);
+        else attn_bwd_dq_ds256_kernel<false, false><<<wg, 256, 0, st>>>(p);
+      }
+      if (p.hsplit > 1) {
+        const long kr = (long)p.B * p.Tk * p.Hkv;
+        attn_kv_reduce_kernel<HDK><<<(int)std::min<long>((kr * (HDK / 8) + 255) / 256, 65536), 256, 0, st>>>(p, 1);
+        attn_kv_reduce_kernel<HDV><<<(int)std::min<long>((kr * (HDV / 8) + 255) / 256, 65536), 256, 0, st>>>(p, 0);
       }
       return;
     }

@@ -123,36 +123,12 @@ __device__ __forceinline__ bf16x8 rd_ks(const char* half, int col0, int s, int l
 // results by construction and are never selected by the op unless SPA_GG8_ABLATE is set.
 // PART (mode 2 only): the "experts" are token slices of one dense dW product (split-K) and each
 // writes its fp32 partial [M, N] at C + e * strideC floats, summed by wgrad_reduce_kernel.
-// EPI (single group, E == 1, no accumulate; gemm8_epi below): fused epilogues of a Linear +
-// activation pair, applied to the bf16-rounded C values exactly as the separate kernels would:
-//   1 (mode 0)  u = C + bias[n] -> ep.aux, C = act(u)                    (fc1 + act forward)
-//   2 (mode 1)  C = C * act'(ep.aux[m, n]), fp32 column sums of C per 256-row tile -> ep.part
-//               [m-tile, N] (the bias gradient of the Linear that produced aux)   (fc2 dgrad + act')
-struct G8Epi {
-  const bf16* bias;
-  bf16* aux;
-  float* part;
-  float alpha;
-};
-// Mode 2 over several token sources (gradient-accumulation micro-batches whose weight gradients
-// were deferred, ops/moe.py defer_expert_wgrad): expert e's reduction range is the concatenation
-// of [off_s[e], off_s[e+1]) of every source s, each read from its own (dY_s, X_s) pair; every
-// source's last K-tile is zero-filled past its end by the buffer range check. n == 0: the
-// kernel's own (A, B, offsets).
-constexpr int G8_MAXSEG = 8;
-struct G8Segs {
-  const bf16* a[G8_MAXSEG];
-  const bf16* b[G8_MAXSEG];
-  const int* off[G8_MAXSEG];
-  int n;
-};
-
-template <int MODE, int ABL = 0, bool ILV = false, bool PART = false, int EPI = 0, int KIND = 0, bool SEGS = false>
+template <int MODE, int ABL = 0, bool ILV = false, bool PART = false>
 __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                                bf16* __restrict__ C, const int* __restrict__ offsets,
                                                                int E, int M, int N, int K, long lda, long ldb, long ldc,
                                                                long strideB, long strideC, int accumulate, long a_rows,
-                                                               long b_rows, G8Epi ep, G8Segs sg) {
+                                                               long b_rows) {
   using namespace g8;
   constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
   // ONE LDS array (a second __shared__ object can make hipcc drain the DMA queue before ds_reads);
@@ -210,15 +186,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       // not yet used stage area; the choice is the same in every block.
       int* cnt = reinterpret_cast<int*>(smem);
       if (tid < E) {
-        int c = 0;
-        if (SEGS) {
-#pragma unroll
-          for (int q = 0; q < G8_MAXSEG; ++q)
-            if (q < sg.n) c += sg.off[q][tid + 1] - sg.off[q][tid];
-        } else {
-          c = offsets[tid + 1] - offsets[tid];
-        }
-        cnt[tid] = c;
+        cnt[tid] = offsets[tid + 1] - offsets[tid];
       }
       __syncthreads();
       long tot = 0;
@@ -255,34 +223,12 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     m0 = (long)mt * BM;
     Cp = C + e * strideC;
   }
-  // mode 2 reduction sources: (A, B, [k0, kend)) per source, its K-tiles in sequence
-  int nseg = 1, sk0[G8_MAXSEG], skend[G8_MAXSEG], skt[G8_MAXSEG];
-  if (MODE == 2 && !SEGS) {
+  if (MODE == 2) {   // the expert's token range is the reduction range
     k0 = __builtin_amdgcn_readfirstlane(offsets[e]);
     kend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
   }
-  if (MODE == 2 && SEGS) {
-    nseg = sg.n > 0 ? sg.n : 1;
-#pragma unroll
-    for (int q = 0; q < G8_MAXSEG; ++q) {
-      sk0[q] = skend[q] = skt[q] = 0;
-      if (q < nseg) {
-        const int* o = sg.n > 0 ? sg.off[q] : offsets;
-        sk0[q] = __builtin_amdgcn_readfirstlane(o[e]);
-        skend[q] = __builtin_amdgcn_readfirstlane(o[e + 1]);
-        skt[q] = skend[q] > sk0[q] ? (skend[q] - sk0[q] + BK - 1) / BK : 0;
-      }
-    }
-    k0 = sk0[0];
-    kend = skend[0];
-  }
   const int n0 = nt * BN;
-  int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
-  if (MODE == 2 && SEGS) {
-    ktiles = 0;
-#pragma unroll
-    for (int q = 0; q < G8_MAXSEG; ++q) ktiles += skt[q];
-  }
+  const int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   unsigned voA[2], voB[2];
 #pragma unroll
@@ -299,40 +245,6 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   auto stage = [&](int t, int which) {       // which: 0 A0, 1 A1, 2 B0, 3 B1
     if (ABL == 1) return;
     char* dst = half(t & 1, which) + wave_u * 1024;
-    if (MODE == 2 && SEGS) {
-      // K-tile t of the concatenated sources: its source q and local tile tt by scalar selects
-      // (no array indexed at run time), then every selected value through readfirstlane so the
-      // buffer descriptor is provably wave-uniform (a VGPR descriptor makes hipcc emit a
-      // waterfall loop around each DMA: cdna_hip_programming.md T20)
-      int q = 0, tt = t;
-#pragma unroll
-      for (int j = 0; j < G8_MAXSEG - 1; ++j) {
-        const bool adv = q == j && j + 1 < nseg && tt >= skt[j];
-        tt = adv ? tt - skt[j] : tt;
-        q = adv ? j + 1 : q;
-      }
-      uint64_t pa = (uint64_t)sg.a[0], pb = (uint64_t)sg.b[0];
-      int kb = sk0[0], ke = skend[0];
-#pragma unroll
-      for (int j = 1; j < G8_MAXSEG; ++j) {
-        const bool h = q == j;
-        pa = h ? (uint64_t)sg.a[j] : pa;
-        pb = h ? (uint64_t)sg.b[j] : pb;
-        kb = h ? sk0[j] : kb;
-        ke = h ? skend[j] : ke;
-      }
-      const bf16* sa = (const bf16*)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(pa >> 32)) << 32) |
-                                     (unsigned)__builtin_amdgcn_readfirstlane((int)pa));
-      const bf16* sb = (const bf16*)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(pb >> 32)) << 32) |
-                                     (unsigned)__builtin_amdgcn_readfirstlane((int)pb));
-      kb = __builtin_amdgcn_readfirstlane(kb);
-      ke = __builtin_amdgcn_readfirstlane(ke);
-      tt = __builtin_amdgcn_readfirstlane(tt);
-      const long kk = (long)kb + (long)tt * BK;
-      if (which < 2) stage_half(sa, kk * lda + m0 + 128 * which, (long)ke * lda, dst, voA);
-      else stage_half(sb, kk * ldb + n0 + 128 * (which - 2), (long)ke * ldb, dst, voB);
-      return;
-    }
     const long kk = k0 + (long)t * BK;       // absolute reduction index of the tile
     if (which < 2) {
       const long r = m0 + 128 * which;
@@ -583,21 +495,6 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   // distinct bank pairs) -> whole-row 16-byte global stores (a per-lane 8-byte store at a row
   // stride would touch 16 cache lines per instruction)
   constexpr int RS = 256 * 2 + 16;
-  // EPI 1: this lane's bias values (columns n0 + nh*128 + wn*32 + 16j + 4(l>>4) + q), added in fp32
-  float bv[2][2][4];
-  if constexpr (EPI == 1) {
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
-        bf16x4 b4 = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-        if (gn < N) b4 = *reinterpret_cast<const bf16x4*>(ep.bias + gn);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bv[nh][j][q] = (float)b4[q];
-      }
-  }
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // EPI 2: column sums of this lane's chunk
   __syncthreads();
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
@@ -610,10 +507,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
           const f32x4 v = acc[mh * 4 + i][nh * 2 + j];
           bf16x4 w4;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if constexpr (EPI == 1) w4[q] = (bf16)(v[q] + bv[nh][j][q]);
-            else w4[q] = (bf16)v[q];
-          }
+          for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
           const int r = wm * 64 + 16 * i + (lane & 15);
           const int cn = nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
           *reinterpret_cast<bf16x4*>(smem + r * RS + cn * 2) = w4;
@@ -627,19 +521,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       if ((MODE == 2 ? gm < M : gm < mend) && gn < N) {
         bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * RS + ch * 16);
         bf16* cp = Cp + gm * ldc + gn;
-        if constexpr (EPI == 1) {
-          *reinterpret_cast<bf16x8*>(ep.aux + gm * ldc + gn) = v;       // pre-activation u
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = (bf16)act_f(KIND, (float)v[q], ep.alpha);
-        } else if constexpr (EPI == 2) {
-          const bf16x8 u = *reinterpret_cast<const bf16x8*>(ep.aux + gm * ldc + gn);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            v[q] = (bf16)((float)v[q] * act_df(KIND, (float)u[q], ep.alpha));
-            csum[q] += (float)v[q];
-          }
-        }
-        if (EPI == 0 && accumulate) {
+        if (accumulate) {
           const bf16x8 old = *reinterpret_cast<const bf16x8*>(cp);
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)old[q]);
@@ -648,21 +530,6 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       }
     }
     __syncthreads();
-  }
-  if constexpr (EPI == 2) {
-    // every thread owns column chunk tid & 31 on rows (tid >> 5) + 16c: 16 partial rows per column
-    float* red = reinterpret_cast<float*>(smem);          // [16][256]
-#pragma unroll
-    for (int q = 0; q < 8; q += 4)
-      *reinterpret_cast<f32x4*>(red + (tid >> 5) * 256 + (tid & 31) * 8 + q) =
-          f32x4{csum[q], csum[q + 1], csum[q + 2], csum[q + 3]};
-    __syncthreads();
-    if (tid < 256 && n0 + tid < N) {
-      float t = 0.f;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) t += red[g * 256 + tid];
-      ep.part[(long)(m0 / BM) * N + n0 + tid] = t;
-    }
   }
 }
 
@@ -743,7 +610,7 @@ at::Tensor wgrad8(const at::Tensor& dy, const at::Tensor& x, const c10::optional
   auto part = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
   grouped_gemm8_kernel<2, 0, false, true><<<S * tiles, 512, 0, st>>>(
       (const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(), reinterpret_cast<bf16*>(part.data_ptr<float>()),
-      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T, G8Epi{}, G8Segs{});
+      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T);
   SPA_LAUNCH_CHECK();
   const long n = (long)N * K;
   const int rb = (int)std::min<long>((n / 4 + 255) / 256, 4096);
@@ -788,10 +655,10 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 #define G8_L(MD, AB)                                                                                          \
   if (abl == 4) grouped_gemm8_kernel<MD, 0, true><<<grid, 512, 0, st>>>(                                     \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,  \
-      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{}, G8Segs{});                                  \
+      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw);                                  \
   else grouped_gemm8_kernel<MD, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),     \
                                                      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
-                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, G8Epi{}, G8Segs{})
+                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw)
     const int abl = ablation();
     if (mode == 0) {
       if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else if (abl == 8) { G8_L(0, 8); } else { G8_L(0, 0); }
@@ -813,10 +680,10 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 #define G8_L2(AB)                                                                                             \
   if (abl == 4) grouped_gemm8_kernel<2, 0, true><<<grid, 512, 0, st>>>(                                      \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N,  \
-      K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{}, G8Segs{});                                     \
+      K, 0, N, K, K, 0, (long)N * K, accumulate ? 1 : 0, T, T);                                     \
   else grouped_gemm8_kernel<2, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),      \
                                                     (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, \
-                                                    K, 0, (long)N * K, accumulate ? 1 : 0, T, T, G8Epi{}, G8Segs{})
+                                                    K, 0, (long)N * K, accumulate ? 1 : 0, T, T)
   const int abl = ablation();
   if (abl == 1) { G8_L2(1); } else if (abl == 2) { G8_L2(2); } else if (abl == 3) { G8_L2(3); } else if (abl == 8) { G8_L2(8); } else { G8_L2(0); }
 #undef G8_L2
@@ -824,114 +691,13 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
   return out;
 }
 
-// Mode 2 over several (dY_s [T_s, N], X_s [T_s, K], offsets_s [E+1]) sources in ONE launch:
-// out[e] (+)= sum_s dY_s[rows_e]^T X_s[rows_e] -- the deferred expert weight gradient of several
-// gradient-accumulation micro-batches (G8Segs).
-at::Tensor grouped_gemm8_wgrad_multi(const std::vector<at::Tensor>& dys, const std::vector<at::Tensor>& xs,
-                                     const std::vector<at::Tensor>& offs, at::Tensor out, bool accumulate) {
-  const int S = (int)dys.size();
-  TORCH_CHECK(S >= 1 && S <= G8_MAXSEG && (int)xs.size() == S && (int)offs.size() == S,
-              "grouped_gemm8_wgrad_multi: 1..8 sources, equal list lengths");
-  const int N = dys[0].size(1), K = xs[0].size(1), E = offs[0].numel() - 1;
-  TORCH_CHECK(E >= 1 && E <= 512 && N % 8 == 0 && K % 8 == 0, "grouped_gemm8_wgrad_multi: shapes");
-  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == (long)E * N * K,
-              "grouped_gemm8_wgrad_multi: out bf16 [E, N, K]");
-  G8Segs sg{};
-  sg.n = S;
-  for (int q = 0; q < S; ++q) {
-    const auto &a = dys[q], &x = xs[q], &o = offs[q];
-    TORCH_CHECK(a.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && a.is_contiguous() &&
-                    x.is_contiguous() && a.dim() == 2 && x.dim() == 2, "grouped_gemm8_wgrad_multi: bf16 2-D");
-    TORCH_CHECK(a.size(1) == N && x.size(1) == K && a.size(0) == x.size(0), "grouped_gemm8_wgrad_multi: source shapes");
-    TORCH_CHECK(o.scalar_type() == at::kInt && o.numel() == E + 1 && o.is_contiguous() && o.is_cuda(),
-                "grouped_gemm8_wgrad_multi: offsets int32 [E+1] on the device");
-    TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)x.data_ptr() % 16 == 0, "16-B aligned");
-    const long T = a.size(0);
-    TORCH_CHECK((T + 64) * (N + 256) * 2 < (1L << 32) && (T + 64) * (K + 256) * 2 < (1L << 32),
-                "grouped_gemm8_wgrad_multi: operands < 4 GiB");
-    sg.a[q] = (const bf16*)a.data_ptr();
-    sg.b[q] = (const bf16*)x.data_ptr();
-    sg.off[q] = o.data_ptr<int>();
-  }
-  DeviceGuard g(out.device());
-  auto st = stream();
-  const int grid = E * cdiv(N, 256) * cdiv(K, 256);
-  grouped_gemm8_kernel<2, 0, false, false, 0, 0, true><<<grid, 512, 0, st>>>(sg.a[0], sg.b[0], (bf16*)out.data_ptr(), sg.off[0], E, N, K, 0, N,
-                                                    K, K, 0, (long)N * K, accumulate ? 1 : 0, 0, 0, G8Epi{}, sg);
-  SPA_LAUNCH_CHECK();
-  return out;
-}
-
-// Linear + activation epilogues on the 8-phase kernel (one group), see G8Epi:
-//   epi 1: a = x [M, K], w = W [N, K], aux = bias [N]      -> (act(x W^T + b), u = x W^T + b)
-//   epi 2: a = dY [M, K], w = W [K, N] (weight [out, in]), aux = u [M, N]
-//                                                           -> (dU = (dY W) * act'(u), colsum(dU) fp32 [N])
-// K % 64 == 0, N % 8 == 0; offsets = the device tensor [0, M].
-std::vector<at::Tensor> gemm8_epi(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t epi,
-                                  const at::Tensor& aux, int64_t kind, double alpha) {
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
-                  aux.scalar_type() == at::kBFloat16, "gemm8_epi: bf16");
-  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.is_contiguous() && w.is_contiguous() && aux.is_contiguous(),
-              "gemm8_epi: contiguous 2-D operands");
-  TORCH_CHECK(offsets.scalar_type() == at::kInt && offsets.numel() == 2, "gemm8_epi: offsets [0, M]");
-  TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)w.data_ptr() % 16 == 0 &&
-                  (uintptr_t)aux.data_ptr() % 16 == 0, "gemm8_epi: 16-B aligned");
-  const int M = a.size(0), K = a.size(1);
-  const int mode = epi == 1 ? 0 : 1;
-  TORCH_CHECK(epi == 1 || epi == 2, "gemm8_epi: epi 1 or 2");
-  const int N = mode == 0 ? w.size(0) : w.size(1);
-  TORCH_CHECK((mode == 0 ? w.size(1) : w.size(0)) == K, "gemm8_epi: A/W shape mismatch");
-  TORCH_CHECK(K % 64 == 0 && N % 8 == 0, "gemm8_epi: reduction % 64, output cols % 8");
-  if (epi == 1) {
-    TORCH_CHECK(aux.numel() == N, "gemm8_epi: bias [N]");
-  } else {
-    TORCH_CHECK(aux.dim() == 2 && aux.size(0) == M && aux.size(1) == N, "gemm8_epi: u [M, N]");
-  }
-  TORCH_CHECK((long)(M + 256) * K * 2 < (1L << 32) && (long)(w.numel() + 256L * K) * 2 < (1L << 32),
-              "gemm8_epi: operands < 4 GiB");
-  TORCH_CHECK(kind == GELU_ERF || kind == GELU_TANH || kind == RELU || kind == SILU, "gemm8_epi: act kind");
-  DeviceGuard g(a.device());
-  auto st = stream();
-  auto out = at::empty({M, N}, a.options());
-  const int mtiles = cdiv(M, 256);
-  at::Tensor second = epi == 1 ? at::empty({M, N}, a.options()) : at::empty({mtiles, N}, a.options().dtype(at::kFloat));
-  if (M == 0) return {out, epi == 1 ? second : at::zeros({N}, a.options().dtype(at::kFloat))};
-  G8Epi ep{};
-  ep.alpha = (float)alpha;
-  if (epi == 1) { ep.bias = (const bf16*)aux.data_ptr(); ep.aux = (bf16*)second.data_ptr(); }
-  else { ep.aux = (bf16*)aux.data_ptr(); ep.part = second.data_ptr<float>(); }
-  const int grid = (mtiles + 1) * cdiv(N, 256);
-  const int Nw = w.size(0), Kw = w.size(1);
-#define G8E(MD, EP, KD)                                                                                      \
-  grouped_gemm8_kernel<MD, 0, false, false, EP, KD><<<grid, 512, 0, st>>>(                                   \
-      (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), 1, M, \
-      N, K, K, Kw, N, (long)Nw * Kw, 0, 0, M, Nw, ep, G8Segs{})
-#define G8E_KIND(MD, EP)                                  \
-  switch (kind) {                                         \
-    case GELU_ERF: G8E(MD, EP, GELU_ERF); break;          \
-    case GELU_TANH: G8E(MD, EP, GELU_TANH); break;        \
-    case RELU: G8E(MD, EP, RELU); break;                  \
-    default: G8E(MD, EP, SILU); break;                    \
-  }
-  if (epi == 1) { G8E_KIND(0, 1); } else { G8E_KIND(1, 2); }
-#undef G8E_KIND
-#undef G8E
-  SPA_LAUNCH_CHECK();
-  if (epi == 1) return {out, second};
-  return {out, reduce_col_parts(second)};
-}
-
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("grouped_gemm8(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def("wgrad8(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate, int splits) -> Tensor");
-  m.def("grouped_gemm8_wgrad_multi(Tensor[] dy, Tensor[] x, Tensor[] offsets, Tensor(a!) out, bool accumulate) -> Tensor");
-  m.def("gemm8_epi(Tensor a, Tensor w, Tensor offsets, int epi, Tensor aux, int kind, float alpha) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("grouped_gemm8", &spa::grouped_gemm8);
   m.impl("wgrad8", &spa::wgrad8);
-  m.impl("gemm8_epi", &spa::gemm8_epi);
-  m.impl("grouped_gemm8_wgrad_multi", &spa::grouped_gemm8_wgrad_multi);
 }

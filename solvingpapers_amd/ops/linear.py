@@ -180,70 +180,11 @@ def linear_act(x, w, b, kind="gelu", alpha=None):
     return act(linear(x, w, b), kind, alpha)
 
 
-# fc1 + act forward and fc2-dgrad + act' backward on the 8-phase kernel's fused epilogues
-# (csrc/kernels/gemm8.hip gemm8_epi). Off by default: at ViT-B/16 widths (K = 768, 12 K-tiles)
-# the 8-phase kernel runs fc1 at 630-770 TF against hipBLASLt's ~1 PF, which costs more than the
-# activation pass it saves (tools/bench_vit_mlp.py: fwd+bwd 1.955 vs 1.901 ms,
-# profiles/r3_vit_mlp_epilogue_ab.txt); hipBLASLt's own GELU epilogues are the tanh form, not the
-# exact erf GELU of the reference ViT. SPA_MLP_EPI=1 selects it.
-MLP_EPI = os.environ.get("SPA_MLP_EPI", "0") == "1"
-
-
-def _mlp_epi_ok(x2, w1, w2):
-    F, D = w1.shape
-    return (MLP_EPI and x2.is_cuda and x2.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16
-            and w2.dtype == torch.bfloat16 and D % 64 == 0 and F % 64 == 0 and w2.shape == (D, F)
-            and x2.shape[0] > 0 and x2.is_contiguous() and w1.is_contiguous() and w2.is_contiguous())
-
-
-class _MLPFn(torch.autograd.Function):
-    """fc2(act(fc1(x))) with both biases (ViT / transformer MLP without inner dropout).
-
-    Forward: fc1 on the 8-phase kernel with the bias + activation epilogue (writes y = act(u) and
-    the pre-activation u in the same pass), fc2 on the library GEMM. Backward: fc2's dX product
-    runs on the same kernel with the act' epilogue -- dU = (dOut W2) * act'(u) and the column
-    sums of dU (fc1's bias gradient) leave the GEMM together -- so the [T, F] activation
-    gradient is written once and never re-read for the bias; then the usual dX / dW products.
-    Rounding matches the unfused chain (bf16 u and y; dY W2 rounded to bf16 before act')."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, kind, alpha):
-        x2 = x.reshape(-1, x.shape[-1])
-        grp = _one_group(x2.shape[0], x2.device)
-        y, u = _ext.ops().gemm8_epi(x2, w1, grp, 1, b1, kind, alpha)
-        out = torch.addmm(b2, y, w2.t())
-        ctx.save_for_backward(x, u, y)
-        ctx.ws, ctx.kind, ctx.alpha = (w1, b1, w2, b2), kind, alpha
-        return torch.ops.aten._unsafe_view(out, (*x.shape[:-1], w2.shape[0]))
-
-    @staticmethod
-    def backward(ctx, dout):
-        x, u, y = ctx.saved_tensors
-        w1, b1, w2, b2 = ctx.ws
-        d2 = dout.reshape(-1, dout.shape[-1]).contiguous()
-        x2 = x.reshape(-1, x.shape[-1])
-        g = [None] * 7
-        if ctx.needs_input_grad[3]:
-            g[3] = commit(w2, lambda out, acc: wgrad(d2, y, out, acc))
-        if ctx.needs_input_grad[4]:
-            g[4] = _commit_bias(b2, bias_grad(d2))
-        du, s1 = _ext.ops().gemm8_epi(d2, w2, _one_group(d2.shape[0], d2.device), 2, u, ctx.kind, ctx.alpha)
-        if ctx.needs_input_grad[2]:
-            g[2] = _commit_bias(b1, s1)
-        if ctx.needs_input_grad[1]:
-            g[1] = commit(w1, lambda out, acc: wgrad(du, x2, out, acc))
-        if ctx.needs_input_grad[0]:
-            g[0] = dgrad(du, w1).view(x.shape)
-        return tuple(g)
-
-
 def mlp(x, w1, b1, w2, b2, kind="gelu", alpha=None):
-    """fc2(act(fc1(x))) -- the fused kernel path where it applies, else linear_act + linear."""
-    from .reference import ACT_KINDS
-    if b1 is not None and b2 is not None and kind in ("gelu", "gelu_erf", "gelu_tanh", "relu", "silu"):
-        x2 = x.reshape(-1, x.shape[-1])
-        if _mlp_epi_ok(x2, w1, w2):
-            return _MLPFn.apply(x, w1, b1, w2, b2, ACT_KINDS[kind], 0.0)
+    """fc2(act(fc1(x))): hipBLASLt GEMMs with the activation backward and fc1's bias gradient fused
+    (linear_act). GEMM epilogues on the 8-phase kernel were measured 2.8 % slower at ViT-B widths
+    (fc1 at 630-770 TF vs hipBLASLt's ~1 PF at K = 768, profiles/r3_vit_mlp_epilogue_ab.txt) and
+    were removed in round 4."""
     return linear(linear_act(x, w1, b1, kind, alpha), w2, b2)
 
 

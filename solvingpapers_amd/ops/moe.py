@@ -16,7 +16,6 @@ the CPU parity tests and the gloo EP tests).
 """
 from __future__ import annotations
 
-import contextlib
 from dataclasses import dataclass
 
 import os

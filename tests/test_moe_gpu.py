@@ -436,31 +436,6 @@ def _counts_offsets(counts):
     return off, int(sum(counts))
 
 
-def test_grouped_gemm8_wgrad_multi_sources():
-    """dW over several (dY_s, X_s, offsets_s) sources in one launch (deferred micro-batches) vs the
-    fp32 sum of per-source per-expert products; ragged tails, empty experts, accumulate."""
-    torch.manual_seed(11)
-    E, N, K = 5, 264, 200
-    srcs = []
-    for counts in ([70, 0, 130, 3, 65], [0, 0, 300, 1, 1], [64, 64, 0, 129, 7]):
-        off, T = _counts_offsets(counts)
-        srcs.append((torch.randn(T, N, device=dev).bfloat16(), torch.randn(T, K, device=dev).bfloat16(), off))
-    ref = torch.zeros(E, N, K)
-    for dy, x, off in srcs:
-        o = off.tolist()
-        for e in range(E):
-            ref[e] += dy[o[e]:o[e + 1]].float().cpu().t() @ x[o[e]:o[e + 1]].float().cpu()
-    out = torch.empty(E, N, K, device=dev, dtype=torch.bfloat16)
-    M.ops().grouped_gemm8_wgrad_multi([s[0] for s in srcs], [s[1] for s in srcs], [s[2] for s in srcs], out, False)
-    assert _rel(out.cpu(), ref) < 1e-2
-    M.ops().grouped_gemm8_wgrad_multi([s[0] for s in srcs], [s[1] for s in srcs], [s[2] for s in srcs], out, True)
-    assert _rel(out.cpu(), 2 * ref) < 1e-2
-    # one source == the single-source kernel, bitwise
-    one = torch.empty_like(out)
-    M.ops().grouped_gemm8_wgrad_multi([srcs[0][0]], [srcs[0][1]], [srcs[0][2]], one, False)
-    assert torch.equal(one, M.grouped_gemm(srcs[0][0], srcs[0][1], srcs[0][2], 2))
-
-
 @pytest.mark.parametrize("ep,fp8", [(1, False), (8, False), (8, True)])
 def test_forward_pair_matches_two_forwards_gpu(ep, fp8):
     """DeepSeekV3.forward_pair on the GPU kernels == two forward() calls: loss and every gradient.
