@@ -37,7 +37,6 @@
 //     f(r) = ((r & 3) << 2) | ((r >> 2) & 3) -- read with ds_read_b64_tr_b16 (conflict-free).
 // Out-of-range rows / columns / tokens read as zero through the buffer descriptor range check
 // (dW descriptors start at the expert's first token and end at its last).
-#include "act_common.h"
 #include "gemm_common.h"
 
 #include <map>
@@ -128,7 +127,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
                                                                bf16* __restrict__ C, const int* __restrict__ offsets,
                                                                int E, int M, int N, int K, long lda, long ldb, long ldc,
                                                                long strideB, long strideC, int accumulate, long a_rows,
-                                                               long b_rows) {
+                                                               long b_rows, int gm = 1) {
   using namespace g8;
   constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
   // ONE LDS array (a second __shared__ object can make hipcc drain the DMA queue before ds_reads);
@@ -141,6 +140,12 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   int nt = lid % nnt;
   int mt = lid / nnt;
+  if (MODE != 2 && gm > 1) {   // groups of gm row tiles x all column tiles (L2 / MALL reuse of B panels)
+    const int mtiles = gridDim.x / nnt, g = lid / (gm * nnt), r = lid % (gm * nnt);
+    const int gs = min(gm, mtiles - g * gm);
+    mt = g * gm + r % gs;
+    nt = r / gs;
+  }
   int e = 0;
   long m0 = 0, mend = M, k0 = 0, kend = K;
   const bf16* Bp = B;
@@ -628,7 +633,13 @@ static int ablation() {
   const char* e = getenv("SPA_GG8_ABLATE");
   return e ? atoi(e) : 0;
 }
-
+// SPA_G8_GM (read per call): row tiles per tile group of a dense (E = 1) forward / dX grid
+// (default 4: 4 x 8 tiles per XCD wave instead of 1 x 32 -- dense 8192^3 +5 % fwd, +14 % dX);
+// grouped GEMMs keep the row-major order (the grouping measured -3 % on their forward)
+static int g8_group(int E) {
+  const char* e = getenv("SPA_G8_GM");
+  return E > 1 ? 1 : (e ? std::max(1, atoi(e)) : 4);
+}
 // same contract as grouped_gemm (moe.hip); requires the reduction dim % 64 == 0 in modes 0/1
 // and N, K % 8 == 0
 at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t mode,
@@ -655,10 +666,10 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
 #define G8_L(MD, AB)                                                                                          \
   if (abl == 4) grouped_gemm8_kernel<MD, 0, true><<<grid, 512, 0, st>>>(                                     \
       (const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(), (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M,  \
-      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw);                                  \
+      N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g8_group(E));                      \
   else grouped_gemm8_kernel<MD, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),     \
                                                      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
-                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw)
+                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g8_group(E))
     const int abl = ablation();
     if (mode == 0) {
       if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else if (abl == 8) { G8_L(0, 8); } else { G8_L(0, 0); }

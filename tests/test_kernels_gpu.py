@@ -718,6 +718,8 @@ def test_bias_grad_rowsum(R, N):
 
 @pytest.mark.parametrize("T,N,K", [(50432, 768, 3072), (50432, 2304, 768), (5000, 24, 40), (4096, 264, 520), (700, 64, 64)])
 def test_wgrad8_dense_dw(T, N, K):
+    """wgrad8 (split-K dense dW on the gemm8 kernel's token-major path, fp32 partials + reduce),
+    contiguous and row-strided operands."""
     from solvingpapers_amd.ops import _ext
     ops = _ext.ops()
     dyb = torch.randn(T, N + 8, device="cuda", dtype=torch.bfloat16)

@@ -236,19 +236,26 @@ def test_grouped_gemv_matches_reference(A, E, N, K):
     assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("gm", ["4", "1"])
 @pytest.mark.parametrize("counts,N,K", [
     ([300, 0, 129, 1, 64, 700, 0, 33], 320, 192),       # ragged tiles, N % 256 != 0
     ([0] * 7 + [513], 256, 512),
     ([257, 255], 1408, 2048),                           # DeepSeek-V2-Lite expert widths
     (None, 576, 256),                                   # 64 experts, skewed routing
+    (300, 256, 192),                                    # 300 experts
+    ([1300], 512, 320),                                 # dense (E = 1): tile groups of 4 + a partial one
 ])
-def test_grouped_gemm8_elementwise(counts, N, K):
+def test_grouped_gemm8_elementwise(counts, N, K, gm, monkeypatch):
     """csrc/kernels/gemm8.hip (LDS-DMA 8-phase kernel) per element against the fp32 oracle in all
-    three modes: a wrong fragment map or a mis-counted vmcnt shows up as a wrong 16x16 block,
-    which a relative-norm check over the whole tensor could hide."""
+    three modes, with the grouped (SPA_G8_GM=4, default) and the row-major tile order: a wrong
+    fragment map or a mis-counted vmcnt shows up as a wrong 16x16 block, which a relative-norm
+    check over the whole tensor could hide."""
+    monkeypatch.setenv("SPA_G8_GM", gm)
     g = torch.Generator().manual_seed(5)
     if counts is None:
         counts = (torch.rand(64, generator=g) ** 3 * 1500).long().tolist()
+    elif isinstance(counts, int):
+        counts = (torch.rand(counts, generator=g) ** 3 * 200).long().tolist()
     E, M_ = len(counts), sum(counts)
     off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
     x = torch.randn(M_, K, generator=g).to(dev, torch.bfloat16)

@@ -18,6 +18,7 @@ ap.add_argument("--modes", default="0,1,2")
 ap.add_argument("--no-blas", action="store_true")
 ap.add_argument("--ab", type=int, default=None, help="also run SPA_GG8_ABLATE=<v> (ABBA, same process) and "
                 "the dsv3_style grouped shapes")
+ap.add_argument("--abenv", default=None, help="NAME=VALUE: the ABBA arm sets this variable instead (e.g. SPA_G8W=0)")
 a = ap.parse_args()
 ops = _ext.ops()
 S = a.S
@@ -46,9 +47,18 @@ ref = torch.mm(xa, wb[0].t()).float()
 
 
 def arm(v):
-    os.environ["SPA_GG8_ABLATE"] = str(v)
+    if a.abenv:
+        k, val = a.abenv.split("=")
+        if v == 0:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = val
+    else:
+        os.environ["SPA_GG8_ABLATE"] = str(v)
 
 
+if a.abenv and a.ab is None:
+    a.ab = 1
 if a.ab is not None:
     from solvingpapers_amd.ops import moe as M
     torch.manual_seed(0)
@@ -88,8 +98,9 @@ if a.ab is not None:
             arm(v)
             t[v].append(tm(fn))
         m0, m1 = sum(t[0]) / 2, sum(t[a.ab]) / 2
-        print(f"{name:12s} default {f / m0 / 1e9:6.0f} TF | sched {a.ab} {f / m1 / 1e9:6.0f} TF "
-              f"({m0 / m1:.3f}x) bitwise-equal {same}", flush=True)
+        rel = ((r0 - r1).norm() / r1.norm().clamp_min(1e-30)).item()
+        print(f"{name:12s} default {f / m0 / 1e9:6.0f} TF | {a.abenv or 'sched %d' % a.ab} {f / m1 / 1e9:6.0f} TF "
+              f"({m0 / m1:.3f}x) bitwise-equal {same} rel {rel:.1e}", flush=True)
     arm(0)
     sys.exit(0)
 for mode in [int(m) for m in a.modes.split(",")]:
