@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="no overlapped chunk pair (default under SP: sequence halves whose collectives "
                          "run on a side stream under the other half's GEMMs)")
+    ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the compute stream")
     ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (tuning/*.csv) to look up")
     a = ap.parse_args()
     info = sdist.init_distributed()
@@ -46,6 +47,11 @@ def main():
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     # global grad norm: TP-sharded squares summed over the group, replicated params counted once
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, tp_group=tp)
+    # AdamW (HBM-bound) on a side stream, each layer's forward waiting only for its own bucket: the
+    # update overlaps the next step's compute-bound forward (as bench.py)
+    overlap = dev.type == "cuda" and not a.no_opt_overlap
+    if overlap:
+        m.param_wait_cb = flat.group_waiter(m.param_groups())
     g = torch.Generator(device=dev).manual_seed(11)                 # same tokens on every TP rank
     last = [None]
 
@@ -55,7 +61,7 @@ def main():
         loss = m(t[:, :-1], t[:, 1:])
         loss.backward()
         m.sync_sequence_parallel_grads()
-        opt.step()
+        opt.step(overlap=overlap)
         last[0] = loss
 
     el = timed(step, a.steps, a.warmup)

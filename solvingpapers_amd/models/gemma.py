@@ -411,6 +411,7 @@ class Gemma(tnn.Module):
         self.norm_f = tnn.Parameter(torch.ones(c.dim, **fk))
         self.norm_f.tp_replicated = True
         self.grad_ready_cb = None
+        self.param_wait_cb = None   # overlapped optimizer: wait for param group i's update before use
         with torch.no_grad():
             # unsharded draws sliced per TP rank: TP=n init == shards of the TP=1 init
             g = torch.Generator(device=self.embed.device).manual_seed(seed)
@@ -476,6 +477,9 @@ class Gemma(tnn.Module):
             from .deepseekv3 import _PairReady
             cb = _PairReady(self.grad_ready_cb)
         L = self.layers
+        wait = self.param_wait_cb or (lambda i: None)   # on the compute stream: the side stream's
+        wait(0)                                         # pieces are ordered after it (side.wait_stream)
+        wait(1)
         h, xf, ev = [None, None], [None, None], [None, None]
         for m in (0, 1):                      # embedding rows on the compute stream (tied head:
             x = vocab_parallel_embedding(self.embed, parts[m], g, scale=math.sqrt(c.dim),   # one stream
@@ -490,6 +494,7 @@ class Gemma(tnn.Module):
                                          want_kv=(m == 0 and split == "sequence"))
                 kv = kvo
                 (h[m], xf[m]), ev[m] = sd.run(lambda p, hh: l.sp_mlp_in(p, hh, g), part[m], h[m])
+            wait(li + 2)                      # the next layer's params (or the final norm's)
             for m in (0, 1):
                 sd.join(ev[m], h[m], xf[m])
                 out = l.sp_mlp(xf[m])
@@ -518,11 +523,15 @@ class Gemma(tnn.Module):
         from ..parallel.tensor_parallel import vocab_parallel_embedding
         c = self.c
         sp = self.sp and cache is None
+        wait = self.param_wait_cb or (lambda i: None)
+        wait(0)
         x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim), sequence_parallel=sp)
         res, delta = None, x
         for i, l in enumerate(self.layers):
+            wait(i + 1)
             delta = mark_ready(delta, self.grad_ready_cb, i + 1)
             res, delta = l(res, delta, self.tp_group, None if cache is None else cache[i], pos, sp)
+        wait(len(self.layers) + 1)
         delta = mark_ready(delta, self.grad_ready_cb, len(self.layers) + 1)
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
         return n

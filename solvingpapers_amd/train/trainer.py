@@ -122,7 +122,7 @@ class Trainer:
         for m in getattr(model, "moe_layers", lambda: [])():
             m.balance_group = dp_group
         # overlapped optimizer: a model that waits for each bucket's update before reading it
-        # (param_wait_cb: LLaMA3, DeepSeek-V3) overlaps it with its next forward; any other model
+        # (param_wait_cb: LLaMA3, Gemma, DeepSeek-V3) overlaps it with its next forward; any other model
         # waits for the whole update right after the step (train_step), never reading stale weights
         self._overlap_waits = bool(cfg.opt_overlap and hasattr(model, "param_wait_cb"))
         if self._overlap_waits:

@@ -82,3 +82,33 @@ def test_optimizer_overlap_bitwise_equal():
         torch.cuda.synchronize()
         res.append(flat.param.clone())
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("tp", [1, 8])
+def test_gemma_optimizer_overlap_bitwise_equal(tp):
+    """Gemma with AdamW on a side stream overlapped with the next forward == serial AdamW: tp 1,
+    and tp 8 on the one-GPU stand-in group (sequence parallel, the overlapped chunk pair: its
+    side-stream pieces are ordered after the compute stream's waits)."""
+    from solvingpapers_amd.models import gemma
+    from solvingpapers_amd.parallel.comm import ProxyGroup
+    from solvingpapers_amd.train.optim import FlatAdamW
+    from solvingpapers_amd.utils.flat import FlatParams
+    c = gemma.config("gemma_tiny", vocab_size=512, dim=256, n_heads=8, head_dim=64, ffn_hidden=512)
+    res = []
+    for overlap in (False, True):
+        grp = ProxyGroup(8, "cuda", mode="off") if tp > 1 else None
+        m = gemma.Gemma(c, device="cuda", dtype=torch.bfloat16, seed=11, tp_group=grp).train()
+        flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
+        opt = FlatAdamW(flat, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
+        if overlap:
+            m.param_wait_cb = flat.group_waiter(m.param_groups())
+        g = torch.Generator(device="cuda").manual_seed(5)
+        for _ in range(4):
+            ids = torch.randint(0, c.vocab_size, (1, 129), device="cuda", generator=g)
+            opt.zero_grad()
+            m(ids[:, :-1], ids[:, 1:]).backward()
+            m.sync_sequence_parallel_grads()
+            opt.step(overlap=overlap)
+        torch.cuda.synchronize()
+        res.append(flat.param.clone())
+    assert torch.equal(res[0], res[1])
