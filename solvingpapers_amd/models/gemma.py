@@ -243,17 +243,11 @@ class GemmaBlock(tnn.Module):
         self.w13.copy_(torch.cat([full["w13"][r * fl:(r + 1) * fl], full["w13"][F + r * fl:F + (r + 1) * fl]]))
         self.w2.copy_(full["w2"][:, r * fl:(r + 1) * fl])
 
-    def forward(self, res, delta, tp_group=None, cache=None, pos=0, sp=False):
-        """``sp``: sequence parallel -- res/delta are [B, T/tp, D] shards; the layer is the
-        four pieces sp_in -> sp_attn -> sp_mlp_in -> sp_mlp + reduce-scatter (see sp_in)."""
-        from ..parallel.tensor_parallel import copy_to_tp, reduce_from_tp, reduce_grad_tp, reduce_scatter_seq
+    def forward(self, res, delta, tp_group=None, cache=None, pos=0):
+        """Plain (replicated residual) TP layer; the sequence-parallel layer is sp_attn + sp_mlp
+        (driven by Gemma._hidden_sp)."""
+        from ..parallel.tensor_parallel import copy_to_tp, reduce_from_tp, reduce_grad_tp
         c = self.c
-        if sp:
-            assert cache is None, "sequence parallelism is a training layout"
-            h, xf = self.sp_in(res, delta, tp_group)
-            part, _ = self.sp_attn(xf, pos)
-            h2, n2f = self.sp_mlp_in(part, h, tp_group)
-            return h2, reduce_scatter_seq(self.sp_mlp(n2f), tp_group)
         if res is None:
             n1, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
         else:
@@ -291,99 +285,40 @@ class GemmaBlock(tnn.Module):
         return h2, reduce_from_tp(linear(f, self.w2), tp_group)
 
     # ---- sequence-parallel pieces. Between the TP regions the residual stream is a [B, T/tp, D]
-    # sequence shard; each piece ends where a collective starts, so Gemma._forward_sp_pair can
-    # run the collectives (and the shard-local norms between them) of one chunk on a side stream
-    # while the other chunk's GEMMs / attention run on the compute stream.
-    def sp_in(self, res, delta, g):
-        """Attention input: norm1 (+ residual) on the shard, the K/V projection on the shard
-        (MQA: K/V are replicated, so computing them once per token and gathering them is 8x
-        less GEMM than projecting the gathered input on every rank, and their activation
-        gradient needs no all-reduce of its own -- the gather's reduce-scatter sums it), then
-        ONE all-gather over T of [n1 | kv]. Returns (h, gathered [B, T, D + 2 KV hd])."""
-        from ..parallel.tensor_parallel import gather_seq
-        c = self.c
-        if res is None:
-            n1, h = rms_norm(delta, self.attn_norm, c.norm_eps), delta
-        else:
-            n1, h = rms_norm(delta, self.attn_norm, c.norm_eps, residual=res)
-        return h, gather_seq(torch.cat([n1, linear(n1, self.wkv)], dim=-1), g)
-
-    def sp_attn(self, xf, pos=0, kv_prefix=None, want_kv=False):
-        """q projection of the gathered input, RoPE, attention, o projection. ``kv_prefix``: the
-        packed (RoPE'd) qkv buffer of the earlier chunk of the same sequences, whose keys this
-        chunk's queries also see (causal with offset). Returns the o projection's TP-partial
+    # sequence shard h; each region starts from the all-gathered full sequence hf (its norm runs on
+    # every rank) and ends with a TP-partial [B, T, D] product into which this rank's residual rows
+    # were added, so the layer boundary is one reduce-scatter -> all-gather pair with no compute
+    # between (tensor_parallel.rs_ag_start / rs_ag_finish) -- Gemma._forward_sp_pair runs one
+    # chunk's pair under the other chunk's GEMMs.
+    def sp_attn(self, h, hf, g, pos=0, kv_prefix=None, want_kv=False):
+        """norm1 of the gathered input, q and K/V projections (MQA K/V of the full sequence on
+        every rank: its activation gradient stays TP-partial and the boundary's reduce-scatter sums
+        it with the q path's), RoPE, attention, o projection + this rank's residual rows.
+        ``kv_prefix``: the packed (RoPE'd) qkv buffer of the earlier chunk of the same sequences,
+        whose keys this chunk's queries also see (causal with offset). Returns the TP-partial
         [B, T, D] and, with ``want_kv``, this chunk's packed qkv buffer for the next chunk."""
         from ..ops.attention import attention_packed_prefix
+        from ..parallel.tensor_parallel import add_owner_rows
         c = self.c
         hd, KV = c.head_dim, c.n_kv_heads
-        n1f, kv = xf.split([c.dim, xf.shape[-1] - c.dim], dim=-1)
+        n1f = rms_norm(hf, self.attn_norm, c.norm_eps)
         q = linear(n1f, self.wq)
         B, T = q.shape[0], q.shape[1]
-        qkv = rope_packed_(torch.cat([q, kv], dim=-1), self.hl + KV, c.rope_theta, pos, interleaved=False,
-                           head_dim=hd)
+        qkv = rope_packed_(torch.cat([q, linear(n1f, self.wkv)], dim=-1), self.hl + KV, c.rope_theta, pos,
+                           interleaved=False, head_dim=hd)
         if kv_prefix is None:
             o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
         else:
             o = attention_packed_prefix(qkv, kv_prefix, self.hl, KV, hd)
-        return linear(o.reshape(B, T, self.hl * hd), self.wo), (qkv if want_kv else None)
+        out = add_owner_rows(linear(o.reshape(B, T, self.hl * hd), self.wo), h, g)
+        return out, (qkv if want_kv else None)
 
-    def sp_mlp_in(self, part, h, g):
-        """Reduce-scatter of the o projection, norm2 + residual on the shard, all-gather of the
-        MLP input. Returns (h2, gathered n2)."""
-        from ..parallel.tensor_parallel import gather_seq, reduce_scatter_seq
-        n2, h2 = rms_norm(reduce_scatter_seq(part, g), self.ffn_norm, self.c.norm_eps, residual=h)
-        return h2, gather_seq(n2, g)
-
-    def sp_mlp(self, n2f):
-        """GeGLU on the gathered input; returns the down projection's TP-partial [B, T, D]."""
-        return linear(glu(linear(n2f, self.w13), "gelu_tanh"), self.w2)
-
-
-class _JoinStreams(torch.autograd.Function):
-    """Identity at the end of the two-stream forward. Its backward runs first in the backward
-    pass and queues an end-of-backward callback that makes the caller's stream wait for the
-    side stream: gradients committed from it (norm weights, K/V projections) are complete
-    before the optimizer (or a DP bucket launched after backward) reads them."""
-
-    @staticmethod
-    def forward(ctx, x, side):
-        ctx.side = side
-        return x.view_as(x)
-
-    @staticmethod
-    def backward(ctx, g):
-        side, main = ctx.side, torch.cuda.current_stream()
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
-        return g, None
-
-
-class _Side:
-    """Runs pieces on the side stream after the compute stream's current point and hands their
-    results back (``join``); inline when there is no GPU."""
-
-    def __init__(self, main, side):
-        self.main, self.side = main, side
-
-    def run(self, fn, *args):
-        if self.side is None:
-            return fn(*args), None
-        self.side.wait_stream(self.main)
-        for a in args:
-            if isinstance(a, torch.Tensor):
-                a.record_stream(self.side)       # produced on the compute stream, read here
-        with torch.cuda.stream(self.side):
-            out = fn(*args)
-            ev = torch.cuda.Event()
-            ev.record(self.side)
-        return out, ev
-
-    def join(self, ev, *ts):
-        if ev is None:
-            return
-        self.main.wait_event(ev)
-        for t in ts:
-            if isinstance(t, torch.Tensor):
-                t.record_stream(self.main)
+    def sp_mlp(self, h, hf, g):
+        """norm2 of the gathered input, GeGLU, down projection + this rank's residual rows
+        (TP-partial [B, T, D])."""
+        from ..parallel.tensor_parallel import add_owner_rows
+        n2f = rms_norm(hf, self.ffn_norm, self.c.norm_eps)
+        return add_owner_rows(linear(glu(linear(n2f, self.w13), "gelu_tanh"), self.w2), h, g)
 
 
 class Gemma(tnn.Module):
@@ -403,7 +338,6 @@ class Gemma(tnn.Module):
         self.tp_rank, self.tp = tp_rank_size(tp_group)
         self.sp = (self.tp > 1) if sequence_parallel is None else (bool(sequence_parallel) and self.tp > 1)
         self.tp_pipeline = (os.environ.get("SPA_TP_PIPE", "1") != "0") if tp_pipeline is None else bool(tp_pipeline)
-        self._side = None
         assert c.vocab_size % self.tp == 0
         fk = dict(device=device, dtype=dtype)
         self.embed = tnn.Parameter(torch.empty(c.vocab_size // self.tp, c.dim, **fk))   # vocab-parallel, tied head
@@ -440,33 +374,49 @@ class Gemma(tnn.Module):
             return "sequence"
         return None
 
+    def _embed_sp(self, ids):
+        """Vocab-parallel embedding rows of ``ids`` (TP-partial [B, T, D]): the first layer
+        boundary's reduce-scatter sums them into the residual shard."""
+        from ..parallel.tensor_parallel import vocab_parallel_embedding
+        return vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(self.c.dim),
+                                        sequence_parallel=True, reduce=False)
+
+    def _hidden_sp(self, ids):
+        """Sequence-parallel forward (one chunk): the final norm of the gathered last residual,
+        [B, T, D] on every rank."""
+        from ..parallel.tensor_parallel import rs_ag
+        c, g = self.c, self.tp_group
+        wait = self.param_wait_cb or (lambda i: None)
+        wait(0)
+        h, hf = rs_ag(self._embed_sp(ids), g)
+        for i, l in enumerate(self.layers):
+            wait(i + 1)
+            hf = mark_ready(hf, self.grad_ready_cb, i + 1)
+            h, hf = rs_ag(l.sp_attn(h, hf, g)[0], g)
+            h, hf = rs_ag(l.sp_mlp(h, hf, g), g)
+        wait(len(self.layers) + 1)
+        hf = mark_ready(hf, self.grad_ready_cb, len(self.layers) + 1)
+        return rms_norm(hf, self.norm_f, c.norm_eps)
+
     def _forward_sp_pair(self, ids, targets, split):
-        """Sequence-parallel TP training step as two chunks on one compute stream. Per layer
-        the compute stream runs
+        """Sequence-parallel TP training step as two chunks on one compute stream. Per layer the
+        compute stream runs
 
             A.attn(l)  B.attn(l)  A.mlp(l)  B.mlp(l)  |  A.attn(l+1) ...
 
-        (attn = q projection, attention, o projection of the gathered input; mlp = GeGLU + down
-        projection), and after each piece its chunk's collectives -- reduce-scatter, the
-        shard-local norm (+ K/V projection), all-gather -- run on a side stream, hidden behind
-        the other chunk's next piece. Every weight GEMM stays on the compute stream and every
-        shard-local op (norm weights, K/V projection) on the side stream, so no parameter gets
-        gradient commits from two streams. The backward replays both streams (autograd runs each
-        backward op on its forward's stream), so the gradient collectives overlap the other
-        chunk's backward GEMMs the same way. ``split`` "sequence": chunk B is the second half
-        of every sequence and attends to chunk A's K/V of the same layer (causal with offset),
-        so the result equals the unsplit model."""
-        from ..parallel.tensor_parallel import gather_seq, reduce_scatter_seq, vocab_parallel_cross_entropy, \
-            vocab_parallel_embedding
+        (attn = norm1, q / K/V projections, attention, o projection of the gathered input; mlp =
+        norm2, GeGLU, down projection), and after each piece its chunk's layer boundary -- the
+        reduce-scatter of the partial output into the residual shard and the all-gather of that
+        shard -- is issued to the communicator at once and waited for only before that chunk's next
+        piece, so it runs under the other chunk's piece. No compute sits between the two
+        collectives (the residual add is folded into the partial output, the norm runs on the
+        gathered sequence), so no side compute stream is needed. The backward replays the pairs
+        in reverse (launched at the finish node, waited at the start node), under the other
+        chunk's backward pieces. ``split`` "sequence": chunk B is the second half of every
+        sequence and attends to chunk A's K/V of the same layer (causal with offset), so the
+        result equals the unsplit model."""
+        from ..parallel.tensor_parallel import rs_ag_finish, rs_ag_start, vocab_parallel_cross_entropy
         c, g = self.c, self.tp_group
-        cuda = ids.is_cuda
-        main = torch.cuda.current_stream(ids.device) if cuda else None
-        if cuda and self._side is None:
-            from ..parallel.comm import side_stream
-            from ..utils.grad import register_side_stream
-            self._side = side_stream(ids.device)
-            register_side_stream(self._side)
-        sd = _Side(main, self._side if cuda else None)
         B, T = ids.shape
         if split == "batch":
             parts, tps, pos = (ids[:B // 2], ids[B // 2:]), (targets[:B // 2], targets[B // 2:]), (0, 0)
@@ -476,80 +426,67 @@ class Gemma(tnn.Module):
         if self.grad_ready_cb is not None:
             from .deepseekv3 import _PairReady
             cb = _PairReady(self.grad_ready_cb)
+        wait = self.param_wait_cb or (lambda i: None)
         L = self.layers
-        wait = self.param_wait_cb or (lambda i: None)   # on the compute stream: the side stream's
-        wait(0)                                         # pieces are ordered after it (side.wait_stream)
-        wait(1)
-        h, xf, ev = [None, None], [None, None], [None, None]
-        for m in (0, 1):                      # embedding rows on the compute stream (tied head:
-            x = vocab_parallel_embedding(self.embed, parts[m], g, scale=math.sqrt(c.dim),   # one stream
-                                         sequence_parallel=True, reduce=False)              # per param)
-            (h[m], xf[m]), ev[m] = sd.run(
-                lambda x: L[0].sp_in(None, mark_ready(reduce_scatter_seq(x, g), cb, 1), g), x)
+        wait(0)
+        pend = [rs_ag_start(self._embed_sp(parts[m]), g) for m in (0, 1)]
         for li, l in enumerate(L):
-            part, kv = [None, None], None
+            wait(li + 1)
+            kv = None
             for m in (0, 1):
-                sd.join(ev[m], h[m], xf[m])
-                part[m], kvo = l.sp_attn(xf[m], pos[m], kv_prefix=kv if (m == 1 and split == "sequence") else None,
-                                         want_kv=(m == 0 and split == "sequence"))
+                h, hf = rs_ag_finish(pend[m])
+                hf = mark_ready(hf, cb, li + 1)
+                o, kvo = l.sp_attn(h, hf, g, pos[m], kv_prefix=kv if (m == 1 and split == "sequence") else None,
+                                   want_kv=(m == 0 and split == "sequence"))
                 kv = kvo
-                (h[m], xf[m]), ev[m] = sd.run(lambda p, hh: l.sp_mlp_in(p, hh, g), part[m], h[m])
-            wait(li + 2)                      # the next layer's params (or the final norm's)
+                pend[m] = rs_ag_start(o, g)
             for m in (0, 1):
-                sd.join(ev[m], h[m], xf[m])
-                out = l.sp_mlp(xf[m])
-                if li + 1 < len(L):
-                    nxt = L[li + 1]
-                    (h[m], xf[m]), ev[m] = sd.run(
-                        lambda o, hh: nxt.sp_in(hh, mark_ready(reduce_scatter_seq(o, g), cb, li + 2), g), out, h[m])
-                else:                          # final norm on the shard, gathered for the vocab-parallel head
-                    def fin(o, hh):
-                        d = mark_ready(reduce_scatter_seq(o, g), cb, len(L) + 1)
-                        n, _ = rms_norm(d, self.norm_f, c.norm_eps, residual=hh)
-                        return None, gather_seq(n, g)
-                    (h[m], xf[m]), ev[m] = sd.run(fin, out, h[m])
+                h, hf = rs_ag_finish(pend[m])
+                pend[m] = rs_ag_start(l.sp_mlp(h, hf, g), g)
+        wait(len(L) + 1)
         ls, nv = [None, None], [None, None]
         for m in (0, 1):
-            sd.join(ev[m], xf[m])
+            _, hf = rs_ag_finish(pend[m])
+            hf = mark_ready(hf, cb, len(L) + 1)
+            n = rms_norm(hf, self.norm_f, c.norm_eps)
             t = tps[m].reshape(-1)
-            # the head's input gradient stays TP-partial: the gather's reduce-scatter sums it
-            ls[m] = vocab_parallel_cross_entropy(xf[m].reshape(-1, c.dim), self.embed, t, g, reduce_dh=False)
+            # the head's input gradient stays TP-partial: the boundary's reduce-scatter sums it
+            ls[m] = vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, t, g, reduce_dh=False)
             nv[m] = (t != -100).sum().clamp_min(1).to(ls[m].dtype)
-        loss = (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
-        return _JoinStreams.apply(loss, sd.side) if sd.side is not None else loss
+        return (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
 
     def hidden(self, ids, cache=None, pos=0):
-        """Final-norm hidden states; a [B, T/tp, D] sequence shard under sequence parallelism."""
+        """Final-norm hidden states [B, T, D] (under sequence parallelism the full sequence on
+        every rank)."""
         from ..parallel.tensor_parallel import vocab_parallel_embedding
         c = self.c
-        sp = self.sp and cache is None
+        if self.sp and cache is None:
+            return self._hidden_sp(ids)
         wait = self.param_wait_cb or (lambda i: None)
         wait(0)
-        x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim), sequence_parallel=sp)
+        x = vocab_parallel_embedding(self.embed, ids, self.tp_group, scale=math.sqrt(c.dim))
         res, delta = None, x
         for i, l in enumerate(self.layers):
             wait(i + 1)
             delta = mark_ready(delta, self.grad_ready_cb, i + 1)
-            res, delta = l(res, delta, self.tp_group, None if cache is None else cache[i], pos, sp)
+            res, delta = l(res, delta, self.tp_group, None if cache is None else cache[i], pos)
         wait(len(self.layers) + 1)
         delta = mark_ready(delta, self.grad_ready_cb, len(self.layers) + 1)
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
         return n
 
     def forward(self, ids, targets=None):
-        from ..parallel.tensor_parallel import gather_seq, vocab_parallel_cross_entropy
+        from ..parallel.tensor_parallel import vocab_parallel_cross_entropy
         c = self.c
         if targets is not None:
             split = self._pair_split(ids)
             if split is not None:
                 return self._forward_sp_pair(ids, targets, split)
         n = self.hidden(ids)
-        if self.sp:   # the vocab-parallel head needs every token on every rank
-            n = gather_seq(n, self.tp_group)
         if targets is None:
             from ..parallel.tensor_parallel import gather_vocab_logits
             return gather_vocab_logits(linear(n, self.embed), self.tp_group)
-        # under SP the head's input gradient stays TP-partial: the gather's reduce-scatter sums it
+        # under SP the head's input gradient stays TP-partial: the boundary's reduce-scatter sums it
         return vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, targets.reshape(-1), self.tp_group,
                                             reduce_dh=not self.sp)
 

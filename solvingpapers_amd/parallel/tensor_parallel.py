@@ -148,6 +148,128 @@ def reduce_scatter_seq(x, group):
     return x if tp_rank_size(group)[1] == 1 else _ReduceScatterSeq.apply(x, group)
 
 
+# ------------------------------------------------ async reduce-scatter -> all-gather
+# The sequence-parallel layer boundary as ONE collective pair with no compute between its halves:
+# a TP region's partial output (with this rank's residual rows already added, add_owner_rows)
+# is reduce-scattered into the new residual shard, and that shard is all-gathered straight away
+# into the next region's full-sequence input (whose norm then runs on every rank). Both are
+# issued back to back on the communicator, so they can run under other work of the compute
+# stream (the other chunk of Gemma._forward_sp_pair) and are waited for only where consumed.
+# Backward mirrors it: the gathered input's gradient (with the residual shard's gradient added
+# into this rank's rows) is reduce-scattered and all-gathered into the partial output's gradient.
+
+def _rs_ag_launch(x, group):
+    """Launch RS(x) -> shard and AG(shard) -> full on ``group``; returns (shard, full, works).
+    x [B, T, ...] TP-partial; shard [B, T/tp, ...] = sum over ranks of this rank's rows."""
+    rank, tp = tp_rank_size(group)
+    B, T = x.shape[0], x.shape[1]
+    assert T % tp == 0, "sequence parallelism needs T divisible by the TP size"
+    if comm.is_proxy(group):       # stand-in: this rank's rows unsummed / every shard = this one
+        shard = x.narrow(1, 0, T // tp).contiguous()
+        full = torch.cat([shard] * tp, dim=1)
+        w1 = group._occupy(group.ag_seconds(x.numel() * x.element_size()))
+        w2 = group._occupy(group.ag_seconds(full.numel() * full.element_size()))
+        return shard, full, (w1, w2)
+    if dist.get_backend(group) == "gloo":                               # synchronous
+        return _reduce_scatter_seq_raw(x, group), None, None
+    xt = x.transpose(0, 1).contiguous()                                 # [T, B, ...]
+    st = torch.empty((T // tp,) + tuple(xt.shape[1:]), dtype=x.dtype, device=x.device)
+    ft = torch.empty_like(xt)
+    w1 = dist.reduce_scatter_tensor(st, xt, group=group, async_op=True)
+    w2 = dist.all_gather_into_tensor(ft, st, group=group, async_op=True)
+    return st.transpose(0, 1), ft.transpose(0, 1), (w1, w2, xt)
+
+
+def _rs_ag_wait(shard, full, works, group):
+    if works is not None:
+        for w in works[:2]:
+            w.wait()
+    if full is None:                                                    # gloo: gather now
+        full = _gather_seq_raw(shard, group)
+    return shard.contiguous(), full.contiguous()
+
+
+class _RSAGStart(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, box):
+        box.pay = _rs_ag_launch(x, box.group)
+        ctx.box = box
+        return x.new_empty(0)                # token: the results travel in the box
+
+    @staticmethod
+    def backward(ctx, g):
+        box = ctx.box
+        dx = _rs_ag_wait(*box.bwork, box.group)[1]
+        box.bwork = None
+        return dx, None
+
+
+class _RSAGFinish(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, token, box):
+        shard, full = _rs_ag_wait(*box.pay, box.group)
+        box.pay = None
+        ctx.box = box
+        return shard, full
+
+    @staticmethod
+    def backward(ctx, g_shard, g_full):
+        box = ctx.box
+        rank, tp = tp_rank_size(box.group)
+        g = g_full.contiguous().clone() if g_full is not None else None
+        if g is None:
+            T = g_shard.shape[1] * tp
+            g = g_shard.new_zeros((g_shard.shape[0], T) + tuple(g_shard.shape[2:]))
+        if g_shard is not None:              # the residual shard's gradient: this rank's rows
+            g.narrow(1, rank * (g.shape[1] // tp), g.shape[1] // tp).add_(g_shard)
+        box.bwork = _rs_ag_launch(g, box.group)
+        return g.new_empty(0), None          # (a defined token gradient: the start node runs)
+
+
+def rs_ag_start(x, group):
+    """Launch the layer-boundary pair on the TP-partial ``x`` [B, T, ...]; finish with
+    :func:`rs_ag_finish` where the results are consumed. In backward the reverse pair is launched
+    at the finish node and waited for at the start node, so autograd work created between the two
+    in the forward runs under it in the backward too."""
+    box = comm._Box()
+    box.group = group
+    return _RSAGStart.apply(x, box), box
+
+
+def rs_ag_finish(handle):
+    """-> (residual shard [B, T/tp, ...], gathered full sequence [B, T, ...])."""
+    token, box = handle
+    return _RSAGFinish.apply(token, box)
+
+
+def rs_ag(x, group):
+    """Blocking form (start + finish back to back)."""
+    return rs_ag_finish(rs_ag_start(x, group))
+
+
+class _AddOwnerRows(torch.autograd.Function):
+    """x[:, rank rows] += h in place (x a fresh TP-partial product, h this rank's residual shard):
+    after the reduce-scatter sums the partials the shard holds h + the region's output."""
+
+    @staticmethod
+    def forward(ctx, x, h, rank, ts):
+        ctx.rank, ctx.ts = rank, ts
+        x.narrow(1, rank * ts, ts).add_(h)
+        ctx.mark_dirty(x)
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g.narrow(1, ctx.rank * ctx.ts, ctx.ts), None, None
+
+
+def add_owner_rows(x, h, group):
+    rank, tp = tp_rank_size(group)
+    if h is None:
+        return x
+    return _AddOwnerRows.apply(x, h, rank, x.shape[1] // tp)
+
+
 def scale_grad(x, s):
     """Identity forward, gradient times ``s``: a replicated consumer whose input gradient is
     already complete on every rank, feeding a gather_seq whose backward sums over ranks."""
