@@ -23,6 +23,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--batch", type=int, default=1,
+                    help="sequences per step (even under SP: the chunk pair splits the batch, not each sequence)")
+    ap.add_argument("--accum", type=int, default=1,
+                    help="micro-batches of --batch sequences per step; even: run in overlapped pairs (Gemma.forward_pair)")
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--no-sp", dest="sp", action="store_false",
                     help="plain Megatron TP (default: sequence parallelism inside the TP group)")
@@ -57,18 +61,24 @@ def main():
 
     def step():
         opt.zero_grad()
-        t = torch.randint(0, c.vocab_size, (1, a.seq + 1), device=dev, generator=g)
-        loss = m(t[:, :-1], t[:, 1:])
-        loss.backward()
+        pair = a.accum % 2 == 0 and m.tp_pipeline
+        for i in range(a.accum // 2 if pair else a.accum):
+            t = torch.randint(0, c.vocab_size, (a.batch, a.seq + 1), device=dev, generator=g)
+            if pair:
+                u = torch.randint(0, c.vocab_size, (a.batch, a.seq + 1), device=dev, generator=g)
+                loss = m.forward_pair(t[:, :-1], t[:, 1:], u[:, :-1], u[:, 1:])
+            else:
+                loss = m(t[:, :-1], t[:, 1:])
+            loss.backward()
         m.sync_sequence_parallel_grads()
         opt.step(overlap=overlap)
-        last[0] = loss
+        last[0] = loss / 2 if pair else loss
 
     el = timed(step, a.steps, a.warmup)
-    tok_s = a.seq * a.steps / el                                     # one sequence per step for the TP group
+    tok_s = a.accum * a.batch * a.seq * a.steps / el                 # accum x batch sequences per step for the TP group
     tf = tok_s * m.flops_per_token(a.seq) / world / 1e12
     report("training tokens/sec, Gemma-7B-shape MQA bf16 (TP)", tok_s, "tokens/s", a.steps, a.warmup, el,
-           {"model": "gemma_7b_mqa" + (f"-L{a.layers}" if a.layers else ""), "global_batch": 1, "seq_len": a.seq,
+           {"model": "gemma_7b_mqa" + (f"-L{a.layers}" if a.layers else ""), "global_batch": a.accum * a.batch, "seq_len": a.seq,
             "parallelism": f"tp{world}" + ("-sp" if m.sp else "") + ("-pair" if m.sp and m.tp_pipeline else "")}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
            loss=round(float(last[0].detach()), 4))
     sdist.cleanup()

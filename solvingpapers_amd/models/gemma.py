@@ -398,7 +398,15 @@ class Gemma(tnn.Module):
         hf = mark_ready(hf, self.grad_ready_cb, len(self.layers) + 1)
         return rms_norm(hf, self.norm_f, c.norm_eps)
 
-    def _forward_sp_pair(self, ids, targets, split):
+    def forward_pair(self, ids0, t0, ids1, t1):
+        """loss(ids0, t0) + loss(ids1, t1) for two gradient-accumulation micro-batches. Under
+        sequence-parallel TP they run as the overlapped chunk pair (each micro-batch at its own
+        full shape: no GEMM is split); otherwise one after the other."""
+        if self.sp and self.tp_pipeline and self.training and torch.is_grad_enabled():
+            return self._forward_sp_pair(None, None, "micro", parts=(ids0, ids1), tps=(t0, t1))
+        return self(ids0, t0) + self(ids1, t1)
+
+    def _forward_sp_pair(self, ids, targets, split, parts=None, tps=None):
         """Sequence-parallel TP training step as two chunks on one compute stream. Per layer the
         compute stream runs
 
@@ -417,10 +425,13 @@ class Gemma(tnn.Module):
         result equals the unsplit model."""
         from ..parallel.tensor_parallel import rs_ag_finish, rs_ag_start, vocab_parallel_cross_entropy
         c, g = self.c, self.tp_group
-        B, T = ids.shape
-        if split == "batch":
+        if split == "micro":                 # two micro-batches (forward_pair)
+            pos = (0, 0)
+        elif split == "batch":
+            B = ids.shape[0]
             parts, tps, pos = (ids[:B // 2], ids[B // 2:]), (targets[:B // 2], targets[B // 2:]), (0, 0)
         else:
+            T = ids.shape[1]
             parts, tps, pos = (ids[:, :T // 2], ids[:, T // 2:]), (targets[:, :T // 2], targets[:, T // 2:]), (0, T // 2)
         cb = None
         if self.grad_ready_cb is not None:
@@ -453,6 +464,8 @@ class Gemma(tnn.Module):
             # the head's input gradient stays TP-partial: the boundary's reduce-scatter sums it
             ls[m] = vocab_parallel_cross_entropy(n.reshape(-1, c.dim), self.embed, t, g, reduce_dh=False)
             nv[m] = (t != -100).sum().clamp_min(1).to(ls[m].dtype)
+        if split == "micro":
+            return ls[0] + ls[1]
         return (ls[0] * nv[0] + ls[1] * nv[1]) / (nv[0] + nv[1])
 
     def hidden(self, ids, cache=None, pos=0):

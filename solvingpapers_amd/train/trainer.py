@@ -36,8 +36,9 @@ from .optim import FlatAdamW, FlatSGD, cosine_lr
 class TrainConfig:
     steps: int = 1000
     grad_accum: int = 1
-    # models with forward_pair (DeepSeek-V3): micro-batches run in layer-interleaved pairs so each
-    # expert-parallel all-to-all overlaps the other micro-batch's compute (even grad_accum only)
+    # models with forward_pair (DeepSeek-V3, Gemma): micro-batches run in layer-interleaved pairs so
+    # each expert-parallel all-to-all / sequence-parallel TP boundary overlaps the other
+    # micro-batch's compute (even grad_accum only)
     pair_microbatches: bool = True
     optimizer: str = "adamw"            # adamw | adam | sgd
     lr: float = 3e-4

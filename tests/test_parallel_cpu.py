@@ -142,14 +142,18 @@ def _tp_worker(rank, world, port, q, mode="plain", nb=2):
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     grp = dist.new_group([0, 1])
-    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=mode != "plain", tp_pipeline=mode == "pair")
+    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=mode != "plain",
+                        tp_pipeline=mode in ("pair", "micro"))
     assert local.sp == (mode != "plain")
     shard_gemma_from_full(full, local, rank, world)
     flat = FlatParams(local)
     ids = torch.randint(0, 64, (2, 13), generator=torch.Generator().manual_seed(2))[:nb]
     if mode == "pair":
         assert local._pair_split(ids[:, :-1]) == ("batch" if nb == 2 else "sequence")
-    loss = local(ids[:, :-1], ids[:, 1:])
+    if mode == "micro":
+        loss = local.forward_pair(ids[:1, :-1], ids[:1, 1:], ids[1:, :-1], ids[1:, 1:])
+    else:
+        loss = local(ids[:, :-1], ids[:, 1:])
     loss.backward()
     local.sync_sequence_parallel_grads()
     grads = {n: p.main_grad.clone().numpy() for n, p in local.named_parameters()}
@@ -159,20 +163,24 @@ def _tp_worker(rank, world, port, q, mode="plain", nb=2):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,nb", [("plain", 2), ("sp", 2), ("pair", 2), ("pair", 1)])
+@pytest.mark.parametrize("mode,nb", [("plain", 2), ("sp", 2), ("pair", 2), ("pair", 1), ("micro", 2)])
 def test_tensor_parallel_gemma_matches_unsharded(mode, nb):
     """TP=2 == the unsharded model: plain Megatron TP ("plain"); sequence parallelism ("sp":
     reduce-scatter / all-gather over T, norms and the MQA K/V projection on sequence shards,
     their grads summed over TP); and the overlapped chunk pair under SP ("pair", Gemma.
     _forward_sp_pair): batch halves (nb 2) or sequence halves with half B attending to half
-    A's K/V (nb 1)."""
+    A's K/V (nb 1); and Gemma.forward_pair over two micro-batches ("micro": == the sum of the
+    two micro-batch losses)."""
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.utils.flat import FlatParams
     c = gemma.config("gemma_tiny", vocab_size=64, dim=64, n_heads=4, head_dim=16, ffn_hidden=128)
     full = gemma.Gemma(c, seed=5)
     FlatParams(full)
     ids = torch.randint(0, 64, (2, 13), generator=torch.Generator().manual_seed(2))[:nb]
-    loss = full(ids[:, :-1], ids[:, 1:])
+    if mode == "micro":
+        loss = full(ids[:1, :-1], ids[:1, 1:]) + full(ids[1:, :-1], ids[1:, 1:])
+    else:
+        loss = full(ids[:, :-1], ids[:, 1:])
     loss.backward()
     fg = {n: p.main_grad for n, p in full.named_parameters()}
     out = _run(_tp_worker, 2, mode, nb)

@@ -63,8 +63,10 @@ def tp_gemma(a):
     layers, fwd + bwd of ``--batch`` sequences of ``--seq`` tokens. Arms:
       compute / blocking   the plain SP forward, collectives skipped / modelled and waited at once
       pair:off / pair:overlap   Gemma._forward_sp_pair (two chunks: batch halves when --batch is
-                           even, else sequence halves; collectives + shard-local norms of one
-                           chunk on a side stream under the other chunk's GEMMs)"""
+                           even, else sequence halves; each chunk's layer-boundary reduce-scatter
+                           -> all-gather runs under the other chunk's compute)
+    --micro: a step is two gradient-accumulation micro-batches of --batch sequences; compute /
+    blocking run them one after the other, the pair arms as Gemma.forward_pair (no chunk split)."""
     from solvingpapers_amd.models import gemma
     dev = torch.device("cuda")
     c = gemma.config("gemma_7b_mqa", n_layers=a.layers, max_seq_len=a.seq)
@@ -72,7 +74,8 @@ def tp_gemma(a):
     m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=g1, seed=1).train()
     FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     ids = torch.randint(0, c.vocab_size, (a.batch, a.seq + 1), device=dev)
-    split = m._pair_split(ids[:, :-1])
+    ids2 = torch.randint(0, c.vocab_size, (a.batch, a.seq + 1), device=dev)
+    split = "micro" if a.micro else m._pair_split(ids[:, :-1])
     assert split is not None, "the pair needs T divisible by 2 x TP (or an even batch)"
 
     def step_of(pair):
@@ -80,7 +83,13 @@ def tp_gemma(a):
             from solvingpapers_amd.utils.grad import next_generation
             next_generation()
             m.tp_pipeline = pair
-            m(ids[:, :-1], ids[:, 1:]).backward()
+            if not a.micro:
+                m(ids[:, :-1], ids[:, 1:]).backward()
+            elif pair:
+                m.forward_pair(ids[:, :-1], ids[:, 1:], ids2[:, :-1], ids2[:, 1:]).backward()
+            else:   # gradient accumulation, one micro-batch after the other
+                m(ids[:, :-1], ids[:, 1:]).backward()
+                m(ids2[:, :-1], ids2[:, 1:]).backward()
             m.sync_sequence_parallel_grads()
         return step
 
@@ -100,7 +109,7 @@ def tp_gemma(a):
                 comm = g1.modelled_s * 1e3 / a.iters
     med = {k: round(statistics.median(v), 3) for k, v in res.items()}
     out = {"config": "gemma_7b_mqa TP=8 SP local shard (2 q-heads x 256, GeGLU 3072, V/8)", "layers": a.layers,
-           "batch": a.batch, "seq": a.seq, "split": split, "ms": med, "modelled_comm_ms": round(comm, 3)}
+           "batch": a.batch, "seq": a.seq, "split": split, "micro_batches": 2 if a.micro else 1, "ms": med, "modelled_comm_ms": round(comm, 3)}
     if not ARMS:
         total = med["blocking"] - med["compute"]
         out["comm_added_blocking_ms"] = round(total, 3)
@@ -171,6 +180,7 @@ def main():
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--batch", type=int, default=1, help="TP: sequences per step (even: the pipeline splits by batch)")
+    ap.add_argument("--micro", action="store_true", help="TP: two accumulation micro-batches per step")
     ap.add_argument("--tokens", type=int, default=4096)
     ap.add_argument("--fp8", action="store_true", default=True, help="EP: fp8 experts + dispatch (config #5)")
     ap.add_argument("--bf16", dest="fp8", action="store_false")
