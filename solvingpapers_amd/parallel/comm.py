@@ -59,8 +59,16 @@ class ProxyGroup:
     kernel at all (compute-only reference)."""
 
     def __init__(self, size: int, device=None, ar_busbw_gbps: float = PROXY_AR_BUSBW_GBPS,
-                 a2a_gbps: float = PROXY_A2A_GBPS, nwg: int = 16, buf_mb: int = 8, mode: str = "overlap"):
+                 a2a_gbps: float = PROXY_A2A_GBPS, nwg: int = 16, buf_mb: int = 8, mode: str = "overlap",
+                 synth_gather: bool = False):
+        """``synth_gather``: an all-gather's output is a cached random buffer of the gathered
+        shape instead of a compute-stream concatenation of this rank's shard -- a real
+        all-gather's output is written by the collective (whose time the stand-in kernel
+        models), so timing runs (tools/overlap_proxy.py) should not charge the compute stream
+        for it. Off by default: value tests want the replicated shard."""
         self.size, self.rank = int(size), 0
+        self.synth_gather = bool(synth_gather)
+        self._gcache = {}
         self.device = torch.device(device or "cuda")
         self.ar_bw, self.a2a_bw = ar_busbw_gbps * 1e9, a2a_gbps * 1e9
         self.nwg, self.mode = int(nwg), mode
@@ -111,6 +119,20 @@ class ProxyGroup:
             w.wait()
             return _DoneWork()
         return w
+
+    def gathered(self, shard, dim: int):
+        """The stand-in all-gather output of ``shard`` along ``dim`` (see ``synth_gather``)."""
+        if not self.synth_gather:
+            return torch.cat([shard] * self.size, dim=dim)
+        shape = list(shard.shape)
+        shape[dim] *= self.size
+        key = (tuple(shape), shard.dtype, shard.device)
+        buf = self._gcache.get(key)
+        if buf is None:       # random (not constant) data: MFMA power / clocks depend on it
+            g = torch.Generator(device=shard.device).manual_seed(len(self._gcache) + 11)
+            buf = torch.randn(shape, generator=g, device=shard.device, dtype=torch.float32).to(shard.dtype)
+            self._gcache[key] = buf
+        return buf
 
     def ar_seconds(self, nbytes: int) -> float:
         n = self.size

@@ -76,7 +76,7 @@ reduce_grad_tp = copy_to_tp  # identity fwd, sum of activation grads over the TP
 def _gather_seq_raw(x, group):
     rank, tp = tp_rank_size(group)
     if comm.is_proxy(group):       # stand-in: every rank's shard is this one; wire time modelled
-        out = torch.cat([x] * tp, dim=1)
+        out = group.gathered(x, 1)
         group._occupy(group.ag_seconds(out.numel() * out.element_size())).wait()
         return out
     if dist.get_backend(group) == "gloo":
@@ -166,7 +166,7 @@ def _rs_ag_launch(x, group):
     assert T % tp == 0, "sequence parallelism needs T divisible by the TP size"
     if comm.is_proxy(group):       # stand-in: this rank's rows unsummed / every shard = this one
         shard = x.narrow(1, 0, T // tp).contiguous()
-        full = torch.cat([shard] * tp, dim=1)
+        full = group.gathered(shard, 1)
         w1 = group._occupy(group.ag_seconds(x.numel() * x.element_size()))
         w2 = group._occupy(group.ag_seconds(full.numel() * full.element_size()))
         return shard, full, (w1, w2)

@@ -65,3 +65,14 @@ def test_proxy_group_ep_forward_pair_matches_plain():
     for n, g in outs[0][1].items():
         assert torch.allclose(g, outs[1][1][n], atol=1e-5, rtol=1e-4), n
     assert g1.calls > 0
+
+
+def test_proxy_group_synth_gather_shape_and_cache():
+    """synth_gather: the stand-in all-gather returns one cached random buffer per gathered shape
+    (no concatenation on the caller's stream); off: the shard replicated tp times."""
+    x = torch.arange(6.0).reshape(1, 3, 2)
+    g = ProxyGroup(4, "cpu")
+    assert torch.equal(g.gathered(x, 1), torch.cat([x] * 4, dim=1))
+    gs = ProxyGroup(4, "cpu", synth_gather=True)
+    a, b = gs.gathered(x, 1), gs.gathered(x + 1, 1)
+    assert a.shape == (1, 12, 2) and a is b and a.std() > 0

@@ -70,7 +70,7 @@ def tp_gemma(a):
     from solvingpapers_amd.models import gemma
     dev = torch.device("cuda")
     c = gemma.config("gemma_7b_mqa", n_layers=a.layers, max_seq_len=a.seq)
-    g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
+    g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg, synth_gather=True)
     m = gemma.Gemma(c, device=dev, dtype=torch.bfloat16, tp_group=g1, seed=1).train()
     FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     ids = torch.randint(0, c.vocab_size, (a.batch, a.seq + 1), device=dev)
