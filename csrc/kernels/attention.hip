@@ -312,6 +312,211 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Forward at head dim 256 (Gemma MQA), S computed once per row group: 8 waves = 4 row groups of
+// 32 queries x 2 roles. The leader (waves 0-3) holds its rows' Q fragments, computes S = K Q^T
+// and the online softmax, writes P (bf16, MFMA-operand order) and the per-row rescale factor to
+// LDS, and accumulates O columns 0..127; the follower (waves 4-7, the leader's SIMD partner)
+// rescales and accumulates O columns 128..255 from that P. Against the split-V launch (two column
+// halves that each recompute S: 1.5x the MFMA work, 24 KB of LDS reads per wave per tile) this
+// is 1x the MFMA work and 136 KB of LDS reads per CU per 32-key tile instead of 192 KB.
+// One barrier per interval, V lagging K by one tile:
+//   interval j, leader:   O[:, :128]  += V(j-1)^T P(j-1)  |  S(j) -> softmax -> P(j), alpha(j) -> LDS
+//   interval j, follower: O[:, 128:] *= alpha(j-1);  O[:, 128:] += V(j-1)^T P(j-1)
+// K(j) and V(j-1) are resident in interval j (2-deep rings each), which commits K(j+1) and V(j).
+// Key split (p.ksplit) as attn_fwd_kernel: fp32 partials of both column halves + (m, l).
+// ---------------------------------------------------------------------------
+template <bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_fwd256p_kernel(AttnParams p) {
+  constexpr int HD = 256, BN = 32, BM = 128, KS = HD / 16, DH = 4, NT = 512;
+  constexpr int TI = BN * HD;                 // one 32-key K or V image (elements)
+  constexpr int PS = 4 * 2 * 64 * 8;          // one P slot: [group][half][lane][8]
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TI + 2 * PS];   // K[2] | V[2] | P[2]
+  __shared__ __attribute__((aligned(16))) float arow[2][4][64];        // [slot][group][lane] alpha
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave & 3, role = wave >> 2;
+  const int lq = lane & 31, hh = lane >> 5;
+  const int nqb = cdiv(p.Tq, BM);
+  const int si = blockIdx.x % p.ksplit;
+  int qb, b, h;
+  q_block_map(p, nqb, CAUSAL, qb, b, h, blockIdx.x / p.ksplit, gridDim.x / p.ksplit);
+  const int hk = h / (p.H / p.Hkv);
+  const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + grp * 32);
+  const int q = q0 + lq;
+  const float c = p.scale_log2;
+
+  int kend = p.Tk;
+  if (CAUSAL) kend = min(p.Tk, qb * BM + BM + p.causal_off);
+  const int wave_kend = q0 >= p.Tq ? 0 : CAUSAL ? min(p.Tk, q0 + 32 + p.causal_off) : p.Tk;
+  const int ntiles_all = kend > 0 ? cdiv(kend, BN) : 0;
+  const int kper = cdiv(ntiles_all, p.ksplit);
+  const int jbeg = min(ntiles_all, si * kper);
+  const int ntiles = min(ntiles_all, jbeg + kper) - jbeg;
+  const int kb0 = jbeg * BN;
+
+  const bf16* kbase = p.k + b * p.skb + hk * p.skh;
+  const bf16* vbase = p.v + b * p.svb + hk * p.svh;
+  TileLoader<HD, BN, NT> lk, lv;
+  lk.init(p.skt, tid);
+  lv.init(p.svt, tid);
+  if (ntiles > 0) {
+    lk.load(kbase, p.skt, kb0, p.Tk);
+    lk.store(smem);
+    lv.load(vbase, p.svt, kb0, p.Tk);
+    if (ntiles > 1) lk.load(kbase, p.skt, kb0 + BN, p.Tk);
+  }
+  bf16x8 qf[KS];
+  if (role == 0) {
+    const bf16* qp = p.q + b * p.sqb + (long)q * p.sqt + h * p.sqh + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = q < p.Tq ? *reinterpret_cast<const bf16x8*>(qp + 16 * s) : zero8();
+  }
+  __syncthreads();
+  LdsOff<HD> off;
+  off.init(lane);
+  f32x16 o[DH];
+#pragma unroll
+  for (int i = 0; i < DH; ++i) o[i] = splat16(0.f);
+  float m = -1e30f, l = 0.f;
+  bf16* pme = smem + 4 * TI + grp * (2 * 64 * 8) + lane * 8;   // + slot * PS + half * 512
+
+  auto interval = [&](const int j, auto bufc, auto rolec) {
+    constexpr int BUF = decltype(bufc)::value, ROLE = decltype(rolec)::value;
+    if (j + 1 < ntiles) lk.store(smem + (1 - BUF) * TI);          // K(j+1)
+    if (j < ntiles) lv.store(smem + (2 + BUF) * TI);              // V(j)
+    if (j + 2 < ntiles) lk.load(kbase, p.skt, kb0 + (j + 2) * BN, p.Tk);
+    if (j + 1 < ntiles) lv.load(vbase, p.svt, kb0 + (j + 1) * BN, p.Tk);
+    const bf16* Vp = smem + (3 - BUF) * TI;                        // V(j-1)
+    const bf16* pr = pme + (1 - BUF) * PS;                         // P(j-1)
+    if (j >= 1 && kb0 + (j - 1) * BN < wave_kend) {
+      if constexpr (ROLE == 1) {
+        const float al = arow[1 - BUF][grp][lane];
+#pragma unroll
+        for (int i = 0; i < DH; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= al;
+      }
+      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pr);
+      const bf16x8 pb = *reinterpret_cast<const bf16x8*>(pr + 512);
+#pragma unroll
+      for (int dt = 0; dt < DH; ++dt) {
+        o[dt] = mfma32(ld_tr(Vp, off.tra[dt + DH * ROLE], off.trb[dt + DH * ROLE]), pa, o[dt]);
+        o[dt] = mfma32(ld_tr(Vp + 16 * HD, off.tra[dt + DH * ROLE], off.trb[dt + DH * ROLE]), pb, o[dt]);
+      }
+      chain_sched<2 * DH, 2, 3, 2>();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (ROLE == 0) {
+      const int k0 = kb0 + j * BN;
+      if (j < ntiles && k0 < wave_kend) {
+        const bf16* Ks = smem + BUF * TI;
+        bf16x8 kr[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) kr[ks] = ld_row(Ks, off.row[ks]);
+        f32x16 s = mfma32(kr[0], qf[0], splat16(0.f));
+#pragma unroll
+        for (int ks = 1; ks < KS; ++ks) s = mfma32(kr[ks], qf[ks], s);
+        __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+        if ((k0 + 32 > p.Tk) || (CAUSAL && k0 + 31 > q0 + p.causal_off)) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= p.Tk || (CAUSAL && key > q + p.causal_off)) s[r] = -INFINITY;
+          }
+        }
+        float mx = s[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
+        const float mxs = halfmax(mx) * c;
+        float al = 1.f;
+        if (mxs > m + kRescaleThr) {
+          al = fexp2(m - mxs);
+          l *= al;
+#pragma unroll
+          for (int i = 0; i < DH; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[i][r] *= al;
+          m = mxs;
+        }
+        const float nm = -m;
+        float ls = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = fexp2(fmaf(s[r], c, nm));
+          s[r] = e;
+          ls += e;
+        }
+        l += ls;
+        bf16* pw = pme + BUF * PS;
+        *reinterpret_cast<bf16x8*>(pw) = pack_acc(s, 0);
+        *reinterpret_cast<bf16x8*>(pw + 512) = pack_acc(s, 1);
+        arow[BUF][grp][lane] = al;
+      }
+    }
+    __syncthreads();
+  };
+  if (role == 0) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(qf[s]));
+    for (int j = 0; j <= ntiles; j += 2) {
+      interval(j, IC<0>{}, IC<0>{});
+      if (j + 1 <= ntiles) interval(j + 1, IC<1>{}, IC<0>{});
+    }
+  } else {
+    for (int j = 0; j <= ntiles; j += 2) {
+      interval(j, IC<0>{}, IC<1>{});
+      if (j + 1 <= ntiles) interval(j + 1, IC<1>{}, IC<1>{});
+    }
+  }
+  // the follower takes the row sum from its leader (arow is free after the last barrier)
+  if (role == 0) {
+    l = halfsum(l);
+    arow[0][grp][lane] = l;
+  }
+  __syncthreads();
+  if (role == 1) l = arow[0][grp][lane];
+  const int vcol = role * 128;
+  if (p.ksplit > 1) {
+    if (q < p.Tq) {
+      const long row = (((long)si * p.B + b) * p.H + h) * p.Tq + q;
+      float* dst = p.part + row * p.part_ld + vcol;
+#pragma unroll
+      for (int dt = 0; dt < DH; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 w;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = o[dt][4 * g + i];
+          *reinterpret_cast<f32x4*>(dst + 32 * dt + 8 * g + 4 * hh) = w;
+        }
+      if (hh == 0 && role == 0) {
+        float2 ml;
+        ml.x = m;
+        ml.y = l;
+        reinterpret_cast<float2*>(p.mlpart)[row] = ml;
+      }
+    }
+    return;
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (q < p.Tq) {
+    bf16* op = p.out + b * p.sob + (long)q * p.sot + h * p.soh + vcol;
+#pragma unroll
+    for (int dt = 0; dt < DH; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = (bf16)(o[dt][4 * g + i] * inv);
+        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * hh) = w;
+      }
+    if (hh == 0 && role == 0 && p.lse)
+      p.lse[((long)b * p.H + h) * p.Tq + q] = (l > 0.f) ? (m + __log2f(l)) * 0.69314718055994531f : INFINITY;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Backward dQ (query-parallel; also writes delta = rowsum(dO*O)).
 //   S^T = K Q^T ; P^T = exp2(S^T*c - lse2) ; dP^T = V dO^T - delta ; dS^T = P^T dP^T
 //   dQ^T += K^T dS^T   (K^T via tr reads of the K image)
@@ -1933,10 +2138,14 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   // producing half of the output columns: the 128-wide O accumulator lets 8 waves (2 per SIMD)
   // share a CU, where the full 256-wide one holds a wave per SIMD, at the price of computing S
   // twice (1.5x the MFMA work). SPA_ATTN_SPLITV=0 (read per call) keeps the single 4-wave kernel.
+  // Default at 256: the S-sharing wave-pair kernel (attn_fwd256p_kernel, 128 queries per block);
+  // SPA_ATTN_FWD256=0 (read per call) falls back to the split-V launch.
+  const char* f2e = getenv("SPA_ATTN_FWD256");
+  const bool pshare = !(f2e && atoi(f2e) == 0) && HDK == 256 && HDV == 256 && !drop;
   const char* sve = getenv("SPA_ATTN_SPLITV");
-  const bool splitv = !(sve && atoi(sve) == 0) && HDK == 256 && HDV == 256 && !drop;
-  const int nw = splitv ? 8 : (HDK <= 192 && HDV <= 192) || (HDK == 256 && HDV == 128) ? 8 : 4;
-  const int blocks = cdiv(Tq, 32 * nw) * H * B * (splitv ? 2 : 1);
+  const bool splitv = !pshare && !(sve && atoi(sve) == 0) && HDK == 256 && HDV == 256 && !drop;
+  const int nw = splitv || pshare ? 8 : (HDK <= 192 && HDV <= 192) || (HDK == 256 && HDV == 128) ? 8 : 4;
+  const int blocks = cdiv(Tq, pshare ? 128 : 32 * nw) * H * B * (splitv ? 2 : 1);
   const int ntk = cdiv(Tk, (HDK >= 256 || HDV >= 256) ? 32 : 64);
   p.ksplit = attn_ksplit(blocks, ntk);
   at::Tensor part;
@@ -1948,7 +2157,10 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
     p.mlpart = p.part + (long)p.ksplit * rows * HDV;
   }
   const int gx = blocks / (splitv ? 2 : 1) * p.ksplit;
-  if (splitv) {
+  if (pshare) {
+    if (causal) attn_fwd256p_kernel<true><<<gx, 512, 0, st>>>(p);
+    else attn_fwd256p_kernel<false><<<gx, 512, 0, st>>>(p);
+  } else if (splitv) {
     p.vhalf = 128;
     if (causal) attn_fwd_kernel<256, 128, 8, true, false><<<dim3(gx, 2), 512, 0, st>>>(p);
     else attn_fwd_kernel<256, 128, 8, false, false><<<dim3(gx, 2), 512, 0, st>>>(p);

@@ -477,20 +477,35 @@ def test_mla_attention_fused_matches_composition(pos_off):
         assert rel(a.cpu(), b) < 3e-2, rel(a.cpu(), b)
 
 
-@pytest.mark.parametrize("causal,Hkv", [(True, 1), (False, 2)])
-def test_attn_fwd_hd256_splitv_matches(causal, Hkv, monkeypatch):
-    """Head dim 256 forward as two (256, 128) half-V column slices of one launch (default) == the
-    single 4-wave kernel (SPA_ATTN_SPLITV=0), output and lse."""
+@pytest.mark.parametrize("causal,Hkv,Tq,Tk", [(True, 1, 333, 333), (False, 2, 333, 333), (True, 1, 200, 333),
+                                              (True, 1, 1024, 1024)])
+def test_attn_fwd_hd256_variants_match(causal, Hkv, Tq, Tk, monkeypatch):
+    """Head dim 256 forward: the S-sharing wave-pair kernel (default) == the two (256, 128) half-V
+    column slices (SPA_ATTN_FWD256=0) == the single 4-wave kernel (and SPA_ATTN_SPLITV=0), output
+    and lse, with and without a key split; and the fp32 oracle."""
     ops = _ext.ops()
     torch.manual_seed(4)
-    q = torch.randn(2, 333, 4, 256, device=DEV, dtype=torch.bfloat16)
-    k = torch.randn(2, 333, Hkv, 256, device=DEV, dtype=torch.bfloat16)
-    v = torch.randn(2, 333, Hkv, 256, device=DEV, dtype=torch.bfloat16)
-    monkeypatch.setenv("SPA_ATTN_SPLITV", "0")
-    o0, l0 = ops.attn_fwd(q, k, v, 0.0625, causal)
-    monkeypatch.setenv("SPA_ATTN_SPLITV", "1")
-    o1, l1 = ops.attn_fwd(q, k, v, 0.0625, causal)
-    assert rel(o1, o0) < 5e-3 and (l1 - l0).abs().max().item() < 1e-3
+    q = torch.randn(2, Tq, 4, 256, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(2, Tk, Hkv, 256, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(2, Tk, Hkv, 256, device=DEV, dtype=torch.bfloat16)
+    res = {}
+    for name, env in (("single", {"SPA_ATTN_FWD256": "0", "SPA_ATTN_SPLITV": "0"}),
+                      ("splitv", {"SPA_ATTN_FWD256": "0", "SPA_ATTN_SPLITV": "1"}),
+                      ("pshare", {"SPA_ATTN_FWD256": "1", "SPA_ATTN_KSPLIT": "1"}),
+                      ("pshare_ks3", {"SPA_ATTN_FWD256": "1", "SPA_ATTN_KSPLIT": "3"})):
+        for kk in ("SPA_ATTN_FWD256", "SPA_ATTN_SPLITV", "SPA_ATTN_KSPLIT"):
+            monkeypatch.delenv(kk, raising=False)
+        for kk, vv in env.items():
+            monkeypatch.setenv(kk, vv)
+        res[name] = ops.attn_fwd(q, k, v, 0.0625, causal)
+    o0, l0 = res["single"]
+    for name in ("splitv", "pshare", "pshare_ks3"):
+        o1, l1 = res[name]
+        assert torch.isfinite(o1).all(), name
+        assert rel(o1, o0) < 5e-3 and (l1 - l0).abs().max().item() < 1e-3, (name, rel(o1, o0))
+    of, lf = R.attention(q.float(), k.float(), v.float(), causal, scale=0.0625)
+    assert rel(res["pshare"][0], of) < 2e-2
+    assert (res["pshare"][1] - lf).abs().max().item() < 1e-2
 
 
 @pytest.mark.parametrize("B,Tq,Tk,H,Hkv,hd,causal", [
