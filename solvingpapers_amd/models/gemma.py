@@ -29,6 +29,7 @@ from .. import nn as snn
 from ..infer.graph import DecodeState
 from ..ops import _ext, attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
 from ..ops.attention import decode_attention, flash_attention
+from ..ops.linear import linear_rows
 from ..ops.misc import dropout
 from ..ops.rope import RopeCache, gemma_ref_rotate
 from ..utils.grad import mark_ready
@@ -253,11 +254,13 @@ class GemmaBlock(tnn.Module):
         else:
             n1, h = rms_norm(delta, self.attn_norm, c.norm_eps, residual=res)
         hd, KV = c.head_dim, c.n_kv_heads
-        n1p = copy_to_tp(n1, tp_group)
-        q = linear(n1p, self.wq)                                         # [B, T, hl*hd]
-        kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)              # replicated K/V, grads summed over TP
-        B, T = q.shape[0], q.shape[1]
-        qkv = torch.cat([q, kv], dim=-1)
+        if self.tp == 1:     # one GEMM over the adjacent q and K/V weights
+            qkv = linear_rows(n1, (self.wq, self.wkv))
+        else:
+            q = linear(copy_to_tp(n1, tp_group), self.wq)                # [B, T, hl*hd]
+            kv = reduce_grad_tp(linear(n1, self.wkv), tp_group)          # replicated K/V, grads summed over TP
+            qkv = torch.cat([q, kv], dim=-1)
+        B, T = qkv.shape[0], qkv.shape[1]
         if isinstance(pos, DecodeState):  # graph-capturable decode step: positions on the device
             x4 = qkv.view(B, T, self.hl + 2 * KV, hd)
             cos, sin = RopeCache.get(pos.max_len, hd, c.rope_theta, qkv.device)
@@ -302,10 +305,9 @@ class GemmaBlock(tnn.Module):
         c = self.c
         hd, KV = c.head_dim, c.n_kv_heads
         n1f = rms_norm(hf, self.attn_norm, c.norm_eps)
-        q = linear(n1f, self.wq)
-        B, T = q.shape[0], q.shape[1]
-        qkv = rope_packed_(torch.cat([q, linear(n1f, self.wkv)], dim=-1), self.hl + KV, c.rope_theta, pos,
-                           interleaved=False, head_dim=hd)
+        qkv = linear_rows(n1f, (self.wq, self.wkv))
+        B, T = qkv.shape[0], qkv.shape[1]
+        qkv = rope_packed_(qkv, self.hl + KV, c.rope_theta, pos, interleaved=False, head_dim=hd)
         if kv_prefix is None:
             o = attention_packed(qkv, self.hl, KV, causal=True, head_dim=hd)
         else:

@@ -299,6 +299,86 @@ def linear(x, w, b=None, fp8=False):
     return _LinearFn.apply(x, w, b)
 
 
+# (id(w) for w in ws) -> (W view, main_grad view, weakrefs, data pointers): the joint views of
+# row-stacked weights that FlatParams placed back to back (linear_rows)
+_JOINT: dict = {}
+
+
+def _joint_views(ws):
+    """([sum N, K] weight view, matching main_grad view) spanning the row-stacked weights ``ws``
+    when they and their main_grad views are contiguous and back to back in memory (FlatParams
+    lays a module's parameters out in registration order), else None. Cached per weight tuple;
+    re-validated by data pointers each call."""
+    from ..utils.grad import is_multi_stream
+    w0 = ws[0]
+    mgs = [getattr(w, "main_grad", None) for w in ws]
+    if any(m is None for m in mgs) or any(is_multi_stream(w) for w in ws):
+        return None
+    ptrs = tuple(w.data_ptr() for w in ws) + tuple(m.data_ptr() for m in mgs)
+    key = tuple(id(w) for w in ws)
+    hit = _JOINT.get(key)
+    if hit is not None and hit[3] == ptrs and all(r() is w for r, w in zip(hit[2], ws)):
+        return hit[0], hit[1]
+    K = w0.shape[1]
+    rows, off_w, off_g = 0, 0, 0
+    for w, m in zip(ws, mgs):
+        if (w.dim() != 2 or w.shape[1] != K or w.dtype != w0.dtype or not w.is_contiguous()
+                or not m.is_contiguous() or m.dtype != mgs[0].dtype or m.shape != w.shape):
+            return None
+        if w.data_ptr() != w0.data_ptr() + off_w or m.data_ptr() != mgs[0].data_ptr() + off_g:
+            return None
+        off_w += w.numel() * w.element_size()
+        off_g += m.numel() * m.element_size()
+        rows += w.shape[0]
+    wd, md = w0.detach(), mgs[0]
+    if wd.storage_offset() + rows * K > wd.untyped_storage().nbytes() // wd.element_size():
+        return None
+    W = wd.as_strided((rows, K), (K, 1), wd.storage_offset())
+    MG = md.as_strided((rows, K), (K, 1), md.storage_offset())
+    if hit is None:
+        weakref.finalize(w0, _JOINT.pop, key, None)
+    _JOINT[key] = (W, MG, tuple(weakref.ref(w) for w in ws), ptrs)
+    return W, MG
+
+
+class _LinearRowsFn(torch.autograd.Function):
+    """y = x W^T with W the joint view of row-stacked weights: one GEMM forward, one dX GEMM and
+    one dW GEMM into the joint main_grad view backward (no concatenation, no dX sum)."""
+
+    @staticmethod
+    def forward(ctx, x, W, MG, *ws):
+        ctx.W, ctx.MG, ctx.ws = W, MG, ws
+        ctx.save_for_backward(x)
+        x2 = x.reshape(-1, x.shape[-1])
+        return torch.ops.aten._unsafe_view(torch.mm(x2, W.t()), (*x.shape[:-1], W.shape[0]))
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..utils.grad import _Gen
+        (x,) = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = dgrad(dy2, ctx.W).view(x.shape) if ctx.needs_input_grad[0] else None
+        if any(ctx.needs_input_grad[3:]):
+            acc = getattr(ctx.ws[0], "_spa_gen", -1) == _Gen.value
+            assert all((getattr(w, "_spa_gen", -1) == _Gen.value) == acc for w in ctx.ws), \
+                "linear_rows: weights committed apart within one iteration"
+            wgrad(dy2, x2, ctx.MG, acc)
+            for w in ctx.ws:
+                w._spa_gen = _Gen.value
+        return (dx, None, None) + (None,) * len(ctx.ws)
+
+
+def linear_rows(x, ws):
+    """x [.., K] times the row-stacked weights ``ws`` ([N_i, K] each) -> [.., sum N_i]: ONE GEMM
+    per pass when the weights sit back to back in a FlatParams buffer (Gemma's q and MQA K/V
+    projections), else the concatenation of separate products."""
+    jv = _joint_views(ws)
+    if jv is not None and not _gemv_ok(x, jv[0], None):
+        return _LinearRowsFn.apply(x, jv[0], jv[1], *ws)
+    return torch.cat([linear(x, w) for w in ws], dim=-1)
+
+
 class Linear(torch.nn.Module):
     """nn.Linear-compatible (weight [out, in]) module using :func:`linear`."""
 

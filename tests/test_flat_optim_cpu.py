@@ -74,3 +74,42 @@ def test_cosine_schedule_matches_reference_formula():
     assert abs(cosine_lr(400, 6e-4, 400, 10000, 6e-5) - 6e-4) < 1e-12
     assert abs(cosine_lr(10000, 6e-4, 400, 10000, 6e-5) - 6e-5) < 1e-12
     assert cosine_lr(20000, 6e-4, 400, 10000, 6e-5) == 6e-5
+
+
+def test_linear_rows_joint_gemm_matches_separate():
+    """ops.linear.linear_rows: row-stacked weights that FlatParams placed back to back run as ONE
+    product over a joint view (forward, dX, dW into the joint main_grad view, accumulating on a
+    second call); weights that are not adjacent fall back to separate products. Same values."""
+    import importlib
+    L = importlib.import_module("solvingpapers_amd.ops.linear")
+
+    class Two(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            g = torch.Generator().manual_seed(0)
+            self.a = torch.nn.Parameter(torch.randn(24, 16, generator=g))
+            self.b = torch.nn.Parameter(torch.randn(8, 16, generator=g))
+            self.c = torch.nn.Parameter(torch.randn(8, 16, generator=g))
+
+    x = torch.randn(5, 16, requires_grad=True)
+    grads = {}
+    for joint in (True, False):
+        m = Two()
+        FlatParams(m)
+        ws = (m.a, m.b) if joint else (m.a, m.c)      # a, c are not adjacent
+        if joint:
+            assert L._joint_views(ws) is not None
+        else:
+            assert L._joint_views(ws) is None
+            with torch.no_grad():
+                m.c.copy_(m.b)
+        from solvingpapers_amd.utils.grad import next_generation
+        next_generation()
+        xx = x.detach().clone().requires_grad_()
+        for _ in range(2):                           # second call accumulates
+            y = L.linear_rows(xx, ws)
+            assert y.shape == (5, 32)
+            (y * torch.arange(32.0)).sum().backward()
+        grads[joint] = (y.detach(), xx.grad.clone(), ws[0].main_grad.clone(), ws[1].main_grad.clone())
+    for a, b in zip(grads[True], grads[False]):
+        assert torch.allclose(a, b, atol=1e-5), (a - b).abs().max()
