@@ -8,6 +8,7 @@ halves overlap each other's collectives (models/gemma.py _forward_sp_pair).
 from __future__ import annotations
 
 import argparse
+import os
 
 import torch
 import torch.distributed as dist
@@ -34,12 +35,17 @@ def main():
                     help="no overlapped chunk pair (default under SP: sequence halves whose collectives "
                          "run on a side stream under the other half's GEMMs)")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the compute stream")
-    ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (tuning/*.csv) to look up")
+    ap.add_argument("--gemm-table", default="auto",
+                    help="TunableOp GEMM table to look up (default tuning/tunableop_gemma7b.csv, tuned at the TP=1 "
+                         "T=8192 shapes: +0.6 %% ABBA, profiles/r4_gemma_gemm_table_abba.txt); 'none' disables")
     a = ap.parse_args()
     info = sdist.init_distributed()
-    if a.gemm_table:   # after init: the device is set, so every rank loads it on its own GPU
-        from solvingpapers_amd.utils.tuning import load_gemm_tuning
-        assert load_gemm_tuning(a.gemm_table), a.gemm_table
+    tuned = False
+    if a.gemm_table != "none":   # after init: the device is set, so every rank loads it on its own GPU
+        from solvingpapers_amd.utils.tuning import ROOT, load_gemm_tuning
+        path = os.path.join(ROOT, "tuning", "tunableop_gemma7b.csv") if a.gemm_table == "auto" else a.gemm_table
+        tuned = load_gemm_tuning(path)
+        assert tuned or a.gemm_table == "auto" or not torch.cuda.is_available(), a.gemm_table
     world, dev = info.world_size, info.device
     kw = {"max_seq_len": a.seq}
     if a.layers:
@@ -79,7 +85,7 @@ def main():
     tf = tok_s * m.flops_per_token(a.seq) / world / 1e12
     report("training tokens/sec, Gemma-7B-shape MQA bf16 (TP)", tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": "gemma_7b_mqa" + (f"-L{a.layers}" if a.layers else ""), "global_batch": a.accum * a.batch, "seq_len": a.seq,
-            "parallelism": f"tp{world}" + ("-sp" if m.sp else "") + ("-pair" if m.sp and m.tp_pipeline else "")}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
+            "parallelism": f"tp{world}" + ("-sp" if m.sp else "") + ("-pair" if m.sp and m.tp_pipeline else "")}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), gemm_table=tuned,
            loss=round(float(last[0].detach()), 4))
     sdist.cleanup()
 
