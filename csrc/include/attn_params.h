@@ -43,7 +43,6 @@ struct AttnParams {
   float* mlpart;
   int part_ld;
   int vhalf;
-  int short_merge;   // short backward: one loop over dQ and dK/dV tiles (non-causal, Tq == Tk)
 };
 
 // 2 KiB dS block index inside one (b, kv-head) region, in the order the dQ pass streams it: per

@@ -1929,86 +1929,6 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnParams p) {
   LdsOff<HD> off;
   off.init(lane);
 
-  // Non-causal, Tq == Tk (ViT): B and C in ONE loop -- tile t is key tile t of this wave's dQ and
-  // query tile t of its dK / dV, four independent MFMA chains per iteration instead of two, so
-  // one wave's LDS and MFMA latencies overlap its own other chain (the loops are latency-bound
-  // at 2 waves per SIMD). SPA_ATTN_SHORT_MERGE=0 (host) keeps the two loops.
-  if constexpr (!CAUSAL) {
-    if (p.short_merge && p.Tq == p.Tk) {
-      if (r0 >= p.Tq) return;
-      const float nlse2 = rowl[row];
-      f32x16 acc[DT], dkt[DT], dvt[DT];
-#pragma unroll
-      for (int i = 0; i < DT; ++i) acc[i] = dkt[i] = dvt[i] = splat16(0.f);
-      const int nt = cdiv(p.Tk, 32);
-      for (int t = 0; t < nt; ++t) {
-        const bf16* Ks = Ki + 32 * t * HD;
-        const bf16* Vs = Vi + 32 * t * HD;
-        const bf16* Qs = Qi + 32 * t * HD;
-        const bf16* Ds = Di + 32 * t * HD;
-        f32x16 dpc;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 dv = *reinterpret_cast<const f32x4*>(rowd + 32 * t + 8 * g + 4 * hh);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) dpc[4 * g + i] = dv[i];
-        }
-        f32x16 sb = splat16(0.f), dpb = splat16(-dlt), sc = splat16(0.f);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          sb = mfma32(ld_row(Ks, off.row[ks]), qf[ks], sb);
-          sc = mfma32(ld_row(Qs, off.row[ks]), kf[ks], sc);
-          dpb = mfma32(ld_row(Vs, off.row[ks]), df[ks], dpb);
-          dpc = mfma32(ld_row(Ds, off.row[ks]), vf[ks], dpc);
-        }
-        if (32 * t + 32 > p.Tk) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Tk) sb[r] = -INFINITY;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sb[r] = fexp2(fmaf(sb[r], c, nlse2)) * dpb[r];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 lv = *reinterpret_cast<const f32x4*>(rowl + 32 * t + 8 * g + 4 * hh);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            const float pr = fexp2(fmaf(sc[r], c, lv[i]));
-            sc[r] = pr;
-            dpc[r] = pr * dpc[r];
-          }
-        }
-        const bf16x8 qa = pack_acc(sb, 0), qb = pack_acc(sb, 1);
-        const bf16x8 pa = pack_acc(sc, 0), pb = pack_acc(sc, 1), da = pack_acc(dpc, 0), db = pack_acc(dpc, 1);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          acc[dt] = mfma32(ld_tr(Ks, off.tra[dt], off.trb[dt]), qa, acc[dt]);
-          dvt[dt] = mfma32(ld_tr(Ds, off.tra[dt], off.trb[dt]), pa, dvt[dt]);
-          dkt[dt] = mfma32(ld_tr(Qs, off.tra[dt], off.trb[dt]), da, dkt[dt]);
-          acc[dt] = mfma32(ld_tr(Ks + 16 * HD, off.tra[dt], off.trb[dt]), qb, acc[dt]);
-          dvt[dt] = mfma32(ld_tr(Ds + 16 * HD, off.tra[dt], off.trb[dt]), pb, dvt[dt]);
-          dkt[dt] = mfma32(ld_tr(Qs + 16 * HD, off.tra[dt], off.trb[dt]), db, dkt[dt]);
-        }
-      }
-      if (row < p.Tq) {
-        bf16* o = p.dq + b * p.sdqb + (long)row * p.sdqt + h * p.sdqh;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            bf16x4 w;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) w[i] = (bf16)(acc[dt][4 * g + i] * p.scale);
-            *reinterpret_cast<bf16x4*>(o + 32 * dt + 8 * g + 4 * hh) = w;
-          }
-      }
-      store_kv_grad<HD>(p, dkt, true, b, h, row, 0, hh);
-      store_kv_grad<HD>(p, dvt, false, b, h, row, 0, hh);
-      return;
-    }
-  }
-
   // ---- B: dQ of queries r0..r0+31 (S^T = K Q^T, dP^T = V dO^T - delta, dQ^T += K^T dS^T)
   if (r0 < p.Tq) {
     const float nlse2 = rowl[row];
@@ -2461,8 +2381,6 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   const bool want_short = !(sse && atoi(sse) == 0);
   if (want_short && !fused && !drop && HDK == 64 && HDV == 64 && H == Hkv && Tq <= 256 && Tk <= 256) {
     p.hsplit = 1;
-    const char* sme = getenv("SPA_ATTN_SHORT_MERGE");
-    p.short_merge = !(sme && atoi(sme) == 0);
     if (causal) attn_bwd_short_kernel<64, true><<<B * H, 512, 0, st>>>(p);
     else attn_bwd_short_kernel<64, false><<<B * H, 512, 0, st>>>(p);
     SPA_LAUNCH_CHECK();
