@@ -129,7 +129,7 @@ def ep_moe(a):
     from solvingpapers_amd.models import deepseekv3 as ds
     dev = torch.device("cuda")
     c = ds.config("dsv3_v3", moe_fp8=a.fp8, n_layers=a.layers, n_dense_layers=0, mtp_heads=0,
-                  vocab_size=1024, block_size=a.tokens)
+                  vocab_size=a.vocab, block_size=a.tokens)
     g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
     m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=3, ep_group=g1).train()
     FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
@@ -163,7 +163,7 @@ def ep_moe(a):
                 comm = g1.modelled_s * 1e3 / a.iters
     med = {k: round(statistics.median(v), 3) for k, v in res.items()}
     out = {"config": f"dsv3_v3 widths EP=8 local shard, {a.layers} MLA+MoE layers (32 of 256 experts, top-8, D 7168, "
-                     f"F 2048, 1 shared){' fp8' if a.fp8 else ''}, 2 micro-batches x {a.tokens} tokens",
+                     f"F 2048, 1 shared){' fp8' if a.fp8 else ''}, 2 micro-batches x {a.tokens} tokens, vocab {a.vocab}",
            "ms": med, "modelled_comm_ms": round(comm, 3)}
     if not ARMS:
         total = med["blocking"] - med["off"]
@@ -182,6 +182,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="TP: sequences per step (even: the pipeline splits by batch)")
     ap.add_argument("--micro", action="store_true", help="TP: two accumulation micro-batches per step")
     ap.add_argument("--tokens", type=int, default=4096)
+    ap.add_argument("--vocab", type=int, default=1024,
+                    help="EP: vocabulary of the tied head (1024 isolates the MoE layers; dsv3_v3 has 129280, whose "
+                         "head is the compute a real step runs under the last combine / first combine-grad)")
     ap.add_argument("--fp8", action="store_true", default=True, help="EP: fp8 experts + dispatch (config #5)")
     ap.add_argument("--bf16", dest="fp8", action="store_false")
     ap.add_argument("--ar-gbps", type=float, default=300.0)
