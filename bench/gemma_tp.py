@@ -1,10 +1,11 @@
 #!/usr/bin/env python
 """Gemma-7B-shape (MQA, 1 KV head) bf16 training tokens/s with tensor parallelism over all
-ranks (BASELINE.json config #4: TP=8 on one node). Sequence parallel by default: column-parallel
-q / GeGLU open with an all-gather over T, row-parallel o / down close with a reduce-scatter,
-the K/V projection runs on the sequence shard, vocab-parallel embedding + CE; the two sequence
-halves overlap each other's collectives (models/gemma.py _forward_sp_pair).
-``[torchrun --nproc-per-node N ...] python bench/gemma_tp.py --steps K --warmup W [--layers L]``"""
+ranks (BASELINE.json config #4: TP=8 on one node). Sequence parallel by default: each layer
+boundary is a reduce-scatter of the row-parallel output followed by an all-gather of the residual
+shard (norms and the MQA K/V projection on the gathered sequence), vocab-parallel embedding + CE;
+two chunks -- the micro-batches of an even --accum (Gemma.forward_pair), else the batch or
+sequence halves -- overlap each other's boundaries (models/gemma.py _forward_sp_pair).
+``[torchrun --nproc-per-node N ...] python bench/gemma_tp.py --steps K --warmup W [--layers L] [--accum 2]``"""
 from __future__ import annotations
 
 import argparse
@@ -32,8 +33,9 @@ def main():
     ap.add_argument("--no-sp", dest="sp", action="store_false",
                     help="plain Megatron TP (default: sequence parallelism inside the TP group)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="no overlapped chunk pair (default under SP: sequence halves whose collectives "
-                         "run on a side stream under the other half's GEMMs)")
+                    help="no overlapped pairs (default under SP: two chunks -- the micro-batches of an even "
+                         "--accum, else batch / sequence halves -- whose layer-boundary reduce-scatter -> "
+                         "all-gather runs under the other chunk's compute)")
     ap.add_argument("--no-opt-overlap", action="store_true", help="run AdamW on the compute stream")
     ap.add_argument("--gemm-table", default="auto",
                     help="TunableOp GEMM table to look up (default tuning/tunableop_gemma7b.csv, tuned at the TP=1 "
