@@ -73,14 +73,17 @@ def _tp_worker(rank, world, port, q, mode, nb):
     c = _gemma_cfg()
     full = gemma.Gemma(c, device="cuda:0", dtype=torch.bfloat16, seed=5)
     grp = dist.new_group([0, 1])
-    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=mode != "plain", tp_pipeline=mode == "pair",
-                        device="cuda:0", dtype=torch.bfloat16)
+    local = gemma.Gemma(c, tp_group=grp, seed=5, sequence_parallel=mode != "plain",
+                        tp_pipeline=mode in ("pair", "micro"), device="cuda:0", dtype=torch.bfloat16)
     shard_gemma_from_full(full, local, rank, world)
     FlatParams(local, grad_dtype=torch.float32)
     ids = _gemma_ids().cuda()[:nb]
-    if mode == "pair":      # the overlapped chunk pair: side-stream collectives + norms
+    if mode == "pair":      # the overlapped chunk pair inside one forward
         assert local._pair_split(ids[:, :-2]) == ("batch" if nb == 2 else "sequence")
-    loss = local(ids[:, :-2], ids[:, 1:-1])
+    if mode == "micro":     # two accumulation micro-batches as the pair (Gemma.forward_pair)
+        loss = local.forward_pair(ids[:1, :-2], ids[:1, 1:-1], ids[1:, :-2], ids[1:, 1:-1])
+    else:
+        loss = local(ids[:, :-2], ids[:, 1:-1])
     loss.backward()
     local.sync_sequence_parallel_grads()
     torch.cuda.synchronize()
@@ -89,7 +92,7 @@ def _tp_worker(rank, world, port, q, mode, nb):
     sdist.cleanup()
 
 
-@pytest.mark.parametrize("mode,nb", [("plain", 2), ("sp", 2), ("pair", 2), ("pair", 1)])
+@pytest.mark.parametrize("mode,nb", [("plain", 2), ("sp", 2), ("pair", 2), ("pair", 1), ("micro", 2)])
 def test_gemma_tp2_on_one_gpu_matches_unsharded(mode, nb):
     from solvingpapers_amd.models import gemma
     from solvingpapers_amd.ops import _ext
@@ -99,7 +102,10 @@ def test_gemma_tp2_on_one_gpu_matches_unsharded(mode, nb):
     full = gemma.Gemma(c, device="cuda:0", dtype=torch.bfloat16, seed=5)
     FlatParams(full, grad_dtype=torch.float32)
     ids = _gemma_ids().cuda()[:nb]
-    loss = full(ids[:, :-2], ids[:, 1:-1])
+    if mode == "micro":
+        loss = full(ids[:1, :-2], ids[:1, 1:-1]) + full(ids[1:, :-2], ids[1:, 1:-1])
+    else:
+        loss = full(ids[:, :-2], ids[:, 1:-1])
     loss.backward()
     fg = {n: p.main_grad.float().cpu() for n, p in full.named_parameters()}
     ref_loss = float(loss.detach())
