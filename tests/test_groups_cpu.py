@@ -64,6 +64,10 @@ CASES = {
                       "--set", "n_heads=4", "--set", "head_dim=16", "--set", "ffn_hidden=128"],
     "gemma_dp2_tp2_sp": ["gemma", "--preset", "gemma_tiny", "--tp", "2", "--sp", "--set", "vocab_size=256", "--set",
                          "dim=64", "--set", "n_heads=4", "--set", "head_dim=16", "--set", "ffn_hidden=128"],
+    # even --accum under SP: the Trainer runs the micro-batches as Gemma.forward_pair
+    "gemma_dp2_tp2_sp_pairs": ["gemma", "--preset", "gemma_tiny", "--tp", "2", "--sp", "--accum", "2", "--set",
+                               "vocab_size=256", "--set", "dim=64", "--set", "n_heads=4", "--set", "head_dim=16",
+                               "--set", "ffn_hidden=128"],
     "dsv3_dp4_ep2": ["dsv3", "--preset", "dsv3_tiny", "--ep", "2", "--set", "vocab_size=256", "--set", "dim=64",
                      "--set", "n_heads=2", "--set", "expert_hidden=32", "--set", "dense_hidden=128",
                      "--set", "kv_lora_rank=32", "--set", "qk_nope_dim=16", "--set", "qk_rope_dim=16",
