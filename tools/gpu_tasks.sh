@@ -144,8 +144,13 @@ attn-pmc)
 secondary)
   run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
   run 300 ${O}_dsv3s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
-  run 300 ${O}_v3.log python -u bench/dsv3_train.py --preset dsv3_v3 --steps 4 --warmup 2
-  run 300 ${O}_v3fp8.log python -u bench/dsv3_train.py --preset dsv3_v3 --fp8 --steps 4 --warmup 2
+  # dsv3_v3 widths at one EP=8 rank's share (4 layers, 1 dense, 32 of the 256 experts): the full
+  # 61-layer model does not fit one GPU
+  V3="--preset dsv3_v3 --layers 4 --dense-layers 1 --experts 32 --mb 1 --accum 4 --steps 3 --warmup 1"
+  run 300 ${O}_v3.log python -u bench/dsv3_train.py $V3
+  run 300 ${O}_v3fp8.log python -u bench/dsv3_train.py $V3 --fp8
+  run 300 ${O}_v3fp8b.log python -u bench/dsv3_train.py $V3 --fp8
+  run 300 ${O}_v3b.log python -u bench/dsv3_train.py $V3
   run 400 ${O}_gemma.log python -u bench/gemma_tp.py --layers 28 --steps 3 --warmup 1
   jsonl ${O}_*.log ;;
 dsv3-prof)
