@@ -1674,13 +1674,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   }
 }
 
-// Head dim 256 form of the above (after attn_bwd_dkdv_kernel<256, 256, .., DSOUT>): a unit is one
-// (q-head, 32-query tile), so a wave's dQ^T accumulator is 32 queries x 256 dims (128 registers,
-// two waves per SIMD); per 32-key step each wave DMAs its one 2 KiB dS block and an eighth of the
-// 16 KiB K tile (4 + 2 pieces: the same vmcnt(6) discipline), 3 slots of 24 KiB.
-template <bool CAUSAL, bool NT>
+// Head dim 256 / 192 form of the above (after attn_bwd_dkdv_kernel<HDK, .., DSOUT>: Gemma's 256 and
+// MLA's q/k 192 with v 128): a unit is one (q-head, 32-query tile), so a wave's dQ^T accumulator is
+// 32 queries x HDK dims (128 / 96 registers, two waves per SIMD); per 32-key step each wave DMAs its
+// one 2 KiB dS block and an eighth of the 16 KiB K tile (4 + 2 pieces: the same vmcnt(6) discipline),
+// 3 slots of 24 KiB.
+template <int HDK, bool CAUSAL, bool NT>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds256_kernel(AttnParams p) {
-  constexpr int HD = 256, DT = 8, KIMG = 32 * HD, WSLOT = 1024, SLOT = KIMG + 4 * WSLOT, NSLOT = 3;
+  // HDK 256 (Gemma) or 192 (MLA q/k): the K image rows are 256 wide either way (img_w<192> = 256;
+  // the DMA moves whole 512-B rows, whose columns past HDK are never read by the MFMAs)
+  static_assert(HDK == 256 || HDK == 192, "dq_ds256: q/k head dim 192 or 256");
+  constexpr int HD = 256, DT = HDK / 32, KIMG = 32 * HD, WSLOT = 1024, SLOT = KIMG + 4 * WSLOT, NSLOT = 3;
   __shared__ __attribute__((aligned(16))) bf16 smem[NSLOT * SLOT];   // [slot][K | 4 waves x 1 dS block]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1719,7 +1723,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds256_kernel(AttnParams p)
   auto issue = [&](int j, int slot) {
     bf16* sl = smem + slot * SLOT;
     const int key0 = 32 * j;
-    const long kbytes = key0 < p.Tk ? ((long)(p.Tk - key0 - 1) * p.skt + HD) * 2 : 0;
+    const long kbytes = key0 < p.Tk ? ((long)(p.Tk - key0 - 1) * p.skt + HDK) * 2 : 0;
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(kbase + (long)key0 * p.skt), 0, (int)min(kbytes, 0x7fffffffL), 0x00020000);
 #pragma unroll
@@ -2243,11 +2247,11 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
       return;
     }
   }
-  if constexpr (HDK == 256 && HDV == 256 && !DROP) {
-    // dS-materialising backward at head dim 256: the single-wave dK/dV kernel also stores dS,
-    // then dQ = dS K streams it (attn_bwd_dq_ds256_kernel) -- instead of the dq kernel's three
-    // products (S and dP recomputed over 256-deep contractions). SPA_ATTN_DQ_DS (per call): 0 keeps
-    // the dq kernel, 2 takes this path at any grid size.
+  if constexpr (((HDK == 256 && HDV == 256) || (HDK == 192 && HDV == 128)) && !DROP) {
+    // dS-materialising backward at head dims 256 (Gemma) and (192, 128) (MLA): the single-wave
+    // dK/dV kernel also stores dS, then dQ = dS K streams it (attn_bwd_dq_ds256_kernel) -- instead
+    // of the dq kernel's three products (S and dP recomputed over 192 / 256-deep contractions).
+    // SPA_ATTN_DQ_DS (per call): 0 keeps the dq kernel, 2 takes this path at any grid size.
     const char* de = getenv("SPA_ATTN_DQ_DS");
     const int dsm = de ? atoi(de) : 1;     // 0 off, 1 by grid size, 2 always
     const bool want = dsm != 0;
@@ -2260,23 +2264,23 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
     if (want && (wg >= 512 || dsm == 2) && p.Tk > 0 && dkdv_mode == 0 && (!causal || p.causal_off == 0) &&
         kv_bytes < 0x7fffffffL) {
       const long rows = (long)p.B * p.Tq * p.H;
-      attn_delta_kernel<HDK><<<(int)cdiv(rows, 256 / (HDK / 8)), 256, 0, st>>>(p);
+      attn_delta_kernel<HDV><<<(int)cdiv(rows, 256 / (HDV / 8)), 256, 0, st>>>(p);   // rowsum(dO O): v dims
       p.ds_nqt = cdiv(p.Tq, 32);
       p.ds_nkt = cdiv(p.Tk, 32);
       p.ds_kvstride = ds_kv_elems(cdiv(p.Tq, 64), p.ds_nkt, G, causal);
       at::Tensor dsb = at::empty({(long)p.B * p.Hkv * p.ds_kvstride}, bf16_opts);   // freed (stream-ordered) on return
       p.dsbuf = (bf16*)dsb.data_ptr();
       const int g2 = nkv * p.hsplit;
-      if (causal) attn_bwd_dkdv_kernel<256, 256, true, 1, false, false, true><<<g2, 256, 0, st>>>(p);
-      else attn_bwd_dkdv_kernel<256, 256, false, 1, false, false, true><<<g2, 256, 0, st>>>(p);
+      if (causal) attn_bwd_dkdv_kernel<HDK, HDV, true, 1, false, false, true><<<g2, 256, 0, st>>>(p);
+      else attn_bwd_dkdv_kernel<HDK, HDV, false, 1, false, false, true><<<g2, 256, 0, st>>>(p);
       const char* ne = getenv("SPA_ATTN_DS_NT");
       const bool nt = !(ne && atoi(ne) == 0);
       if (nt) {
-        if (causal) attn_bwd_dq_ds256_kernel<true, true><<<wg, 256, 0, st>>>(p);
-        else attn_bwd_dq_ds256_kernel<false, true><<<wg, 256, 0, st>>>(p);
+        if (causal) attn_bwd_dq_ds256_kernel<HDK, true, true><<<wg, 256, 0, st>>>(p);
+        else attn_bwd_dq_ds256_kernel<HDK, false, true><<<wg, 256, 0, st>>>(p);
       } else {
-        if (causal) attn_bwd_dq_ds256_kernel<true, false><<<wg, 256, 0, st>>>(p);
-        else attn_bwd_dq_ds256_kernel<false, false><<<wg, 256, 0, st>>>(p);
+        if (causal) attn_bwd_dq_ds256_kernel<HDK, true, false><<<wg, 256, 0, st>>>(p);
+        else attn_bwd_dq_ds256_kernel<HDK, false, false><<<wg, 256, 0, st>>>(p);
       }
       if (p.hsplit > 1) {
         const long kr = (long)p.B * p.Tk * p.Hkv;

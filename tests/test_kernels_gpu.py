@@ -403,16 +403,20 @@ def test_flash_attention(B, Tq, Tk, H, Hkv, hd, causal):
     (1, 1024, 2, 1, True, 256),     # its TP=8 rank (dK/dV iteration split)
     (2, 200, 4, 2, True, 256),      # ragged tail
     (1, 300, 3, 1, False, 256),     # non-causal, G = 3 (units span two query tiles per block)
+    (1, 1024, 8, 8, True, (192, 128)),   # MLA (q/k 128 nope + 64 rope, v 128)
+    (2, 200, 4, 4, True, (192, 128)),    # MLA, ragged tail
+    (1, 300, 2, 2, False, (192, 128)),   # MLA, non-causal
 ])
 def test_attn_bwd_ds_path(B, T, H, Hkv, causal, hd, monkeypatch):
     """Backward through the materialised dS (the dK/dV kernel stores dS, dQ = dS K in a separate
-    streaming pass; the default at head dims 128 and 256) == the dq kernel that recomputes S and
-    dP (SPA_ATTN_DQ_DS=0), and both track the fp32 reference."""
+    streaming pass; the default at head dims 128, 256 and MLA's (192, 128)) == the dq kernel that
+    recomputes S and dP (SPA_ATTN_DQ_DS=0), and both track the fp32 reference."""
     from solvingpapers_amd.ops import _ext
     torch.manual_seed(3)
+    hd, hdv = hd if isinstance(hd, tuple) else (hd, hd)
     q = torch.randn(B, T, H, hd, device=DEV, dtype=torch.bfloat16)
     k = torch.randn(B, T, Hkv, hd, device=DEV, dtype=torch.bfloat16)
-    v = torch.randn(B, T, Hkv, hd, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, T, Hkv, hdv, device=DEV, dtype=torch.bfloat16)
     sc = 1 / math.sqrt(hd)
     out, lse = _ext.ops().attn_fwd(q, k, v, sc, causal)
     do = torch.randn_like(out)
