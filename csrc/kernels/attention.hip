@@ -1304,10 +1304,16 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
 // DSOUT: role B also stores the bf16 dS of each live 32 x 32 block to p.dsbuf (ds_slot layout),
 // the operand of the separate dQ = dS K pass (attn_bwd_dq_ds_kernel) that replaces the dq
 // kernel's recomputation of S and dP.
-template <int HD, bool CAUSAL, bool DSOUT = false>
+// HDK != HDV (MLA's q/k 192, v 128): role A's fragments / accumulator span HDK / HDV and role B's
+// HDV / HDK; the Q and dO images keep their own widths; 32-query intervals (MT = 1) past head dim
+// 128, where a 3-deep ring of 64-query tiles would not fit the LDS.
+template <int HDK, int HDV, bool CAUSAL, bool DSOUT = false>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
-  constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KS = HD / 16, DT = HD / 32, NT = 512, IW = img_w<HD>();
-  constexpr int TQ = BMQ * IW, TB = 2 * TQ, PSLOT = 4 * MT * 2 * 64 * 8;
+  constexpr int MT = (HDK > 128 || HDV > 128) ? 1 : 2, BMQ = 32 * MT, BNK = 128, NT = 512;
+  constexpr int KSK = HDK / 16, KSV = HDV / 16, DTK = HDK / 32, DTV = HDV / 32;
+  constexpr int KSX = KSK > KSV ? KSK : KSV, DTX = DTK > DTV ? DTK : DTV;
+  constexpr int IWK = img_w<HDK>(), IWV = img_w<HDV>();
+  constexpr int TQ = BMQ * IWK, TB = TQ + BMQ * IWV, PSLOT = 4 * MT * 2 * 64 * 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[3 * TB];     // [ring][Q | dO]
   __shared__ __attribute__((aligned(16))) bf16 pimg[2 * PSLOT];  // [slot][pair][t][half][lane][8]
   __shared__ __attribute__((aligned(16))) float rowc[3][2 * BMQ]; // [ring][-lse2 | -delta]
@@ -1327,16 +1333,17 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   const bool kvalid = key < p.Tk;
   const float c = p.scale_log2;
 
-  bf16x8 xf[KS];  // A: K fragments, B: V fragments of this lane's key
+  bf16x8 xf[KSX];  // A: K fragments (KSK), B: V fragments (KSV) of this lane's key
   {
     const bf16* xp = role == 0 ? p.k + b * p.skb + (long)key * p.skt + hk * p.skh + 8 * hh
                                : p.v + b * p.svb + (long)key * p.svt + hk * p.svh + 8 * hh;
+    const int nks = role == 0 ? KSK : KSV;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) xf[s] = kvalid ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
+    for (int s = 0; s < KSX; ++s) xf[s] = kvalid && s < nks ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
   }
-  f32x16 acc[DT];  // A: dV^T, B: dK^T
+  f32x16 acc[DTX];  // A: dV^T (DTV), B: dK^T (DTK)
 #pragma unroll
-  for (int i = 0; i < DT; ++i) acc[i] = splat16(0.f);
+  for (int i = 0; i < DTX; ++i) acc[i] = splat16(0.f);
 
   int qstart = 0, wave_qstart = 0;
   if (CAUSAL) {
@@ -1347,8 +1354,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
   const int nper = ntq - t0 > 0 ? ntq - t0 : 0;
   const int total = nper * Gs;
-  TileLoader<HD, BMQ, NT> lq_;
-  TileLoader<HD, BMQ, NT> ld_;
+  TileLoader<HDK, BMQ, NT> lq_;
+  TileLoader<HDV, BMQ, NT> ld_;
   lq_.init(p.sqt, tid);
   ld_.init(p.sdot, tid);
   float rl = 0.f, rd = 0.f;   // raw row constants of the prefetched tile (transformed at commit)
@@ -1384,8 +1391,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
     if (total > 1) fetch(1);
   }
   __syncthreads();
-  LdsOff<IW> off;
-  off.init(lane);
+  LdsOff<IWK> offk;   // Q image
+  LdsOff<IWV> offv;   // dO image
+  offk.init(lane);
+  offv.init(lane);
   bf16* pme = pimg + pair * (MT * 2 * 64 * 8) + lane * 8;   // + slot * PSLOT + (t * 2 + half) * 512
   bool prev_act = false;
   // interval k (slot SC = k % 3): tiles k-1 (slot (SC+2)%3) and k (slot SC) resident; commits k+1
@@ -1411,11 +1420,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 0) * 512);
           const bf16x8 pb = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 1) * 512);
 #pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            acc[dt] = mfma32(ld_tr(Dp + 32 * t * IW, off.tra[dt], off.trb[dt]), pa, acc[dt]);
-            acc[dt] = mfma32(ld_tr(Dp + (32 * t + 16) * IW, off.tra[dt], off.trb[dt]), pb, acc[dt]);
+          for (int dt = 0; dt < DTV; ++dt) {
+            acc[dt] = mfma32(ld_tr(Dp + 32 * t * IWV, offv.tra[dt], offv.trb[dt]), pa, acc[dt]);
+            acc[dt] = mfma32(ld_tr(Dp + (32 * t + 16) * IWV, offv.tra[dt], offv.trb[dt]), pb, acc[dt]);
           }
-          if (DKDV3_SCHED) chain_sched<2 * DT, 2, 2, 2>();
+          if (DKDV3_SCHED) chain_sched<2 * DTV, 2, 2, 2>();
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -1425,10 +1434,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
         bf16* pw = pme + (k & 1) * PSLOT;
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
-          f32x16 s = mfma32(ld_row(Qc + 32 * t * IW, off.row[0]), xf[0], splat16(0.f));
+          f32x16 s = mfma32(ld_row(Qc + 32 * t * IWK, offk.row[0]), xf[0], splat16(0.f));
 #pragma unroll
-          for (int ks = 1; ks < KS; ++ks) s = mfma32(ld_row(Qc + 32 * t * IW, off.row[ks]), xf[ks], s);
-          if (DKDV3_SCHED) chain_sched<KS, 1, 2>();
+          for (int ks = 1; ks < KSK; ++ks) s = mfma32(ld_row(Qc + 32 * t * IWK, offk.row[ks]), xf[ks], s);
+          if (DKDV3_SCHED) chain_sched<KSK, 1, 2>();
           const int qt0 = qq0 + 32 * t;
           if (CAUSAL && qt0 + p.causal_off < kw0 + 31) {
             const int d = key - qt0 - 4 * hh - p.causal_off;   // row offsets below d are masked
@@ -1473,8 +1482,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           for (int i = 0; i < 4; ++i) dp[4 * g + i] = dv[i];
         }
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) dp = mfma32(ld_row(Dpr + 32 * t * IW, off.row[ks]), xf[ks], dp);
-        if (DKDV3_SCHED) chain_sched<KS, 1, 2, 4>();      // + the 4 delta reads
+        for (int ks = 0; ks < KSV; ++ks) dp = mfma32(ld_row(Dpr + 32 * t * IWV, offv.row[ks]), xf[ks], dp);
+        if (DKDV3_SCHED) chain_sched<KSV, 1, 2, 4>();     // + the 4 delta reads
         const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 0) * 512);
         const bf16x8 pb = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 1) * 512);
         f32x16 ds;
@@ -1497,11 +1506,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          acc[dt] = mfma32(ld_tr(Qp + 32 * t * IW, off.tra[dt], off.trb[dt]), sa, acc[dt]);
-          acc[dt] = mfma32(ld_tr(Qp + (32 * t + 16) * IW, off.tra[dt], off.trb[dt]), sb, acc[dt]);
+        for (int dt = 0; dt < DTK; ++dt) {
+          acc[dt] = mfma32(ld_tr(Qp + 32 * t * IWK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
+          acc[dt] = mfma32(ld_tr(Qp + (32 * t + 16) * IWK, offk.tra[dt], offk.trb[dt]), sb, acc[dt]);
         }
-        if (DKDV3_SCHED) chain_sched<2 * DT, 2, 2, 2>();  // + the P(k-1) reads
+        if (DKDV3_SCHED) chain_sched<2 * DTK, 2, 2, 2>();  // + the P(k-1) reads
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -1521,7 +1530,21 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
       if (k + 2 <= total) interval(k + 2, IC<2>{}, IC<1>{});
     }
   }
-  store_kv_grad<HD>(p, acc, role == 1, b, hk, key, split, hh);
+  if constexpr (HDK == HDV) {
+    store_kv_grad<HDK>(p, acc, role == 1, b, hk, key, split, hh);
+  } else {
+    if (role == 1) {
+      f32x16 ak[DTK];
+#pragma unroll
+      for (int i = 0; i < DTK; ++i) ak[i] = acc[i];
+      store_kv_grad<HDK>(p, ak, true, b, hk, key, split, hh);
+    } else {
+      f32x16 av[DTV];
+#pragma unroll
+      for (int i = 0; i < DTV; ++i) av[i] = acc[i];
+      store_kv_grad<HDV>(p, av, false, b, hk, key, split, hh);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2229,8 +2252,8 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
       p.ds_kvstride = ds_kv_elems(cdiv(p.Tq, 64), p.ds_nkt, p.H / p.Hkv, causal);
       at::Tensor dsb = at::empty({(long)p.B * p.Hkv * p.ds_kvstride}, bf16_opts);   // freed (stream-ordered) on return
       p.dsbuf = (bf16*)dsb.data_ptr();
-      if (causal) attn_bwd_dkdv3_kernel<HDK, true, true><<<nkv, 512, 0, st>>>(p);
-      else attn_bwd_dkdv3_kernel<HDK, false, true><<<nkv, 512, 0, st>>>(p);
+      if (causal) attn_bwd_dkdv3_kernel<HDK, HDV, true, true><<<nkv, 512, 0, st>>>(p);
+      else attn_bwd_dkdv3_kernel<HDK, HDV, false, true><<<nkv, 512, 0, st>>>(p);
       const int G = p.H / p.Hkv;
       const int wg = cdiv(cdiv(p.Tq, 64) * G, 4) * p.B * p.Hkv;
       // SPA_ATTN_DS_NT (read per call, default 1): dS streamed with non-temporal loads, so the
@@ -2271,8 +2294,22 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
       at::Tensor dsb = at::empty({(long)p.B * p.Hkv * p.ds_kvstride}, bf16_opts);   // freed (stream-ordered) on return
       p.dsbuf = (bf16*)dsb.data_ptr();
       const int g2 = nkv * p.hsplit;
-      if (causal) attn_bwd_dkdv_kernel<HDK, HDV, true, 1, false, false, true><<<g2, 256, 0, st>>>(p);
-      else attn_bwd_dkdv_kernel<HDK, HDV, false, 1, false, false, true><<<g2, 256, 0, st>>>(p);
+      // MLA without a head split: the paired, pipelined dK/dV kernel (role A: K fragments + dV^T,
+      // role B: V fragments + dK^T, 2 waves per SIMD); SPA_ATTN_DKDV_MLA=1 (per call) keeps the
+      // single-wave kernel (both accumulator sets in one wave, 1 wave per SIMD)
+      bool paired_mla = false;
+      if constexpr (HDK == 192 && HDV == 128) {
+        const char* me = getenv("SPA_ATTN_DKDV_MLA");
+        paired_mla = p.hsplit == 1 && !(me && atoi(me) == 1);
+        if (paired_mla) {
+          if (causal) attn_bwd_dkdv3_kernel<HDK, HDV, true, true><<<g2, 512, 0, st>>>(p);
+          else attn_bwd_dkdv3_kernel<HDK, HDV, false, true><<<g2, 512, 0, st>>>(p);
+        }
+      }
+      if (!paired_mla) {
+        if (causal) attn_bwd_dkdv_kernel<HDK, HDV, true, 1, false, false, true><<<g2, 256, 0, st>>>(p);
+        else attn_bwd_dkdv_kernel<HDK, HDV, false, 1, false, false, true><<<g2, 256, 0, st>>>(p);
+      }
       const char* ne = getenv("SPA_ATTN_DS_NT");
       const bool nt = !(ne && atoi(ne) == 0);
       if (nt) {
@@ -2309,8 +2346,8 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
   const bool piped = PAIRED_OK && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
   if (piped) {
     if constexpr (PAIRED_OK) {
-      if (causal) attn_bwd_dkdv3_kernel<HDK, true><<<g2, 512, 0, st>>>(p);
-      else attn_bwd_dkdv3_kernel<HDK, false><<<g2, 512, 0, st>>>(p);
+      if (causal) attn_bwd_dkdv3_kernel<HDK, HDV, true><<<g2, 512, 0, st>>>(p);
+      else attn_bwd_dkdv3_kernel<HDK, HDV, false><<<g2, 512, 0, st>>>(p);
     }
   } else if (paired) {
     if constexpr (PAIRED_OK) {

@@ -406,6 +406,8 @@ def test_flash_attention(B, Tq, Tk, H, Hkv, hd, causal):
     (1, 1024, 8, 8, True, (192, 128)),   # MLA (q/k 128 nope + 64 rope, v 128)
     (2, 200, 4, 4, True, (192, 128)),    # MLA, ragged tail
     (1, 300, 2, 2, False, (192, 128)),   # MLA, non-causal
+    (1, 1024, 64, 64, True, (192, 128)),  # MLA with >= 512 key blocks: the paired dK/dV kernel
+    (1, 520, 128, 128, False, (192, 128)),  # paired, non-causal, ragged
 ])
 def test_attn_bwd_ds_path(B, T, H, Hkv, causal, hd, monkeypatch):
     """Backward through the materialised dS (the dK/dV kernel stores dS, dQ = dS K in a separate
@@ -421,15 +423,18 @@ def test_attn_bwd_ds_path(B, T, H, Hkv, causal, hd, monkeypatch):
     out, lse = _ext.ops().attn_fwd(q, k, v, sc, causal)
     do = torch.randn_like(out)
     grads = {}
-    for mode in ("2", "0"):      # 2: the dS path whatever the grid size
-        monkeypatch.setenv("SPA_ATTN_DQ_DS", mode)
+    for mode in ("2", "0") + (("mla1",) if hdv != hd else ()):   # 2: the dS path whatever the grid size
+        if mode == "mla1":     # MLA dS path with the single-wave dK/dV kernel instead of the paired one
+            monkeypatch.setenv("SPA_ATTN_DKDV_MLA", "1")
+        monkeypatch.setenv("SPA_ATTN_DQ_DS", "2" if mode == "mla1" else mode)
         dq, dk, dv = torch.full_like(q, float("nan")), torch.empty_like(k), torch.empty_like(v)
         _ext.ops().attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal)
         torch.cuda.synchronize()
         grads[mode] = (dq, dk, dv)
-    for a, b in zip(grads["2"], grads["0"]):
-        assert torch.isfinite(a).all()
-        assert rel(a, b) < 1e-2, rel(a, b)     # same bf16 dS and fp32 sums, different order
+    for other in [m for m in grads if m != "2"]:
+        for a, b in zip(grads["2"], grads[other]):
+            assert torch.isfinite(a).all()
+            assert rel(a, b) < 1e-2, (other, rel(a, b))     # same bf16 dS and fp32 sums, different order
     qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
     of, _ = R.attention(qf, kf, vf, causal)
     of.backward(do.float())
