@@ -309,10 +309,9 @@ def _joint_views(ws):
     when they and their main_grad views are contiguous and back to back in memory (FlatParams
     lays a module's parameters out in registration order), else None. Cached per weight tuple;
     re-validated by data pointers each call."""
-    from ..utils.grad import is_multi_stream
     w0 = ws[0]
     mgs = [getattr(w, "main_grad", None) for w in ws]
-    if any(m is None for m in mgs) or any(is_multi_stream(w) for w in ws):
+    if any(m is None for m in mgs):
         return None
     ptrs = tuple(w.data_ptr() for w in ws) + tuple(m.data_ptr() for m in mgs)
     key = tuple(id(w) for w in ws)

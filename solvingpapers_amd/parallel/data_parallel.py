@@ -68,9 +68,6 @@ class DataParallel:
         if idx in self._launched or idx >= len(self.flat.buckets):
             return
         self._launched.add(idx)
-        if self.flat.grad.is_cuda:
-            from ..utils.grad import wait_side_streams
-            wait_side_streams()          # gradients committed from a chunk pipeline's side stream
         b = self.flat.buckets[idx]
         g = self.flat.grad[b.start:b.end]
         if idx in self.expert_buckets:

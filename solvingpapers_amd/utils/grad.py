@@ -23,58 +23,6 @@ def next_generation():
     _Gen.value += 1
 
 
-def mark_multi_stream(params):
-    """Put these parameters in multi-stream mode: their model runs its backward on more than one
-    compute stream (tensor- / expert-parallel chunk pipelining), so every commit to one of them
-    waits for the previous commit to it (an event recorded on the stream that made it) when that
-    came from another stream -- the first-writer-overwrites / later-writers-accumulate order
-    decided on the host is the order the device applies. The direct-write shortcuts (direct_out,
-    claim_main_grad, deferred expert Wgrad) are off for them: their writes happen after they
-    return, outside the ordering. Per parameter, so other models in the process keep them."""
-    for p in params:
-        p._spa_multi = True
-
-
-def is_multi_stream(p) -> bool:
-    return getattr(p, "_spa_multi", False)
-
-
-_SIDE_STREAMS: list = []
-
-
-def register_side_stream(stream):
-    """A model's second compute stream (chunk pipelines): consumers of the gradient buffer that
-    launch work mid-backward (DataParallel buckets) order themselves after it."""
-    if stream is not None and all(stream != s for s in _SIDE_STREAMS):
-        _SIDE_STREAMS.append(stream)
-
-
-def wait_side_streams():
-    """Make the current stream wait for every registered side stream (no-op when none)."""
-    if _SIDE_STREAMS:
-        cur = torch.cuda.current_stream()
-        for s in _SIDE_STREAMS:
-            cur.wait_stream(s)
-
-
-def _order_before(p, t):
-    if not is_multi_stream(p) or not t.is_cuda:
-        return None
-    cur = torch.cuda.current_stream(t.device)
-    ev = getattr(p, "_spa_ev", None)
-    if ev is not None and getattr(p, "_spa_stream", None) != cur:
-        cur.wait_event(ev)
-    return cur
-
-
-def _order_after(p, cur):
-    if cur is None:
-        return
-    ev = torch.cuda.Event()
-    ev.record(cur)
-    p._spa_ev, p._spa_stream = ev, cur
-
-
 def commit(p: torch.Tensor, compute: Callable[[Optional[torch.Tensor], bool], Optional[torch.Tensor]]):
     """Commit a parameter gradient.
 
@@ -85,13 +33,11 @@ def commit(p: torch.Tensor, compute: Callable[[Optional[torch.Tensor], bool], Op
     mg = getattr(p, "main_grad", None)
     if mg is None:
         return compute(None, False)
-    cur = _order_before(p, mg)
     if getattr(p, "_spa_gen", -1) != _Gen.value:
         compute(mg, False)
         p._spa_gen = _Gen.value
     else:
         compute(mg, True)
-    _order_after(p, cur)
     return None
 
 
@@ -100,8 +46,7 @@ def direct_out(p: torch.Tensor):
     with p's dtype, claim it and return it so a kernel can write the gradient
     straight into it (no temporary + copy). Returns None otherwise."""
     mg = getattr(p, "main_grad", None)
-    if mg is None or getattr(p, "_spa_gen", -1) == _Gen.value or mg.dtype != p.dtype or not mg.is_contiguous() \
-            or is_multi_stream(p):
+    if mg is None or getattr(p, "_spa_gen", -1) == _Gen.value or mg.dtype != p.dtype or not mg.is_contiguous():
         return None
     p._spa_gen = _Gen.value
     return mg
@@ -112,7 +57,7 @@ def claim_main_grad(p: torch.Tensor):
     ``(main_grad, accumulate)`` -- accumulate is False on the first commit of this iteration --
     and marks the commit, or None when ``p`` has no contiguous main_grad of its own dtype."""
     mg = getattr(p, "main_grad", None)
-    if mg is None or mg.dtype != p.dtype or not mg.is_contiguous() or is_multi_stream(p):
+    if mg is None or mg.dtype != p.dtype or not mg.is_contiguous():
         return None
     accumulate = getattr(p, "_spa_gen", -1) == _Gen.value
     p._spa_gen = _Gen.value
