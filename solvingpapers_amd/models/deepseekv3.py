@@ -340,20 +340,19 @@ class MoE(tnn.Module):
     """DeepSeekMoE: shared experts + top-k routed experts with aux-free load balancing.
     Under EP (``ep_group`` of size P) this rank holds experts [r*E/P, (r+1)*E/P)."""
 
-    def __init__(self, c: DSV3Config, ep_group=None, ep_chunks=1, **fk):
+    def __init__(self, c: DSV3Config, ep_group=None, **fk):
         """One forward is four stages (expert_parallel.EPStage): prepare (routing, count exchange,
         fp8 payload) -> shared expert -> dispatch (the one host sync; the all-to-all starts right
         after the payload, so the shared expert queued before the sync runs beside it) -> experts +
         combine. DeepSeekV3.forward_pair interleaves the stages of two micro-batches so every
-        exchange also overlaps the other micro-batch's attention / experts. ``ep_chunks > 1``
-        instead splits this layer's tokens into chunks whose exchanges overlap each other's experts
-        (fewer rows per expert: measured slower, kept for comparison)."""
+        exchange also overlaps the other micro-batch's attention / experts. (Splitting one layer's
+        tokens into chunks instead cost grouped-GEMM efficiency -- fewer rows per expert -- and
+        was removed in round 4.)"""
         super().__init__()
         from ..parallel.expert_parallel import ep_rank_size
         self.c = c
         self.ep_group = ep_group
         self.ep_rank, self.ep = ep_rank_size(ep_group)
-        self.ep_chunks = int(ep_chunks) if self.ep > 1 else 1
         assert c.n_experts % self.ep == 0
         El = c.n_experts // self.ep
         D, F = c.dim, c.ffn_hidden
@@ -447,32 +446,11 @@ class MoE(tnn.Module):
     def forward(self, x):
         B, T, D = x.shape
         x2 = x.reshape(-1, D)
-        if self.ep_chunks > 1 and x2.shape[0] >= self.ep_chunks:
-            return self._forward_chunked(x2).view(B, T, D)
         st = self.stage_prepare(x2)
         self.stage_shared(st)                   # queued before the dispatch's host sync
         self.stage_dispatch(st)
         self.stage_experts(st)
         return self.stage_finish(st).view(B, T, D)
-
-    def _forward_chunked(self, x2):
-        """``ep_chunks`` token chunks of this layer, one stream (expert_parallel.ep_run_interleaved)."""
-        from ..parallel.expert_parallel import ep_run_interleaved
-        c = self.c
-        self.finish_pending()
-        parts = torch.tensor_split(x2, self.ep_chunks)
-        idxs, ws = [], []
-        for xp in parts:
-            idx, w = route(self._logits(xp), c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
-            idxs.append(idx)
-            ws.append(w)
-        ys = ep_run_interleaved(parts, idxs, ws, self.w13, self.w2, c.n_experts, self.ep_group, fp8=self._fp8(x2),
-                                shared=self.shared)
-        self.last_counts = None
-        if c.aux_free and self.training:
-            for idx, w in zip(idxs, ws):
-                self._update_bias(idx, w, None)
-        return torch.cat(ys)
 
     @torch.no_grad()
     def _update_bias(self, idx, w, plan):

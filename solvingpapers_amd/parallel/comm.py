@@ -34,20 +34,11 @@ import torch.distributed as dist
 PROXY_AR_BUSBW_GBPS = 300.0
 PROXY_A2A_GBPS = 300.0
 
-# Stream priorities of the two-chunk pipelines (models/gemma.py, models/deepseekv3.py) and of
-# the TP / EP collective streams (RCCL is_high_priority_stream; the proxy's comm stream). The
-# idea: the chunk running ahead keeps its lead instead of sharing the chip evenly with the one
-# behind (lockstep makes both chunks' collectives coincide). Measured on the 1-GPU proxy
-# (profiles/r3_overlap_proxy_priorities.jsonl): TP hidden 0.30 -> 0.35, but the EP layer's
-# two-stream compute slowed 15 % and its overlap vanished, so both default to normal (0);
-# SPA_SIDE_PRIO=-1 / SPA_COMM_PRIO=-1 select high priority.
-SIDE_PRIORITY = int(os.environ.get("SPA_SIDE_PRIO", "0"))
+# Stream priority of the TP / EP collective streams (RCCL is_high_priority_stream; the proxy's
+# comm stream). Measured with round 3's two-stream pipelines on the 1-GPU proxy
+# (profiles/r3_overlap_proxy_priorities.jsonl): high priority helped TP (hidden 0.30 -> 0.35) but
+# slowed the EP layer's compute 15 %, so it defaults to normal (0); SPA_COMM_PRIO=-1 selects high.
 COMM_PRIORITY = int(os.environ.get("SPA_COMM_PRIO", "0"))
-
-
-def side_stream(device):
-    """The second compute stream of a two-chunk pipeline (priority SIDE_PRIORITY)."""
-    return torch.cuda.Stream(device, priority=SIDE_PRIORITY)
 
 
 class ProxyGroup:
@@ -418,5 +409,5 @@ def grad_ar_finish(handle):
     return _GradARFinish.apply(y, box)
 
 
-__all__ = ["launch_stream", "alloc_for_launch", "grad_ar_start", "grad_ar_finish", "ProxyGroup", "side_stream", "SIDE_PRIORITY", "COMM_PRIORITY", "is_proxy", "group_rank_size", "backend", "all_reduce", "all_to_all_single",
+__all__ = ["launch_stream", "alloc_for_launch", "grad_ar_start", "grad_ar_finish", "ProxyGroup", "COMM_PRIORITY", "is_proxy", "group_rank_size", "backend", "all_reduce", "all_to_all_single",
            "all_to_all_counts", "a2a_start", "a2a_finish", "a2a", "ar_start", "ar_finish"]

@@ -299,30 +299,6 @@ def ep_run(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     return ep_stage_finish(st), plan
 
 
-def ep_run_interleaved(parts, idxs, ws, W13, W2, n_experts, group, act="silu", fp8=False, shared=None):
-    """Token chunks of ONE MoE layer, their exchanges interleaved on one compute stream:
-    prepare all | shared(chunk 0) | dispatch all | for c: experts(c) | shared(others) | finish all.
-    Splitting a layer's tokens costs grouped-GEMM efficiency (fewer rows per expert), so the model
-    overlaps micro-batches instead (DeepSeekV3.forward_pair); kept for ``ep_chunks > 1``."""
-    n = len(parts)
-    sts = [ep_stage_prepare(parts[i], idxs[i], ws[i], n_experts, group, fp8, W13) for i in range(n)]
-    sh = [None] * n
-    if shared is not None:
-        sh[0] = shared(parts[0])                             # queued before the first host sync
-    for st in sts:
-        ep_stage_dispatch(st)
-    for st in sts:
-        ep_stage_experts(st, W13, W2, act)
-    if shared is not None:
-        for i in range(1, n):
-            sh[i] = shared(parts[i])
-    out = []
-    for i, st in enumerate(sts):
-        y = ep_stage_finish(st)
-        out.append(y + sh[i] if sh[i] is not None else y)
-    return out
-
-
 def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
     """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
     [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
