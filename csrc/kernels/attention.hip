@@ -1048,252 +1048,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// Backward dK/dV with paired waves (HD <= 128): 8 waves = 4 pairs x 32 keys (128 keys per
-// block); key on the lane. Splitting the four products of a key column over two waves
-// halves each wave's live registers (one of K/V fragments, one of dK^T/dV^T), which puts
-// two waves on every SIMD (one wave per SIMD in the single-wave kernel above), and the
-// two roles' matrix and vector work interleave on the SIMD:
-//   role A (waves 0-3):  S = Q K^T -> P = exp2(S c - lse2) -> P to LDS (fp32);  | dV^T += dO^T P
-//   role B (waves 4-7):  dP = dO V^T - delta (kept in registers)                | dS = P dP; dK^T += Q^T dS
-// '|' is a block barrier: phase 1 = the left column, phase 2 = the right column, so the
-// pair's P crosses LDS once per 32x32 sub-tile ([pair][t][j][lane][4] fp32 image,
-// conflict-free 16-byte rows). Q / dO tiles of 64 rows are double-buffered as before.
-// ---------------------------------------------------------------------------
-template <int HDK, int HDV, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(512) void attn_bwd_dkdv2_kernel(AttnParams p) {
-  constexpr int MT = 2, BMQ = 32 * MT, BNK = 128, KSK = HDK / 16, KSV = HDV / 16, DTK = HDK / 32;
-  constexpr int DTV = HDV / 32, NT = 512, IK = img_w<HDK>(), IV = img_w<HDV>();
-  constexpr int TQ = BMQ * IK, TD = BMQ * IV, TB = TQ + TD;
-  constexpr int KSX = KSK > KSV ? KSK : KSV, DTX = DTK > DTV ? DTK : DTV;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TB];                 // [buf][Q|dO]
-  __shared__ __attribute__((aligned(16))) float pimg[4 * MT * 4 * 64 * 4];  // [pair][t][j][lane][4]
-  __shared__ __attribute__((aligned(16))) float rowc[2][2 * BMQ];           // [buf][-lse2 | -delta]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pair = wave & 3, role = wave >> 2;
-  const int lk = lane & 31, hh = lane >> 5;
-  const int nbh = p.Hkv * p.B;
-  const int bh = blockIdx.x % nbh;
-  const int rest = blockIdx.x / nbh;             // causal: low key blocks are heaviest, launched first
-  const int split = rest % p.hsplit, kb = rest / p.hsplit;
-  const int hk = bh % p.Hkv, b = bh / p.Hkv;
-  const int Gs = p.H / p.Hkv / p.hsplit;         // q-heads handled by this block
-  const int h0 = hk * (p.H / p.Hkv) + split * Gs;
-  const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + pair * 32);
-  const int key = kw0 + lk;
-  const bool kvalid = key < p.Tk;
-  const float c = p.scale_log2;
-
-  bf16x8 xf[KSX];  // A: K fragments (KSK), B: V fragments (KSV) of this lane's key
-  {
-    const bf16* xp = role == 0 ? p.k + b * p.skb + (long)key * p.skt + hk * p.skh + 8 * hh
-                               : p.v + b * p.svb + (long)key * p.svt + hk * p.svh + 8 * hh;
-    const int ks_n = role == 0 ? KSK : KSV;
-#pragma unroll
-    for (int s = 0; s < KSX; ++s)
-      xf[s] = (kvalid && s < ks_n) ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
-  }
-  f32x16 acc[DTX];  // A: dV^T (DTV tiles), B: dK^T (DTK tiles)
-#pragma unroll
-  for (int i = 0; i < DTX; ++i) acc[i] = splat16(0.f);
-
-  int qstart = 0, wave_qstart = 0;
-  if (CAUSAL) {
-    qstart = max(0, kb * BNK - p.causal_off);
-    wave_qstart = max(0, kw0 - p.causal_off);
-  }
-  const int t0 = qstart / BMQ;
-  const int ntq = p.Tq > 0 ? cdiv(p.Tq, BMQ) : 0;
-  const int nper = ntq - t0 > 0 ? ntq - t0 : 0;
-  const int total = nper * Gs;
-  TileLoader<HDK, BMQ, NT> lq_;
-  TileLoader<HDV, BMQ, NT> ld_;
-  lq_.init(p.sqt, tid);
-  ld_.init(p.sdot, tid);
-  float rl = 0.f, rd = 0.f;   // raw row constants, transformed at commit (see the kernel above)
-  bool rv = false;
-  auto fetch = [&](int it) {
-    const int h = h0 + it / nper;
-    const int qq0 = (t0 + it % nper) * BMQ;
-    lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq);
-    ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq);
-    if (tid < BMQ) {
-      const int qq = qq0 + tid;
-      const long rbase = ((long)b * p.H + h) * p.Tq;
-      rv = qq < p.Tq;
-      const long r = rbase + min(qq, p.Tq - 1);
-      rl = p.lse_in[r];
-      rd = p.delta[r];
-    }
-  };
-  auto commit_tile = [&](int buf) {
-    lq_.store(smem + buf * TB);
-    ld_.store(smem + buf * TB + TQ);
-    if (tid < BMQ) {
-      rowc[buf][tid] = rv ? -rl * 1.4426950408889634f : -INFINITY;
-      rowc[buf][BMQ + tid] = rv ? -rd : 0.f;
-    }
-  };
-  if (total > 0) {
-    fetch(0);
-    commit_tile(0);
-    if (total > 1) fetch(1);
-  }
-  __syncthreads();
-  LdsOff<IK> offk;
-  LdsOff<IV> offv;
-  offk.init(lane);
-  offv.init(lane);
-  float* pme = pimg + pair * (MT * 4 * 64 * 4) + lane * 4;  // + (t*4 + j) * 256
-  long long seg[5] = {0, 0, 0, 0, 0};
-  const bool stamp = p.stamp != nullptr;
-  auto tick = [&]() -> long long { return stamp ? (long long)__builtin_amdgcn_s_memtime() : 0LL; };
-  auto body = [&](const int it, auto bufc) {
-    constexpr int BUF = decltype(bufc)::value;
-    const int qq0 = (t0 + it % nper) * BMQ;
-    const bf16* Qs = smem + BUF * TB;
-    const bf16* Ds = Qs + TQ;
-    const float* rc = rowc[BUF];
-    long long ts = tick();
-    if (it + 1 < total) {
-      commit_tile(1 - BUF);
-      if (it + 2 < total) fetch(it + 2);
-    }
-    if (stamp) { const long long tn = tick(); seg[0] += tn - ts; ts = tn; }
-    const bool active = kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
-    unsigned dbase = 0;
-    if constexpr (DROP) dbase = drop_base(p, b, h0 + it / nper);
-    bf16x8 pk[2 * MT];  // A: packed P (dropped) of both sub-tiles (kept over the barrier)
-    f32x16 dp[MT];      // B: dP - delta of both sub-tiles (kept over the barrier)
-    // ---- phase 1
-    if (active) {
-      if (role == 0) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          f32x16 s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[0]), xf[0], splat16(0.f));
-#pragma unroll
-          for (int ks = 1; ks < KSK; ++ks) s = mfma32(ld_row(Qs + 32 * t * IK, offk.row[ks]), xf[ks], s);
-          const int qt0 = qq0 + 32 * t;
-          if (CAUSAL && qt0 + p.causal_off < kw0 + 31) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              if (key > qt0 + 8 * (r >> 2) + 4 * hh + (r & 3) + p.causal_off) s[r] = -INFINITY;
-          }
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 lv = *reinterpret_cast<const f32x4*>(rc + 32 * t + 8 * g + 4 * hh);
-            f32x4 pv;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              pv[i] = fexp2(fmaf(s[4 * g + i], c, lv[i]));  // rows >= Tq: -lse2 = -inf -> 0
-              s[4 * g + i] = pv[i];
-              if constexpr (DROP)
-                s[4 * g + i] = drop_keep(dbase, qt0 + 8 * g + 4 * hh + i, key, p.drop_thr) ? pv[i] * p.drop_scale
-                                                                                            : 0.f;
-            }
-            *reinterpret_cast<f32x4*>(pme + (t * 4 + g) * 256) = pv;   // undropped P for role B
-          }
-          pk[2 * t] = pack_acc(s, 0);
-          pk[2 * t + 1] = pack_acc(s, 1);
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dp[t][4 * g + i] = DROP ? 0.f : dv[i];
-          }
-#pragma unroll
-          for (int ks = 0; ks < KSV; ++ks) dp[t] = mfma32(ld_row(Ds + 32 * t * IV, offv.row[ks]), xf[ks], dp[t]);
-          if constexpr (DROP) {
-            const int qt0 = qq0 + 32 * t;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const f32x4 dv = *reinterpret_cast<const f32x4*>(rc + BMQ + 32 * t + 8 * g + 4 * hh);
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int r = 4 * g + i;
-                dp[t][r] = (drop_keep(dbase, qt0 + 8 * g + 4 * hh + i, key, p.drop_thr) ? dp[t][r] * p.drop_scale
-                                                                                         : 0.f) + dv[i];
-              }
-            }
-          }
-        }
-      }
-    }
-    if (stamp) { const long long tn = tick(); seg[1] += tn - ts; ts = tn; }
-    __syncthreads();  // P images complete
-    if (stamp) { const long long tn = tick(); seg[2] += tn - ts; ts = tn; }
-    // ---- phase 2
-    if (active) {
-      if (role == 0) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-          for (int dt = 0; dt < DTV; ++dt) {
-            acc[dt] = mfma32(ld_tr(Ds + 32 * t * IV, offv.tra[dt], offv.trb[dt]), pk[2 * t], acc[dt]);
-            acc[dt] = mfma32(ld_tr(Ds + (32 * t + 16) * IV, offv.tra[dt], offv.trb[dt]), pk[2 * t + 1], acc[dt]);
-          }
-      } else {
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          f32x16 ds;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 pv = *reinterpret_cast<const f32x4*>(pme + (t * 4 + g) * 256);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ds[4 * g + i] = pv[i] * dp[t][4 * g + i];
-          }
-          const bf16x8 sa = pack_acc(ds, 0), sb = pack_acc(ds, 1);
-#pragma unroll
-          for (int dt = 0; dt < DTK; ++dt) {
-            acc[dt] = mfma32(ld_tr(Qs + 32 * t * IK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
-            acc[dt] = mfma32(ld_tr(Qs + (32 * t + 16) * IK, offk.tra[dt], offk.trb[dt]), sb, acc[dt]);
-          }
-        }
-      }
-    }
-    if (stamp) { const long long tn = tick(); seg[3] += tn - ts; ts = tn; }
-    __syncthreads();
-    if (stamp) { const long long tn = tick(); seg[4] += tn - ts; }
-  };
-  for (int it = 0; it < total; it += 2) {
-    body(it, IC<0>{});
-    if (it + 1 < total) body(it + 1, IC<1>{});
-  }
-  if (stamp && lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) p.stamp[((long)blockIdx.x * 8 + wave) * 8 + i] = seg[i];
-    p.stamp[((long)blockIdx.x * 8 + wave) * 8 + 5] = total;
-  }
-  if constexpr (HDK == HDV) {
-    store_kv_grad<HDK>(p, acc, role == 1, b, hk, key, split, hh);
-  } else {
-    if (role == 1) {
-      f32x16 ak[DTK];
-#pragma unroll
-      for (int i = 0; i < DTK; ++i) ak[i] = acc[i];
-      store_kv_grad<HDK>(p, ak, true, b, hk, key, split, hh);
-    } else {
-      f32x16 av[DTV];
-#pragma unroll
-      for (int i = 0; i < DTV; ++i) av[i] = acc[i];
-      store_kv_grad<HDV>(p, av, false, b, hk, key, split, hh);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Backward dK/dV, paired waves, software-pipelined (HD <= 128, no dropout). Same pairing as
-// dkdv2 (role A holds K and dV^T, role B holds V and dK^T of the pair's 32 keys), but role A
-// produces P one interval ahead of its consumers, so every interval has ONE block barrier and
-// the same MFMA count per role:
+// Backward dK/dV, paired waves, software-pipelined (no dropout): 8 waves = 4 pairs x 32 keys (128
+// keys per block), key on the lane. Splitting the four products of a key column over two waves
+// halves each wave's live registers, which puts two waves on every SIMD: role A holds K and dV^T,
+// role B holds V and dK^T of the pair's 32 keys, and role A produces P one interval ahead of its
+// consumers, so every interval has ONE block barrier and the same MFMA count per role:
 //   interval k, role A:  dV^T += dO(k-1)^T P(k-1)          |  S(k) = Q(k) K^T -> P(k) -> LDS
 //   interval k, role B:  dP(k-1) = dO(k-1) V^T - delta;  dS = P(k-1) dP(k-1);  dK^T += Q(k-1)^T dS
-// (dkdv2 runs both roles in two phases with a barrier each; s_memtime stamps showed each role
-// idle about a third of the time at those barriers: profiles/r2_attn_dkdv_stamps.txt). Nothing
+// (a two-phase variant with a barrier per role left each role idle about a third of the time at
+// those barriers by s_memtime stamps, profiles/r2_attn_dkdv_stamps.txt, and was removed). Nothing
 // but the accumulators is carried across intervals: P travels through a 2-deep bf16 LDS ring
 // in MFMA-operand order (role A re-reads its own P for dV). Q / dO tiles live in a 3-deep LDS
 // ring (tiles k-1 and k are read while k+1 is committed); lse / delta travel with their tile.
@@ -2342,17 +2105,11 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
     attn_dq_reduce_kernel<HDK><<<(int)cdiv(n, 256L), 256, 0, st>>>(p);
   }
   if (p.Tk == 0) return;
-  const bool paired = PAIRED_OK && dkdv_mode == 2;
   const bool piped = PAIRED_OK && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
   if (piped) {
     if constexpr (PAIRED_OK) {
       if (causal) attn_bwd_dkdv3_kernel<HDK, HDV, true><<<g2, 512, 0, st>>>(p);
       else attn_bwd_dkdv3_kernel<HDK, HDV, false><<<g2, 512, 0, st>>>(p);
-    }
-  } else if (paired) {
-    if constexpr (PAIRED_OK) {
-      if (causal) attn_bwd_dkdv2_kernel<HDK, HDV, true, DROP><<<g2, 512, 0, st>>>(p);
-      else attn_bwd_dkdv2_kernel<HDK, HDV, false, DROP><<<g2, 512, 0, st>>>(p);
     }
   } else {
     if (causal) attn_bwd_dkdv_kernel<HDK, HDV, true, MT, false, DROP><<<g2, 256, 0, st>>>(p);
@@ -2435,12 +2192,12 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   // dK/dV grid: key blocks x kv-heads x batch, times a q-head split when that grid cannot
   // fill the chip (MQA: Hkv = 1 launched 32 blocks at T = 4096); partials are summed by
   // attn_kv_reduce_kernel. dK/dV kernel: software-pipelined paired-wave (3) for v head dim
-  // 128, single-wave (1) else; the two-phase paired kernel (2) stays selectable.
-  // SPA_ATTN_DKDV overrides (read per call, so one process can A/B them). Measured on
-  // MI355X (rocprofv3, LLaMA3-8B shape B1 T8192 H32/8 hd128 causal): dK/dV kernel 1.31 ms
-  // pipelined vs 1.46 ms two-phase (whole bwd 2.22 ms two-phase vs 2.45 ms single-wave);
-  // ViT-B hd 64 (T 197, B 64) whole bwd 0.113 pipelined / 0.121 two-phase / 0.097-0.103
-  // single-wave.
+  // 128, single-wave (1) else.
+  // SPA_ATTN_DKDV overrides (1 single-wave, 3 pipelined; read per call, so one process can
+  // A/B them). Measured on MI355X (rocprofv3, LLaMA3-8B shape B1 T8192 H32/8 hd128 causal):
+  // dK/dV kernel 1.31 ms pipelined vs 1.46 ms for the removed two-phase paired kernel (whole
+  // bwd 2.22 ms two-phase vs 2.45 ms single-wave); ViT-B hd 64 (T 197, B 64) whole bwd 0.113
+  // pipelined / 0.097-0.103 single-wave.
   const int dkdv_mode = getenv("SPA_ATTN_DKDV") ? atoi(getenv("SPA_ATTN_DKDV")) : 0;
   const int G = H / Hkv;
   const int nkv = cdiv(Tk, 128) * Hkv * B;
@@ -2453,8 +2210,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
     }
   // the single-wave dK/dV kernel splits the (q-head, q-tile) iterations of a kv-head in any
   // number of shares: past the q-heads (TP-sharded MQA: G = 2), split the q-tiles too
-  const bool pairedk = HDK == HDV && HDK <= 128 && !drop &&
-                       (dkdv_mode == 2 || dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
+  const bool pairedk = HDK == HDV && HDK <= 128 && !drop && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
   if (!fused && !pairedk)
     while (nkv * hsplit < 512 && hsplit < 16 && cdiv(Tq, 32) / (2 * hsplit) >= 4) hsplit *= 2;
   p.hsplit = hsplit;
