@@ -25,6 +25,7 @@
 #   attn-quick     attention GPU tests, packed-layout ABBA vs the dq kernel, per-kernel times
 #   ep-pair        micro-batch-pair EP overlap: MoE GPU tests, EP=8 proxy, dsv3_style pairs vs one-by-one ABBA
 #   headline-ab ENV  bench.py default vs ENV=VAL, separate processes in ABBA order
+#   headline-args A  bench.py default vs extra bench.py arguments A, ABBA
 #   attn-pmc       attention counters + clocks in the headline step (4 layers) and in isolation; GEMM-interleaved timing
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 set -o pipefail
@@ -130,6 +131,14 @@ headline-ab)
     if [ $arm = var ]; then run 400 ${O}_$arm.log env $ab python -u bench.py --steps 6 --warmup 2
     else run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2; fi
     echo "$arm $ab $(grep -ho '"value": [0-9.]*' ${O}_$arm.log)"
+  done ;;
+headline-args)
+  # headline bench.py default vs extra bench.py arguments, ABBA: headline-args "--mb 2 --accum 2"
+  extra=${1:?bench args}
+  for arm in base var var base; do
+    if [ $arm = var ]; then run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2 $extra
+    else run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2; fi
+    echo "$arm $extra $(grep -ho '"value": [0-9.]*\|"mem_gb": [0-9.]*' ${O}_$arm.log | tr '\n' ' ')"
   done ;;
 attn-pmc)
   run 200 ${O}_il.log python -u tools/bench_attn.py --iters 20 --interleave
