@@ -1064,6 +1064,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 #ifndef DKDV3_SCHED
 #define DKDV3_SCHED 0   // 1: chain_sched hints (no effect at 256 VGPRs: one operand register quad; kept for experiments)
 #endif
+// SPA_DKDV3_STAMP=1 (a profiling build, never the shipped one: each s_memtime read drains the
+// LDS counter): per-wave s_memtime segment sums of the interval loop into p.stamp when the host
+// sets it (SPA_ATTN_STAMP=1), [blocks * 8 waves, 8] int64: staging, compute 1 (A: dV^T; B: dP,
+// dS), compute 2 (A: S -> P; B: dK^T), barrier wait, epilogue, intervals, whole wave, 0
+#ifndef SPA_DKDV3_STAMP
+#define SPA_DKDV3_STAMP 0
+#endif
+#if SPA_DKDV3_STAMP
+#define DK3_TICK(i)                                                   \
+  do {                                                                \
+    const long long tn_ = (long long)__builtin_amdgcn_s_memtime();    \
+    seg[i] += tn_ - ts_;                                              \
+    ts_ = tn_;                                                        \
+  } while (0)
+#else
+#define DK3_TICK(i) \
+  do {              \
+  } while (0)
+#endif
 // DSOUT: role B also stores the bf16 dS of each live 32 x 32 block to p.dsbuf (ds_slot layout),
 // the operand of the separate dQ = dS K pass (attn_bwd_dq_ds_kernel) that replaces the dq
 // kernel's recomputation of S and dP.
@@ -1095,6 +1114,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   const int key = kw0 + (lane & 31);
   const bool kvalid = key < p.Tk;
   const float c = p.scale_log2;
+#if SPA_DKDV3_STAMP
+  long long seg[5] = {0, 0, 0, 0, 0};
+  const long long t_start = (long long)__builtin_amdgcn_s_memtime();
+  long long ts_ = t_start;
+#endif
 
   bf16x8 xf[KSX];  // A: K fragments (KSK), B: V fragments (KSV) of this lane's key
   {
@@ -1123,12 +1147,15 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   ld_.init(p.sdot, tid);
   float rl = 0.f, rd = 0.f;   // raw row constants of the prefetched tile (transformed at commit)
   bool rv = false;
-  auto fetch = [&](int it) {
+  // the row constants are loaded and committed by threads tid < BMQ (role A's wave 0); ROWS = 0
+  // leaves them out of role B's copy of the loop entirely, so no rl / rd load is pending there
+  // (one was, in a register hipcc reused: a vmcnt(0) before role B's first dP MFMA)
+  auto fetch = [&](int it, auto rowsc) {
     const int h = h0 + it / nper;
     const int qq0 = (t0 + it % nper) * BMQ;
     lq_.load(p.q + b * p.sqb + h * p.sqh, p.sqt, qq0, p.Tq);
     ld_.load(p.dout + b * p.sdob + h * p.sdoh, p.sdot, qq0, p.Tq);
-    if (tid < BMQ) {
+    if (decltype(rowsc)::value && tid < BMQ) {
       const int qq = qq0 + tid;
       const long r = ((long)b * p.H + h) * p.Tq + min(qq, p.Tq - 1);
       rv = qq < p.Tq;
@@ -1136,10 +1163,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
       rd = p.delta[r];
     }
   };
-  auto commit_tile = [&](int slot) {
+  auto commit_tile = [&](int slot, auto rowsc) {
     lq_.store(smem + slot * TB);
     ld_.store(smem + slot * TB + TQ);
-    if (tid < BMQ) {
+    if (decltype(rowsc)::value && tid < BMQ) {
       rowc[slot][tid] = rv ? -rl * 1.4426950408889634f : -INFINITY;
       rowc[slot][BMQ + tid] = rv ? -rd : 0.f;
     }
@@ -1149,9 +1176,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
     return kw0 < p.Tk && !(CAUSAL && qq0 + BMQ - 1 < wave_qstart);
   };
   if (total > 0) {
-    fetch(0);
-    commit_tile(0);
-    if (total > 1) fetch(1);
+    fetch(0, IC<1>{});
+    commit_tile(0, IC<1>{});
+    if (total > 1) fetch(1, IC<1>{});
   }
   __syncthreads();
   LdsOff<IWK> offk;   // Q image
@@ -1167,10 +1194,12 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   auto interval = [&](const int k, auto slotc, auto rolec) {
     constexpr int SC = decltype(slotc)::value, SP = (SC + 2) % 3;
     constexpr int ROLE = decltype(rolec)::value;
-    if (k + 1 < total) {
-      commit_tile((SC + 1) % 3);
-      if (k + 2 < total) fetch(k + 2);
-    }
+    // unconditional staging (past the end: the slot of tile k - 2, no longer read, and a re-fetch
+    // of the last tile): a conditional prefetch made hipcc merge the load registers through
+    // copies that waited vmcnt(0) right behind the loads
+    commit_tile((SC + 1) % 3, IC<ROLE == 0>{});
+    fetch(min(k + 2, total - 1), IC<ROLE == 0>{});
+    DK3_TICK(0);
     const bool cur = k < total && tile_active(k);
     const bf16* Qc = smem + SC * TB;
     const bf16* Qp = smem + SP * TB;
@@ -1191,6 +1220,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      DK3_TICK(1);
       if (cur) {                                         // S(k) -> P(k) -> LDS slot k & 1
         const int qq0 = (t0 + k % nper) * BMQ;
         const float* rc = rowc[SC];
@@ -1219,10 +1249,12 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      DK3_TICK(2);
     } else {
       if (!prev_act) {
         prev_act = cur;
         __syncthreads();
+        DK3_TICK(3);
         return;
       }
       // tile k-1: dP, dS, dK^T
@@ -1268,6 +1300,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        DK3_TICK(1);
 #pragma unroll
         for (int dt = 0; dt < DTK; ++dt) {
           acc[dt] = mfma32(ld_tr(Qp + 32 * t * IWK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
@@ -1275,11 +1308,18 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
         }
         if (DKDV3_SCHED) chain_sched<2 * DTK, 2, 2, 2>();  // + the P(k-1) reads
         __builtin_amdgcn_sched_barrier(0);
+        DK3_TICK(2);
       }
     }
     prev_act = cur;
     __syncthreads();
+    DK3_TICK(3);
   };
+  // as in the forward: the prefetch is conditional, so hipcc could not count the fragment loads
+  // of the prologue past it and waited vmcnt(0) -- the Q / dO prefetch just issued -- before
+  // role A's first S MFMA of every interval; an empty asm using the fragments waits for them here, once
+#pragma unroll
+  for (int s = 0; s < KSX; ++s) asm volatile("" ::"v"(xf[s]));
   if (role == 0) {
     for (int k = 0; k <= total; k += 3) {
       interval(k, IC<0>{}, IC<0>{});
@@ -1308,6 +1348,16 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
       store_kv_grad<HDV>(p, av, false, b, hk, key, split, hh);
     }
   }
+#if SPA_DKDV3_STAMP
+  DK3_TICK(4);
+  if (p.stamp != nullptr && lane < 8) {   // one value per lane: vector stores
+    long long v = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) v = lane == i ? seg[i] : v;
+    v = lane == 5 ? (long long)(total + 1) : lane == 6 ? ts_ - t_start : v;
+    p.stamp[((long)blockIdx.x * 8 + wave) * 8 + lane] = v;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2126,8 +2176,8 @@ static at::Tensor& last_stamps() {
   static at::Tensor t;
   return t;
 }
-// profiling: the segment sums of the last SPA_ATTN_STAMP backward ([blocks * 8 waves, 8] int64:
-// staging, phase-1 issue, barrier-1 wait, phase-2 issue, barrier-2 wait, iterations)
+// profiling: the segment sums of the last SPA_ATTN_STAMP backward ([blocks * 8 waves, 8] int64,
+// columns as listed at SPA_DKDV3_STAMP)
 at::Tensor attn_bwd_stamps() { return last_stamps().defined() ? last_stamps().view({-1, 8}).clone() : at::Tensor(); }
 
 // Gradients written into dq/dk/dv (strided views allowed, e.g. slices of one dqkv buffer).
@@ -2214,8 +2264,9 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   if (!fused && !pairedk)
     while (nkv * hsplit < 512 && hsplit < 16 && cdiv(Tq, 32) / (2 * hsplit) >= 4) hsplit *= 2;
   p.hsplit = hsplit;
-  // SPA_ATTN_STAMP=1: per-wave s_memtime segment sums of the paired dK/dV loop, kept in a
-  // process-global buffer the profiling tool reads back (attn_bwd_stamps)
+  // SPA_ATTN_STAMP=1: per-wave s_memtime segment sums of the pipelined dK/dV loop (in a build
+  // with -DSPA_DKDV3_STAMP=1, tools/build_variant.sh), kept in a process-global buffer the
+  // profiling tool reads back (attn_bwd_stamps)
   static at::Tensor stamps;
   const char* se = getenv("SPA_ATTN_STAMP");
   if (se && atoi(se) != 0) {

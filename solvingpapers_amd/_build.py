@@ -25,6 +25,13 @@ CSRC = ROOT / "csrc"
 BUILD = ROOT / "build"
 OUT = PKG / "_C.so"
 ARCH = os.environ.get("SPA_OFFLOAD_ARCH", "gfx950")
+# variant builds for kernel A/B and profiling (tools/build_variant.sh): SPA_BUILD_VARIANT=name puts
+# objects under build/name and the library at ab/_C_name.so (loaded through SPA_EXT_SO),
+# SPA_BUILD_DEFINES adds device-compile flags (e.g. -DSPA_DKDV3_STAMP=1); the in-tree _C.so is untouched
+VARIANT = os.environ.get("SPA_BUILD_VARIANT", "")
+if VARIANT:
+    BUILD = ROOT / "build" / VARIANT
+    OUT = ROOT / "ab" / f"_C_{VARIANT}.so"
 # per-file device flags (none at present; a translation unit can get its own scheduler flags here)
 EXTRA_FLAGS = {}
 
@@ -57,6 +64,8 @@ def write_ninja(debug: bool = False) -> Path:
     )
     opt = "-O0 -g" if debug else "-O3"
     dev_flags = f"{common} {opt} --offload-arch={ARCH} -munsafe-fp-atomics"
+    if VARIANT:
+        dev_flags += " " + os.environ.get("SPA_BUILD_DEFINES", "")
     host_flags = f"{common} {opt} -pthread"
     ldflags = (
         f"-shared -fPIC --offload-arch={ARCH} -L{lib} -Wl,-rpath,{lib} "
@@ -106,6 +115,8 @@ def write_ninja(debug: bool = False) -> Path:
 
 
 def build(jobs: int | None = None, debug: bool = False, verbose: bool = False) -> Path:
+    OUT.parent.mkdir(parents=True, exist_ok=True)
+    (BUILD / "obj").mkdir(parents=True, exist_ok=True)
     nf = write_ninja(debug)
     jobs = jobs or min(8, os.cpu_count() or 4, int(os.environ.get("MAX_JOBS", "16")))
     cmd = [shutil.which("ninja") or "ninja", "-f", str(nf), "-j", str(jobs)]

@@ -121,12 +121,15 @@ for setting in filter(None, a.ab.split(",")):
           f"{tb3*1e3:.3f} ms", flush=True)
 
 if os.environ.get("SPA_ATTN_STAMP"):
-    st = ops.attn_bwd_stamps().double()
-    live = st[st[:, 5] > 0]
-    seg = live[:, :5].sum(0) / live[:, 5].sum()
-    names = ["staging", "phase-1 issue", "barrier-1 wait", "phase-2 issue", "barrier-2 wait"]
-    for role, sel in (("A (S/P, dV)", (torch.arange(live.shape[0]) % 8) < 4), ("B (dP, dK)", (torch.arange(live.shape[0]) % 8) >= 4)):
-        r = live[sel]
-        per = r[:, :5].sum(0) / r[:, 5].sum()
-        print(f"   dK/dV loop, role {role}: cycles per iteration " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist()))
-              + f" | total {per.sum().item():.0f}", flush=True)
+    st = ops.attn_bwd_stamps().double().cpu()
+    # pipelined dK/dV kernel built with -DSPA_DKDV3_STAMP=1 (tools/build_variant.sh): per wave
+    # staging, compute 1, compute 2, barrier wait, epilogue, intervals, whole wave (s_memtime)
+    wave = torch.arange(st.shape[0]) % 8
+    live = st[:, 5] > 0
+    names = ["staging", "compute 1", "compute 2", "barrier wait"]
+    for role, sel in (("A (1 dV^T, 2 S->P)", wave < 4), ("B (1 dP+dS, 2 dK^T)", wave >= 4)):
+        r = st[live & sel]
+        per = r[:, :4].sum(0) / r[:, 5].sum()
+        print(f"   dK/dV loop, role {role}: cycles per interval " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist()))
+              + f" | loop {per.sum().item():.0f} | epilogue per wave {r[:, 4].mean().item():.0f}"
+              + f" | whole wave {r[:, 6].mean().item():.0f} over {r[:, 5].mean().item():.0f} intervals", flush=True)
