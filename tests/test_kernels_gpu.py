@@ -337,6 +337,31 @@ def test_adamw_matches_torch():
     assert abs(K.sqsum(grads[0]).item() - grads[0].pow(2).sum().item()) < 1e-2 * grads[0].pow(2).sum().item()
 
 
+def test_adamw_large_flat_buffer_matches_torch():
+    """> 2 x 4096 x 256 x 8 elements: the grid-stride loop's paired-chunk path (two 8-element
+    chunks per thread per iteration, non-temporal accesses) runs, then the single-chunk tail
+    (odd n: a partial last chunk)."""
+    from solvingpapers_amd.ops import optim_kernels as K
+    n = 20_000_003
+    torch.manual_seed(0)
+    p0 = torch.randn(n, device=DEV)
+    grads = [torch.randn(n, device=DEV) for _ in range(2)]
+    tp = p0.clone().requires_grad_()
+    topt = torch.optim.AdamW([tp], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    p, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    pb, master = p0.bfloat16(), p0.clone()
+    mb, vb = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    for s, g in enumerate(grads, 1):
+        tp.grad = g.clone()
+        topt.step()
+        K.adamw_(p, None, g, m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, s)
+        K.adamw_(pb, master, g.bfloat16(), mb, vb, 1e-2, 0.9, 0.95, 1e-8, 0.1, s)
+    ref = tp.detach()
+    assert (p - ref).abs().max().item() < 1e-5
+    assert rel(master, ref) < 1e-2
+    assert (pb.float() - master).abs().max().item() <= 1e-2 * master.abs().max().item()
+
+
 def test_adamw_bf16_moments_match_cpu_oracle():
     """bf16 moments (DeepSeek-V3 recipe) with an fp32 master: the HIP kernel against the CPU
     oracle doing the same rounding, and close to the fp32-moment trajectory."""

@@ -26,6 +26,7 @@
 #   ep-pair        micro-batch-pair EP overlap: MoE GPU tests, EP=8 proxy, dsv3_style pairs vs one-by-one ABBA
 #   headline-ab ENV  bench.py default vs ENV=VAL, separate processes in ABBA order
 #   headline-args A  bench.py default vs extra bench.py arguments A, ABBA
+#   ext-ab K C     in-tree build vs $BASE_SO: GPU tests -k K, bench_kernels case C, headline, B N N B
 #   attn-pmc       attention counters + clocks in the headline step (4 layers) and in isolation; GEMM-interleaved timing
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 set -o pipefail
@@ -140,6 +141,23 @@ headline-args)
     else run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2; fi
     echo "$arm $extra $(grep -ho '"value": [0-9.]*\|"mem_gb": [0-9.]*' ${O}_$arm.log | tr '\n' ' ')"
   done ;;
+ext-ab)
+  # in-tree extension (N) vs another build (B, SPA_EXT_SO=$BASE_SO): pytest -k EXPR, the
+  # bench_kernels.py case KCASE and the headline bench, each in separate processes B N N B
+  expr=${1:?pytest -k expr}; kcase=${2:?bench_kernels case}; base=${BASE_SO:-ab/_C_base.so}
+  run 300 ${O}_pytest.log python -u -m pytest tests -m gpu -k "$expr" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -1 ${O}_pytest.log
+  for arm in B N N B; do
+    if [ $arm = B ]; then export SPA_EXT_SO=$base; else unset SPA_EXT_SO; fi
+    run 120 ${O}_k.log python -u tools/bench_kernels.py --only $kcase --iters 20
+    echo "$arm $(grep -h '^{' ${O}_k.log)"
+  done
+  for arm in B N N B; do
+    if [ $arm = B ]; then export SPA_EXT_SO=$base; else unset SPA_EXT_SO; fi
+    run 400 ${O}_h.log python -u bench.py --steps 6 --warmup 2
+    echo "$arm headline $(grep -ho '"value": [0-9.]*' ${O}_h.log)"
+  done
+  unset SPA_EXT_SO ;;
 attn-pmc)
   run 200 ${O}_il.log python -u tools/bench_attn.py --iters 20 --interleave
   grep -h 'attn B\|after a GEMM' ${O}_il.log
