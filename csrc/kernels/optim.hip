@@ -17,40 +17,7 @@
 // tracked in BF16, master weights fp32) -- 20 instead of 28 bytes of HBM traffic per parameter.
 #include "spa_common.h"
 
-// SPA_ADAMW_PAIR=1 (build define): two non-temporal 8-element chunks per thread per iteration on
-// buffers past one grid sweep (> 8.4M elements); off until it measures ahead of the plain loop
-// (tools/build_variant.sh adamw_pair -DSPA_ADAMW_PAIR=1; tools/gpu_tasks.sh ext-ab)
-#ifndef SPA_ADAMW_PAIR
-#define SPA_ADAMW_PAIR 0
-#endif
-
 namespace spa {
-
-// non-temporal 8-element streaming accesses (bf16x8 or two f32x4)
-__device__ __forceinline__ void load8_nt(const bf16* p, float (&f)[8]) {
-  const bf16x8 v = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
-#pragma unroll
-  for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
-}
-__device__ __forceinline__ void load8_nt(const float* p, float (&f)[8]) {
-  const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-  const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { f[i] = a[i]; f[i + 4] = b[i]; }
-}
-__device__ __forceinline__ void store8_nt(bf16* p, const float (&f)[8]) {
-  bf16x8 v;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = (bf16)f[i];
-  __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
-}
-__device__ __forceinline__ void store8_nt(float* p, const float (&f)[8]) {
-  f32x4 a, b;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { a[i] = f[i]; b[i] = f[i + 4]; }
-  __builtin_nontemporal_store(a, reinterpret_cast<f32x4*>(p));
-  __builtin_nontemporal_store(b, reinterpret_cast<f32x4*>(p + 4));
-}
 
 template <typename PT, typename GT, bool MASTER, typename MT = float>
 __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* __restrict__ master,
@@ -71,45 +38,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(PT* __restrict__ p, float* _
   }
   const long nv = n / 8;
   const long stride = (long)gridDim.x * 256;
-  long i = blockIdx.x * 256L + threadIdx.x;
-#if SPA_ADAMW_PAIR
-  // whole 8-element chunks two at a time (chunks i and i + stride): both chunks' 7 streaming
-  // loads are in flight before either update, and every access is non-temporal (nothing here is
-  // re-read before it leaves the caches: 28 B per parameter against ~256 MB of MALL)
-  for (; i + stride < nv; i += 2 * stride) {
-    float pv[2][8], gv[2][8], mv[2][8], vv[2][8];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const long base = (i + u * stride) * 8;
-      if constexpr (MASTER) load8_nt(master + base, pv[u]); else load8_nt(p + base, pv[u]);
-      load8_nt(g + base, gv[u]);
-      load8_nt(m + base, mv[u]);
-      load8_nt(v + base, vv[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float gr = gv[u][k] * coef;
-        if (adam_l2) gr += wd * pv[u][k];
-        mv[u][k] = b1 * mv[u][k] + (1.f - b1) * gr;
-        vv[u][k] = b2 * vv[u][k] + (1.f - b2) * gr * gr;
-        const float denom = sqrtf(vv[u][k]) * inv_sqrt_bc2 + eps;
-        float pp = pv[u][k];
-        if (!adam_l2) pp *= (1.f - lr * wd);
-        pv[u][k] = pp - lr * inv_bc1 * mv[u][k] / denom;
-      }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const long base = (i + u * stride) * 8;
-      if constexpr (MASTER) store8_nt(master + base, pv[u]);
-      store8_nt(p + base, pv[u]);
-      store8_nt(m + base, mv[u]);
-      store8_nt(v + base, vv[u]);
-    }
-  }
-#endif
-  for (; i < nv + (n % 8 ? 1 : 0); i += stride) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nv + (n % 8 ? 1 : 0); i += stride) {
     const long base = i * 8;
     float pv[8], gv[8], mv[8], vv[8];
     const bool full = base + 8 <= n;

@@ -338,9 +338,8 @@ def test_adamw_matches_torch():
 
 
 def test_adamw_large_flat_buffer_matches_torch():
-    """> 2 x 4096 x 256 x 8 elements: the grid-stride loop's paired-chunk path (two 8-element
-    chunks per thread per iteration, non-temporal accesses) runs, then the single-chunk tail
-    (odd n: a partial last chunk)."""
+    """> 2 x 4096 x 256 x 8 elements: several sweeps of the capped grid-stride loop, then a
+    partial last chunk (odd n), as in the 8B-parameter buckets."""
     from solvingpapers_amd.ops import optim_kernels as K
     n = 20_000_003
     torch.manual_seed(0)
