@@ -417,6 +417,11 @@ class MoE(tnn.Module):
         idx, w = route(self._logits(x2), c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
         st = ep_stage_prepare(x2, idx, w, c.n_experts, self.ep_group, self._fp8(x2), self.w13)
         st.x2, st.idx, st.sh = x2, idx, None
+        if c.aux_free and self.training:
+            # the bias moves right after this routing (the reference updates it after every
+            # forward, deepseekv3.ipynb:1082-1086): under forward_pair micro-batch 1 then routes
+            # this layer with micro-batch 0's update applied, exactly as two forward() calls do
+            self._update_bias(idx, w, st.prep.plan)
         return st
 
     def stage_shared(self, st):
@@ -433,13 +438,11 @@ class MoE(tnn.Module):
 
     def stage_finish(self, st):
         from ..parallel.expert_parallel import ep_stage_finish
-        plan, idx, w = st.prep.plan, st.idx, st.w
+        plan = st.prep.plan
         y = ep_stage_finish(st)
         if st.sh is not None:
             y = y + st.sh
         self.last_counts = plan.counts
-        if self.c.aux_free and self.training:
-            self._update_bias(idx, w, plan)
         st.x2 = st.sh = None
         return y
 
@@ -586,6 +589,11 @@ class DeepSeekV3(tnn.Module):
     def moe_layers(self) -> List[MoE]:
         return [l.ffn for l in list(self.layers) + list(self.mtp_layers) if isinstance(l.ffn, MoE)]
 
+    def pair_overlaps(self):
+        """True when forward_pair hides something (expert-parallel exchanges). At EP 1 the pair
+        only keeps two micro-batches' activations alive, so the Trainer runs them one by one."""
+        return bool(self.training and torch.is_grad_enabled() and any(m.ep > 1 for m in self.moe_layers()))
+
     def param_groups(self):
         """Buckets: [embed], per-layer dense params, [head + MTP dense], then the expert
         buckets (kept apart so DP skips them under EP)."""
@@ -723,7 +731,9 @@ class DeepSeekV3(tnn.Module):
     def forward_pair(self, ids0, targets0, ids1, targets1):
         """loss(micro-batch 0) + loss(micro-batch 1) with the two run layer-interleaved
         (hidden_pair): the same values and gradients as two forward() calls, with each MoE
-        layer's all-to-alls overlapped by the other micro-batch's compute. Training only."""
+        layer's all-to-alls overlapped by the other micro-batch's compute. Training only.
+        Aux-free balancing keeps the sequential semantics: each MoE layer moves its routing bias
+        right after micro-batch 0's routing (MoE.stage_prepare), before micro-batch 1 routes."""
         final, x0s = self.hidden_pair(ids0, ids1)
         D = self.c.dim
         loss = None

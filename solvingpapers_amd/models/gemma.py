@@ -406,7 +406,22 @@ class Gemma(tnn.Module):
         full shape: no GEMM is split); otherwise one after the other."""
         if self.sp and self.tp_pipeline and self.training and torch.is_grad_enabled():
             return self._forward_sp_pair(None, None, "micro", parts=(ids0, ids1), tps=(t0, t1))
-        return self(ids0, t0) + self(ids1, t1)
+        # one backward covers both micro-batches and autograd finishes micro-batch 1's before it
+        # starts micro-batch 0's: a layer's DP bucket may launch only once BOTH passed its marker
+        cb = self.grad_ready_cb
+        if cb is None:
+            return self(ids0, t0) + self(ids1, t1)
+        from .deepseekv3 import _PairReady
+        self.grad_ready_cb = _PairReady(cb)
+        try:
+            return self(ids0, t0) + self(ids1, t1)
+        finally:
+            self.grad_ready_cb = cb
+
+    def pair_overlaps(self):
+        """True when forward_pair overlaps something (the sequence-parallel TP chunk pair);
+        otherwise pairing only keeps two micro-batches' activations alive (Trainer pairs only then)."""
+        return bool(self.sp and self.tp_pipeline and self.training and torch.is_grad_enabled())
 
     def _forward_sp_pair(self, ids, targets, split, parts=None, tps=None):
         """Sequence-parallel TP training step as two chunks on one compute stream. Per layer the

@@ -213,6 +213,9 @@ def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int
     if after is not None and async_op and inp.is_cuda:
         ls = launch_stream(inp.device)
         ls.wait_event(after)
+        # inp was allocated on the compute stream and may be freed there (a temporary) before the
+        # exchange on the launch stream has read it: keep its block out of the pool until then
+        inp.record_stream(ls)
         with torch.cuda.stream(ls):
             w = all_to_all_single(out, inp, out_splits, in_splits, group, async_op=True)
         return w

@@ -237,8 +237,10 @@ class Trainer:
         self.opt.zero_grad()
         tot = None
         ntok = 0
+        # pair only where the model overlaps something across the two (EP exchanges, TP chunk
+        # pipeline): a pair otherwise just doubles the live activations
         pair = (c.pair_microbatches and c.grad_accum % 2 == 0 and hasattr(self.model, "forward_pair")
-                and self.model.training)
+                and self.model.training and bool(getattr(self.model, "pair_overlaps", lambda: False)()))
         n = 2 if pair else 1
         for mi in range(0, c.grad_accum, n):
             xs = [self.train_batch(step * c.grad_accum + mi + j) for j in range(n)]

@@ -243,21 +243,42 @@ def test_moe_ops_match_dense_loop():
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)
 
 
-def test_trainer_pairs_microbatches_like_one_by_one():
+@pytest.mark.parametrize("aux_free", [False, True])
+def test_trainer_pairs_microbatches_like_one_by_one(aux_free):
     """Trainer.pair_microbatches (DeepSeekV3.forward_pair on each two micro-batches of an even
-    grad_accum) trains to the same parameters as the one-by-one loop."""
+    grad_accum) trains to the same parameters -- and, with aux-free balancing, the same routing
+    biases -- as the one-by-one loop. (At EP 1 the Trainer would not pair: forced here.)"""
     from solvingpapers_amd.train.trainer import TrainConfig, Trainer
-    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0, aux_free=False)
+    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0, aux_free=aux_free)
     gen = torch.Generator().manual_seed(1)
     ids = torch.randint(0, c.vocab_size, (8, 2, 33), generator=gen)
-    params = []
+    params, biases = [], []
     for pair in (False, True):
         m = ds.DeepSeekV3(c, seed=0)
+        assert not m.pair_overlaps()                       # EP 1: nothing to hide
+        m.pair_overlaps = lambda: True
         tr = Trainer(m, TrainConfig(steps=2, grad_accum=4, lr=1e-3, pair_microbatches=pair),
                      lambda i: (ids[i, :, :-1], ids[i, :, 1:]))
         tr.fit()
         params.append(tr.flat.param.clone())
-    assert torch.allclose(params[0], params[1], atol=1e-6)
+        biases.append(torch.cat([l.routing_bias for l in m.moe_layers()]))
+    assert torch.allclose(params[0], params[1], atol=1e-5)     # summation order only
+    assert torch.equal(biases[0], biases[1])
+    if aux_free:
+        assert biases[0].abs().max() > 0
+
+
+def test_trainer_does_not_pair_without_overlap():
+    """Pairing keeps two micro-batches' activations alive; the Trainer does it only when the
+    model reports an overlap (pair_overlaps): at EP 1 / TP 1 it runs them one by one."""
+    from solvingpapers_amd.train.trainer import TrainConfig, Trainer
+    c = ds.config("dsv3_tiny", dropout=0.0, attn_dropout=0.0)
+    ids = torch.randint(0, c.vocab_size, (4, 2, 17))
+    m = ds.DeepSeekV3(c, seed=0)
+    calls = []
+    m.forward_pair = lambda *a: calls.append(1)
+    Trainer(m, TrainConfig(steps=1, grad_accum=2, lr=1e-3), lambda i: (ids[i, :, :-1], ids[i, :, 1:])).fit()
+    assert not calls
 
 
 @pytest.mark.parametrize("which", ["dsv3", "llama3"])

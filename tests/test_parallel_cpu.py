@@ -466,14 +466,12 @@ def _pair_worker(rank, world, port, q, aux_free):
         res[mode] = (float(loss), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
                      [l.routing_bias.clone() for l in m.moe_layers()])
     (l2, g2, b2), (lp, gp, bp) = res["two_calls"], res["pair"]
+    ok = abs(l2 - lp) < 1e-5 and set(g2) == set(gp) and all(torch.allclose(g2[k], gp[k], atol=1e-5) for k in g2)
+    # each MoE layer moves its routing bias right after micro-batch 0's routing, so micro-batch 1
+    # routes with it in both modes (the reference's update-after-every-forward order)
+    ok = ok and all(torch.equal(a, b) for a, b in zip(b2, bp))
     if aux_free:
-        # each micro-batch updates the routing bias once per MoE layer (its counts summed over the
-        # DP group); in the pair, micro-batch 1 routes before micro-batch 0's update of that layer
-        # lands, so only the update count is compared
-        ok = all(torch.allclose(b.abs().sum(), a.abs().sum(), atol=2.1e-3 * b.numel()) and b.abs().max() > 0
-                 for a, b in zip(b2, bp))
-    else:
-        ok = abs(l2 - lp) < 1e-5 and set(g2) == set(gp) and all(torch.allclose(g2[k], gp[k], atol=1e-5) for k in g2)
+        ok = ok and all(b.abs().max() > 0 for b in bp)
     q.put((rank, ok, l2, lp))
     if world > 1:
         dist.destroy_process_group()
@@ -487,3 +485,38 @@ def test_dsv3_forward_pair_matches_two_forwards(world, aux_free):
     layers."""
     for rank, ok, l2, lp in _run(_pair_worker, world, aux_free):
         assert ok, (rank, l2, lp)
+
+
+def _gemma_dp_pair_worker(rank, world, port, q, forced_pair):
+    _init(rank, world, port)
+    from solvingpapers_amd.models import gemma
+    from solvingpapers_amd.train.trainer import TrainConfig, Trainer
+    m = gemma.Gemma(_gemma_tp_cfg(), seed=5)
+    assert not m.pair_overlaps()
+    calls = []
+    if forced_pair:   # the Trainer pairs only on an overlap: force it; TP 1 takes the fallback pair
+        m.pair_overlaps = lambda: True
+        real_fp = m.forward_pair
+        m.forward_pair = lambda *a: calls.append(1) or real_fp(*a)
+    ids = torch.randint(0, 64, (4, world, 2, 13), generator=torch.Generator().manual_seed(7))
+    tr = Trainer(m, TrainConfig(steps=2, grad_accum=2, lr=1e-2, clip=1.0, resume="never"),
+                 lambda i: (ids[i, rank, :, :-1], ids[i, rank, :, 1:]))
+    assert tr.dp is not None
+    tr.fit()
+    assert len(calls) == (2 if forced_pair else 0)
+    q.put((rank, tr.flat.param.clone().numpy()))
+    dist.destroy_process_group()
+
+
+def test_gemma_dp_paired_fallback_matches_one_by_one():
+    """Gemma.forward_pair at TP 1 runs the two micro-batches one after the other
+    under ONE backward; its layer markers must fire the DP bucket only after BOTH micro-batches'
+    backward passed them (_PairReady), or the async all-reduce races micro-batch 0's commits.
+    DP = 2 (gloo), grad_accum 2: paired fallback == unpaired loop, identical on both ranks."""
+    ref = _run(_gemma_dp_pair_worker, 2, False)
+    out = _run(_gemma_dp_pair_worker, 2, True)
+    p0 = torch.from_numpy(ref[0][1])
+    for (_, a), (_, b) in zip(ref, out):
+        a, b = torch.from_numpy(a), torch.from_numpy(b)
+        assert torch.allclose(a, p0, atol=1e-6)
+        assert torch.allclose(b, p0, atol=1e-5), (b - p0).abs().max()
