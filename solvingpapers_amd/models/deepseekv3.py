@@ -469,7 +469,8 @@ class MoE(tnn.Module):
         load = (plan.counts if plan is not None else
                 torch.bincount(idx.reshape(-1).long(), minlength=c.n_experts)).float()
         grp = self.balance_group
-        if grp is not None or (dist.is_initialized() and dist.get_world_size() > 1):
+        from ..parallel.dist import is_dist
+        if grp is not None or is_dist():
             self._pending_bias.append((dist.all_reduce(load, group=grp, async_op=True), load))
         else:
             self._apply_bias(load)

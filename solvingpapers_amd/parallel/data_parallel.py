@@ -49,7 +49,10 @@ class DataParallel:
         self._launched = set()
         self._works: List = []
         self._avg_after: List[torch.Tensor] = []
-        if self.world > 1:
+        from .dist import force_collectives
+        # the collective paths run at world > 1, or at world 1 under SPA_FORCE_COLLECTIVES (tests)
+        self.active = self.world > 1 or (dist.is_initialized() and force_collectives())
+        if self.active:
             model.grad_ready_cb = self._on_ready
             for b in flat.buckets:
                 assert b.numel % self.world == 0, "FlatParams align must be a multiple of world size"
@@ -92,7 +95,7 @@ class DataParallel:
         self._works.append(w)
 
     def _on_ready(self, key):
-        if self._sync and self.world > 1:
+        if self._sync and self.active:
             self._reduce_bucket(int(key))
 
     @contextmanager
@@ -107,7 +110,7 @@ class DataParallel:
 
     def finish_grad_sync(self):
         """Launch any bucket not yet launched (e.g. the embedding) and wait for all."""
-        if self.world == 1:
+        if not self.active:
             return
         for i in range(len(self.flat.buckets) - 1, -1, -1):
             self._reduce_bucket(i)
@@ -121,7 +124,7 @@ class DataParallel:
 
     def gather_params(self):
         """ZeRO-1: all-gather each bucket's updated parameter shards."""
-        if not self.zero1 or self.world == 1:
+        if not self.zero1 or not self.active:
             return
         works = []
         for b in self.flat.buckets:
@@ -138,7 +141,7 @@ class DataParallel:
         of the DP group (a group-local rank), expert-parallel buckets only over
         ``expert_dp_group`` -- each EP rank holds DIFFERENT experts, so broadcasting those
         over the whole DP group would overwrite every rank's experts with rank 0's."""
-        if self.world <= 1:
+        if not self.active:
             return
         gsrc = dist.get_global_rank(self.group, src) if self.group is not None else src
         dense = [b for b in self.flat.buckets if b.index not in self.expert_buckets]

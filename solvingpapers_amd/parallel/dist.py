@@ -31,6 +31,13 @@ class DistInfo:
 _INFO = DistInfo()
 
 
+def force_collectives() -> bool:
+    """``SPA_FORCE_COLLECTIVES=1`` (tests): create the process group and run every collective path
+    (DP buckets, ZeRO-1, EP exchanges, the routing-bias all-reduce) even at world size 1, so one GPU
+    drives them through RCCL before a multi-GPU run does (tests/test_rccl_gpu.py)."""
+    return os.environ.get("SPA_FORCE_COLLECTIVES", "0") == "1"
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> DistInfo:
     """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*). With more than
     one RCCL rank it also selects hipBLASLt's data-parallel stream-K grid (SPA_STREAMK_DP=0
@@ -58,7 +65,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> Di
         device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_collectives()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
@@ -72,7 +79,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> Di
             store, _, _ = next(dist.rendezvous("env://", rank, world, timeout=kw["timeout"]))
             kw["store"] = dist.PrefixStore(f"spa_restart{restart}", store)
         dist.init_process_group(**kw)
-    _INFO = DistInfo(rank, world, local, backend if world > 1 else "none", device)
+    _INFO = DistInfo(rank, world, local, backend if dist.is_initialized() else "none", device)
     return _INFO
 
 
@@ -81,7 +88,7 @@ def info() -> DistInfo:
 
 
 def is_dist() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or force_collectives())
 
 
 def barrier(group=None):

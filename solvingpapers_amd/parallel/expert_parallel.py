@@ -39,6 +39,14 @@ def ep_rank_size(group):
     return comm.group_rank_size(group)
 
 
+def _local(group, P):
+    """No exchange: one EP rank -- unless SPA_FORCE_COLLECTIVES drives a real size-1 group."""
+    if P > 1:
+        return False
+    from .dist import force_collectives
+    return not (force_collectives() and group is not None and not comm.is_proxy(group))
+
+
 def all_to_all(x, out_splits, in_splits, group):
     """Autograd all-to-all (the reverse exchange in backward) through parallel/comm.py."""
     return comm.a2a(x, out_splits, in_splits, group)
@@ -178,7 +186,7 @@ def ep_prepare(idx, n_experts, group):
     copied to (pinned) host memory asynchronously."""
     plan = permute(idx, n_experts)
     rank, P = ep_rank_size(group)
-    if P == 1:
+    if _local(group, P):
         return EPPrep(plan)
     counts = plan.counts.to(torch.int64)
     recv = torch.empty_like(counts)
@@ -224,7 +232,8 @@ def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None):
     D = x.shape[-1]
     st.fp8 = bool(fp8)
     rank, P = ep_rank_size(group)
-    st.fp8_dispatch = st.fp8 and P > 1 and D % 128 == 0 and (W13 is None or W13.shape[1] % 128 == 0)
+    local = _local(group, P)
+    st.fp8_dispatch = st.fp8 and not local and D % 128 == 0 and (W13 is None or W13.shape[1] % 128 == 0)
     if st.fp8_dispatch:
         box = comm._Box()
         KB = D // 128
@@ -234,7 +243,7 @@ def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None):
         box.D, box.dtype, box.group = D, x.dtype, group
         st.box = box
     st.ev = None
-    if P > 1 and x.is_cuda:
+    if not local and x.is_cuda:
         st.ev = torch.cuda.Event()
         st.ev.record()
     return st
@@ -242,7 +251,7 @@ def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None):
 
 def ep_stage_dispatch(st):
     rank, P = ep_rank_size(st.group)
-    if P == 1:
+    if _local(st.group, P):
         return st
     El = st.n_experts // P
     send_splits, rc = st.prep.splits(P, El)                  # the single host sync of the chunk
@@ -263,7 +272,7 @@ def ep_stage_dispatch(st):
 
 def ep_stage_experts(st, W13, W2, act="silu"):
     rank, P = ep_rank_size(st.group)
-    if P == 1:
+    if _local(st.group, P):
         plan = st.prep.plan
         h = glu(grouped_linear(st.xp, W13, plan, st.fp8), act)
         st.yp = grouped_linear(h, W2, plan, st.fp8)
@@ -284,7 +293,7 @@ def ep_stage_experts(st, W13, W2, act="silu"):
 
 def ep_stage_finish(st):
     rank, P = ep_rank_size(st.group)
-    yp = st.yp if P == 1 else comm.a2a_finish(st.chandle)
+    yp = st.yp if _local(st.group, P) else comm.a2a_finish(st.chandle)
     y = combine(yp, st.w, st.prep.plan)
     st.xp = st.yp = st.handle = st.chandle = st.box = st.token = None
     return y

@@ -520,3 +520,20 @@ def test_gemma_dp_paired_fallback_matches_one_by_one():
         a, b = torch.from_numpy(a), torch.from_numpy(b)
         assert torch.allclose(a, p0, atol=1e-6)
         assert torch.allclose(b, p0, atol=1e-5), (b - p0).abs().max()
+
+
+def test_forced_collectives_world1_gloo():
+    """SPA_FORCE_COLLECTIVES=1 at world size 1 (the path tests/test_rccl_gpu.py drives through RCCL
+    on the GPU box): DP buckets, ZeRO-1, the launch all-to-all, the EP exchange and the async
+    routing-bias all-reduce run through a real size-1 gloo group and match the group-less run."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_port()), SPA_FORCE_COLLECTIVES="1", SPA_TEST_DEVICE="cpu",
+               SPA_DIST_BACKEND="gloo", PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "rccl_world1_child.py")], env=env, cwd=root,
+                       timeout=300, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "RCCL_WORLD1_OK" in r.stdout

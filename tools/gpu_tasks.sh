@@ -29,6 +29,7 @@
 #   ext-ab K C     in-tree build vs $BASE_SO: GPU tests -k K, bench_kernels case C, headline, B N N B
 #   attn-pmc       attention counters + clocks in the headline step (4 layers) and in isolation; GEMM-interleaved timing
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
+#   rccl           world-1 RCCL test (every collective path) + headline ABBA with TENSILE_STREAMK_DATA_PARALLEL=1
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -46,6 +47,14 @@ run() {  # run <seconds> <log> <cmd...>: one GPU step under its own limit; stop 
 jsonl() { grep -h '^{' "$@" | cut -c1-600; }
 
 case $task in
+rccl)
+  run 300 ${O}_pytest.log python -u -m pytest tests/test_rccl_gpu.py -x -v -s -p no:cacheprovider --timeout 240 --timeout-method thread
+  grep -h 'rccl-world1\|passed\|failed' ${O}_pytest.log | cut -c1-200
+  for arm in base var var base; do
+    if [ $arm = var ]; then run 400 ${O}_$arm.log env TENSILE_STREAMK_DATA_PARALLEL=1 python -u bench.py --steps 6 --warmup 2
+    else run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2; fi
+    echo "$arm streamk_dp $(grep -ho '"value": [0-9.]*' ${O}_$arm.log)"
+  done ;;
 start)
   run 300 ${O}_attn.log python -u tools/bench_attn.py
   grep -i 'attn B' ${O}_attn.log | cut -c1-300
