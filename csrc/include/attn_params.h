@@ -43,7 +43,14 @@ struct AttnParams {
   float* mlpart;
   int part_ld;
   int vhalf;
+  // attn_bwd_dkdv5_kernel: row constants [B*H][2][rowk_ld] = -lse*log2(e) | -delta per query row
+  // (rowk_ld = Tq rounded up to 64, zeros past Tq), DMA'd into LDS with each Q / dO tile
+  float* rowk;
+  int rowk_ld;
 };
+
+// host launcher of the dK/dV v5 path (csrc/kernels/attention_dkdv5.hip): rowk pass + dK/dV kernel
+void launch_dkdv5(AttnParams& p, bool causal, hipStream_t st);
 
 // 2 KiB dS block index inside one (b, kv-head) region, in the order the dQ pass streams it: per
 // 64-query block qb its key steps kt (causal Tq == Tk: kt <= 2qb + 1, non-causal: all nkt), per

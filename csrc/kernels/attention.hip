@@ -2059,13 +2059,23 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
     if (want && p.hsplit == 1 && p.Tk > 0 && dkdv_mode == 0 && (!causal || p.causal_off == 0) &&
         kv_bytes < 0x7fffffffL) {
       const long rows = (long)p.B * p.Tq * p.H;
-      attn_delta_kernel<HDK><<<(int)cdiv(rows, 256 / (HDK / 8)), 256, 0, st>>>(p);
+      const char* v5e = getenv("SPA_ATTN_DKDV5");
+      const bool v5 = !(v5e && atoi(v5e) == 0);
+      if (!v5) attn_delta_kernel<HDK><<<(int)cdiv(rows, 256 / (HDK / 8)), 256, 0, st>>>(p);
       p.ds_nqt = cdiv(p.Tq, 32);
       p.ds_nkt = cdiv(p.Tk, 32);
       p.ds_kvstride = ds_kv_elems(cdiv(p.Tq, 64), p.ds_nkt, p.H / p.Hkv, causal);
       at::Tensor dsb = at::empty({(long)p.B * p.Hkv * p.ds_kvstride}, bf16_opts);   // freed (stream-ordered) on return
       p.dsbuf = (bf16*)dsb.data_ptr();
-      if (causal) attn_bwd_dkdv3_kernel<HDK, HDV, true, true><<<nkv, 512, 0, st>>>(p);
+      // default: the LDS-DMA-staged dK/dV kernel with incremental bookkeeping (attention_dkdv5.hip,
+      // its row-constant pass replaces the delta pass); SPA_ATTN_DKDV5=0 (read per call) keeps dkdv3
+      at::Tensor rowk;
+      if (v5) {
+        p.rowk_ld = cdiv(p.Tq, 64) * 64;
+        rowk = at::empty({(long)p.B * p.H * 2 * p.rowk_ld}, bf16_opts.dtype(at::kFloat));
+        p.rowk = rowk.data_ptr<float>();
+        launch_dkdv5(p, causal, st);
+      } else if (causal) attn_bwd_dkdv3_kernel<HDK, HDV, true, true><<<nkv, 512, 0, st>>>(p);
       else attn_bwd_dkdv3_kernel<HDK, HDV, false, true><<<nkv, 512, 0, st>>>(p);
       const int G = p.H / p.Hkv;
       const int wg = cdiv(cdiv(p.Tq, 64) * G, 4) * p.B * p.Hkv;

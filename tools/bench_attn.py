@@ -126,10 +126,14 @@ if os.environ.get("SPA_ATTN_STAMP"):
     # staging, compute 1, compute 2, barrier wait, epilogue, intervals, whole wave (s_memtime)
     wave = torch.arange(st.shape[0]) % 8
     live = st[:, 5] > 0
-    names = ["staging", "compute 1", "compute 2", "barrier wait"]
-    for role, sel in (("A (1 dV^T, 2 S->P)", wave < 4), ("B (1 dP+dS, 2 dK^T)", wave >= 4)):
+    v5 = os.environ.get("SPA_ATTN_DKDV5", "0") != "0"
+    names = ["DMA issue", "compute", "DMA wait", "barrier wait"] if v5 else ["staging", "compute 1", "compute 2", "barrier wait"]
+    roles = (("A (S -> P, dV^T)", wave < 4), ("B (dP, dS, dK^T)", wave >= 4)) if v5 else \
+        (("A (1 dV^T, 2 S->P)", wave < 4), ("B (1 dP+dS, 2 dK^T)", wave >= 4))
+    for role, sel in roles:
         r = st[live & sel]
         per = r[:, :4].sum(0) / r[:, 5].sum()
         print(f"   dK/dV loop, role {role}: cycles per interval " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, per.tolist()))
               + f" | loop {per.sum().item():.0f} | epilogue per wave {r[:, 4].mean().item():.0f}"
-              + f" | whole wave {r[:, 6].mean().item():.0f} over {r[:, 5].mean().item():.0f} intervals", flush=True)
+              + f" | whole wave {r[:, 6].mean().item():.0f} over {r[:, 5].mean().item():.0f} intervals"
+              + (f" ({r[:, 7].sum().item() / r[:, 5].sum().item() * 100:.0f} % pipelined)" if v5 else ""), flush=True)

@@ -29,6 +29,8 @@
 #   ext-ab K C     in-tree build vs $BASE_SO: GPU tests -k K, bench_kernels case C, headline, B N N B
 #   attn-pmc       attention counters + clocks in the headline step (4 layers) and in isolation; GEMM-interleaved timing
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
+#   dkdv5          dS-path GPU tests (incl. the v5 dK/dV kernel), LLaMA-shape ABBA SPA_ATTN_DKDV5=1, kernel times
+#   dkdv5-var      dkdv5 variants vs dkdv3 (ABBA, one process) + stamp profiles of dkdv3 / dkdv5 variants
 #   rccl           world-1 RCCL test (every collective path) + headline ABBA with TENSILE_STREAMK_DATA_PARALLEL=1
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -47,6 +49,27 @@ run() {  # run <seconds> <log> <cmd...>: one GPU step under its own limit; stop 
 jsonl() { grep -h '^{' "$@" | cut -c1-600; }
 
 case $task in
+dkdv5)
+  run 300 ${O}_pytest.log python -u -m pytest tests/test_kernels_gpu.py -k "ds_path" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 200 ${O}_ab.log python -u tools/bench_attn.py --iters 20 --packed --ab SPA_ATTN_DKDV5=1
+  grep -h 'attn B\|with SPA' ${O}_ab.log | cut -c1-300
+  run 200 ${O}_ab2.log python -u tools/bench_attn.py --iters 20 --packed --ab SPA_ATTN_DKDV5=1
+  grep -h 'with SPA' ${O}_ab2.log | cut -c1-300
+  export SPA_ATTN_DKDV5=1
+  run 200 ${O}_prof.log rocprofv3 --kernel-trace --stats -d /tmp/$task -o run -- python3 tools/bench_attn.py --iters 10 --packed
+  unset SPA_ATTN_DKDV5
+  python tools/rocpd_summary.py /tmp/$task/run_results.db --top 8 > ${O}_summary.txt 2>&1
+  head -14 ${O}_summary.txt | cut -c1-150 ;;
+dkdv5-var)
+  # dkdv5-var "1,5,9" "1 9": SPA_ATTN_DKDV5 variants vs dkdv3 (ABBA, one process), then stamp profiles
+  vs=${1:-1,3,5,7}; sv=${2:-0 1}
+  run 300 ${O}_ab.log python -u tools/bench_attn.py --iters 20 --packed --ab $(echo $vs | sed 's/\([0-9]*\)/SPA_ATTN_DKDV5=\1/g')
+  grep -h 'attn B\|with SPA' ${O}_ab.log | cut -c1-300
+  for v in $sv; do
+    run 200 ${O}_st$v.log env SPA_EXT_SO=ab/_C_stamp5.so SPA_ATTN_STAMP=1 SPA_ATTN_DKDV5=$v python -u tools/bench_attn.py --iters 5 --packed
+    echo "== SPA_ATTN_DKDV5=$v (stamp build)"; grep -h 'attn B\|role' ${O}_st$v.log | cut -c1-300
+  done ;;
 rccl)
   run 300 ${O}_pytest.log python -u -m pytest tests/test_rccl_gpu.py -x -v -s -p no:cacheprovider --timeout 240 --timeout-method thread
   grep -h 'rccl-world1\|passed\|failed' ${O}_pytest.log | cut -c1-200
