@@ -108,6 +108,8 @@ struct LdsOff {
       tra.v[dt] = ra * HD + 8 * (ch ^ swz<HD>(ra)) + within;
       trb.v[dt] = rb * HD + 8 * (ch ^ swz<HD>(rb)) + within;
     }
+    SPA_DBG_LDS(row.v[NR - 1] + 7, 32 * HD);
+    SPA_DBG_LDS(trb.v[NTR - 1] + 3, 16 * HD);
   }
 };
 __device__ __forceinline__ bf16x8 ld_row(const bf16* img, int off) {
@@ -206,6 +208,8 @@ struct TileLoader {
     }
   }
   __device__ __forceinline__ void store(bf16* img) const {
+    // debug build: this lane's last 16-B chunk ends inside the ROWS x IW image
+    SPA_DBG_LDS(loff + (NP - 1) * R * IW + 128 * (NC - 1) + 7, ROWS * IW);
 #pragma unroll
     for (int ps = 0; ps < NP; ++ps)
 #pragma unroll

@@ -2,6 +2,10 @@
 #pragma once
 #include "attn_common.h"
 
+// debug build (spa_debug.h): the (batch, row, head) a block derived from its tile ids, checked
+// against the problem at every global store (`if (SPA_DBG_BRH(...)) *dst = ...`); `true` otherwise
+#define SPA_DBG_BRH(b, r, R, h, H) (SPA_DBG_OK(b, p.B) & SPA_DBG_OK(r, R) & SPA_DBG_OK(h, H))
+
 namespace spa {
 
 struct AttnParams {
@@ -79,6 +83,7 @@ template <int HD>
 __device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 (&acc)[HD / 32], bool is_k,
                                               int b, int hk, int key, int split, int hh) {
   if (key >= p.Tk) return;
+  if (!(SPA_DBG_BRH(b, key, p.Tk, hk, p.Hkv) & SPA_DBG_OK(split, p.hsplit))) return;
   constexpr int DT = HD / 32;
   if (p.hsplit == 1) {
     bf16* dst = is_k ? p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh

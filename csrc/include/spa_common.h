@@ -16,6 +16,8 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <cstdint>
 
+#include "spa_debug.h"  // SPA_DBG_* device bounds guards (empty unless -DSPA_DEBUG_BOUNDS=1)
+
 namespace spa {
 
 typedef __bf16 bf16;

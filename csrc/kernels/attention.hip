@@ -51,6 +51,8 @@
 #include "attn_common.h"
 #include "attn_params.h"
 
+SPA_DEBUG_TU("attention.hip")
+
 namespace spa {
 
 
@@ -127,6 +129,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   int qb, b, h;
   q_block_map(p, nqb, CAUSAL, qb, b, h, blockIdx.x / p.ksplit, gridDim.x / p.ksplit);
   const int hk = h / (p.H / p.Hkv);
+  SPA_DBG_CHECK(qb, nqb);
+  SPA_DBG_CHECK(hk, p.Hkv);
+  (void)SPA_DBG_BRH(b, 0, 1, h, p.H);
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
   const float c = p.scale_log2;
@@ -273,8 +278,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
   }
   l = halfsum(l);
   if (p.ksplit > 1) {      // fp32 partial: unnormalised O and the (m, l) softmax state
-    if (q < p.Tq) {
+    if (q < p.Tq && SPA_DBG_OK(si, p.ksplit)) {
       const long row = (((long)si * p.B + b) * p.H + h) * p.Tq + q;
+      SPA_DBG_CHECK(row, (long)p.ksplit * p.B * p.H * p.Tq);
       float* dst = p.part + row * p.part_ld + vcol;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnParams p) {
     return;
   }
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  if (q < p.Tq) {
+  if (q < p.Tq && SPA_DBG_BRH(b, q, p.Tq, h, p.H)) {
     bf16* op = p.out + b * p.sob + (long)q * p.sot + h * p.soh + vcol;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -341,6 +347,9 @@ __global__ __launch_bounds__(512) void attn_fwd256p_kernel(AttnParams p) {
   int qb, b, h;
   q_block_map(p, nqb, CAUSAL, qb, b, h, blockIdx.x / p.ksplit, gridDim.x / p.ksplit);
   const int hk = h / (p.H / p.Hkv);
+  SPA_DBG_CHECK(qb, nqb);
+  SPA_DBG_CHECK(hk, p.Hkv);
+  (void)SPA_DBG_BRH(b, 0, 1, h, p.H);
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + grp * 32);
   const int q = q0 + lq;
   const float c = p.scale_log2;
@@ -478,8 +487,9 @@ __global__ __launch_bounds__(512) void attn_fwd256p_kernel(AttnParams p) {
   if (role == 1) l = arow[0][grp][lane];
   const int vcol = role * 128;
   if (p.ksplit > 1) {
-    if (q < p.Tq) {
+    if (q < p.Tq && SPA_DBG_OK(si, p.ksplit)) {
       const long row = (((long)si * p.B + b) * p.H + h) * p.Tq + q;
+      SPA_DBG_CHECK(row, (long)p.ksplit * p.B * p.H * p.Tq);
       float* dst = p.part + row * p.part_ld + vcol;
 #pragma unroll
       for (int dt = 0; dt < DH; ++dt)
@@ -500,7 +510,7 @@ __global__ __launch_bounds__(512) void attn_fwd256p_kernel(AttnParams p) {
     return;
   }
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  if (q < p.Tq) {
+  if (q < p.Tq && SPA_DBG_BRH(b, q, p.Tq, h, p.H)) {
     bf16* op = p.out + b * p.sob + (long)q * p.sot + h * p.soh + vcol;
 #pragma unroll
     for (int dt = 0; dt < DH; ++dt)
@@ -535,6 +545,9 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
   int qb, b, h;
   q_block_map(p, nqb, CAUSAL, qb, b, h, blockIdx.x / p.ksplit, gridDim.x / p.ksplit);
   const int hk = h / (p.H / p.Hkv);
+  SPA_DBG_CHECK(qb, nqb);
+  SPA_DBG_CHECK(hk, p.Hkv);
+  (void)SPA_DBG_BRH(b, 0, 1, h, p.H);
   const int q0 = __builtin_amdgcn_readfirstlane(qb * BM + wave * 32);
   const int q = q0 + lq;
   const bool qvalid = q < p.Tq;
@@ -560,7 +573,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     dlt = halfsum(dlt);
   }
   const long srow = ((long)b * p.H + h) * p.Tq + q;
-  if (qvalid && hh == 0 && si == 0) p.delta[srow] = dlt;
+  if (qvalid && hh == 0 && si == 0 && SPA_DBG_OK(srow, (long)p.B * p.H * p.Tq)) p.delta[srow] = dlt;
   const float nlse2 = qvalid ? -p.lse_in[srow] * 1.4426950408889634f : -INFINITY;
   f32x16 acc[DT];
 #pragma unroll
@@ -669,6 +682,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnParams p) {
     body(j, IC<0>{});
     if (j + 1 < ntiles) body(j + 1, IC<1>{});
   }
+  if (qvalid && !SPA_DBG_BRH(b, q, p.Tq, h, p.H)) return;
   if (qvalid && p.ksplit > 1) {   // fp32 partial (unscaled), summed by attn_dq_reduce_kernel
     float* dst = p.part + ((((long)si * p.B + b) * p.Tq + q) * p.H + h) * p.part_ld;
 #pragma unroll
@@ -735,6 +749,7 @@ __global__ __launch_bounds__(256) void attn_fwd_merge_kernel(AttnParams p) {
   bf16x8 o;
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = (bf16)(acc[i] * inv);
+  if (!SPA_DBG_BRH(b, q, p.Tq, h, p.H)) return;
   *reinterpret_cast<bf16x8*>(p.out + b * p.sob + (long)q * p.sot + h * p.soh + c8) = o;
   if (c8 == 0 && p.lse) p.lse[row] = L > 0.f ? (M + __log2f(L)) * 0.69314718055994531f : INFINITY;
 }
@@ -765,6 +780,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnParams p) {
   bf16x8 o;
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = (bf16)(acc[i] * p.scale);
+  if (!SPA_DBG_BRH(b, q, p.Tq, h, p.H)) return;
   *reinterpret_cast<bf16x8*>(p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh + c8) = o;
 }
 
@@ -805,6 +821,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int rest = blockIdx.x / nbh;  // causal: low key blocks are heaviest, launched first
   const int split = rest % p.hsplit, kb = rest / p.hsplit;
   const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  SPA_DBG_CHECK(b, p.B);
+  SPA_DBG_CHECK(split, p.hsplit);
   const int G = p.H / p.Hkv;             // q-heads sharing this kv-head
   const int h0 = hk * G;
   const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + wave * 32);
@@ -977,6 +995,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
             const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(p.dsbuf + ((long)b * p.Hkv + hk) * p.ds_kvstride), 0, (int)(p.ds_kvstride * 2), 0x00020000);
             const int bo = (int)(ds_index(qt, kt, (it + ib) / nper, G, p.ds_nkt, CAUSAL) * 2048);
+            SPA_DBG_CHECK(bo / 2048, p.ds_kvstride / 1024);
             const int vo = 16 * ds_slot(0, hh, lk);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sa), dsr, vo, bo, 0);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sb), dsr, vo + 128, bo, 0);
@@ -1033,7 +1052,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qq = q0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (qq < p.Tq) atomicAdd(dst + (long)qq * p.H * HDK, acc[r]);
+          if (qq < p.Tq && SPA_DBG_BRH(b, qq, p.Tq, h, p.H)) atomicAdd(dst + (long)qq * p.H * HDK, acc[r]);
         }
       }
     }
@@ -1108,6 +1127,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
   const int rest = blockIdx.x / nbh;
   const int split = rest % p.hsplit, kb = rest / p.hsplit;
   const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  SPA_DBG_CHECK(b, p.B);
+  SPA_DBG_CHECK(split, p.hsplit);
   const int Gs = p.H / p.Hkv / p.hsplit;
   const int h0 = hk * (p.H / p.Hkv) + split * Gs;
   const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + pair * 32);
@@ -1294,6 +1315,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
             const __amdgpu_buffer_rsrc_t dsr = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(p.dsbuf + ((long)b * p.Hkv + hk) * p.ds_kvstride), 0, (int)(p.ds_kvstride * 2), 0x00020000);
             const int bo = (int)(ds_index(qt, kt, hp - hk * (p.H / p.Hkv), p.H / p.Hkv, p.ds_nkt, CAUSAL) * 2048);
+            SPA_DBG_CHECK(bo / 2048, p.ds_kvstride / 1024);
             const int vo = 16 * ds_slot(0, (int)(__lane_id() >> 5), (int)(__lane_id() & 31));
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sa), dsr, vo, bo, 0);        // s = 0
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sb), dsr, vo + 128, bo, 0);  // s = 1: slot + 8
@@ -1392,6 +1414,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   const int bkv = blockIdx.x % nbkv;                            // = XCD group when B*Hkv == 8
   const int w = CAUSAL ? wgpkv - 1 - (int)(blockIdx.x / nbkv) : (int)(blockIdx.x / nbkv);  // heaviest first
   const int b = bkv / p.Hkv, hk = bkv % p.Hkv;
+  SPA_DBG_CHECK(b, p.B);
   const int u = 4 * w + wave;
   const bool uvalid = u < upkv;
   const int qb = uvalid ? u / G : 0;
@@ -1427,6 +1450,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
     // this wave's two blocks of the step (t = 0, 1) are one contiguous 4 KiB piece; a step past the
     // unit's range, or a missing unit, reads zeros (same DMA count in every wave and step)
     const bool lv = live(2 * qb + 1, j) || live(2 * qb, j);
+    if (lv) SPA_DBG_CHECK(ds_index(2 * qb, j, g, G, p.ds_nkt, CAUSAL), p.ds_kvstride / 1024);
     const bf16* src = lv ? dskv + ds_index(2 * qb, j, g, G, p.ds_nkt, CAUSAL) * 1024 : p.dsbuf;
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, lv ? 4096 : 0, 0x00020000);
     bf16* dst = sl + KIMG + wave * WSLOT;
@@ -1496,7 +1520,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int q = qb * 64 + 32 * t + (lane & 31);
-    if (q >= p.Tq) continue;
+    if (q >= p.Tq || !SPA_DBG_BRH(b, q, p.Tq, h, p.H)) continue;
     bf16* op = p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -1533,6 +1557,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds256_kernel(AttnParams p)
   const int bkv = blockIdx.x % nbkv;
   const int w = CAUSAL ? wgpkv - 1 - (int)(blockIdx.x / nbkv) : (int)(blockIdx.x / nbkv);  // heaviest first
   const int b = bkv / p.Hkv, hk = bkv % p.Hkv;
+  SPA_DBG_CHECK(b, p.B);
   const int u = 4 * w + wave;
   const bool uvalid = u < upkv;
   const int qt = uvalid ? u / G : 0;
@@ -1565,6 +1590,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds256_kernel(AttnParams p)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) dma16_asm(rk, kvo[jj], lds_addr(sl + (8 * wave + 2 * jj) * HD));
     const bool lv = live(j);
+    if (lv) SPA_DBG_CHECK(ds_index(qt, j, g, G, p.ds_nkt, CAUSAL), p.ds_kvstride / 1024);
     const bf16* src = lv ? dskv + ds_index(qt, j, g, G, p.ds_nkt, CAUSAL) * 1024 : p.dsbuf;
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, lv ? 2048 : 0, 0x00020000);
     bf16* dst = sl + KIMG + wave * WSLOT;
@@ -1616,7 +1642,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds256_kernel(AttnParams p)
   }
   if (!uvalid) return;
   const int q = qt * 32 + (lane & 31);
-  if (q >= p.Tq) return;
+  if (q >= p.Tq || !SPA_DBG_BRH(b, q, p.Tq, h, p.H)) return;
   bf16* op = p.dq + b * p.sdqb + (long)q * p.sdqt + h * p.sdqh;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -1679,7 +1705,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p) {
   }
 #pragma unroll
   for (int o = TPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, TPR);
-  if (row < nrows && t == 0) p.delta[(b * p.H + h) * p.Tq + q] = acc;
+  if (row < nrows && t == 0 && SPA_DBG_BRH(b, q, p.Tq, h, p.H)) p.delta[(b * p.H + h) * p.Tq + q] = acc;
 }
 // dq (strided bf16) = scale * dqacc
 template <int HD>
@@ -1694,7 +1720,7 @@ __global__ __launch_bounds__(256) void attn_dq_store_kernel(AttnParams p) {
     load8(p.dqacc + row * HD + 8 * t, a);
 #pragma unroll
     for (int k = 0; k < 8; ++k) a[k] *= p.scale;
-    store8(p.dq + b * p.sdqb + q * p.sdqt + h * p.sdqh + 8 * t, a);
+    if (SPA_DBG_BRH(b, q, p.Tq, h, p.H)) store8(p.dq + b * p.sdqb + q * p.sdqt + h * p.sdqh + 8 * t, a);
   }
 }
 
@@ -1726,6 +1752,8 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   const int h = blockIdx.x % p.H, b = blockIdx.x / p.H;  // H == Hkv
+  SPA_DBG_CHECK(b, p.B);
+  SPA_DBG_ASSERT(p.Tq <= TMAX && p.Tk <= TMAX, p.Tq, TMAX);
   const int r0 = __builtin_amdgcn_readfirstlane(wave * 32);
   const int row = r0 + l32;
   const float c = p.scale_log2;
@@ -1803,7 +1831,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnParams p) {
         acc[dt] = mfma32(ld_tr(Ks + 16 * HD, off.tra[dt], off.trb[dt]), sb, acc[dt]);
       }
     }
-    if (row < p.Tq) {
+    if (row < p.Tq && SPA_DBG_BRH(b, row, p.Tq, h, p.H)) {
       bf16* o = p.dq + b * p.sdqb + (long)row * p.sdqt + h * p.sdqh;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)

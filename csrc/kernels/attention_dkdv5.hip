@@ -21,6 +21,8 @@
 #include "attn_common.h"
 #include "attn_params.h"
 
+SPA_DEBUG_TU("attention_dkdv5.hip")
+
 namespace spa {
 
 // 4 B per lane of a buffer straight into LDS (lane i -> lds + 4 i); as dma16_asm (attn_common.h)
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(256) void attn_rowk_kernel(AttnParams p) {
   }
 #pragma unroll
   for (int o = TPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, TPR);
-  if (row < nrows && t == 0) {
+  if (row < nrows && t == 0 && SPA_DBG_OK(((b * p.H + h) * 2 + 1) * (long)Tqp + q, (long)p.B * p.H * 2 * Tqp)) {
     float* dst = p.rowk + ((b * p.H + h) * 2) * (long)Tqp + q;
     const bool v = q < p.Tq;
     dst[0] = v ? -p.lse_in[(b * p.H + h) * p.Tq + q] * 1.4426950408889634f : 0.f;
@@ -111,6 +113,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv5_kernel(AttnParams p) {
   const int bh = blockIdx.x % nbh;
   const int kb = blockIdx.x / nbh;                    // causal: low key blocks (heaviest) first
   const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  SPA_DBG_CHECK(b, p.B);
   const int G = p.H / p.Hkv;
   const int h0 = hk * G;
   const int kw0 = __builtin_amdgcn_readfirstlane(kb * BNK + pair * 32);
@@ -202,6 +205,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv5_kernel(AttnParams p) {
     }
   };
   auto issue = [&](const D5Tile& t, auto slotc) {
+    // debug build: the incremental bookkeeping still names a tile of this block's sweep, and its
+    // row constants lie inside rowk
+    SPA_DBG_CHECK(t.g, G);
+    SPA_DBG_CHECK(t.qi, nper);
+    SPA_DBG_CHECK((long)(b * p.H + h0) * 2 * Tqp + t.roff + Tqp + BMQ - 1, (long)p.B * p.H * 2 * Tqp);
     piece(t, 0, slotc);
     piece(t, 1, slotc);
     piece(t, 2, slotc);
@@ -221,6 +229,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv5_kernel(AttnParams p) {
     const int qb = qt >> 1, t = qt & 1;
     const int step = CAUSAL ? qb * (qb + 1) + kt : qb * p.ds_nkt + kt;
     const int bo = ((step * G + g) * 2 + t) * 2048;
+    SPA_DBG_CHECK(bo / 2048, p.ds_kvstride / 1024);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sa), dsr, dsvo, bo, 0);        // s = 0
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, sb), dsr, dsvo + 128, bo, 0);  // s = 1
   };

@@ -26,6 +26,8 @@
 #include "spa_common.h"
 #include "gemm_common.h"
 
+SPA_DEBUG_TU("conv.hip")
+
 namespace spa {
 
 struct ConvGeo {
@@ -44,6 +46,7 @@ struct ConvGeo {
   float* part;
   const bf16* bias;
   int kchunk;                        // wgrad: rows per split
+  long gnumel;                       // elements of g (debug-build gather guard)
 };
 
 constexpr int CBM = 128, CBN = 128, CBK = 32, CNT = 256;
@@ -96,10 +99,12 @@ __global__ __launch_bounds__(CNT, 2) void conv_gemm_kernel(ConvGeo p) {
     const int h = h0 + t.y, w = w0 + t.z;
     if (MODE == 2) {
       ok = ok && h >= 0 && w >= 0 && h % p.ssh == 0 && w % p.ssw == 0 && h / p.ssh < p.gH && w / p.ssw < p.gW;
+      if (ok) SPA_DBG_CHECK(base + (long)(h / p.ssh) * p.sH + (long)(w / p.ssw) * p.sW + t.x + 7, p.gnumel);
       return ok ? *reinterpret_cast<const bf16x8*>(p.g + base + (long)(h / p.ssh) * p.sH + (long)(w / p.ssw) * p.sW + t.x)
                 : bf16x8{};
     }
     ok = ok && (unsigned)h < (unsigned)p.gH && (unsigned)w < (unsigned)p.gW;
+    if (ok) SPA_DBG_CHECK(base + t.x + 7, p.gnumel);   // debug build: the tap lies inside the image
     return ok ? *reinterpret_cast<const bf16x8*>(p.g + base + t.x) : bf16x8{};
   };
   auto load_tiles = [&](int kk) {
@@ -212,6 +217,7 @@ __global__ __launch_bounds__(CNT, 2) void conv_gemm_kernel(ConvGeo p) {
     for (int j = 0; j < IM; ++j) {
       const int gm = m0 + wm * TM + j * 32 + l32;
       if (gm >= p.M) continue;
+      if (MODE == 3) SPA_DBG_CHECK(blockIdx.y * p.kchunk, p.K);   // debug build: a live split
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int gn = n0 + wn * TN + i * 32 + 8 * g + 4 * hh;
@@ -408,6 +414,7 @@ struct Geo {
 
 static void fill_gather(ConvGeo& p, const Geo& G, const at::Tensor& x) {
   p.g = (const bf16*)x.data_ptr();
+  p.gnumel = x.numel();
   p.gN = (long)G.Cp * G.H * G.W;
   p.gH = G.H; p.gW = G.W;
   p.sH = G.nhwc ? G.W * G.Cp : G.W;
@@ -475,6 +482,7 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& wp, const at::Tens
   ConvGeo p{};
   p.M = G.N * G.H * G.W; p.N = G.Cp; p.K = Kd;
   p.g = (const bf16*)dy.data_ptr();
+  p.gnumel = dy.numel();
   p.gN = (long)G.OH * G.OW * G.OC;
   p.gH = G.OH; p.gW = G.OW;
   p.sH = G.OW * G.OC; p.sW = G.OC;

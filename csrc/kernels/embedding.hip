@@ -14,12 +14,14 @@
 #include <map>
 #include <tuple>
 
+SPA_DEBUG_TU("embedding.hip")
+
 namespace spa {
 
 template <typename T, bool POS>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const T* __restrict__ W, const int64_t* __restrict__ idx,
                                                       const T* __restrict__ pos, T* __restrict__ out, long N, int D,
-                                                      int T_, float scale) {
+                                                      int T_, float scale, long V) {
   const int dv = D / 8;
   const long total = N * dv;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -27,7 +29,7 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const T* __restrict__ W, c
     const int c = (i % dv) * 8;
     float v[8];
     const int64_t r = idx[n];
-    if (r >= 0) {
+    if (r >= 0 && SPA_DBG_OK(r, V)) {   // debug build: a token id inside the table
       load8(W + r * D + c, v);
     } else {   // negative id (vocab-parallel: a token of another rank's shard): a zero row
 #pragma unroll
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const T* __restrict__ W, c
 template <typename T>
 __global__ __launch_bounds__(256) void emb_bwd_kernel(const T* __restrict__ dout, const int64_t* __restrict__ idx,
                                                       float* __restrict__ dW, long N, int D, float scale,
-                                                      int* __restrict__ flag) {
+                                                      int* __restrict__ flag, long V) {
   // one wave per (row n, 256-column chunk): lane l adds column chunk*256 + 4l .. +3
   const int lane = threadIdx.x & 63;
   const int nchunk = (D + 255) / 256;
@@ -60,6 +62,7 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const T* __restrict__ dout
     if (c >= D) continue;
     const int64_t r = idx[n];
     if (r < 0) continue;              // zero row of the forward: no gradient
+    if (!SPA_DBG_OK(r, V)) continue;  // debug build: a token id inside the table
     if (flag && c == 0) flag[r] = 1;  // row touched (every writer stores the same value)
     float* dst = dW + r * D + c;
     const T* src = dout + n * D + c;
@@ -134,7 +137,7 @@ at::Tensor emb_fwd(const at::Tensor& W, const at::Tensor& idx, const c10::option
 #define EL(T, P)                                                                                             \
   emb_fwd_kernel<T, P><<<grid, 256, 0, st>>>((const T*)W.data_ptr(), ix.data_ptr<int64_t>(),                 \
                                              P ? (const T*)pos->data_ptr() : nullptr, (T*)out.data_ptr(), N, D, \
-                                             T_, (float)scale)
+                                             T_, (float)scale, (long)W.size(0))
   if (W.scalar_type() == at::kBFloat16) { if (pos) EL(bf16, true); else EL(bf16, false); }
   else if (W.scalar_type() == at::kFloat) { if (pos) EL(float, true); else EL(float, false); }
   else TORCH_CHECK(false, "embedding: bf16/fp32 only");
@@ -159,10 +162,10 @@ at::Tensor emb_bwd(const at::Tensor& dout_, const at::Tensor& idx, int64_t V, do
     const int grid = (int)std::min<long>((nw + 3) / 4, 16384);
     if (dout.scalar_type() == at::kBFloat16)
       emb_bwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dout.data_ptr(), ix.data_ptr<int64_t>(),
-                                                 acc.data_ptr<float>(), N, D, (float)scale, nullptr);
+                                                 acc.data_ptr<float>(), N, D, (float)scale, nullptr, V);
     else
       emb_bwd_kernel<float><<<grid, 256, 0, st>>>(dout.data_ptr<float>(), ix.data_ptr<int64_t>(),
-                                                  acc.data_ptr<float>(), N, D, (float)scale, nullptr);
+                                                  acc.data_ptr<float>(), N, D, (float)scale, nullptr, V);
     SPA_LAUNCH_CHECK();
   }
   if (dtype_like.scalar_type() == at::kFloat) return acc;
@@ -207,11 +210,11 @@ void emb_bwd_into(const at::Tensor& dout_, const at::Tensor& idx, double scale, 
   int* flag = sc.second.data_ptr<int>();
   if (out.scalar_type() == at::kBFloat16) {
     emb_bwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dout.data_ptr(), ix.data_ptr<int64_t>(), acc, N, D,
-                                               (float)scale, flag);
+                                               (float)scale, flag, V);
     emb_flush_kernel<bf16><<<fgrid, 256, 0, st>>>(acc, flag, ix.data_ptr<int64_t>(), (bf16*)out.data_ptr(), N, D);
   } else if (out.scalar_type() == at::kFloat) {
     emb_bwd_kernel<float><<<grid, 256, 0, st>>>(dout.data_ptr<float>(), ix.data_ptr<int64_t>(), acc, N, D,
-                                                (float)scale, flag);
+                                                (float)scale, flag, V);
     emb_flush_kernel<float><<<fgrid, 256, 0, st>>>(acc, flag, ix.data_ptr<int64_t>(), out.data_ptr<float>(), N, D);
   } else {
     TORCH_CHECK(false, "emb_bwd_into: bf16/fp32");

@@ -15,6 +15,8 @@
 // to_em = 0: y[j] = x[expert-major position of j]   (combine side; also the backward)
 #include "spa_common.h"
 
+SPA_DEBUG_TU("ep.hip")
+
 namespace spa {
 
 constexpr int kRegroupMaxSeg = 1024;
@@ -80,6 +82,8 @@ __global__ __launch_bounds__(256) void ep_regroup_kernel(const char* __restrict_
   const int s = seg / El, e = seg % El;
   const long dest = (long)em_k[e * P + s] + (j - sm[seg]);
   const long src_row = to_em ? j : dest, dst_row = to_em ? dest : j;
+  // debug build: the counts sum to R, so every row lands in a segment and every destination exists
+  if (!(SPA_DBG_OK(seg, nseg) & SPA_DBG_OK(dest, R))) return;
   const char* src = x + src_row * (long)row_bytes;
   char* dst = y + dst_row * (long)row_bytes;
   for (int o = lane * 16; o < row_bytes; o += 64 * 16)

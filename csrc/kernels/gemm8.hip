@@ -44,6 +44,8 @@
 #include <tuple>
 #include <vector>
 
+SPA_DEBUG_TU("gemm8.hip")
+
 namespace spa {
 
 namespace g8 {
@@ -232,6 +234,10 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     k0 = __builtin_amdgcn_readfirstlane(offsets[e]);
     kend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
   }
+  // debug build: the tile -> (expert, row tile) scan and the group offsets name real rows
+  SPA_DBG_CHECK(e, E);
+  SPA_DBG_ASSERT(offsets[e] >= 0 && offsets[e] <= offsets[e + 1], offsets[e], offsets[e + 1]);
+  SPA_DBG_ASSERT(MODE == 2 ? kend <= a_rows && kend <= b_rows : mend <= a_rows && m0 < mend, MODE == 2 ? kend : mend, a_rows);
   const int n0 = nt * BN;
   const int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -491,7 +497,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
           for (int j = 0; j < 2; ++j) {
             const long gm = m0 + mh * 128 + wm * 64 + 16 * i + (lane & 15);
             const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
-            if (gm < M && gn < N) *reinterpret_cast<f32x4*>(Cf + gm * ldc + gn) = acc[mh * 4 + i][nh * 2 + j];
+            if (gm < M && gn < N && SPA_DBG_OK(gn + 3, ldc)) *reinterpret_cast<f32x4*>(Cf + gm * ldc + gn) = acc[mh * 4 + i][nh * 2 + j];
           }
     return;
   }
@@ -523,7 +529,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
       const long gm = m0 + mh * 128 + r;
       const int gn = n0 + ch * 8;
-      if ((MODE == 2 ? gm < M : gm < mend) && gn < N) {
+      if ((MODE == 2 ? gm < M : gm < mend) && gn < N && SPA_DBG_OK(gm, M) & SPA_DBG_OK(gn + 7, ldc)) {
         bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * RS + ch * 16);
         bf16* cp = Cp + gm * ldc + gn;
         if (accumulate) {

@@ -27,6 +27,8 @@
 #include "act_common.h"
 #include "gemm_common.h"
 
+SPA_DEBUG_TU("gemm8_fp8.hip")
+
 namespace spa {
 
 namespace g8f {
@@ -128,6 +130,11 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
     kend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
   }
   const int n0 = nt * BN;
+  // debug build: the tile -> (expert, row tile) scan and the group offsets name real rows
+  SPA_DBG_CHECK(e, E);
+  SPA_DBG_ASSERT(offsets[e] >= 0 && offsets[e] <= offsets[e + 1], offsets[e], offsets[e + 1]);
+  // (WG: the token range runs along the rows of the transposed K-contiguous images, stride lda / ldb)
+  SPA_DBG_ASSERT(WG ? kend <= lda && kend <= ldb : mend <= a_rows && m0 < mend, WG ? kend : mend, WG ? lda : a_rows);
   const uint8_t* Bp = WG ? B : B + e * strideB;
   const int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -284,7 +291,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
             for (int j = 0; j < 2; ++j) {
               const long gm = m0 + mh * 128 + wm * 64 + 16 * i + (lane & 15);
               const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
-              if (gm < M && gn < N) {
+              if (gm < M && gn < N && SPA_DBG_OK(gn + 3, N)) {
                 f32x4 v = acc[mh * 4 + i][nh * 2 + j];
                 f32x4* cp = reinterpret_cast<f32x4*>(Cf + gm * N + gn);
                 if (accumulate) v += *cp;
@@ -322,7 +329,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
       const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
       const long gm = m0 + mh * 128 + r;
       const int gn = n0 + ch * 8;
-      if (gm < mlim && gn < N) {
+      if (gm < mlim && gn < N && SPA_DBG_OK(gn + 7, N)) {
         bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * RS + ch * 16);
         bf16* cp = Cb + gm * N + gn;
         if (accumulate) {

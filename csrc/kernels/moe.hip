@@ -15,6 +15,8 @@
 #include "spa_common.h"
 #include "gemm_common.h"
 
+SPA_DEBUG_TU("moe.hip")
+
 namespace spa {
 
 // --------------------------------------------------------------------------- router
@@ -118,11 +120,13 @@ __global__ __launch_bounds__(256) void moe_scatter_kernel(const int* __restrict_
 // --------------------------------------------------------------------------- gather / combine
 // rows are moved as 16-byte units (bf16 or fp32 rows alike): nv = row_bytes / 16
 __global__ __launch_bounds__(256) void gather_rows_kernel(const uint4* __restrict__ x, const int* __restrict__ perm,
-                                                          uint4* __restrict__ out, int rows, int nv, int div) {
+                                                          uint4* __restrict__ out, int rows, int nv, int div,
+                                                          long x_rows) {
   const long total = (long)rows * nv;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long r = i / nv;
     const int c = i % nv;
+    if (!SPA_DBG_OK(perm[r] / div, x_rows)) continue;   // debug build: a routed row of x
     out[r * nv + c] = x[(long)(perm[r] / div) * nv + c];
   }
 }
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint4* __restric
 template <typename T>
 __global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ yp, const int* __restrict__ inv,
                                                       const float* __restrict__ w, T* __restrict__ y, int N, int D,
-                                                      int k) {
+                                                      int k, long yrows) {
   const int dv = D / 8;
   const long total = (long)N * dv;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -139,6 +143,7 @@ __global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ yp, 
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < k; ++j) {
       const float wj = w ? w[n * k + j] : 1.f;
+      if (!SPA_DBG_OK(inv[n * k + j], yrows)) continue;   // debug build: a row of yp
       float v[8];
       load8(yp + (long)inv[n * k + j] * D + c, v);
 #pragma unroll
@@ -156,6 +161,7 @@ __global__ __launch_bounds__(256) void combine_dw_kernel(const T* __restrict__ d
   const int lane = threadIdx.x & 63;
   if (a >= N * k) return;
   const long n = a / k;
+  if (!SPA_DBG_OK(inv[a], N * k)) return;   // debug build: inv is a permutation of the assignments
   const T* yr = yp + (long)inv[a] * D;
   const T* dr = dy + n * D;
   float acc = 0.f;
@@ -180,6 +186,7 @@ __global__ __launch_bounds__(256) void scatter_grad_kernel(const T* __restrict__
     const long r = i / dv;
     const int c = (i % dv) * 8;
     const int a = perm[r];
+    if (!SPA_DBG_OK(a, rows)) continue;   // debug build: perm is a permutation of the assignments
     const float wa = w[a];
     float v[8];
     load8(g + (long)(a / k) * D + c, v);
@@ -250,6 +257,8 @@ void grouped_gemm_kernel(
     mt = s_mt;
     m0 = offsets[e] + mt * BM;
     mend = offsets[e + 1];
+    SPA_DBG_CHECK(e, E);
+    SPA_DBG_ASSERT(m0 < mend && mend <= M, m0, mend);   // debug build: a live tile of expert e
     Bp = B + e * strideB;
   } else {
     const int nmt = (M + BM - 1) / BM;
@@ -477,7 +486,7 @@ at::Tensor moe_gather(const at::Tensor& x_, const at::Tensor& perm, int64_t div)
   const int nv = D * (int)x.element_size() / 16;
   const int grid = (int)std::min<long>(((long)rows * nv + 255) / 256, 16384);
   gather_rows_kernel<<<grid, 256, 0, stream()>>>((const uint4*)x.data_ptr(), perm.data_ptr<int>(),
-                                                 (uint4*)out.data_ptr(), rows, nv, div);
+                                                 (uint4*)out.data_ptr(), rows, nv, div, (long)x.size(0));
   SPA_LAUNCH_CHECK();
   return out;
 }
@@ -493,10 +502,10 @@ at::Tensor moe_combine(const at::Tensor& yp_, const at::Tensor& inv, const c10::
   const float* wp = w ? w->data_ptr<float>() : nullptr;
   if (yp.scalar_type() == at::kBFloat16)
     combine_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)yp.data_ptr(), inv.data_ptr<int>(), wp,
-                                                     (bf16*)y.data_ptr(), N, D, k);
+                                                     (bf16*)y.data_ptr(), N, D, k, (long)yp.size(0));
   else
     combine_kernel<float><<<grid, 256, 0, stream()>>>(yp.data_ptr<float>(), inv.data_ptr<int>(), wp,
-                                                      y.data_ptr<float>(), N, D, k);
+                                                      y.data_ptr<float>(), N, D, k, (long)yp.size(0));
   SPA_LAUNCH_CHECK();
   return y;
 }

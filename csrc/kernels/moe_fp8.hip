@@ -21,6 +21,8 @@
 // moe.hip), XCD-remapped tile order.
 #include "spa_common.h"
 
+SPA_DEBUG_TU("moe_fp8.hip")
+
 namespace spa {
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -202,6 +204,9 @@ __global__ __launch_bounds__(256) void quant_t_fp8_seg_kernel(const bf16* __rest
     if (poff[mid] <= p0) lo = mid; else hi = mid;
   }
   const long src0 = offsets[lo] + (p0 - poff[lo]), send = offsets[lo + 1];
+  // debug build: the padded segment of expert lo covers this block and starts at a real token
+  SPA_DBG_ASSERT(poff[lo] <= p0 && p0 < poff[lo + 1] && offsets[lo] <= offsets[lo + 1], p0, poff[lo + 1]);
+  SPA_DBG_ASSERT(poff[lo + 1] - poff[lo] >= offsets[lo + 1] - offsets[lo], poff[lo + 1] - poff[lo], offsets[lo + 1] - offsets[lo]);
   const int c8 = (tid & 15) * 8, rg = tid >> 4;
   const int KB = C / 128;
   float v[8][8];
@@ -336,6 +341,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
   const int m0 = WG ? mt * BM : offsets[e] + mt * BM, mend = WG ? Mw : offsets[e + 1];
   const int n0 = nt * BN;
   const long kbeg = WG ? offsets[e] : 0, kstop = WG ? offsets[e + 1] : K;
+  SPA_DBG_ASSERT(m0 < mend && kbeg <= kstop, m0, mend);   // debug build: a live tile of expert e
   const long lda = WG ? ld : K;
   const uint8_t* Bp = WG ? B : B + e * strideB;
   uint4 ra[CA], rb[CB];

@@ -15,6 +15,8 @@
 // so there is no host sync. ignore_index rows get loss 0 and zero gradient.
 #include "spa_common.h"
 
+SPA_DEBUG_TU("xent.hip")
+
 namespace spa {
 
 // Block-wide (max, sum exp(x - max), sum x) of one row x[0..V), every thread gets the result.
@@ -101,6 +103,7 @@ __global__ __launch_bounds__(256) void xent_kernel(T* __restrict__ logits, const
   const int row = blockIdx.x;
   T* x = logits + (long)row * ld;
   const int64_t y = tgt[row];
+  SPA_DBG_ASSERT(y == ignore_index || (y >= 0 && y < V), y, V);   // debug build: a real class or ignored
   float M, S, SX;
   int h0, nv;
   row_stats<T, VEC>(x, V, M, S, SX, h0, nv, red_m, red_s, red_x);

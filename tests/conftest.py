@@ -19,3 +19,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _device_bounds_guards():
+    """In a debug-bounds build (SPA_EXT_SO=ab/_C_dbg.so with SPA_DEBUG_SYNC=1, see
+    tests/test_debug_bounds_gpu.py) fail any test after which a device guard recorded a violation,
+    including ones reached through torch.ops.spa directly (not via the checked ops() wrapper)."""
+    yield
+    if os.environ.get("SPA_DEBUG_SYNC") != "1" or not os.environ.get("SPA_EXT_SO"):
+        return
+    from solvingpapers_amd.ops import _ext
+    if _ext.debug_bounds_enabled():
+        rep = _ext.debug_bounds_report(True)
+        assert rep == "", f"device bounds guard fired:\n{rep}"

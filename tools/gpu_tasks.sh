@@ -31,6 +31,8 @@
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 #   dkdv5          dS-path GPU tests (incl. the v5 dK/dV kernel), LLaMA-shape ABBA SPA_ATTN_DKDV5=1, kernel times
 #   dkdv5-var      dkdv5 variants vs dkdv3 (ABBA, one process) + stamp profiles of dkdv3 / dkdv5 variants
+#   dbgbounds      debug-bounds build (device guards) over the ragged-shape GPU cases
+#   gradprec [N]   bf16-vs-fp32 gradient accumulation: 8B-width error test + N-step loss-curve A/B
 #   rccl           world-1 RCCL test (every collective path) + headline ABBA with TENSILE_STREAMK_DATA_PARALLEL=1
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -78,6 +80,16 @@ rccl)
     else run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2; fi
     echo "$arm streamk_dp $(grep -ho '"value": [0-9.]*' ${O}_$arm.log)"
   done ;;
+dbgbounds)
+  # debug-bounds build (ab/_C_dbg.so) over the ragged-shape GPU cases; guards must stay silent
+  run 900 ${O}_pytest.log python -u -m pytest tests/test_debug_bounds_gpu.py -x -v -s -p no:cacheprovider --timeout 900 --timeout-method thread
+  grep -h "passed\|failed\|SPA_DEBUG_BOUNDS\|Error" ${O}_pytest.log | cut -c1-300 | tail -20 ;;
+gradprec)
+  # bf16 vs fp32 gradient accumulation: the 8B-width GPU test, then the loss-curve A/B
+  run 300 ${O}_pytest.log python -u -m pytest tests/test_grad_precision_gpu.py -x -v -s -p no:cacheprovider --timeout 240 --timeout-method thread
+  grep -h "rel_err\|passed\|failed" ${O}_pytest.log | cut -c1-900
+  run 900 ${O}_curve.log python -u tools/grad_precision.py --mode curve --steps ${1:-500}
+  grep -h summary ${O}_curve.log ;;
 start)
   run 300 ${O}_attn.log python -u tools/bench_attn.py
   grep -i 'attn B' ${O}_attn.log | cut -c1-300
