@@ -126,8 +126,13 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint4* __restric
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long r = i / nv;
     const int c = i % nv;
-    if (!SPA_DBG_OK(perm[r] / div, x_rows)) continue;   // debug build: a routed row of x
-    out[r * nv + c] = x[(long)(perm[r] / div) * nv + c];
+    const int src = perm[r];
+    if (src < 0) {            // no source row (EP capacity maps: an empty block slot): zeros
+      out[r * nv + c] = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    if (!SPA_DBG_OK(src / div, x_rows)) continue;   // debug build: a routed row of x
+    out[r * nv + c] = x[(long)(src / div) * nv + c];
   }
 }
 // y[n] = sum_j w[n, j] * yp[inv[n*k + j]]; also usable for the dX of the gather (w = 1)
@@ -475,10 +480,13 @@ std::vector<at::Tensor> moe_permute(const at::Tensor& idx_, int64_t E) {
   return {perm, inv, offsets, counts};
 }
 
+// out[r] = x[perm[r] / div], or a zero row where perm[r] < 0; rows of any dtype whose byte width
+// is a multiple of 16 (bf16 / fp32 activations, the uint8 fp8 dispatch payload)
 at::Tensor moe_gather(const at::Tensor& x_, const at::Tensor& perm, int64_t div) {
   auto x = x_.contiguous();
   const int D = x.size(-1);
-  TORCH_CHECK(D % 8 == 0 && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat));
+  TORCH_CHECK(x.dim() == 2 && (long)D * x.element_size() % 16 == 0, "moe_gather: [rows, D] with 16-byte rows");
+  TORCH_CHECK(perm.scalar_type() == at::kInt && perm.is_contiguous(), "moe_gather: int32 map");
   const int rows = perm.numel();
   DeviceGuard g(x.device());
   auto out = at::empty({rows, D}, x.options());

@@ -74,6 +74,9 @@ class DSV3Config:
     n_dense_layers: int = 0         # leading layers with a dense SwiGLU FFN
     dense_hidden: int = 0
     moe_fp8: bool = False           # routed-expert fwd/dX GEMMs in OCP e4m3 (BASELINE config #5)
+    # EP dispatch: 0 = exact split sizes (one host sync per MoE layer per micro-batch); > 0 = the
+    # host-sync-free padded dispatch with this capacity factor (parallel/expert_parallel.py)
+    ep_capacity: float = 0.0
     fp8_linears: bool = False       # dense projections too (MLA, shared / dense FFN): the V3 recipe
     noisy_topk: bool = False        # ref (deepseekv3.ipynb:390,1026-1039): + softplus(noise(x)) * N(0,1)
     aux_free: bool = True
@@ -370,6 +373,7 @@ class MoE(tnn.Module):
         self.balance_group = None      # DP group for the counts all-reduce (set by the trainer)
         self.last_counts = None
         self._pending_bias = []        # (work, load): bias updates whose counts all-reduce is in flight
+        self.cap_state = SimpleNamespace(rows=None)   # capacity-mode EP: this layer's block rows
 
     @torch.no_grad()
     def reset_parameters(self, std, g):
@@ -415,7 +419,8 @@ class MoE(tnn.Module):
         c = self.c
         self.finish_pending()                   # last step's bias updates before this routing
         idx, w = route(self._logits(x2), c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
-        st = ep_stage_prepare(x2, idx, w, c.n_experts, self.ep_group, self._fp8(x2), self.w13)
+        st = ep_stage_prepare(x2, idx, w, c.n_experts, self.ep_group, self._fp8(x2), self.w13,
+                              capacity=c.ep_capacity, cap_state=self.cap_state)
         st.x2, st.idx, st.sh = x2, idx, None
         if c.aux_free and self.training:
             # the bias moves right after this routing (the reference updates it after every
@@ -729,12 +734,51 @@ class DeepSeekV3(tnn.Module):
         n, _ = rms_norm(delta, self.norm_f, c.norm_eps, residual=res)
         return n
 
+    # ---- capacity-mode EP (DSV3Config.ep_capacity > 0): no host sync inside the layers; one read
+    # of the overflow flags per forward, and an exact re-run with doubled capacity on overflow
+    def _capacity_run(self, fn, *args):
+        if not self.c.ep_capacity > 0:
+            return fn(*args)
+        from ..parallel.expert_parallel import capacity_overflowed
+        capacity_overflowed()                   # flags of work outside this forward are not ours
+        snap = self._routing_snapshot()
+        for _ in range(8):
+            out = fn(*args)
+            if not capacity_overflowed():
+                return out
+            self._routing_restore(snap)         # the failed attempt's graph is dropped with `out`;
+            # the layers' capacity states now hold the overflowing loads (x margin): the re-run fits
+        raise RuntimeError("EP capacity dispatch still overflowing after 8 doublings")
+
+    def _routing_snapshot(self):
+        # outstanding bias updates of the previous step land first (each layer's routing would
+        # apply them anyway), so the snapshot is the bias every attempt starts from
+        self.finish_pending_updates()
+        rng = (torch.get_rng_state(), torch.cuda.get_rng_state() if torch.cuda.is_available() and
+               self.embed.is_cuda else None)
+        return [(m, m.routing_bias.clone()) for m in self.moe_layers()], rng
+
+    @torch.no_grad()
+    def _routing_restore(self, snap):
+        layers, (cpu_rng, gpu_rng) = snap
+        for m, bias in layers:
+            while m._pending_bias:                    # the failed attempt's async load all-reduces
+                work, _ = m._pending_bias.pop()
+                work.wait()
+            m.routing_bias.copy_(bias)
+        torch.set_rng_state(cpu_rng)
+        if gpu_rng is not None:
+            torch.cuda.set_rng_state(gpu_rng)
+
     def forward_pair(self, ids0, targets0, ids1, targets1):
         """loss(micro-batch 0) + loss(micro-batch 1) with the two run layer-interleaved
         (hidden_pair): the same values and gradients as two forward() calls, with each MoE
         layer's all-to-alls overlapped by the other micro-batch's compute. Training only.
         Aux-free balancing keeps the sequential semantics: each MoE layer moves its routing bias
         right after micro-batch 0's routing (MoE.stage_prepare), before micro-batch 1 routes."""
+        return self._capacity_run(self._forward_pair, ids0, targets0, ids1, targets1)
+
+    def _forward_pair(self, ids0, targets0, ids1, targets1):
         final, x0s = self.hidden_pair(ids0, ids1)
         D = self.c.dim
         loss = None
@@ -756,6 +800,9 @@ class DeepSeekV3(tnn.Module):
         return linear(n, self.embed)
 
     def forward(self, ids, targets=None):
+        return self._capacity_run(self._forward, ids, targets)
+
+    def _forward(self, ids, targets=None):
         n, x0 = self.hidden(ids)
         if targets is None:
             return self.logits(n)

@@ -252,10 +252,10 @@ def all_to_all_counts(recv: torch.Tensor, counts: torch.Tensor, group):
 # ----------------------------------------------------------------- autograd pieces
 class _Box:
     """Hand-off between a collective's start and finish nodes (forward and backward)."""
-    __slots__ = ("work", "bwork", "splits", "group", "dx", "gkeep", "ev", "pay", "recv", "D", "dtype")
+    __slots__ = ("work", "bwork", "splits", "group", "dx", "gkeep", "ev", "pay", "recv", "D", "dtype", "cap")
 
     def __init__(self):
-        self.work = self.bwork = self.dx = self.gkeep = self.ev = self.pay = self.recv = None
+        self.work = self.bwork = self.dx = self.gkeep = self.ev = self.pay = self.recv = self.cap = None
 
 
 class _A2AStart(torch.autograd.Function):

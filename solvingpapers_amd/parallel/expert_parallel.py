@@ -17,15 +17,29 @@ The reference keeps all 8 experts on every replica and runs them in a Python loo
 5. the inverse regroup + all-to-all return the rows; ``combine`` applies the gate
    weights in the original token order.
 
+Capacity mode (``capacity`` > 0, DSV3Config.ep_capacity): no host sync at all. Every rank
+sends every peer a fixed block of C rows (C = capacity x the balanced share A / P, capped at the
+exact bound A / k * min(k, El)), so the exchange sizes are host constants; the slot maps (which
+expert-sorted row goes to which block slot, which received slot lands in which (local expert,
+src) row) are built on the device from the exchanged counts, and the grouped GEMMs take their
+offsets from the device (tiles past the last expert exit). A block that would overflow sets a
+device flag (max over the EP group, async); the model reads the flags once per forward
+(``capacity_overflowed``) -- by then the GPU is still busy with the queued layers -- and re-runs
+the forward with twice the capacity, so results never depend on C. The price is the padded wire
+bytes (P*C rows per rank instead of A).
+
 Expert parameters carry ``p.expert_parallel = True``: DataParallel does not
 all-reduce them across the EP group (each rank holds different experts) and the
 optimizer's grad-norm sums their squares over the EP group.
 """
 from __future__ import annotations
 
+import math
+import os
 from types import SimpleNamespace
 
 import torch
+import torch.distributed as dist
 
 from . import comm
 from ..ops._ext import ops
@@ -114,6 +128,8 @@ class _Fp8DispatchStart(torch.autograd.Function):
         box = ctx.box
         box.bwork.wait()
         dx, box.dx, box.gkeep = box.dx, None, None
+        if box.cap is not None:                 # [P*C] block slots -> expert-sorted rows
+            dx = _map_rows(dx, box.cap.send_back)
         return dx, None
 
 
@@ -129,7 +145,7 @@ class _Fp8DispatchFinish(torch.autograd.Function):
         box.work.wait()
         D = box.D
         KB = D // 128
-        pl = regroup_rows(box.recv, rc, True)
+        pl = regroup_rows(box.recv, rc, True) if box.cap is None else _map_rows(box.recv, box.cap.recv_to)
         box.recv = box.pay = None
         xq_l = pl[:, :D].contiguous().view(torch.float8_e4m3fn)
         sx_l = pl[:, D:D + KB].contiguous()
@@ -153,7 +169,7 @@ class _Fp8DispatchFinish(torch.autograd.Function):
             dq, sd = quant_act_fp8_blk(dh)
         _, wtq, _, swt = quant_weight_fp8_blk(W)
         dxl = grouped_gemm_fp8_blk(dq, sd, wtq, swt, offsets).to(dh.dtype)
-        dxr = regroup_rows(dxl, rc, False)
+        dxr = regroup_rows(dxl, rc, False) if box.cap is None else _map_rows(dxl, box.cap.recv_back)
         box.dx = dxr.new_empty((sum(in_splits), dxr.shape[1]))
         box.gkeep = dxr                       # the source must live until the exchange is done
         box.bwork = comm.all_to_all_single(box.dx, dxr, in_splits, out_splits, box.group, async_op=True)
@@ -181,9 +197,9 @@ class EPPrep:
         return both[0].view(P, El).sum(1).tolist(), both[1].view(P, El)
 
 
-def ep_prepare(idx, n_experts, group):
+def ep_prepare(idx, n_experts, group, to_host=True):
     """Local permutation + the count exchange of a chunk, all on the device; the counts are
-    copied to (pinned) host memory asynchronously."""
+    copied to (pinned) host memory asynchronously (not in capacity mode: ``to_host=False``)."""
     plan = permute(idx, n_experts)
     rank, P = ep_rank_size(group)
     if _local(group, P):
@@ -191,6 +207,8 @@ def ep_prepare(idx, n_experts, group):
     counts = plan.counts.to(torch.int64)
     recv = torch.empty_like(counts)
     comm.all_to_all_counts(recv, counts, group)              # recv[(src, e_local)]
+    if not to_host:
+        return EPPrep(plan, counts, recv)
     both = torch.stack([counts, recv])
     if both.is_cuda:
         host = torch.empty(both.shape, dtype=both.dtype, pin_memory=True)
@@ -199,6 +217,125 @@ def ep_prepare(idx, n_experts, group):
         ev.record()
         return EPPrep(plan, counts, recv, host, ev)
     return EPPrep(plan, counts, recv, both.clone())
+
+
+# ----------------------------------------------------------------------------- capacity mode
+_CAP = {"scale": 1.0, "pending": [], "margin": float(os.environ.get("SPA_EP_CAP_MARGIN", "1.1"))}
+
+
+def capacity_rows(A, P, El, k, cf):
+    """Rows per peer block: cf x the balanced share A / P, rounded up to 16, never above the
+    exact bound (a token sends at most min(k, El) rows to one peer) rounded the same way."""
+    bound = (A // max(k, 1)) * min(k, El)
+    c = min(max(int(math.ceil(cf * A / P)), 1), max(bound, 1))
+    return (c + 15) // 16 * 16
+
+
+def capacity_scale() -> float:
+    """Multiplier on every layer's capacity factor (doubled after each overflow of this process)."""
+    return _CAP["scale"]
+
+
+def capacity_overflowed() -> bool:
+    """Read (and clear) the peer-block loads of the capacity dispatches issued since the last call:
+    ONE host read of the group-max load of each. Each layer's capacity state then tracks its load
+    (rows = max(margin x this load, 0.99 x the previous rows), SPA_EP_CAP_MARGIN default 1.1: a
+    slowly decaying max, so alternating micro-batches with different loads do not flip-flop), and
+    capacities follow the routing instead of a fixed factor. True if any block of any rank
+    overflowed: the caller re-runs the step, which then fits (the same routing against the grown
+    capacities)."""
+    pend, _CAP["pending"] = _CAP["pending"], []
+    if not pend:
+        return False
+    for work, *_ in pend:
+        if work is not None:
+            work.wait()
+    loads = torch.cat([mx for _, mx, _, _ in pend]).tolist()
+    over = False
+    for (_, _, C, state), mx in zip(pend, loads):
+        over |= mx > C
+        if state is not None:
+            want = max(mx * _CAP["margin"], 0.99 * (state.rows or 0))
+            state.rows = max(16, (int(math.ceil(want)) + 15) // 16 * 16)
+        elif mx > C:
+            grow_capacity()
+    return over
+
+
+def grow_capacity(factor: float = 2.0):
+    _CAP["scale"] *= factor
+
+
+def _cap_flag(counts, P, El, C, group, state):
+    """This rank's largest peer block (rows), max over the group (async); read by
+    :func:`capacity_overflowed` against the capacity C it was sent with."""
+    mx = counts.view(P, El).sum(1).max().to(torch.int32).reshape(1)
+    work = None
+    if group is not None and not comm.is_proxy(group):
+        work = comm.all_reduce(mx, group, async_op=True, op=dist.ReduceOp.MAX)
+    _CAP["pending"].append((work, mx, C, state))
+
+
+def _cap_send_index(offsets, P, El, C, A):
+    """Slot of every expert-sorted row in the [P*C] send blocks (its peer's block, in expert order),
+    or the dummy slot P*C for rows past a block's capacity. Device only."""
+    starts = offsets.long()[::El].contiguous()          # [P + 1]: first row of each peer's experts, A
+    r = torch.arange(A, device=offsets.device)
+    p = torch.searchsorted(starts[1:].contiguous(), r, right=True).clamp_(max=P - 1)
+    pos = r - starts[p]
+    return torch.where(pos < C, p * C + pos, torch.full_like(pos, P * C))
+
+
+def _cap_recv_dest(rc, C):
+    """[P*C] received slots (src-major blocks, each block's rows by local expert) -> row of the
+    (local expert, src)-major layout the grouped GEMMs read, or the dummy P*C for empty slots.
+    Device only (batched searchsorted over the per-source count prefix sums)."""
+    P, El = rc.shape
+    rc = rc.long()
+    cum = rc.cumsum(1)
+    i = torch.arange(C, device=rc.device).expand(P, C).contiguous()
+    e = torch.searchsorted(cum.contiguous(), i, right=True)
+    valid = i < cum[:, -1:]
+    e = e.clamp_(max=El - 1)
+    excl = cum - rc
+    emc = rc.t().reshape(-1)
+    em = (emc.cumsum(0) - emc).view(El, P).t()          # em[s, e]: first row of (e, s)
+    dest = em.gather(1, e) + i - excl.gather(1, e)
+    valid &= dest < P * C                               # only on an overflowing (discarded) attempt
+    return torch.where(valid, dest, torch.full_like(dest, P * C)).reshape(-1)
+
+
+def _map_rows(x, m):
+    """out[j] = x[m[j]], a zero row where m[j] < 0: ONE pass over the rows (csrc/kernels/moe.hip
+    gather_rows_kernel, any 16-byte-multiple row width); the CPU path indexes a zero-padded copy."""
+    if x.is_cuda:
+        return ops().moe_gather(x, m, 1)
+    xz = torch.cat([x, x.new_zeros((1,) + tuple(x.shape[1:]))])
+    return xz[torch.where(m < 0, torch.full_like(m, x.shape[0]), m).long()]
+
+
+class _RowMap(torch.autograd.Function):
+    """Injective row move ``fwd`` (dest j <- src fwd[j], -1: zero row); its gradient is the move
+    back along the inverse map ``inv`` (src i <- dest inv[i], -1: no dest). No atomics, no zero fill."""
+
+    @staticmethod
+    def forward(ctx, x, fwd, inv):
+        ctx.inv = inv
+        return _map_rows(x.contiguous(), fwd)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _map_rows(g.contiguous(), ctx.inv), None, None
+
+
+def _cap_maps(slot, n):
+    """From slot[i] (row i -> position in an n-row layout, n = dropped): (gather map of the n-row
+    layout: position <- row or -1, gather map back: row <- position or -1), int32."""
+    A = slot.numel()
+    to = torch.full((n + 1,), -1, dtype=torch.int32, device=slot.device)
+    to.index_copy_(0, slot, torch.arange(A, dtype=torch.int32, device=slot.device))
+    back = torch.where(slot < n, slot, torch.full_like(slot, -1)).to(torch.int32)
+    return to[:n].contiguous(), back
 
 
 class EPStage:
@@ -219,12 +356,18 @@ class EPStage:
     the combine bf16. P == 1: no exchange, the same stages run the local experts."""
 
     def __init__(self):
-        self.prep = self.xp = self.w = self.box = self.handle = self.chandle = None
+        self.prep = self.xp = self.w = self.box = self.handle = self.chandle = self.cap = None
 
 
-def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None):
+def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None, capacity=0.0, cap_state=None):
+    """``capacity`` > 0: host-sync-free dispatch (module docstring), issued right here -- the
+    exchange sizes are host constants, so nothing waits for the counts. ``cap_state``: the layer's
+    capacity tracker (``.rows``, set from the loads it has seen; None on first use -> ``capacity``
+    x the balanced share)."""
     st = EPStage()
-    st.prep = ep_prepare(idx, n_experts, group)
+    rank, P = ep_rank_size(group)
+    cap = capacity > 0 and not _local(group, P)
+    st.prep = ep_prepare(idx, n_experts, group, to_host=not cap)
     st.w = w
     st.group = group
     st.n_experts = n_experts
@@ -243,6 +386,41 @@ def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None):
         box.D, box.dtype, box.group = D, x.dtype, group
         st.box = box
     st.ev = None
+    if cap:
+        El = n_experts // P
+        A = idx.numel()
+        C = capacity_rows(A, P, El, idx.shape[-1] if idx.dim() > 1 else 1, capacity * capacity_scale())
+        if cap_state is not None and getattr(cap_state, "rows", None):
+            C = cap_state.rows
+        st.cap = SimpleNamespace(C=C, P=P, El=El)
+        # send: block slot <- expert-sorted row (send_to), and back (send_back); receive: (local
+        # expert, src) row <- received slot (recv_to), and back (recv_back)
+        st.cap.send_to, st.cap.send_back = _cap_maps(_cap_send_index(st.prep.plan.offsets, P, El, C, A), P * C)
+        rc = st.prep.recv.view(P, El)
+        st.cap.recv_to, st.cap.recv_back = _cap_maps(_cap_recv_dest(rc, C), P * C)
+        _cap_flag(st.prep.counts, P, El, C, group, cap_state)
+        per_e = rc.sum(0)
+        st.rc_dev = rc
+        # clamped to the P*C rows that exist: an overflowing attempt (re-run by the model) must still
+        # never index past the buffers
+        st.lplan = SimpleNamespace(offsets=torch.cat([per_e.new_zeros(1), per_e.cumsum(0)]).clamp_(max=P * C)
+                                   .to(torch.int32))
+        eq = [C] * P
+        st.splits = (eq, eq)
+        if st.fp8_dispatch:
+            st.box.pay = _map_rows(st.box.pay, st.cap.send_to)
+            st.box.splits, st.box.cap = (eq, eq), st.cap
+        else:
+            send = _RowMap.apply(st.xp, st.cap.send_to, st.cap.send_back)
+        if x.is_cuda:
+            st.ev = torch.cuda.Event()
+            st.ev.record()
+        if st.fp8_dispatch:
+            st.box.ev = st.ev
+            st.token = _Fp8DispatchStart.apply(st.xp, st.box)
+        else:
+            st.handle = comm.a2a_start(send, eq, eq, group, after=st.ev)
+        return st
     if not local and x.is_cuda:
         st.ev = torch.cuda.Event()
         st.ev.record()
@@ -251,7 +429,7 @@ def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None):
 
 def ep_stage_dispatch(st):
     rank, P = ep_rank_size(st.group)
-    if _local(st.group, P):
+    if _local(st.group, P) or st.cap is not None:   # capacity mode: issued by ep_stage_prepare
         return st
     El = st.n_experts // P
     send_splits, rc = st.prep.splits(P, El)                  # the single host sync of the chunk
@@ -280,13 +458,18 @@ def ep_stage_experts(st, W13, W2, act="silu"):
     El = st.n_experts // P
     assert El * P == st.n_experts and W13.shape[0] == El, "experts must divide evenly over the EP group"
     send_splits, recv_splits = st.splits
+    cap = st.cap
     if st.fp8_dispatch:
         h13 = _Fp8DispatchFinish.apply(st.token, W13, st.rc_dev, st.lplan.offsets, st.box)
+    elif cap is not None:
+        xl = _RowMap.apply(comm.a2a_finish(st.handle), cap.recv_to, cap.recv_back)
+        h13 = grouped_linear(xl, W13, st.lplan, st.fp8)
     else:
         xl = _Regroup.apply(comm.a2a_finish(st.handle), st.rc_dev, True)   # (src, e) -> (e, src) rows
         h13 = grouped_linear(xl, W13, st.lplan, st.fp8)
     h = glu(h13, act)
-    yr = _Regroup.apply(grouped_linear(h, W2, st.lplan, st.fp8), st.rc_dev, False)
+    yl = grouped_linear(h, W2, st.lplan, st.fp8)
+    yr = _RowMap.apply(yl, cap.recv_back, cap.recv_to) if cap is not None else _Regroup.apply(yl, st.rc_dev, False)
     st.chandle = comm.a2a_start(yr, send_splits, recv_splits, st.group)
     return st
 
@@ -294,25 +477,28 @@ def ep_stage_experts(st, W13, W2, act="silu"):
 def ep_stage_finish(st):
     rank, P = ep_rank_size(st.group)
     yp = st.yp if _local(st.group, P) else comm.a2a_finish(st.chandle)
+    if st.cap is not None:                                   # [P*C] block slots -> expert-sorted rows
+        yp = _RowMap.apply(yp, st.cap.send_back, st.cap.send_to)
     y = combine(yp, st.w, st.prep.plan)
-    st.xp = st.yp = st.handle = st.chandle = st.box = st.token = None
+    st.xp = st.yp = st.handle = st.chandle = st.box = st.token = st.cap = None
     return y
 
 
-def ep_run(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
+def ep_run(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False, capacity=0.0, cap_state=None):
     """Dispatch -> local grouped experts -> combine of one chunk, stage after stage (blocking).
     Returns (y, plan)."""
-    st = ep_stage_prepare(x, idx, w, n_experts, group, fp8, W13)
+    st = ep_stage_prepare(x, idx, w, n_experts, group, fp8, W13, capacity, cap_state)
     ep_stage_experts(ep_stage_dispatch(st), W13, W2, act)
     plan = st.prep.plan
     return ep_stage_finish(st), plan
 
 
-def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False):
+def ep_moe_ffn(x, idx, w, W13, W2, n_experts, group, act="silu", fp8=False, capacity=0.0):
     """Routed experts under expert parallelism. ``x`` [N, D] local tokens, ``idx``/``w``
     [N, k] local routing over ``n_experts`` global experts; ``W13`` [E/P, 2F, D] and
-    ``W2`` [E/P, D, F] are this rank's experts. Returns (y [N, D], local plan)."""
-    return ep_run(x, idx, w, W13, W2, n_experts, group, act, fp8)
+    ``W2`` [E/P, D, F] are this rank's experts. ``capacity`` > 0: host-sync-free padded
+    dispatch (the caller checks :func:`capacity_overflowed`). Returns (y [N, D], local plan)."""
+    return ep_run(x, idx, w, W13, W2, n_experts, group, act, fp8, capacity)
 
 
 def shard_experts(full_w, rank, P):

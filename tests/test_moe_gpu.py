@@ -487,3 +487,52 @@ def test_forward_pair_matches_two_forwards_gpu(ep, fp8):
         assert (torch.uint8 in seen) == fp8                   # fp8 payload on the default path
 
 
+
+
+@pytest.mark.parametrize("fp8,cap", [(False, 1.25), (True, 1.25), (False, 0.05)])
+def test_ep_capacity_dispatch_matches_exact_gpu(fp8, cap):
+    """Host-sync-free EP dispatch (DSV3Config.ep_capacity) on the GPU kernels, one EP=8 rank's
+    share on the stand-in group: padded [P*C] send blocks built on the device, the grouped GEMMs
+    over device offsets with dead rows past them, the fp8 payload packed the same way == the
+    exact-split path, loss and every gradient; no split-size host read. cap 0.05 overflows and
+    must re-run (exactly) with doubled capacity."""
+    from dataclasses import replace
+    from solvingpapers_amd.models import deepseekv3 as ds
+    from solvingpapers_amd.parallel import comm, expert_parallel as ep
+    from solvingpapers_amd.utils.flat import FlatParams
+    from solvingpapers_amd.utils.grad import next_generation
+    c = ds.config("dsv3_tiny", dim=256, n_heads=4, n_experts=16, top_k=2, expert_hidden=256, dense_hidden=512,
+                  n_layers=3, n_dense_layers=1, dropout=0.0, attn_dropout=0.0, aux_free=True, moe_fp8=fp8)
+    grp = comm.ProxyGroup(8, dev)
+    gen = torch.Generator().manual_seed(4)
+    ids = torch.randint(0, c.vocab_size, (2, 129), generator=gen).to(dev)
+    res = []
+    real_splits = ep.EPPrep.splits
+    calls = []
+    for capf in (0.0, cap):
+        m = ds.DeepSeekV3(replace(c, ep_capacity=capf), device=dev, dtype=torch.bfloat16, seed=2, ep_group=grp)
+        if capf:
+            inner = m._forward
+            m._forward = lambda *a, _r=inner, **k: (calls.append(1), _r(*a, **k))[1]
+        flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.float32)
+        flat.grad.zero_()
+        next_generation()
+        if capf:
+            def no_host_sync(*a, **k):
+                raise AssertionError("capacity mode read the split sizes on the host")
+            ep.EPPrep.splits = no_host_sync
+        try:
+            loss = m(ids[:, :-1], ids[:, 1:])
+            loss.backward()
+        finally:
+            ep.EPPrep.splits = real_splits
+        torch.cuda.synchronize()
+        m.finish_pending_updates()
+        res.append((float(loss), flat.grad.clone(), [l.routing_bias.clone() for l in m.moe_layers()]))
+    assert abs(res[0][0] - res[1][0]) < 1e-3 * abs(res[0][0]), (res[0][0], res[1][0])
+    assert _rel(res[1][1], res[0][1]) < 1e-2
+    for a, b in zip(res[0][2], res[1][2]):
+        assert torch.equal(a, b)
+    # 0.05 overflows once and then fits; 1.25 fits unless this init's routing is skewed past it
+    assert len(calls) == 2 if cap < 0.1 else len(calls) in (1, 2), calls
+    assert all(l.cap_state.rows for l in m.moe_layers())   # capacities now track the loads

@@ -222,9 +222,19 @@ def _moe_inputs():
 
 def _ep_worker(rank, world, port, q, mode="plain"):
     _init(rank, world, port)
+    from dataclasses import replace
     from solvingpapers_amd.models import deepseekv3 as ds
+    from solvingpapers_amd.parallel import expert_parallel as ep
     from solvingpapers_amd.parallel.expert_parallel import shard_experts
     c = _moe_cfg()
+    if mode == "capacity":
+        # host-sync-free padded dispatch; capacity 4 = the exact bound here (never overflows), and
+        # the split-size host read must never happen
+        c = replace(c, ep_capacity=4.0)
+
+        def no_host_sync(*a, **k):
+            raise AssertionError("capacity mode read the split sizes on the host")
+        ep.EPPrep.splits = no_host_sync
     torch.manual_seed(0)
     full = ds.MoE(c)
     full.reset_parameters(0.1, torch.Generator().manual_seed(3))
@@ -240,11 +250,13 @@ def _ep_worker(rank, world, port, q, mode="plain"):
     xr = x[rank].clone().requires_grad_(True)
     y = m(xr)
     (y * gy[rank]).sum().backward()
+    if mode == "capacity":
+        assert not ep.capacity_overflowed()
     q.put((rank, y.detach().numpy(), xr.grad.numpy(), m.w13.grad.numpy(), m.w2.grad.numpy(), m.gate.grad.numpy()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["plain"])
+@pytest.mark.parametrize("mode", ["plain", "capacity"])
 def test_expert_parallel_moe_matches_local(mode):
     """EP=2 (all-to-all dispatch/combine, 2 experts per rank) == one process holding all
     4 experts: outputs, input grads, and each rank's expert grads (which collect the
@@ -338,7 +350,7 @@ def _ep_fp8_inputs():
     return x, idx, w, W13, W2, gy
 
 
-def _ep_fp8_worker(rank, world, port, q):
+def _ep_fp8_worker(rank, world, port, q, capacity=0.0):
     _init(rank, world, port)
     from solvingpapers_amd.parallel.expert_parallel import ep_moe_ffn, shard_experts
     x, idx, w, W13, W2, gy = _ep_fp8_inputs()
@@ -354,14 +366,18 @@ def _ep_fp8_worker(rank, world, port, q):
         seen.append((str(inp.dtype), inp.shape[1] * inp.element_size()))
         return real(out, inp, out_splits, in_splits, group, async_op=async_op, after=after)
     comm.all_to_all_single = spy
-    y, _ = ep_moe_ffn(xr, idx[rank], w[rank], w13, w2, 4, grp, fp8=True)
+    y, _ = ep_moe_ffn(xr, idx[rank], w[rank], w13, w2, 4, grp, fp8=True, capacity=capacity)
     (y * gy[rank]).sum().backward()
     comm.all_to_all_single = real
+    if capacity:
+        from solvingpapers_amd.parallel.expert_parallel import capacity_overflowed
+        assert not capacity_overflowed()
     q.put((rank, y.detach().numpy(), xr.grad.numpy(), w13.grad.numpy(), w2.grad.numpy(), seen))
     dist.destroy_process_group()
 
 
-def test_expert_parallel_fp8_dispatch_matches_local_fp8():
+@pytest.mark.parametrize("capacity", [0.0, 4.0])
+def test_expert_parallel_fp8_dispatch_matches_local_fp8(capacity):
     """fp8 dispatch (e4m3 rows + E8M0 1x128 scales over the all-to-all, fused with the
     block-scaled W13 GEMM) == the single-process block-scaled fp8 MoE: outputs and input grads
     to fp32 rounding; expert grads to the fp8 rounding of the dW operands (the EP path forms dW13
@@ -373,7 +389,7 @@ def test_expert_parallel_fp8_dispatch_matches_local_fp8():
     xs = x.clone().requires_grad_(True)
     ys = [moe_ffn(xs[r], idx[r], w[r], W13r, W2r, fp8=True)[0] for r in range(2)]
     sum((y * gy[r]).sum() for r, y in enumerate(ys)).backward()
-    for rank, y, gx, g13, g2, seen in _run(_ep_fp8_worker, 2):
+    for rank, y, gx, g13, g2, seen in _run(_ep_fp8_worker, 2, capacity):
         # the default EP path's dispatch payload: e4m3 rows + E8M0 scales, 144 B per 128-wide row
         # (128 + 1 scale byte, padded to 16) -- 0.56x a bf16 row; combine and the backward's dX in
         # the activation dtype
@@ -537,3 +553,47 @@ def test_forced_collectives_world1_gloo():
                        timeout=300, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert "RCCL_WORLD1_OK" in r.stdout
+
+
+def _cap_overflow_worker(rank, world, port, q, fp8):
+    """DeepSeekV3 EP=2 with a capacity far below the routed load: every forward overflows first,
+    is re-run with doubled capacity until it fits, and must then equal the exact-split model."""
+    _init(rank, world, port)
+    from dataclasses import replace
+    from solvingpapers_amd.models import deepseekv3 as ds
+    from solvingpapers_amd.parallel import expert_parallel as ep
+    c = ds.config("dsv3_tiny", dim=128, n_experts=4, top_k=2, expert_hidden=128, n_layers=2, n_dense_layers=0,
+                  dropout=0.0, attn_dropout=0.0, moe_fp8=fp8)
+    grp = dist.new_group([0, 1])
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, c.vocab_size, (2, 2, 33), generator=g)[rank]
+    res = {}
+    for cap in (0.0, 0.1):
+        m = ds.DeepSeekV3(replace(c, ep_capacity=cap), seed=3, ep_group=grp)
+        m.train()
+        calls = []
+        real = m._forward
+        m._forward = lambda *a, _r=real, **k: (calls.append(1), _r(*a, **k))[1]
+        loss = m(ids[:, :-1], ids[:, 1:])
+        loss.backward()
+        m.finish_pending_updates()
+        res[cap] = (loss.item(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
+                    [l.routing_bias.clone() for l in m.moe_layers()], len(calls))
+    (l0, g0, b0, n0), (l1, g1, b1, n1) = res[0.0], res[0.1]
+    # the tiny capacity overflowed once; the layers' capacity states then track the loads, so the
+    # re-run fits
+    assert n0 == 1 and n1 == 2, (n0, n1)
+    assert abs(l0 - l1) < 1e-5, (l0, l1)
+    assert g0.keys() == g1.keys()
+    for n in g0:
+        assert torch.allclose(g0[n], g1[n], atol=1e-5, rtol=1e-4), (n, (g0[n] - g1[n]).abs().max())
+    for a, b in zip(b0, b1):                            # the bias moved once, not once per attempt
+        assert torch.equal(a, b)
+    q.put((rank, n1))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_ep_capacity_overflow_reruns_exactly(fp8):
+    out = _run(_cap_overflow_worker, 2, fp8)
+    assert len(out) == 2 and out[0][1] == out[1][1]     # both ranks agreed on every re-run

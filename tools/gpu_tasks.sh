@@ -31,6 +31,7 @@
 #   secondary      ViT-B/16, dsv3_style, dsv3_v3 (bf16 + fp8), Gemma-7B benches
 #   dkdv5          dS-path GPU tests (incl. the v5 dK/dV kernel), LLaMA-shape ABBA SPA_ATTN_DKDV5=1, kernel times
 #   dkdv5-var      dkdv5 variants vs dkdv3 (ABBA, one process) + stamp profiles of dkdv3 / dkdv5 variants
+#   epcap [CF]     capacity-mode EP dispatch: MoE GPU tests + EP=8 proxy one-by-one exact vs capacity
 #   dbgbounds      debug-bounds build (device guards) over the ragged-shape GPU cases
 #   gradprec [N]   bf16-vs-fp32 gradient accumulation: 8B-width error test + N-step loss-curve A/B
 #   rccl           world-1 RCCL test (every collective path) + headline ABBA with TENSILE_STREAMK_DATA_PARALLEL=1
@@ -80,6 +81,13 @@ rccl)
     else run 400 ${O}_$arm.log python -u bench.py --steps 6 --warmup 2; fi
     echo "$arm streamk_dp $(grep -ho '"value": [0-9.]*' ${O}_$arm.log)"
   done ;;
+epcap)
+  # host-sync-free (capacity) EP dispatch: MoE GPU tests, then the EP=8 proxy at accum-1 form
+  run 400 ${O}_pytest.log python -u -m pytest tests/test_moe_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  run 600 ${O}_proxy.log python -u tools/overlap_proxy.py --which ep --layers 2 --capacity ${1:-1.25}
+  run 600 ${O}_proxyb.log python -u tools/overlap_proxy.py --which ep --layers 2 --capacity ${1:-1.25} --balanced
+  grep -hv amdgpu.ids ${O}_proxy.log ${O}_proxyb.log | cut -c1-1200 ;;
 dbgbounds)
   # debug-bounds build (ab/_C_dbg.so) over the ragged-shape GPU cases; guards must stay silent
   run 900 ${O}_pytest.log python -u -m pytest tests/test_debug_bounds_gpu.py -x -v -s -p no:cacheprovider --timeout 900 --timeout-method thread

@@ -125,21 +125,38 @@ def ep_moe(a):
     GEMMs), two micro-batches of ``--tokens`` tokens per step, fwd + bwd. Arms:
       off / blocking   the micro-batches one after the other (forward()), collectives skipped /
                        modelled and waited at once
-      pair:off / pair:overlap   DeepSeekV3.forward_pair (layer-interleaved micro-batches)"""
+      pair:off / pair:overlap   DeepSeekV3.forward_pair (layer-interleaved micro-batches)
+    --capacity CF adds the accum-1 comparison (micro-batches one after the other, collectives
+    modelled and overlapped as far as each path allows):
+      one:overlap     exact split sizes: one host sync per MoE layer (the pipeline drains there)
+      cap:overlap / cap:off   the host-sync-free padded dispatch at capacity factor CF (P*C rows on
+                      the wire instead of N*k; one overflow-flag read per forward)"""
     from solvingpapers_amd.models import deepseekv3 as ds
     dev = torch.device("cuda")
     c = ds.config("dsv3_v3", moe_fp8=a.fp8, n_layers=a.layers, n_dense_layers=0, mtp_heads=0,
                   vocab_size=a.vocab, block_size=a.tokens)
     g1 = ProxyGroup(8, dev, a.ar_gbps, a.a2a_gbps, a.nwg)
+    if a.balanced:
+        # a trained, aux-free-balanced router stand-in: token t -> experts (t k + j) mod E (every
+        # expert and every peer gets exactly its share), weights softmax over the chosen logits
+        def balanced_route(logits, k, bias=None, bias_in_weights=True):
+            N, E = logits.shape
+            idx = ((torch.arange(N, device=logits.device)[:, None] * k + torch.arange(k, device=logits.device))
+                   % E).to(torch.int32)
+            return idx, torch.softmax(logits.gather(1, idx.long()).float(), -1)
+        ds.route = balanced_route
     m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=3, ep_group=g1).train()
     FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16)
     ids = torch.randint(0, c.vocab_size, (2, 1, a.tokens + 1), device=dev)
     x0, y0, x1, y1 = ids[0, :, :-1], ids[0, :, 1:], ids[1, :, :-1], ids[1, :, 1:]
 
-    def step_of(pair):
+    def step_of(pair, cap=0.0):
         def step():
             from solvingpapers_amd.utils.grad import next_generation
             next_generation()
+            m.c.ep_capacity = cap
+            for l in m.moe_layers():
+                l.c.ep_capacity = cap
             if pair:
                 m.forward_pair(x0, y0, x1, y1).backward()
             else:
@@ -149,6 +166,9 @@ def ep_moe(a):
 
     arms = {"off": (step_of(False), "off"), "blocking": (step_of(False), "blocking"),
             "pair:off": (step_of(True), "off"), "pair:overlap": (step_of(True), "overlap")}
+    if a.capacity > 0:
+        arms.update({"one:overlap": (step_of(False), "overlap"), "cap:off": (step_of(False, a.capacity), "off"),
+                     "cap:overlap": (step_of(False, a.capacity), "overlap")})
     if ARMS:
         arms = {k: v for k, v in arms.items() if k in ARMS}
     res = {k: [] for k in arms}
@@ -164,13 +184,19 @@ def ep_moe(a):
     med = {k: round(statistics.median(v), 3) for k, v in res.items()}
     out = {"config": f"dsv3_v3 widths EP=8 local shard, {a.layers} MLA+MoE layers (32 of 256 experts, top-8, D 7168, "
                      f"F 2048, 1 shared){' fp8' if a.fp8 else ''}, 2 micro-batches x {a.tokens} tokens, vocab {a.vocab}",
-           "ms": med, "modelled_comm_ms": round(comm, 3)}
+           "ms": med, "modelled_comm_ms": round(comm, 3), "routing": "balanced" if a.balanced else "model"}
     if not ARMS:
         total = med["blocking"] - med["off"]
         out["comm_added_blocking_ms"] = round(total, 3)
         out["pair_compute_cost_ms"] = round(med["pair:off"] - med["off"], 3)
         out["hidden_pair"] = round(1 - (med["pair:overlap"] - med["pair:off"]) / total, 3) if total > 0 else None
         out["pair_vs_blocking"] = round(med["pair:overlap"] / med["blocking"], 3)
+        if a.capacity > 0:
+            from solvingpapers_amd.parallel.expert_parallel import capacity_scale
+            out["capacity_factor"] = a.capacity
+            out["capacity_scale_after"] = capacity_scale()     # > 1: some forward overflowed and re-ran
+            out["cap_vs_one"] = round(med["cap:overlap"] / med["one:overlap"], 3)
+            out["cap_compute_cost_ms"] = round(med["cap:off"] - med["off"], 3)
     return out
 
 
@@ -193,6 +219,10 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--arms", default="", help="comma list of arm names (default all), e.g. pair:overlap")
+    ap.add_argument("--balanced", action="store_true", help="EP: round-robin routing (every peer exactly its "
+                    "share) instead of the random-init router, whose loads are skewed")
+    ap.add_argument("--capacity", type=float, default=0.0, help="EP: also time the host-sync-free dispatch at this "
+                    "capacity factor against the exact-split path, micro-batches one by one (accum-1 form)")
     a = ap.parse_args()
     global ARMS
     ARMS = [x for x in a.arms.split(",") if x] or None
