@@ -127,6 +127,39 @@ class _PackedFn(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, None
 
 
+FLASH_F32_HD = (16, 32, 64, 128, 256)
+
+
+class _FlashF32Fn(torch.autograd.Function):
+    """fp32 flash attention (csrc/kernels/attention_f32.hip, fp32 MFMA): the reference's training
+    precision (gpt/gpt-jax.ipynb:344-353, llama3/LLaMA-jax.ipynb:809-829) on a HIP kernel."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, dropout_p, seed):
+        si, st = _seed_args(seed)
+        out, lse = _ext.ops().attn_f32_fwd(q, k, v, scale, causal, dropout_p, si, st)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.causal, ctx.scale, ctx.dropout_p, ctx.seed = causal, scale, dropout_p, seed
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        dq, dk, dv = (torch.empty(t.shape, dtype=t.dtype, device=t.device) for t in (q, k, v))
+        si, st = _seed_args(ctx.seed)
+        _ext.ops().attn_f32_bwd(dout.contiguous(), q, k, v, out, lse, dq, dk, dv, ctx.scale, ctx.causal,
+                                ctx.dropout_p, si, st)
+        return dq, dk, dv, None, None, None, None
+
+
+def _f32_ready(t, hd):
+    """t padded to head dim hd, with 16-byte-aligned rows (the fp32 kernel's float4 accesses)."""
+    t = _pad_last(t, hd)
+    if t.stride(-1) != 1 or any(s % 4 for s in t.stride()[:-1]) or t.data_ptr() % 16:
+        t = t.contiguous()
+    return t
+
+
 def _materialised(q, k, v, causal, scale, dropout_p=0.0, seed=0, neg=float("-inf")):
     """GEMM + softmax path (CPU autograd, and the oracle of the fused kernels): with
     ``dropout_p`` it applies exactly the kernels' hash mask for ``seed``."""
@@ -184,9 +217,16 @@ def flash_attention(q, k, v, causal=True, scale=None, dropout_p=0.0, seed=None):
         if _wide_ok(q, k, v) and dropout_p == 0.0:
             from .attention_wide import wide_attention
             return wide_attention(q, k, v, causal, scale)
+    if q.is_cuda and q.dtype == torch.float32 and q.dim() == 4 and max(dqk, dv) <= 256:
+        # fp32 (the reference's precision in the parity runs): the fp32-MFMA kernels, head dims
+        # zero-padded to the next of 16 / 32 / 64 / 128 / 256 exactly as above
+        hd = next(h for h in FLASH_F32_HD if h >= max(dqk, dv))
+        o = _FlashF32Fn.apply(_f32_ready(q, hd), _f32_ready(k, hd), _f32_ready(v, hd), causal, scale, dropout_p,
+                              seed)
+        return o if dv == hd else o[..., :dv]
     if q.is_cuda:
-        # no flash kernel for this dtype / head-dim pair (fp32 parity runs at the reference's
-        # precision: gpt/gpt-jax.ipynb fp32, ViT-MNIST hd 16): GEMM + softmax on the GPU
+        # no flash kernel for this dtype / head-dim pair (fp16, or wider than 256 in fp32): GEMM +
+        # softmax on the GPU
         return _materialised(q, k, v, causal, scale, dropout_p, seed)
     if dropout_p > 0.0 or (torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)):
         return _materialised(q, k, v, causal, scale, dropout_p, seed)

@@ -817,3 +817,53 @@ def test_wgrad_odd_token_count_falls_back():
     dy8, x8 = dy[:4088], x[:4088]
     assert wgrad_nt_ok(dy8, x8)
     assert rel(wgrad(dy8, x8), dy8.float().t() @ x8.float()) < 1e-2
+
+
+F32_ATTN_CASES = [
+    # B, Tq, Tk, H, Hkv, hd, causal, dropout
+    (2, 128, 128, 4, 2, 64, True, 0.0),      # LLaMA-ref parity shape (B1), GQA
+    (2, 256, 256, 1, 1, 256, True, 0.0),     # GPT-ref parity shape (B5): one 256-wide head
+    (2, 256, 256, 1, 1, 256, True, 0.2),     # ... with the reference's attention dropout
+    (3, 50, 50, 4, 4, 16, False, 0.0),       # ViT-MNIST head dim 16, non-causal, ragged
+    (1, 200, 333, 6, 2, 128, True, 0.1),     # Tq < Tk, ragged tails, GQA + dropout
+    (1, 77, 77, 2, 1, 48, True, 0.0),        # head dim 48 zero-padded to 64
+]
+
+
+@pytest.mark.parametrize("B,Tq,Tk,H,Hkv,hd,causal,p", F32_ATTN_CASES)
+def test_flash_attention_fp32(B, Tq, Tk, H, Hkv, hd, causal, p):
+    """fp32 flash attention (csrc/kernels/attention_f32.hip, fp32 MFMA) == the fp64 GEMM + softmax
+    oracle with the kernels' own dropout mask, forward and every gradient (fp32 rounding)."""
+    from solvingpapers_amd.ops import flash_attention
+    from solvingpapers_amd.ops.attention import _materialised
+    torch.manual_seed(2)
+    q = torch.randn(B, Tq, H, hd, device=DEV, requires_grad=True)
+    k = torch.randn(B, Tk, Hkv, hd, device=DEV, requires_grad=True)
+    v = torch.randn(B, Tk, Hkv, hd, device=DEV, requires_grad=True)
+    seed = 1234567
+    o = flash_attention(q, k, v, causal=causal, dropout_p=p, seed=seed)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qd, kd, vd = (t.detach().double().requires_grad_() for t in (q, k, v))
+    od = _materialised(qd, kd, vd, causal, 1.0 / math.sqrt(hd), p, seed)
+    od.backward(do.double())
+    assert rel(o, od) < 2e-5, rel(o, od)
+    assert rel(q.grad, qd.grad) < 5e-5, rel(q.grad, qd.grad)
+    assert rel(k.grad, kd.grad) < 5e-5, rel(k.grad, kd.grad)
+    assert rel(v.grad, vd.grad) < 5e-5, rel(v.grad, vd.grad)
+
+
+def test_fp32_models_take_the_hip_attention(monkeypatch):
+    """the fp32 parity models (GPT-ref, LLaMA-ref) attend on the fp32 HIP kernel, not the fallback"""
+    from solvingpapers_amd.models import gpt, llama3
+    from solvingpapers_amd.ops import attention as A
+    calls = []
+    real = A._FlashF32Fn.apply
+    monkeypatch.setattr(A._FlashF32Fn, "apply", lambda *a: (calls.append(a[0].shape), real(*a))[1])
+    monkeypatch.setattr(A, "_materialised", lambda *a, **k: (_ for _ in ()).throw(AssertionError("fallback")))
+    for m in (gpt.GPT(gpt.config("gpt_ref"), device=DEV, dtype=torch.float32, seed=0),
+              llama3.Llama3(llama3.config("llama3_ref"), device=DEV, dtype=torch.float32, seed=0)):
+        m.train()
+        ids = torch.randint(0, 60, (2, 65), device=DEV)
+        m(ids[:, :-1], ids[:, 1:]).backward()
+    assert len(calls) >= 2, calls
