@@ -22,6 +22,17 @@ def pytest_collection_modifyitems(config, items):
 
 
 @pytest.fixture(autouse=True)
+def _test_sync():
+    """SPA_TEST_SYNC=1: drain the device after every test, so asynchronous work of one test can
+    never land in the next one's (stream-ordered, reused) allocations."""
+    yield
+    if os.environ.get("SPA_TEST_SYNC") == "1":
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+
+@pytest.fixture(autouse=True)
 def _device_bounds_guards():
     """In a debug-bounds build (SPA_EXT_SO=ab/_C_dbg.so with SPA_DEBUG_SYNC=1, see
     tests/test_debug_bounds_gpu.py) fail any test after which a device guard recorded a violation,
