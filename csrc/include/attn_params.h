@@ -55,6 +55,8 @@ struct AttnParams {
 
 // host launcher of the dK/dV v5 path (csrc/kernels/attention_dkdv5.hip): rowk pass + dK/dV kernel
 void launch_dkdv5(AttnParams& p, bool causal, hipStream_t st);
+// host launcher of the short-sequence fused backward (csrc/kernels/attention_short.hip)
+void launch_bwd_short(AttnParams& p, bool causal, hipStream_t st);
 
 // 2 KiB dS block index inside one (b, kv-head) region, in the order the dQ pass streams it: per
 // 64-query block qb its key steps kt (causal Tq == Tk: kt <= 2qb + 1, non-causal: all nkt), per

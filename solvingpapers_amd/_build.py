@@ -32,8 +32,10 @@ VARIANT = os.environ.get("SPA_BUILD_VARIANT", "")
 if VARIANT:
     BUILD = ROOT / "build" / VARIANT
     OUT = ROOT / "ab" / f"_C_{VARIANT}.so"
-# per-file device flags (none at present; a translation unit can get its own scheduler flags here)
-EXTRA_FLAGS = {}
+# per-file device flags: attention_short.hip without SLP vectorisation (hipcc packed its P * dP
+# products into v_pk_mul_f32 behind register shuffles: 24-34 more VALU per call on a VALU-bound
+# kernel; the other attention kernels keep it: the hd-256 forward needs 46 more VALU without it)
+EXTRA_FLAGS = {"attention_short.hip": "-fno-slp-vectorize"}
 
 
 def _torch_paths():

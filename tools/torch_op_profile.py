@@ -1,7 +1,8 @@
 """Which framework ops launch the non-GEMM "glue" kernels (fills, copies, casts, cats) of a
 DeepSeek-V3-style training step: torch.profiler over one fwd+bwd+AdamW step, ops sorted by
 device time with their input shapes.
-    python tools/torch_op_profile.py [--fp8] [--rows 40] [--preset dsv3_style --mb 2]"""
+    python tools/torch_op_profile.py [--fp8] [--rows 40] [--preset dsv3_style --mb 2] [--stack]
+--stack: only aten ops, grouped by the framework frames that launched them."""
 import os
 import sys
 
@@ -36,9 +37,20 @@ def main():
         step()
     torch.cuda.synchronize()
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-    with torch.profiler.profile(activities=acts, record_shapes=True) as prof:
+    stack = "--stack" in sys.argv
+    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=stack) as prof:
         step()
         torch.cuda.synchronize()
+    if stack:
+        # the aten (non-HIP-extension) ops by device time, each with the framework frames that issued it
+        ev = [e for e in prof.key_averages(group_by_stack_n=8) if e.key.startswith("aten::") and e.self_device_time_total > 0]
+        ev.sort(key=lambda e: -e.self_device_time_total)
+        for e in ev[:rows]:
+            frames = [f for f in e.stack if "solvingpapers_amd" in f or "bench" in f][:4]
+            print(f"{e.self_device_time_total / 1e3:8.3f} ms  {e.count:5d}x  {e.key}")
+            for f in frames:
+                print(f"            {f}")
+        return
     print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=rows,
                                                              max_name_column_width=60, max_shapes_column_width=70))
 
