@@ -116,6 +116,22 @@ __device__ __forceinline__ bf16x8 rd_ks(const char* half, int col0, int s, int l
     __builtin_amdgcn_sched_barrier(0);                 \
   } while (0)
 
+// SPA_G8_STAMP=1 (profiling build only, tools/build_variant.sh): wave 0 of each block records
+// s_memtime segment lengths of its tile -- mapping, prologue (first DMA issue to landed), K-loop,
+// epilogue -- plus its K-tile count into g8_stamp[block % G8_NSTAMP] (read by the g8_stamps op)
+#ifndef SPA_G8_STAMP
+#define SPA_G8_STAMP 0
+#endif
+constexpr int G8_NSTAMP = 16384;
+#if SPA_G8_STAMP
+__device__ long long g8_stamp[G8_NSTAMP * 8];
+#define G8_T(i) g8t[i] = (long long)__builtin_amdgcn_s_memtime()
+#else
+#define G8_T(i) \
+  do {          \
+  } while (0)
+#endif
+
 // ABL: ablation switch for profiling only (tools/bench_moe.py --ablate): 0 normal, 1 no DMA
 // (compute on whatever LDS holds), 2 no LDS fragment reads, 3 no vmcnt waits (1-3 on the
 // round-2 schedule), 8 the round-2 schedule itself (A/B reference); env value 4 selects the ILV schedule (DMA pieces issued between the MFMAs of each cluster). Measured at
@@ -136,6 +152,10 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   // the tile -> expert scan scratch sits past the two stages, where no DMA lands
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 64];
   int* scratch = reinterpret_cast<int*>(smem + 2 * STAGE);   // [0] expert, [1] tile, [8..15] wave sums
+#if SPA_G8_STAMP
+  long long g8t[5] = {0, 0, 0, 0, 0};
+#endif
+  G8_T(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int nnt = (N + BN - 1) / BN;
@@ -154,7 +174,9 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   bf16* Cp = C;
   if (MODE != 2) {
     int* wsum = scratch + 8;
-    const int cnt = tid < E ? offsets[tid + 1] - offsets[tid] : 0;
+    // the expert's row range travels through LDS with its id (no second global round trip)
+    const int o0 = tid < E ? offsets[tid] : 0, o1 = tid < E ? offsets[tid + 1] : 0;
+    const int cnt = o1 - o0;
     const int tiles = (cnt + BM - 1) / BM;
     int inc = tiles;
 #pragma unroll
@@ -167,13 +189,15 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     __syncthreads();
     int pre = inc - tiles;
     for (int w = 0; w < wave; ++w) pre += wsum[w];
-    if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) { scratch[0] = tid; scratch[1] = mt - pre; }
+    if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) {
+      scratch[0] = tid; scratch[1] = mt - pre; scratch[2] = o0; scratch[3] = o1;
+    }
     __syncthreads();
     e = __builtin_amdgcn_readfirstlane(scratch[0]);
     if (e < 0) return;
     mt = __builtin_amdgcn_readfirstlane(scratch[1]);
-    m0 = __builtin_amdgcn_readfirstlane(offsets[e]) + (long)mt * BM;
-    mend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
+    m0 = __builtin_amdgcn_readfirstlane(scratch[2]) + (long)mt * BM;
+    mend = __builtin_amdgcn_readfirstlane(scratch[3]);
     Bp = B + e * strideB;
   } else {
     const int nmt = (M + BM - 1) / BM;
@@ -191,16 +215,21 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       // to 7-0, ...), heaviest first on each; otherwise (a hot expert would pin its XCD) plain
       // dispatch order, which spreads every expert's tiles over all XCDs. Counts are staged in the
       // not yet used stage area; the choice is the same in every block.
+      // (counts zero-padded to a multiple of 4 and read as int4: the one-int-per-iteration loops
+      // below waited out an LDS round trip per expert, ~2K cycles of the tile's ~7.7K mapping)
       int* cnt = reinterpret_cast<int*>(smem);
-      if (tid < E) {
-        cnt[tid] = offsets[tid + 1] - offsets[tid];
-      }
+      const int E4 = (E + 3) & ~3;
+      const int o0 = tid < E ? offsets[tid] : 0, o1 = tid < E ? offsets[tid + 1] : 0;
+      if (tid < E4) cnt[tid] = o1 - o0;
       __syncthreads();
+      const int4* cnt4 = reinterpret_cast<const int4*>(cnt);
       long tot = 0;
       int mx = 0;
-      for (int j = 0; j < E; ++j) {
-        tot += cnt[j];
-        mx = max(mx, cnt[j]);
+#pragma unroll 4
+      for (int j = 0; j < E4 / 4; ++j) {
+        const int4 v = cnt4[j];
+        tot += (long)v.x + v.y + v.z + v.w;
+        mx = max(max(mx, max(v.x, v.y)), max(v.z, v.w));
       }
       const bool snake = E % 8 == 0 && (long)mx * E <= 2 * tot;
       const int per_e = nmt * nnt;
@@ -216,23 +245,30 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
       nt = r % nnt;
       mt = r / nnt;
       if (tid < E) {
-        const int c = cnt[tid];
+        const int c = o1 - o0;
         int rank = 0;
-        for (int j = 0; j < E; ++j) {
-          const int cj = cnt[j];
-          rank += (cj > c) || (cj == c && j < tid);
+#pragma unroll 4
+        for (int j = 0; j < E4 / 4; ++j) {   // (zero padding never outranks: c >= 0, index > tid)
+          const int4 v = cnt4[j];
+          rank += (v.x > c) || (v.x == c && 4 * j < tid);
+          rank += (v.y > c) || (v.y == c && 4 * j + 1 < tid);
+          rank += (v.z > c) || (v.z == c && 4 * j + 2 < tid);
+          rank += (v.w > c) || (v.w == c && 4 * j + 3 < tid);
         }
-        if (rank == pos) scratch[0] = tid;
+        if (rank == pos) { scratch[0] = tid; scratch[2] = o0; scratch[3] = o1; }
       }
       __syncthreads();
       e = __builtin_amdgcn_readfirstlane(scratch[0]);
+    } else {
+      if (tid == 0) { scratch[2] = offsets[e]; scratch[3] = offsets[e + 1]; }
+      __syncthreads();
     }
     m0 = (long)mt * BM;
     Cp = C + e * strideC;
   }
-  if (MODE == 2) {   // the expert's token range is the reduction range
-    k0 = __builtin_amdgcn_readfirstlane(offsets[e]);
-    kend = __builtin_amdgcn_readfirstlane(offsets[e + 1]);
+  if (MODE == 2) {   // the expert's token range is the reduction range (staged in LDS with its id)
+    k0 = __builtin_amdgcn_readfirstlane(scratch[2]);
+    kend = __builtin_amdgcn_readfirstlane(scratch[3]);
   }
   // debug build: the tile -> (expert, row tile) scan and the group offsets name real rows
   SPA_DBG_CHECK(e, E);
@@ -404,12 +440,14 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     //   P1 -        P2 A1(t+1)   P3 A0(t+2)   P4 B0(t+2) B1(t+2)
     // Waits: end of P1 retires B1(t) (younger: A1(t) + A0 B0 B1(t+1)), end of P2 A1(t) (younger:
     // A0 B0 B1 A1(t+1)), end of P4 A0, B0(t+1) (younger: B1 A1(t+1) + A0 B0 B1(t+2)).
+    G8_T(1);
     if (ktiles > 0) {
       stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
       if (ktiles > 1) { stage(1, 0); stage(1, 2); stage(1, 3); G8_WAIT_VM(10); } else { G8_WAIT_VM(4); }  // A0, B0 (0)
       __builtin_amdgcn_s_barrier();
       if (late) __builtin_amdgcn_s_barrier();
     }
+    G8_T(2);
     for (int t = 0; t < ktiles; ++t) {
       const int s = t & 1;
       const bool n1 = t + 1 < ktiles, n2 = t + 2 < ktiles;
@@ -484,6 +522,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   }
   }
   if (ktiles > 0 && !late) __builtin_amdgcn_s_barrier();   // equal barrier counts on exit
+  G8_T(3);
   if constexpr (PART) {
     // fp32 partials straight from the fragments: 16 rows x 64 contiguous bytes per store
     float* Cf = reinterpret_cast<float*>(C) + (long)e * strideC;
@@ -506,6 +545,25 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   // distinct bank pairs) -> whole-row 16-byte global stores (a per-lane 8-byte store at a row
   // stride would touch 16 cache lines per instruction)
   constexpr int RS = 256 * 2 + 16;
+  // accumulate: all 16 old-value chunks of this thread are loaded up front (buffer loads, zero past
+  // the tile's rows / columns), so their latency overlaps the image writes; one load-wait-add-store
+  // per chunk made the epilogue 30.7K cycles against 6.5K without accumulate (profiles/r5_gemm8_stamps.txt)
+  const long rowlim = MODE == 2 ? (long)M : mend;
+  const bool pre = accumulate && rowlim * ldc * 2 < 0x7fffffffL;
+  bf16x8 old[2][8];
+  if (pre) {
+    const __amdgpu_buffer_rsrc_t cr = rsrc(Cp, rowlim * ldc * 2);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
+        const long gm = m0 + mh * 128 + r;
+        const int gn = n0 + ch * 8;
+        const unsigned off = gn < N ? (unsigned)((gm * ldc + gn) * 2) : 0x80000000u;
+        old[mh][c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(cr, off, 0, 0));
+      }
+  }
   __syncthreads();
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
@@ -533,15 +591,24 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
         bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * RS + ch * 16);
         bf16* cp = Cp + gm * ldc + gn;
         if (accumulate) {
-          const bf16x8 old = *reinterpret_cast<const bf16x8*>(cp);
+          const bf16x8 o = pre ? old[mh][c] : *reinterpret_cast<const bf16x8*>(cp);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)old[q]);
+          for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)o[q]);
         }
         *reinterpret_cast<bf16x8*>(cp) = v;
       }
     }
     __syncthreads();
   }
+#if SPA_G8_STAMP
+  if (ABL == 0 && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the epilogue's stores left
+    G8_T(4);
+    long long* st = g8_stamp + (blockIdx.x % G8_NSTAMP) * 8;
+    st[0] = g8t[1] - g8t[0]; st[1] = g8t[2] - g8t[1]; st[2] = g8t[3] - g8t[2]; st[3] = g8t[4] - g8t[3];
+    st[4] = ktiles; st[5] = MODE;
+  }
+#endif
 }
 
 // out[i] (+)= sum_s part[s, i] over n elements (n % 4 == 0), bf16 or fp32 out
@@ -708,9 +775,26 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
   return out;
 }
 
+// profiling build (SPA_G8_STAMP=1): the per-block segment stamps since the last call, then cleared
+// [G8_NSTAMP, 8] int64 (mapping, prologue, K-loop, epilogue cycles, K-tiles, mode); empty otherwise
+at::Tensor g8_stamps() {
+#if SPA_G8_STAMP
+  auto out = at::empty({G8_NSTAMP, 8}, at::TensorOptions().dtype(at::kLong));
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(out.data_ptr(), HIP_SYMBOL(g8_stamp),
+              sizeof(long long) * G8_NSTAMP * 8, 0, hipMemcpyDeviceToHost) == hipSuccess, "g8_stamps: copy failed");
+  void* sym = nullptr;   // read-and-clear: the next launch's blocks are the only live entries
+  TORCH_CHECK(hipGetSymbolAddress(&sym, HIP_SYMBOL(g8_stamp)) == hipSuccess &&
+              hipMemset(sym, 0, sizeof(long long) * G8_NSTAMP * 8) == hipSuccess, "g8_stamps: clear failed");
+  return out;
+#else
+  return at::Tensor();
+#endif
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("g8_stamps() -> Tensor", &spa::g8_stamps);
   m.def("grouped_gemm8(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def("wgrad8(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate, int splits) -> Tensor");
 }
