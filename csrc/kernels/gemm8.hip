@@ -538,6 +538,15 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
             const int gn = n0 + nh * 128 + wn * 32 + 16 * j + 4 * (lane >> 4);
             if (gm < M && gn < N && SPA_DBG_OK(gn + 3, ldc)) *reinterpret_cast<f32x4*>(Cf + gm * ldc + gn) = acc[mh * 4 + i][nh * 2 + j];
           }
+#if SPA_G8_STAMP
+    if (ABL == 0 && tid == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      G8_T(4);
+      long long* st = g8_stamp + (blockIdx.x % G8_NSTAMP) * 8;
+      st[0] = g8t[1] - g8t[0]; st[1] = g8t[2] - g8t[1]; st[2] = g8t[3] - g8t[2]; st[3] = g8t[4] - g8t[3];
+      st[4] = ktiles; st[5] = 10 + MODE;
+    }
+#endif
     return;
   }
   // ---- epilogue through LDS, one 128-row half at a time: C^T fragments (n = 4 (l >> 4) + q,

@@ -39,6 +39,15 @@ cases = {
     "dense fwd K 768": lambda: ops.grouped_gemm8(xa, wa, off1, 0, None, False),
     "dense dW K 768": lambda: ops.grouped_gemm8(ta, ta, offk, 2, None, False),
 }
+# ViT-B/16 weight gradients (wgrad8: token slices of one dense dW, fp32 partials), T = 256 x 197
+Tv = 256 * 197
+vit = {}
+for nm, (n_, k_) in {"qkv": (2304, 768), "proj": (768, 768), "fc1": (3072, 768), "fc2": (768, 3072)}.items():
+    dyv = torch.randn(Tv, n_, device=dev, dtype=torch.bfloat16)
+    xv = torch.randn(Tv, k_, device=dev, dtype=torch.bfloat16)
+    vit[nm] = (dyv, xv)
+for nm, (dyv, xv) in vit.items():
+    cases[f"ViT wgrad8 {nm}"] = (lambda d=dyv, xx=xv: ops.wgrad8(d, xx, None, False, 0))
 out_acc = ops.grouped_gemm8(dy13, x, plan.offsets, 2, None, False)
 for name, fn in cases.items():
     for _ in range(3):
