@@ -16,6 +16,7 @@
 #   parity         fp32 reference-loop parity rows B1/B3/B5/B7 and B8 end to end
 #   overlap        TP / EP collective-overlap proxy (tools/overlap_proxy.py)
 #   dsv3-prof      dsv3_style at accum 1 and 4, kernel trace at accum 4
+#   vit-gemma-prof kernel traces of one ViT-B/16 and one Gemma-7B (28 layers) optimizer step
 #   gemm-ab V..    gemm8 default vs SPA_GG8_ABLATE=V (dense 8192^3 + dsv3_style grouped), ABBA
 #   gemm-validate  GEMM/MoE GPU tests, schedule A/B vs the round-2 one, dsv3_style + ViT benches
 #   defer-ab       MoE GPU tests; dsv3_style accum 4 with / without deferred expert Wgrad, ABBA
@@ -239,6 +240,13 @@ dsv3-prof)
   run 400 ${O}_prof.log rocprofv3 --kernel-trace --stats -d /tmp/$task -o run -- python3 bench/dsv3_train.py --preset dsv3_style --steps 2 --warmup 1 --accum 4
   python tools/rocpd_summary.py /tmp/$task/run_results.db --last-step adamw --top 45 > ${O}_summary.txt 2>&1
   head -60 ${O}_summary.txt | cut -c1-170 ;;
+vit-gemma-prof)
+  run 300 ${O}_vit.log rocprofv3 --kernel-trace --stats -d /tmp/${task}_v -o run -- python3 bench/vit_train.py --steps 3 --warmup 2
+  python tools/rocpd_summary.py /tmp/${task}_v/run_results.db --last-step adamw --top 30 > ${O}_vit_summary.txt 2>&1
+  head -40 ${O}_vit_summary.txt | cut -c1-170
+  run 400 ${O}_gemma.log rocprofv3 --kernel-trace --stats -d /tmp/${task}_g -o run -- python3 bench/gemma_tp.py --layers 28 --steps 2 --warmup 1
+  python tools/rocpd_summary.py /tmp/${task}_g/run_results.db --last-step adamw --top 30 > ${O}_gemma_summary.txt 2>&1
+  head -40 ${O}_gemma_summary.txt | cut -c1-170 ;;
 gemm-ab)
   for v in "${@:?schedule}"; do
     run 300 ${O}_$v.log python -u tools/bench_gemm8_dense.py 8192 --iters 10 --ab $v
