@@ -22,7 +22,8 @@ DEFAULT_TABLE = os.path.join(ROOT, "tuning", "tunableop_llama8b.csv")
 
 def load_gemm_tuning(path: Optional[str] = None) -> bool:
     """Use the tuned GEMM table at ``path`` (default: tuning/tunableop_llama8b.csv).
-    SPA_GEMM_TUNING=0 disables it. Returns True if the table was loaded."""
+    SPA_GEMM_TUNING=0 disables it; SPA_GEMM_RECORD_UNTUNED=<csv> records the GEMMs it misses.
+    Returns True if the table was loaded."""
     if os.environ.get("SPA_GEMM_TUNING", "1") == "0" or not torch.cuda.is_available():
         return False
     path = path or DEFAULT_TABLE
@@ -31,7 +32,11 @@ def load_gemm_tuning(path: Optional[str] = None) -> bool:
     import torch.cuda.tunable as tunable
     tunable.enable(True)
     tunable.tuning_enable(False)
-    tunable.record_untuned_enable(False)
+    # SPA_GEMM_RECORD_UNTUNED=<csv>: list the GEMMs the table does not cover (table-coverage check)
+    untuned = os.environ.get("SPA_GEMM_RECORD_UNTUNED")
+    if untuned:
+        os.environ["PYTORCH_TUNABLEOP_UNTUNED_FILENAME"] = untuned
+    tunable.record_untuned_enable(bool(untuned))
     # results of this process (none: tuning is off) go to a scratch file, never the repo table
     tunable.set_filename(os.path.join(os.environ.get("TMPDIR", "/tmp"), "spa_tunableop_out.csv"), True)
     return bool(tunable.read_file(path))
