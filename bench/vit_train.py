@@ -6,6 +6,7 @@ all-reduced during backward; fused AdamW over the flat buffers.
 from __future__ import annotations
 
 import argparse
+import os
 
 import torch
 
@@ -22,12 +23,17 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mb", type=int, default=256, help="images per GPU per step")
-    ap.add_argument("--gemm-table", default=None, help="TunableOp GEMM table (tuning/*.csv) to look up")
+    ap.add_argument("--gemm-table", default="auto",
+                    help="TunableOp GEMM table to look up (default tuning/tunableop_vit_b16.csv, tuned at these "
+                         "shapes: +2.0 %% B N N B, profiles/r5_vit_gemm_table_abba.txt); 'none' disables")
     a = ap.parse_args()
     info = sdist.init_distributed()
-    if a.gemm_table:   # after init: the device is set, so every rank loads it on its own GPU
-        from solvingpapers_amd.utils.tuning import load_gemm_tuning
-        assert load_gemm_tuning(a.gemm_table), a.gemm_table
+    tuned = False
+    if a.gemm_table != "none" and info.device.type == "cuda":   # after init: every rank loads it on its own GPU
+        from solvingpapers_amd.utils.tuning import ROOT, load_gemm_tuning
+        path = os.path.join(ROOT, "tuning", "tunableop_vit_b16.csv") if a.gemm_table == "auto" else a.gemm_table
+        tuned = load_gemm_tuning(path)
+        assert tuned or a.gemm_table == "auto", path
     world, dev = info.world_size, info.device
     c = vit.config("vit_b16")
     m = vit.ViT(c, device=dev, dtype=torch.bfloat16)
@@ -59,7 +65,7 @@ def main():
     report("training images/sec, ViT-B/16 bf16", ips, "images/s", a.steps, a.warmup, el,
            {"model": "vit_b16", "global_batch": world * a.mb, "seq_len": tokens, "parallelism": f"dp{world}",
             "params": n}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
-           loss=round(float(last[0].detach()), 4))
+           loss=round(float(last[0].detach()), 4), gemm_table=tuned)
     sdist.cleanup()
 
 
