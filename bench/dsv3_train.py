@@ -6,6 +6,7 @@ all-to-all dispatch) and the dense parameters data-parallel (RCCL buckets)."""
 from __future__ import annotations
 
 import argparse
+import os
 import contextlib
 
 import torch
@@ -41,9 +42,23 @@ def main():
     ap.add_argument("--no-pair", dest="pair", action="store_false",
                     help="with --accum even: run the micro-batches one by one instead of in layer-interleaved "
                          "pairs (DeepSeekV3.forward_pair: each EP all-to-all overlaps the other micro-batch)")
+    ap.add_argument("--gemm-table", default="auto",
+                    help="TunableOp GEMM table to look up (default tuning/tunableop_<preset>.csv where one exists "
+                         "and the bench runs bf16 at the preset's own shapes); 'none' disables")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
+    tuned = False
+    if a.gemm_table != "none" and dev.type == "cuda":   # after init: every rank loads it on its own GPU
+        from solvingpapers_amd.utils.tuning import ROOT, load_gemm_tuning
+        path = a.gemm_table
+        if path == "auto":
+            path = os.path.join(ROOT, "tuning", f"tunableop_{a.preset}.csv")
+            native = not (a.fp8 or a.layers or a.experts or a.dense_layers is not None or a.seq != 4096)
+            path = path if native and os.path.exists(path) else None
+        if path:
+            tuned = load_gemm_tuning(path)
+            assert tuned, path
     kw = {"block_size": a.seq}
     if a.layers:
         kw["n_layers"] = a.layers
@@ -98,7 +113,8 @@ def main():
             "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu",
             "params": m.num_params(),
             "active_params": m.num_params(active=True)},
-           tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4))
+           tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4),
+           gemm_table=tuned)
     sdist.cleanup()
 
 
