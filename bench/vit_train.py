@@ -26,6 +26,10 @@ def main():
     ap.add_argument("--gemm-table", default="auto",
                     help="TunableOp GEMM table to look up (default tuning/tunableop_vit_b16.csv, tuned at these "
                          "shapes: +2.0 %% B N N B, profiles/r5_vit_gemm_table_abba.txt); 'none' disables")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step (fwd + bwd + AdamW) in one HIP graph and replay it "
+                         "(measured 1.3 %% slower than eager at batch 256: the step is not launch bound, "
+                         "profiles/r5_vit_gemm_table_abba.txt)")
     a = ap.parse_args()
     info = sdist.init_distributed()
     tuned = False
@@ -41,7 +45,8 @@ def main():
     dp = DataParallel(m, flat) if world > 1 else None
     if dp is not None:
         dp.broadcast_params()
-    opt = FlatAdamW(flat, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.05, max_grad_norm=1.0)
+    graph = a.graph and world == 1 and dev.type == "cuda"
+    opt = FlatAdamW(flat, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.05, max_grad_norm=1.0, graph_safe=graph)
     g = torch.Generator(device=dev).manual_seed(3 + info.rank)
     x = torch.randn(a.mb, 3, 224, 224, device=dev, dtype=torch.bfloat16, generator=g)
     y = torch.randint(0, 1000, (a.mb,), device=dev, generator=g)
@@ -56,6 +61,9 @@ def main():
         opt.step()
         last[0] = loss
 
+    if graph:
+        from solvingpapers_amd.utils.graphs import StepGraph
+        step = StepGraph(step, warmup=2).replay
     el = timed(step, a.steps, a.warmup)
     ips = world * a.mb * a.steps / el
     n = sum(p.numel() for p in m.parameters())
@@ -65,7 +73,7 @@ def main():
     report("training images/sec, ViT-B/16 bf16", ips, "images/s", a.steps, a.warmup, el,
            {"model": "vit_b16", "global_batch": world * a.mb, "seq_len": tokens, "parallelism": f"dp{world}",
             "params": n}, tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4),
-           loss=round(float(last[0].detach()), 4), gemm_table=tuned)
+           loss=round(float(last[0].detach()), 4), gemm_table=tuned, hip_graph=graph)
     sdist.cleanup()
 
 
