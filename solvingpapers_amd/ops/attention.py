@@ -17,6 +17,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 
 from . import _ext, reference
@@ -234,7 +236,7 @@ def flash_attention(q, k, v, causal=True, scale=None, dropout_p=0.0, seed=None):
 
 
 class _MLAFn(torch.autograd.Function):
-    """DeepSeek-V3 MLA attention core on the (192, 128) flash kernels with the head assembly
+    """DeepSeek-V3 MLA attention core on the (192, 128) (or hd-128) flash kernels with the head assembly
     fused around them (deepseekv3/deepseekv3.ipynb:1152-1189 for the reference's latent heads):
 
     forward:  q = q_raw with RoPE on its last dr columns (one copy + one in-place rope),
@@ -289,8 +291,10 @@ def mla_attention(q_raw, kv, kr, dn, scale, theta, pos_off=0):
     default) at positions pos_off.. ."""
     dr = q_raw.shape[-1] - dn
     dv = kv.shape[-1] - dn
-    if (q_raw.is_cuda and q_raw.dtype == torch.bfloat16 and (dn + dr, dv) == (192, 128)
-            and kv.stride(-1) == 1 and kr.shape[2] == 1):
+    # fused on the (192, 128) kernels (V3 widths) and the hd-128 ones (dsv3_style: 64 nope + 64 rope,
+    # v 128); SPA_MLA_FUSED=0 (read per call) keeps the op-by-op composition
+    if (q_raw.is_cuda and q_raw.dtype == torch.bfloat16 and (dn + dr, dv) in ((192, 128), (128, 128))
+            and kv.stride(-1) == 1 and kr.shape[2] == 1 and os.environ.get("SPA_MLA_FUSED", "1") != "0"):
         return _MLAFn.apply(q_raw, kv, kr, int(dn), float(scale), int(pos_off), float(theta))
     from .rope import apply_rope
     B, T, H, _ = q_raw.shape

@@ -496,12 +496,14 @@ def test_flash_attention_mixed_head_dims(Hkv, dqk, dv):
 
 
 @pytest.mark.parametrize("pos_off", [0, 5])
-def test_mla_attention_fused_matches_composition(pos_off):
-    """ops.mla_attention (rope + head assembly fused around the (192, 128) flash kernels, dV
-    written into the dkv buffer, rope key grad summed over heads) vs the op-by-op fp32 CPU path."""
+@pytest.mark.parametrize("dn", [128, 64])
+def test_mla_attention_fused_matches_composition(pos_off, dn):
+    """ops.mla_attention (rope + head assembly fused around the (192, 128) flash kernels -- or the
+    hd-128 ones at dsv3_style's 64 nope + 64 rope --, dV written into the dkv buffer, rope key grad
+    summed over heads) vs the op-by-op fp32 CPU path."""
     from solvingpapers_amd.ops.attention import mla_attention
     torch.manual_seed(7)
-    B, T, H, dn, dr, dv = 2, 300, 4, 128, 64, 128
+    B, T, H, dr, dv = 2, 300, 4, 64, 128
     q = torch.randn(B, T, H, dn + dr, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     kv = torch.randn(B, T, H, dn + dv, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     kr = torch.randn(B, T, 1, dr, device=DEV, dtype=torch.bfloat16, requires_grad=True)
