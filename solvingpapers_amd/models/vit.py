@@ -114,7 +114,8 @@ class TransformerEncoder(tnn.Module):
         a = self.multihead_attention(n1)
         n2, h2 = self.layer_norm2(a, residual=x)     # h2 = x + attn, n2 = LN2(h2)
         fc1, gelu, fc2 = self.mlp
-        # one op: fc1 + bias + GELU forward epilogue, fc2-dX + GELU' + fc1 bias-grad backward epilogue
+        # ops.linear.mlp: hipBLASLt fc1 (+ bias) and a GELU pass forward; backward GELU' and fc1's bias
+        # gradient in one pass (GEMM-epilogue forms measured slower, profiles/r5_vit_mlp_epilogue_and_fast_erf_rejected.txt)
         return h2, mlp(n2, fc1.weight, fc1.bias, fc2.weight, fc2.bias, gelu.kind, gelu.alpha)
 
 
