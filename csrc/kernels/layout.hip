@@ -11,14 +11,28 @@
 
 namespace spa {
 
+// build-time A/B knobs (profiles/r5_transpose_variants.txt): tile size, diagonal block order
+#ifndef SPA_TRANSPOSE_TS
+#define SPA_TRANSPOSE_TS 64
+#endif
+#ifndef SPA_TRANSPOSE_DIAG
+#define SPA_TRANSPOSE_DIAG 0
+#endif
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int R, int C,
                                                         long ldx, long ldy, long bsx, long bsy) {
   x += blockIdx.z * bsx;   // batch (e.g. one expert's [N, K] weight per z)
   y += blockIdx.z * bsy;
-  constexpr int TS = 64, PAD = 16 / sizeof(T), LD = TS + PAD, VE = 16 / sizeof(T);  // VE elements per 16 B
+  constexpr int TS = SPA_TRANSPOSE_TS, PAD = 16 / sizeof(T), LD = TS + PAD, VE = 16 / sizeof(T);  // VE elements per 16 B
   __shared__ __attribute__((aligned(16))) T tile[TS * LD];
+#if SPA_TRANSPOSE_DIAG
+  // diagonal block order: blocks that run together read one input row band but write output
+  // row bands that start at different column offsets (spreads the writes over HBM channels)
+  const int bx = (blockIdx.x + blockIdx.y) % gridDim.x;
+  const int r0 = blockIdx.y * TS, c0 = bx * TS;
+#else
   const int r0 = blockIdx.y * TS, c0 = blockIdx.x * TS;
+#endif
   constexpr int CPR = TS / VE;                  // 16-byte chunks per tile row
   constexpr int NCH = TS * CPR;                 // chunks per tile
 #pragma unroll
@@ -59,7 +73,7 @@ at::Tensor transpose2d(const at::Tensor& x_) {
   DeviceGuard g(x.device());
   auto y = batched ? at::empty({Bt, C, R}, x.options()) : at::empty({C, R}, x.options());
   if (R == 0 || C == 0 || Bt == 0) return y;
-  dim3 grid(cdiv(C, 64), cdiv(R, 64), Bt);
+  dim3 grid(cdiv(C, SPA_TRANSPOSE_TS), cdiv(R, SPA_TRANSPOSE_TS), Bt);
   const long ld = x.stride(-2), bsx = batched ? x.stride(0) : 0, bsy = (long)R * C;
   if (x.scalar_type() == at::kBFloat16)
     transpose_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)x.data_ptr(), (bf16*)y.data_ptr(), R, C, ld, R,
