@@ -44,7 +44,7 @@ def main():
                          "pairs (DeepSeekV3.forward_pair: each EP all-to-all overlaps the other micro-batch)")
     ap.add_argument("--gemm-table", default="auto",
                     help="TunableOp GEMM table to look up (default tuning/tunableop_<preset>.csv where one exists "
-                         "and the bench runs bf16 at the preset's own shapes); 'none' disables")
+                         "and the bench runs at T 4096); 'none' disables")
     a = ap.parse_args()
     info = sdist.init_distributed()
     world, dev = info.world_size, info.device
@@ -54,8 +54,8 @@ def main():
         path = a.gemm_table
         if path == "auto":
             path = os.path.join(ROOT, "tuning", f"tunableop_{a.preset}.csv")
-            native = not (a.fp8 or a.layers or a.experts or a.dense_layers is not None or a.seq != 4096)
-            path = path if native and os.path.exists(path) else None
+            # depth and expert count leave every dense GEMM shape as it is; the sequence length does not
+            path = path if a.seq == 4096 and os.path.exists(path) else None
         if path:
             tuned = load_gemm_tuning(path)
             assert tuned, path
