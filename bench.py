@@ -22,9 +22,10 @@ per step). Every micro-batch runs its full forward + backward inside the timed
 region; only the inner micro-batches skip the gradient all-reduce (no_sync) and
 the last one launches it, so the per-step optimizer / grad-norm / all-reduce
 cost (~40 ms on 1 GPU, more at N=8) is paid once per 32K tokens as in a real
-LLaMA-scale run (global batches of millions of tokens). Measured on 1 MI355X in round 1:
-accum 1: 18.6K tok/s, 2: 19.4K, 4: 20.35K, 8: 20.6K; accum 4 at the end of round 2: 21.0K
-(BASELINE.md).
+LLaMA-scale run (global batches of millions of tokens). The accumulation sweep (round 1,
+1 MI355X, profiles/r1_bench_accum_sweep.jsonl): accum 1: 18.6K tok/s, 2: 19.4K, 4: 20.35K,
+8: 20.6K. The current figure is the driver's own run of this file (BENCH_rNN.json; history in
+BASELINE.md).
 """
 from __future__ import annotations
 
@@ -125,7 +126,10 @@ def run(a):
     model = llama3.Llama3(cfg, device=dev, dtype=dtype, seed=1234)
     gdt = torch.float32 if a.grad_fp32 else dtype
     flat = FlatParams(model, groups=model.param_groups(), grad_dtype=gdt, align=64 * world)
-    dp = DataParallel(model, flat, zero1=a.zero1) if world > 1 else None
+    # SPA_FORCE_COLLECTIVES=1 under a 1-rank torch.distributed.run drives the DP buckets / ZeRO-1
+    # through RCCL at world size 1 (the multi-GPU pre-flight, profiles/r6_rccl_preflight.txt)
+    multi = world > 1 or (sdist.force_collectives() and tdist.is_initialized())
+    dp = DataParallel(model, flat, zero1=a.zero1) if multi else None
     if dp is not None:
         dp.broadcast_params(0)
     shard = (dp.shard_ranges(), None) if (dp is not None and a.zero1) else None
@@ -197,7 +201,7 @@ def run(a):
                 "model": a.model if a.layers is None else f"{a.model}-L{a.layers}",
                 "global_batch": world * B * a.accum,
                 "seq_len": T,
-                "parallelism": f"dp{world}" + ("-zero1" if a.zero1 else ""),
+                "parallelism": f"dp{world}" + ("-zero1" if a.zero1 else "") + ("-forced-collectives" if multi and world == 1 else ""),
                 "micro_batch": B,
                 "grad_accum": a.accum,
                 "params": model.num_params(),

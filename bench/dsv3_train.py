@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--no-pair", dest="pair", action="store_false",
                     help="with --accum even: run the micro-batches one by one instead of in layer-interleaved "
                          "pairs (DeepSeekV3.forward_pair: each EP all-to-all overlaps the other micro-batch)")
+    ap.add_argument("--ep-capacity", type=float, default=None,
+                    help="DSV3Config.ep_capacity (> 0: host-sync-free padded EP dispatch)")
     ap.add_argument("--gemm-table", default="auto",
                     help="TunableOp GEMM table to look up (default tuning/tunableop_<preset>.csv where one exists "
                          "and the bench runs at T 4096); 'none' disables")
@@ -70,11 +72,17 @@ def main():
         kw["moe_fp8"] = True
         kw["fp8_linears"] = not a.fp8_experts_only
     c = ds.config(a.preset, **kw)
-    ep = torch.distributed.group.WORLD if world > 1 else None
+    # SPA_FORCE_COLLECTIVES=1 under a 1-rank torch.distributed.run: the EP exchanges, DP buckets and
+    # routing-bias all-reduce go through RCCL at world size 1 (multi-GPU pre-flight on one GPU)
+    multi = world > 1 or (sdist.force_collectives() and torch.distributed.is_initialized())
+    if a.ep_capacity is not None:
+        kw["ep_capacity"] = a.ep_capacity
+        c = ds.config(a.preset, **kw)
+    ep = torch.distributed.group.WORLD if multi else None
     m = ds.DeepSeekV3(c, device=dev, dtype=torch.bfloat16, seed=1, ep_group=ep)
     pair = a.pair and a.accum % 2 == 0
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=torch.bfloat16, align=64 * world)
-    dp = DataParallel(m, flat) if world > 1 else None
+    dp = DataParallel(m, flat) if multi else None
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0, ep_group=ep,
                     moment_dtype=torch.bfloat16 if a.bf16_moments else torch.float32)
     overlap = not a.no_opt_overlap and torch.cuda.is_available()
@@ -110,7 +118,8 @@ def main():
            tok_s, "tokens/s", a.steps, a.warmup, el,
            {"model": a.preset + (f"-L{a.layers}" if a.layers else "") + (f"-E{a.experts}" if a.experts else "")
             + ("-fp8" if a.fp8 else ""), "global_batch": world * B * a.accum, "seq_len": T, "grad_accum": a.accum, "microbatch_pairs": pair, "adam_moments": "bf16" if a.bf16_moments else "fp32",
-            "parallelism": f"ep{world}-dp{world}" if world > 1 else "1gpu",
+            "parallelism": f"ep{world}-dp{world}" + ("-forced-collectives" if world == 1 else "") if multi else "1gpu",
+            "ep_capacity": c.ep_capacity,
             "params": m.num_params(),
             "active_params": m.num_params(active=True)},
            tflops_per_gpu=round(tf, 1), mfu_vs_2_5PF=round(tf * 1e12 / PEAK_BF16, 4), loss=round(float(last[0].detach()), 4),

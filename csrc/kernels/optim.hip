@@ -220,6 +220,54 @@ at::Tensor sqsum(const at::Tensor& g) {
   return out;
 }
 
+// DP reduce-scatter over the xGMI mesh (parallel/data_parallel.py reduce="a2a"): after one
+// all-to-all every rank holds the N bf16 copies of its gradient shard, [N, n] rows; this sums them
+// in fp32 and rounds ONCE (out = bf16(scale * sum_s in[s])), instead of the N-1 bf16 roundings of
+// a ring reduce-scatter's running partial (profiles/r6_dp_reduce_numerics.txt). HBM-bound: reads
+// N*n, writes n.
+template <typename T>
+__global__ __launch_bounds__(256) void shard_sum_kernel(const T* __restrict__ in, T* __restrict__ out, long n,
+                                                        int N, float scale) {
+  const long nv = n / 8;
+  const long stride = (long)gridDim.x * 256;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nv; i += stride) {
+    float acc[8], v[8];
+    load8(in + i * 8, acc);
+    for (int s = 1; s < N; ++s) {
+      load8(in + (long)s * n + i * 8, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= scale;
+    store8(out + i * 8, acc);
+  }
+  for (long j = nv * 8 + blockIdx.x * 256L + threadIdx.x; j < n; j += stride) {
+    float a = 0.f;
+    for (int s = 0; s < N; ++s) a += (float)in[(long)s * n + j];
+    out[j] = (T)(a * scale);
+  }
+}
+
+void shard_sum_(const at::Tensor& out, const at::Tensor& in, int64_t N, double scale) {
+  SPA_CHECK_CUDA(in);
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.scalar_type() == out.scalar_type(),
+              "shard_sum: contiguous, same dtype");
+  const long n = out.numel();
+  TORCH_CHECK(N >= 1 && in.numel() == N * n, "shard_sum: in must hold N x out.numel() values");
+  if (n == 0) return;
+  DeviceGuard gd(in.device());
+  const int grid = opt_grid(n);
+  if (in.scalar_type() == at::kBFloat16)
+    shard_sum_kernel<bf16><<<grid, 256, 0, stream()>>>((const bf16*)in.data_ptr(), (bf16*)out.data_ptr(), n,
+                                                        (int)N, (float)scale);
+  else if (in.scalar_type() == at::kFloat)
+    shard_sum_kernel<float><<<grid, 256, 0, stream()>>>(in.data_ptr<float>(), out.data_ptr<float>(), n, (int)N,
+                                                         (float)scale);
+  else TORCH_CHECK(false, "shard_sum: bf16/fp32 only");
+  SPA_LAUNCH_CHECK();
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
@@ -228,9 +276,11 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("sgd_(Tensor(a!) p, Tensor(b!)? master, Tensor g, Tensor(c!)? buf, float lr, float momentum, float wd, "
         "Tensor? coef, Tensor? hyper=None) -> ()");
   m.def("sqsum(Tensor g) -> Tensor");
+  m.def("shard_sum_(Tensor(a!) out, Tensor inp, int N, float scale) -> ()");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("adamw_", &spa::adamw_);
   m.impl("sgd_", &spa::sgd_);
   m.impl("sqsum", &spa::sqsum);
+  m.impl("shard_sum_", &spa::shard_sum_);
 }

@@ -31,6 +31,7 @@ exporter slices the padding off.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass, replace
@@ -374,6 +375,10 @@ class MoE(tnn.Module):
         self.last_counts = None
         self._pending_bias = []        # (work, load): bias updates whose counts all-reduce is in flight
         self.cap_state = SimpleNamespace(rows=None)   # capacity-mode EP: this layer's block rows
+        # EP dispatch override (DeepSeekV3.ep_dispatch): None -> DSV3Config.ep_capacity; "exact" ->
+        # split-size dispatch; "bound" -> host-sync-free blocks at the exact per-peer bound (cannot
+        # overflow, no flag: HIP-graph decode)
+        self.dispatch_mode = None
 
     @torch.no_grad()
     def reset_parameters(self, std, g):
@@ -420,7 +425,7 @@ class MoE(tnn.Module):
         self.finish_pending()                   # last step's bias updates before this routing
         idx, w = route(self._logits(x2), c.top_k, self.routing_bias if c.aux_free else None, c.bias_in_weights)
         st = ep_stage_prepare(x2, idx, w, c.n_experts, self.ep_group, self._fp8(x2), self.w13,
-                              capacity=c.ep_capacity, cap_state=self.cap_state)
+                              capacity=self._capacity(), cap_state=self.cap_state)
         st.x2, st.idx, st.sh = x2, idx, None
         if c.aux_free and self.training:
             # the bias moves right after this routing (the reference updates it after every
@@ -428,6 +433,13 @@ class MoE(tnn.Module):
             # this layer with micro-batch 0's update applied, exactly as two forward() calls do
             self._update_bias(idx, w, st.prep.plan)
         return st
+
+    def _capacity(self):
+        if self.dispatch_mode == "exact":
+            return 0.0
+        if self.dispatch_mode == "bound":
+            return math.inf
+        return self.c.ep_capacity
 
     def stage_shared(self, st):
         if self.shared is not None:
@@ -735,20 +747,38 @@ class DeepSeekV3(tnn.Module):
         return n
 
     # ---- capacity-mode EP (DSV3Config.ep_capacity > 0): no host sync inside the layers; one read
-    # of the overflow flags per forward, and an exact re-run with doubled capacity on overflow
+    # of the overflow flags per forward. On overflow the forward re-runs with every layer's block
+    # rows set from the load it saw (x margin); a layer downstream of an overflow saw perturbed
+    # inputs, so that re-run can overflow again -- then the last attempt takes the exact split-size
+    # dispatch (one host sync per layer), which cannot overflow. Training never stops on capacity.
+    _CAP_ATTEMPTS = 2
+
     def _capacity_run(self, fn, *args):
         if not self.c.ep_capacity > 0:
             return fn(*args)
         from ..parallel.expert_parallel import capacity_overflowed
         capacity_overflowed()                   # flags of work outside this forward are not ours
         snap = self._routing_snapshot()
-        for _ in range(8):
+        for _ in range(self._CAP_ATTEMPTS):
             out = fn(*args)
             if not capacity_overflowed():
                 return out
-            self._routing_restore(snap)         # the failed attempt's graph is dropped with `out`;
-            # the layers' capacity states now hold the overflowing loads (x margin): the re-run fits
-        raise RuntimeError("EP capacity dispatch still overflowing after 8 doublings")
+            self._routing_restore(snap)         # the failed attempt's graph is dropped with `out`
+        with self.ep_dispatch("exact"):
+            return fn(*args)
+
+    @contextlib.contextmanager
+    def ep_dispatch(self, mode):
+        """Every MoE layer on EP dispatch ``mode`` ("exact" | "bound", MoE.dispatch_mode) for the duration."""
+        layers = list(self.moe_layers())
+        prev = [m.dispatch_mode for m in layers]
+        for m in layers:
+            m.dispatch_mode = mode
+        try:
+            yield
+        finally:
+            for m, p in zip(layers, prev):
+                m.dispatch_mode = p
 
     def _routing_snapshot(self):
         # outstanding bias updates of the previous step land first (each layer's routing would
@@ -849,8 +879,10 @@ class DeepSeekV3(tnn.Module):
         return self.c.block_size if self.c.pos_emb == "sinusoidal" else None
 
     def step(self, ids, cache, pos):
-        """Write ids' latents at cache rows [pos, pos+T), return the last position's logits [B, V]."""
-        n, _ = self.hidden(ids, cache, pos)
+        """Write ids' latents at cache rows [pos, pos+T), return the last position's logits [B, V].
+        Always the exact EP dispatch: capacity mode's overflow re-run exists only for forward()."""
+        with self.ep_dispatch("exact"):
+            n, _ = self.hidden(ids, cache, pos)
         return self.logits(n[:, -1:]).float()[:, -1]
 
     def step_graph(self, ids, cache, state):
@@ -860,7 +892,9 @@ class DeepSeekV3(tnn.Module):
         MoE routing / permutation / grouped GEMMs never read device values on the host."""
         if self.c.attention == "ref":
             raise NotImplementedError("graph decode needs the paper MLA (the ref preset adds sinusoidal PE by position)")
-        n, _ = self.hidden(ids, cache, state)
+        # EP > 1: fixed blocks at the exact per-peer bound (no host read, no overflow, no flag)
+        with self.ep_dispatch("bound"):
+            n, _ = self.hidden(ids, cache, state)
         return self.logits(n).float()[:, -1]
 
     @torch.no_grad()

@@ -76,7 +76,10 @@ class _CheckedOp:
 
     def __call__(self, *a, **k):
         out = self._op(*a, **k)
-        if torch.cuda.is_available() and torch.cuda.is_initialized():
+        # inside a HIP-graph capture a device sync is illegal: the guard records are read after
+        # replay instead (debug_sync / debug_bounds_report by the caller)
+        if torch.cuda.is_available() and torch.cuda.is_initialized() and \
+                not torch.cuda.is_current_stream_capturing():
             torch.cuda.synchronize()
             if _DEBUG_BOUNDS[0]:
                 rep = debug_bounds_report(True)
@@ -116,7 +119,8 @@ def on_gpu(t: torch.Tensor) -> bool:
 def debug_sync(name: str):
     """SPA_DEBUG_SYNC=1 -> synchronise here (and, in a debug-bounds build, check the guards) -- for
     code that launches kernels outside :func:`ops` (e.g. hipBLASLt GEMMs between two HIP ops)."""
-    if os.environ.get("SPA_DEBUG_SYNC") == "1" and torch.cuda.is_available():
+    if os.environ.get("SPA_DEBUG_SYNC") == "1" and torch.cuda.is_available() and \
+            not torch.cuda.is_current_stream_capturing():
         torch.cuda.synchronize()
         if debug_bounds_enabled():
             rep = debug_bounds_report(True)

@@ -14,6 +14,16 @@ reduced gradients onto cuda:0. Here:
   layer i overlaps the backward GEMMs of layers i-1..0;
 * ``zero1=True`` switches each bucket to reduce-scatter, shards AdamW state
   across ranks (optimizer memory/compute / N) and all-gathers updated params;
+* ``reduce="a2a"`` (default for bf16 gradient buffers; SPA_DP_REDUCE=ring|a2a): a bucket's
+  reduce-scatter is ONE all-to-all -- every rank receives the N bf16 copies of its shard straight
+  from the N-1 peers, which on the xGMI full mesh uses all 7 links at once -- followed by an fp32
+  sum of the copies on the device (``spa::shard_sum_``, one bf16 rounding) and, without ZeRO-1, an
+  all-gather. The wire bytes equal a ring all-reduce's (2(N-1)/N of the bucket per rank), but a
+  ring's reduce-scatter rounds its running bf16 partial at every hop: N-1 = 7 roundings at N = 8,
+  2.2x one bf16 rounding of the exact average on LLaMA-8B gradients vs 1.0x here
+  (tools/grad_precision.py --mode ring, profiles/r6_dp_reduce_numerics.txt). The reference
+  reduces fp32 gradients (deepseekv3/deepseekv3.ipynb:2427). ``reduce="ring"``: RCCL all-reduce /
+  reduce-scatter (ReduceOp.AVG);
 * expert-parallel buckets (every param tagged ``expert_parallel``) hold different
   experts on each EP rank and already contain the gradient contributions of every
   rank's tokens (the all-to-all backward brought them home): they are summed only
@@ -22,6 +32,7 @@ reduced gradients onto cuda:0. Here:
 """
 from __future__ import annotations
 
+import os
 from contextlib import contextmanager
 from typing import List, Optional
 
@@ -33,7 +44,7 @@ from ..utils.flat import FlatParams
 
 class DataParallel:
     def __init__(self, model: torch.nn.Module, flat: FlatParams, group=None, zero1: bool = False,
-                 expert_dp_group=None):
+                 expert_dp_group=None, reduce: Optional[str] = None):
         self.model = model
         self.expert_dp_group = expert_dp_group
         self.expert_buckets = {b.index for b in flat.buckets
@@ -52,6 +63,13 @@ class DataParallel:
         from .dist import force_collectives
         # the collective paths run at world > 1, or at world 1 under SPA_FORCE_COLLECTIVES (tests)
         self.active = self.world > 1 or (dist.is_initialized() and force_collectives())
+        if reduce is None:
+            reduce = os.environ.get("SPA_DP_REDUCE") or ("a2a" if flat.grad.dtype == torch.bfloat16 else "ring")
+        assert reduce in ("a2a", "ring"), reduce
+        self.reduce = reduce
+        self._keep: List[torch.Tensor] = []       # a2a receive buffers (CPU / gloo path)
+        self._rstream = torch.cuda.Stream(device=flat.grad.device) \
+            if (self.active and reduce == "a2a" and flat.grad.is_cuda) else None
         if self.active:
             model.grad_ready_cb = self._on_ready
             for b in flat.buckets:
@@ -80,6 +98,9 @@ class DataParallel:
             self._avg_after.append((g, self.world))
             return
         group, world = self.group, self.world
+        if self.reduce == "a2a":
+            self._works.append(self._a2a_reduce(g, b.numel // world))
+            return
         use_avg = self.backend == "nccl"
         op = dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM
         if self.zero1:
@@ -93,6 +114,36 @@ class DataParallel:
             if not use_avg:
                 self._avg_after.append((g, world))
         self._works.append(w)
+
+    def _a2a_reduce(self, g: torch.Tensor, n: int):
+        """Reduce-scatter of bucket ``g`` as one all-to-all + an fp32 device sum of the N received
+        shard copies (one rounding), then (no ZeRO-1) the in-place all-gather. On the GPU the three
+        run on a side stream that first waits for the compute stream (the bucket's gradients are
+        complete there); returns a handle whose wait() orders the caller's stream after them."""
+        shard = g[self.rank * n:(self.rank + 1) * n]
+        scale = 1.0 / self.world
+        if self._rstream is None:                  # CPU / gloo
+            recv = torch.empty_like(g)
+            dist.all_to_all_single(recv, g, group=self.group)
+            shard.copy_((recv.view(self.world, n).float().sum(0) * scale).to(g.dtype))
+            if self.zero1:
+                return _Done()
+            return dist.all_gather_into_tensor(g, shard.clone(), group=self.group, async_op=True)
+        from ..ops._ext import ops
+        s = self._rstream
+        s.wait_stream(torch.cuda.current_stream(g.device))
+        with torch.cuda.stream(s):
+            recv = torch.empty_like(g)             # allocated on s: reused only after s passes here
+            w = dist.all_to_all_single(recv, g, group=self.group, async_op=True)
+            w.wait()                               # s waits for the RCCL stream (no host block)
+            ops().shard_sum_(shard, recv, self.world, scale)
+            del recv
+            if self.zero1:
+                ev = torch.cuda.Event()
+                ev.record(s)
+                return _EventWork(ev)
+            # in place: the input is this rank's slice of the output (RCCL's in-place all-gather)
+            return dist.all_gather_into_tensor(g, shard, group=self.group, async_op=True)
 
     def _on_ready(self, key):
         if self._sync and self.active:
@@ -157,6 +208,22 @@ class DataParallel:
                     if b.index in self.expert_buckets:
                         dist.broadcast(self.flat.param[b.start:b.end], src=esrc, group=grp)
         _invalidate()
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
+class _EventWork:
+    """wait(): the current stream waits for the event (no host block), like an RCCL work's wait."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
 
 
 def _invalidate():

@@ -25,8 +25,11 @@ src) row) are built on the device from the exchanged counts, and the grouped GEM
 offsets from the device (tiles past the last expert exit). A block that would overflow sets a
 device flag (max over the EP group, async); the model reads the flags once per forward
 (``capacity_overflowed``) -- by then the GPU is still busy with the queued layers -- and re-runs
-the forward with twice the capacity, so results never depend on C. The price is the padded wire
-bytes (P*C rows per rank instead of A).
+the forward with every layer's C set from the load it saw (x SPA_EP_CAP_MARGIN >= 1); if that
+re-run still overflows (a downstream layer saw perturbed inputs), the next attempt uses the exact
+split-size dispatch, so results never depend on C and training never stops on it
+(models/deepseekv3.py ``_capacity_run``). Decode / prefill with a cache always takes the exact
+path. The price is the padded wire bytes (P*C rows per rank instead of A).
 
 Expert parameters carry ``p.expert_parallel = True``: DataParallel does not
 all-reduce them across the EP group (each rank holds different experts) and the
@@ -220,7 +223,8 @@ def ep_prepare(idx, n_experts, group, to_host=True):
 
 
 # ----------------------------------------------------------------------------- capacity mode
-_CAP = {"scale": 1.0, "pending": [], "margin": float(os.environ.get("SPA_EP_CAP_MARGIN", "1.1"))}
+# margin < 1 would size a re-run below the load it just saw (and overflow again): clamped to >= 1
+_CAP = {"scale": 1.0, "pending": [], "margin": max(1.0, float(os.environ.get("SPA_EP_CAP_MARGIN", "1.1")))}
 
 
 def capacity_rows(A, P, El, k, cf):
@@ -229,6 +233,12 @@ def capacity_rows(A, P, El, k, cf):
     bound = (A // max(k, 1)) * min(k, El)
     c = min(max(int(math.ceil(cf * A / P)), 1), max(bound, 1))
     return (c + 15) // 16 * 16
+
+
+def capacity_bound_rows(A, El, k):
+    """The exact per-peer bound (a token sends at most min(k, El) of its k rows to one peer),
+    rounded up to 16: blocks of this size can never overflow (``capacity`` = inf)."""
+    return (max((A // max(k, 1)) * min(k, El), 1) + 15) // 16 * 16
 
 
 def capacity_scale() -> float:
@@ -255,7 +265,7 @@ def capacity_overflowed() -> bool:
     for (_, _, C, state), mx in zip(pend, loads):
         over |= mx > C
         if state is not None:
-            want = max(mx * _CAP["margin"], 0.99 * (state.rows or 0))
+            want = max(mx * _CAP["margin"], mx, 0.99 * (state.rows or 0))
             state.rows = max(16, (int(math.ceil(want)) + 15) // 16 * 16)
         elif mx > C:
             grow_capacity()
@@ -389,16 +399,22 @@ def ep_stage_prepare(x, idx, w, n_experts, group, fp8=False, W13=None, capacity=
     if cap:
         El = n_experts // P
         A = idx.numel()
-        C = capacity_rows(A, P, El, idx.shape[-1] if idx.dim() > 1 else 1, capacity * capacity_scale())
-        if cap_state is not None and getattr(cap_state, "rows", None):
-            C = cap_state.rows
+        k = idx.shape[-1] if idx.dim() > 1 else 1
+        bound = math.isinf(capacity)        # blocks at the exact per-peer bound: cannot overflow
+        if bound:
+            C = capacity_bound_rows(A, El, k)
+        else:
+            C = capacity_rows(A, P, El, k, capacity * capacity_scale())
+            if cap_state is not None and getattr(cap_state, "rows", None):
+                C = cap_state.rows
         st.cap = SimpleNamespace(C=C, P=P, El=El)
         # send: block slot <- expert-sorted row (send_to), and back (send_back); receive: (local
         # expert, src) row <- received slot (recv_to), and back (recv_back)
         st.cap.send_to, st.cap.send_back = _cap_maps(_cap_send_index(st.prep.plan.offsets, P, El, C, A), P * C)
         rc = st.prep.recv.view(P, El)
         st.cap.recv_to, st.cap.recv_back = _cap_maps(_cap_recv_dest(rc, C), P * C)
-        _cap_flag(st.prep.counts, P, El, C, group, cap_state)
+        if not bound:
+            _cap_flag(st.prep.counts, P, El, C, group, cap_state)
         per_e = rc.sum(0)
         st.rc_dev = rc
         # clamped to the P*C rows that exist: an overflowing attempt (re-run by the model) must still

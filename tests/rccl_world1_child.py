@@ -7,6 +7,8 @@ Checked here, each against the same computation without a process group:
   * DataParallel per-layer buckets with ReduceOp.AVG on a bf16 gradient buffer, launched from the
     backward's ready markers, with no_sync accumulation over two micro-batches;
   * ZeRO-1: reduce_scatter_tensor + sharded AdamW + all_gather_into_tensor;
+  * both DP reductions: "ring" (the two above) and "a2a" (all_to_all_single of the bucket, the
+    fp32 shard sum kernel on a side stream, in-place all_gather_into_tensor);
   * comm.all_to_all_single with explicit splits issued from the launch stream (after=event);
   * the EP dispatch: count all-to-all, pinned D2H of the split sizes, row exchange, device regroup,
     combine exchange -- bf16 and fp8 (e4m3 + E8M0) payloads, forward and backward;
@@ -45,14 +47,14 @@ def llama():
     return llama3.Llama3(c, device=DEV, dtype=DT, seed=3)
 
 
-def dp_run(use_dp, zero1, ids):
+def dp_run(use_dp, zero1, ids, reduce=None):
     import torch.distributed as dist
     from solvingpapers_amd.parallel.data_parallel import DataParallel
     from solvingpapers_amd.train.optim import FlatAdamW
     from solvingpapers_amd.utils.flat import FlatParams
     m = llama()
     flat = FlatParams(m, groups=m.param_groups(), grad_dtype=DT, align=64)
-    dp = DataParallel(m, flat, zero1=zero1) if use_dp else None
+    dp = DataParallel(m, flat, zero1=zero1, reduce=reduce) if use_dp else None
     if dp is not None:
         assert dp.active and dp.backend == dist.get_backend() == ("gloo" if CPU else "nccl")
     shard = (dp.shard_ranges(), None) if zero1 else None
@@ -119,13 +121,16 @@ def main():
     step("barrier/all_reduce_max/AVG")
 
     # an AVG over one rank is the identity: equal up to the run-to-run atomics of a few kernels
-    g, p = dp_run(True, False, ids)
-    assert rel(g, ref_g) < 1e-3, ("DP AVG bucket grads", rel(g, ref_g))
-    assert (p - ref_p).abs().max().item() < 1e-2, ("DP params", (p - ref_p).abs().max().item())
-    step("dp buckets + no_sync", f"grad numel={g.numel()} rel={rel(g, ref_g):.2e}")
-    g, p = dp_run(True, True, ids)
-    assert (p - ref_p).abs().max().item() < 1e-2, ("ZeRO-1 params", (p - ref_p).abs().max().item())
-    step("zero1 reduce_scatter + all_gather")
+    # reduce="ring": RCCL all-reduce / reduce-scatter (AVG); "a2a": all-to-all + device fp32 shard
+    # sum (spa::shard_sum_ on a side stream) + in-place all-gather -- the bf16 default
+    for red in ("ring", "a2a"):
+        g, p = dp_run(True, False, ids, red)
+        assert rel(g, ref_g) < 1e-3, ("DP bucket grads", red, rel(g, ref_g))
+        assert (p - ref_p).abs().max().item() < 1e-2, ("DP params", red, (p - ref_p).abs().max().item())
+        step("dp buckets + no_sync", f"reduce={red} grad numel={g.numel()} rel={rel(g, ref_g):.2e}")
+        g, p = dp_run(True, True, ids, red)
+        assert (p - ref_p).abs().max().item() < 1e-2, ("ZeRO-1 params", red, (p - ref_p).abs().max().item())
+        step("zero1 reduce-scatter + all_gather", f"reduce={red}")
 
     # all_to_all_single with explicit splits from the launch stream
     src = torch.randn(300, 64, device=DEV)

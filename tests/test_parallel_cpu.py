@@ -37,19 +37,20 @@ def _llama(seed=0):
     return llama3.Llama3(c, seed=seed)
 
 
-def _dp_worker(rank, world, port, q, zero1, accum=1):
+def _dp_worker(rank, world, port, q, zero1, accum=1, reduce=None):
     _init(rank, world, port)
     from solvingpapers_amd.parallel.data_parallel import DataParallel
     from solvingpapers_amd.train.optim import FlatAdamW
     from solvingpapers_amd.utils.flat import FlatParams
     m = _llama()
     flat = FlatParams(m, groups=m.param_groups(), align=64)
-    dp = DataParallel(m, flat, zero1=zero1)
+    dp = DataParallel(m, flat, zero1=zero1, reduce=reduce)
     shard = (dp.shard_ranges(), None) if zero1 else None
     opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=1.0, shard=shard)
     g = torch.Generator().manual_seed(1)
     ids = torch.randint(0, 64, (4, 17), generator=g)
-    mine = ids[rank * 2:(rank + 1) * 2]
+    per = 4 // world
+    mine = ids[rank * per:(rank + 1) * per]
     for _ in range(2):
         opt.zero_grad()
         if accum == 1:
@@ -118,6 +119,21 @@ def test_dp_grad_accumulation_no_sync_matches_single_process(zero1):
     one launches it; the result equals the un-accumulated single-process step."""
     ref_g, ref_p = _single_reference()
     out = _run(_dp_worker, 2, zero1, 2)
+    for rank, g, p in out:
+        if g is not None:
+            g = torch.from_numpy(g)
+            assert torch.allclose(g, ref_g, atol=1e-5, rtol=1e-4), (rank, (g - ref_g).abs().max())
+        p = torch.from_numpy(p)
+        assert torch.allclose(p, ref_p, atol=1e-5), (rank, (p - ref_p).abs().max())
+
+
+@pytest.mark.parametrize("world,zero1,accum", [(2, False, 1), (2, True, 2), (4, False, 1), (4, True, 1)])
+def test_dp_a2a_reduce_matches_single_process(world, zero1, accum):
+    """reduce="a2a" (the bf16 default: one all-to-all of the bucket, an fp32 sum of the N received
+    shard copies, then the all-gather; ZeRO-1 stops after the sum) equals the single-process step
+    at world 2 and 4, with and without ZeRO-1 / accumulation."""
+    ref_g, ref_p = _single_reference()
+    out = _run(_dp_worker, world, zero1, accum, "a2a")
     for rank, g, p in out:
         if g is not None:
             g = torch.from_numpy(g)
@@ -557,7 +573,8 @@ def test_forced_collectives_world1_gloo():
 
 def _cap_overflow_worker(rank, world, port, q, fp8):
     """DeepSeekV3 EP=2 with a capacity far below the routed load: every forward overflows first,
-    is re-run with doubled capacity until it fits, and must then equal the exact-split model."""
+    is re-run with each layer's rows set from the load it saw, and must then equal the exact-split
+    model."""
     _init(rank, world, port)
     from dataclasses import replace
     from solvingpapers_amd.models import deepseekv3 as ds
@@ -597,3 +614,57 @@ def _cap_overflow_worker(rank, world, port, q, fp8):
 def test_ep_capacity_overflow_reruns_exactly(fp8):
     out = _run(_cap_overflow_worker, 2, fp8)
     assert len(out) == 2 and out[0][1] == out[1][1]     # both ranks agreed on every re-run
+
+
+def _cap_decode_worker(rank, world, port, q, mode):
+    """Capacity-mode EP (ep_capacity > 0) at EP=2 on the inference paths: step() with a cache takes
+    the exact dispatch, the "bound" dispatch (graph decode) uses never-overflowing fixed blocks, and
+    neither leaves overflow flags behind; forward() falls back to the exact dispatch after
+    _CAP_ATTEMPTS overflowing attempts instead of raising."""
+    _init(rank, world, port)
+    from dataclasses import replace
+    from solvingpapers_amd.models import deepseekv3 as ds
+    from solvingpapers_amd.parallel import expert_parallel as ep
+    c = ds.config("dsv3_tiny", dim=128, n_experts=4, top_k=2, expert_hidden=128, n_layers=2, n_dense_layers=0,
+                  dropout=0.0, attn_dropout=0.0, mtp_heads=0)
+    grp = dist.new_group([0, 1])
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(0, c.vocab_size, (2, 2, 17), generator=g)[rank]
+    ref = ds.DeepSeekV3(replace(c, ep_capacity=0.0), seed=3, ep_group=grp).eval()
+    cap = ds.DeepSeekV3(replace(c, ep_capacity=0.1), seed=3, ep_group=grp).eval()
+    with torch.no_grad():
+        if mode == "step":
+            outs = []
+            for m in (ref, cap):
+                cache = m.new_cache(2, 32)
+                a = m.step(ids[:, :12], cache, 0)
+                b = m.step(ids[:, 12:13], cache, 12)
+                outs.append((a, b))
+            assert not ep._CAP["pending"], "step() left capacity flags behind"
+            for x, y in zip(*outs):
+                assert torch.allclose(x, y, atol=1e-5, rtol=1e-4), (x - y).abs().max()
+        elif mode == "bound":
+            n0, _ = ref.hidden(ids)
+            with cap.ep_dispatch("bound"):
+                n1, _ = cap.hidden(ids)
+            assert not ep._CAP["pending"], "bound dispatch set overflow flags"
+            assert torch.allclose(n0, n1, atol=1e-5, rtol=1e-4), (n0 - n1).abs().max()
+        else:                                   # "fallback": one capacity attempt, then exact
+            cap.train()
+            ref.train()
+            cap._CAP_ATTEMPTS = 1
+            calls = []
+            real = cap._forward
+            cap._forward = lambda *a, _r=real, **k: (calls.append(1), _r(*a, **k))[1]
+            l1 = cap(ids[:, :-1], ids[:, 1:]).item()
+            l0 = ref(ids[:, :-1], ids[:, 1:]).item()
+            assert len(calls) == 2 and abs(l0 - l1) < 1e-5, (calls, l0, l1)
+            assert all(m.dispatch_mode is None for m in cap.moe_layers())
+    q.put((rank, mode))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["step", "bound", "fallback"])
+def test_ep_capacity_inference_paths_and_fallback(mode):
+    out = _run(_cap_decode_worker, 2, mode)
+    assert len(out) == 2

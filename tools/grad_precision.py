@@ -20,6 +20,15 @@ path (--grad-fp32) pays when the optimizer reads it. Two measurements:
     bf16 grads with a different data/init seed (the run-to-run noise scale). Prints one JSON line
     per arm with the loss every 10 steps, then a summary line.
 
+``--mode ring``  the DP reduction at N ranks: N ranks' bf16-accumulated flat
+    gradients at LLaMA3-8B widths (same weights, different batches), reduced three ways against the
+    exact fp64 average of what the ranks hold: RCCL's ring all-reduce in bf16 (reduce-scatter in ring
+    chunk order: every hop reads the running bf16 partial, adds its own value in fp32 and rounds to
+    bf16 -> N-1 roundings per element; ReduceOp.AVG's 1/N pre-scale is exact for N = 2^k; the
+    all-gather only copies), the all-to-all reduce-scatter (every rank receives all N shards of its
+    chunk and sums them in fp32 -> one rounding; parallel/data_parallel.py reduce="a2a"), and fp32
+    buckets. Reports each error as a multiple of one bf16 rounding of the exact average.
+
 The reference keeps fp32 gradients (deepseekv3/deepseekv3.ipynb:2411,2427-2447 under fp16
 autocast; llama3/LLaMA-jax.ipynb:993-1001 trains in fp32).
 """
@@ -90,6 +99,77 @@ def grad_error(layers=2, T=8192, accum=4, seed=1234):
             "worst": sorted(rows, key=lambda r: -r["ratio"])[:4]}
 
 
+def ring_allreduce_bf16(xs, chunk_order=True):
+    """Emulate RCCL's bf16 ring all-reduce (SUM) of the equal-shape bf16 tensors ``xs`` (one per
+    rank): the buffer is cut into N chunks; chunk c's reduce-scatter starts at rank c+1 and walks the
+    ring, each hop computing bf16(float(partial) + float(own)). Returns the bf16 result every rank
+    holds after the all-gather."""
+    N = len(xs)
+    flat = [x.reshape(-1) for x in xs]
+    n = flat[0].numel()
+    out = torch.empty_like(flat[0])
+    bounds = [n * c // N for c in range(N + 1)]
+    for c in range(N):
+        a, b = bounds[c], bounds[c + 1]
+        order = [(c + 1 + i) % N for i in range(N)] if chunk_order else list(range(N))
+        acc = flat[order[0]][a:b].clone()
+        for r in order[1:]:
+            acc = (acc.float() + flat[r][a:b].float()).to(torch.bfloat16)
+        out[a:b] = acc
+    return out.view_as(xs[0])
+
+
+def a2a_reduce_bf16(xs):
+    """The all-to-all reduce-scatter + all-gather (data_parallel reduce="a2a"): every shard summed in
+    fp32 from the N received bf16 copies, rounded once."""
+    acc = xs[0].float()
+    for x in xs[1:]:
+        acc += x.float()
+    return acc.to(torch.bfloat16)
+
+
+def ring_error(ranks=8, layers=2, T=8192, accum=4, seed=1234, chunk=1 << 26):
+    """Relative errors of the N-rank DP average (ring bf16 / a2a bf16 / fp32 buckets) against the
+    exact fp64 average of the ranks' bf16 gradients, and their ratio to one bf16 rounding."""
+    dev = torch.device("cuda")
+    cfg = llama3.config("llama3_8b", n_layers=layers, max_seq_len=T)
+    model = llama3.Llama3(cfg, device=dev, dtype=torch.bfloat16, seed=seed)
+    grads = []
+    for r in range(ranks):
+        g = torch.Generator(device=dev).manual_seed(seed + 101 * (r + 1))
+        batches = []
+        for _ in range(accum):
+            t = torch.randint(0, cfg.vocab_size, (1, T + 1), device=dev, generator=g)
+            batches.append((t[:, :-1], t[:, 1:]))
+        f = accumulated_grad(model, torch.bfloat16, batches)
+        grads.append(f.grad.clone())
+        del f
+    inv = 1.0 / ranks
+    acc = {"ring": [0.0, 0.0], "a2a": [0.0, 0.0], "fp32": [0.0, 0.0], "floor": [0.0, 0.0]}
+    n = grads[0].numel()
+    nrm = 0.0
+    for a in range(0, n, chunk):
+        xs = [g[a:a + chunk] for g in grads]
+        exact = torch.zeros(xs[0].shape, dtype=torch.float64, device=dev)
+        for x in xs:
+            exact += x.double()
+        exact *= inv
+        nrm += exact.square().sum().item()
+        # ReduceOp.AVG pre-scales each input by 1/N (exact in bf16 for N = 2^k)
+        pre = [(x.float() * inv).to(torch.bfloat16) for x in xs]
+        outs = {"ring": ring_allreduce_bf16(pre), "a2a": a2a_reduce_bf16(pre),
+                "fp32": sum(x.float() for x in xs) * inv, "floor": exact.to(torch.bfloat16)}
+        for k, v in outs.items():
+            acc[k][0] += (v.double() - exact).square().sum().item()
+    nrm = math.sqrt(nrm)
+    rel = {k: math.sqrt(v[0]) / nrm for k, v in acc.items()}
+    fl = rel["floor"]
+    return {"ranks": ranks, "layers": layers, "T": T, "accum": accum, "numel": n,
+            "rel_err_ring_bf16": rel["ring"], "rel_err_a2a_bf16": rel["a2a"], "rel_err_fp32": rel["fp32"],
+            "bf16_floor": fl, "ratio_ring": rel["ring"] / fl, "ratio_a2a": rel["a2a"] / fl,
+            "ratio_fp32": rel["fp32"] / fl}
+
+
 def corpus(V, n, dev, seed):
     """B8's learnable stream (bench/parity.py run_b8): 1024-token affine chains mod V with 10 %
     uniform noise tokens."""
@@ -133,11 +213,15 @@ def loss_curve(gdt, steps, seed, B=4, T=512, accum=4, lr=6e-4, every=10):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["grad", "curve"], default="grad")
+    ap.add_argument("--mode", choices=["grad", "curve", "ring"], default="grad")
+    ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--seed", type=int, default=1)
     a = ap.parse_args()
+    if a.mode == "ring":
+        print(json.dumps(ring_error(ranks=a.ranks, layers=a.layers)), flush=True)
+        return
     if a.mode == "grad":
         print(json.dumps(grad_error(layers=a.layers)), flush=True)
         return
