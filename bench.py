@@ -211,6 +211,9 @@ def run(a):
             "gemm_table": tuned,
             "loss": round(loss_v, 4),
             "mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,
+            # device-wide use at the end (torch's pool + RCCL / hipBLASLt / runtime buffers)
+            "dev_mem_used_gb": round((lambda f, t: (t - f) / 1e9)(*torch.cuda.mem_get_info()), 1) if cuda else None,
+            "dp_reduce": dp.reduce if dp is not None else None,
             "world_size": world,
             "backend": tdist.get_backend() if tdist.is_initialized() else "none",
             "device_count": torch.cuda.device_count() if cuda else 0,

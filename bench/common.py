@@ -40,4 +40,6 @@ def report(metric, value, unit, steps, warmup, elapsed, config, **extra):
         out.update(extra)
         if torch.cuda.is_available():
             out["mem_gb"] = round(torch.cuda.max_memory_allocated() / 1e9, 1)
+            free, total = torch.cuda.mem_get_info()     # device-wide: RCCL / hipBLASLt buffers included
+            out["dev_mem_used_gb"] = round((total - free) / 1e9, 1)
         print(json.dumps(out), flush=True)

@@ -191,7 +191,9 @@ class GPT(tnn.Module):
         return idx
 
     # ------------------------------------------------------------ Flax pytree layout
-    def to_reference_params(self) -> Dict[str, torch.Tensor]:
+    def to_reference_params(self, dtype=torch.float32) -> Dict[str, torch.Tensor]:
+        """The Flax pytree (gpt-jax.ipynb GPT.init), kernels (in, out); ``dtype`` None keeps the
+        model's (fp64 for the numeric parity test)."""
         d = {"token_embed/embedding": self.token_embed.detach(), "pos_embed": self.pos_embed.detach()}
         for i, l in enumerate(self.layers):
             p = f"layers_{i}/"
@@ -203,11 +205,11 @@ class GPT(tnn.Module):
             d[p + "mlp/fc2/kernel"], d[p + "mlp/fc2/bias"] = l.fc2.weight.detach().t(), l.fc2.bias.detach()
         d["ln_f/scale"], d["ln_f/bias"] = self.ln_f.weight.detach(), self.ln_f.bias.detach()
         d["lm_head/kernel"] = self.lm_head.detach().t()
-        return {k: v.float().clone() for k, v in d.items()}
+        return {k: (v if dtype is None else v.to(dtype)).clone() for k, v in d.items()}
 
     @torch.no_grad()
     def from_reference_params(self, d):
-        t = lambda k: torch.as_tensor(d[k], dtype=torch.float32)
+        t = lambda k: torch.as_tensor(d[k], dtype=self.token_embed.dtype)
         self.token_embed.copy_(t("token_embed/embedding"))
         self.pos_embed.copy_(t("pos_embed"))
         for i, l in enumerate(self.layers):

@@ -171,7 +171,8 @@ def _materialised(q, k, v, causal, scale, dropout_p=0.0, seed=0, neg=float("-inf
     qh = q.transpose(1, 2)
     kh = k.transpose(1, 2).repeat_interleave(rep, dim=1)
     vh = v.transpose(1, 2).repeat_interleave(rep, dim=1)
-    s = torch.matmul(qh, kh.transpose(-1, -2)).float() * scale
+    s = torch.matmul(qh, kh.transpose(-1, -2))
+    s = (s if s.dtype == torch.float64 else s.float()) * scale      # fp64 parity tests keep fp64
     if causal:
         i = torch.arange(Tq, device=q.device)[:, None]
         j = torch.arange(Tk, device=q.device)[None, :]

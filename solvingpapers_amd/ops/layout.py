@@ -112,4 +112,4 @@ def bias_grad(dy2: torch.Tensor) -> torch.Tensor:
     if (dy2.is_cuda and dy2.dtype == torch.bfloat16 and dy2.dim() == 2 and dy2.stride(1) == 1
             and dy2.shape[1] % 8 == 0 and dy2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0):
         return _ext.ops().rowsum_bf16(dy2)
-    return dy2.sum(0, dtype=torch.float32)
+    return dy2.sum(0, dtype=torch.float64 if dy2.dtype == torch.float64 else torch.float32)

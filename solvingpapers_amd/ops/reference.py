@@ -11,6 +11,11 @@ import math
 import torch
 import torch.nn.functional as F
 
+def _f(t):
+    """fp32 compute, or fp64 for fp64 inputs (the CPU numeric-parity tests run whole models in fp64)."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
 ACT_KINDS = {
     "relu": 0, "leaky_relu": 1, "prelu": 2, "elu": 3, "gelu_tanh": 4, "gelu": 5, "gelu_erf": 5,
     "silu": 6, "swish": 6, "sigmoid": 7, "tanh": 8, "identity": 9,
@@ -19,22 +24,22 @@ ACT_KINDS = {
 
 def rms_norm(x, w, eps, residual=None):
     """llama3/LLaMA-jax.ipynb:536-538; gemma/gemma.ipynb:139-150 (fp32 compute)."""
-    h = x if residual is None else (x.float() + residual.float()).to(x.dtype)
-    hf = h.float()
-    y = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    h = x if residual is None else (_f(x) + _f(residual)).to(x.dtype)
+    hf = _f(h)
+    y = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps) * _f(w)
     return y.to(x.dtype), h
 
 
 def layer_norm(x, w, b, eps, residual=None):
     """gpt/gpt-jax.ipynb:414-416 (flax LayerNorm eps 1e-6); ViT.ipynb:205-206."""
-    h = x if residual is None else (x.float() + residual.float()).to(x.dtype)
-    y = F.layer_norm(h.float(), (h.shape[-1],), w.float(), b.float(), eps)
+    h = x if residual is None else (_f(x) + _f(residual)).to(x.dtype)
+    y = F.layer_norm(_f(h), (h.shape[-1],), _f(w), _f(b), eps)
     return y.to(x.dtype), h
 
 
 def act(x, kind: str, alpha: float = 0.0):
     """activation functions/GELU.ipynb:54-55, ReLU.ipynb:20-54."""
-    xf = x.float()
+    xf = _f(x)
     if kind == "relu":
         y = F.relu(xf)
     elif kind in ("leaky_relu", "prelu"):
@@ -60,8 +65,8 @@ def act(x, kind: str, alpha: float = 0.0):
 
 def glu(gu, kind: str):
     """SwiGLU llama3/LLaMA-jax.ipynb:854-855 (gate=w3 in the ref), GeGLU gemma.ipynb:281-286."""
-    g, u = gu.float().chunk(2, dim=-1)
-    return (act(g, kind).float() * u).to(gu.dtype)
+    g, u = _f(gu).chunk(2, dim=-1)
+    return (_f(act(g, kind)) * u).to(gu.dtype)
 
 
 def rope_tables(T, hd, theta=10000.0, device=None, ref_freqs=False):
@@ -87,7 +92,7 @@ def rope(x, cos, sin, pos_off=0, interleaved=True, inverse=False, positions=None
         s = sin[positions.long()][:, :, None, :]
     if inverse:
         s = -s
-    xf = x.float()
+    xf = _f(x)
     if interleaved:
         x0, x1 = xf[..., 0::2], xf[..., 1::2]
         o0 = x0 * c - x1 * s
@@ -110,9 +115,9 @@ def attention(q, k, v, causal=True, scale=None):
     Tk, Hkv = k.shape[1], k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(hd)
     rep = H // Hkv
-    kf = k.float().repeat_interleave(rep, dim=2)
-    vf = v.float().repeat_interleave(rep, dim=2)
-    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), kf) * scale
+    kf = _f(k).repeat_interleave(rep, dim=2)
+    vf = _f(v).repeat_interleave(rep, dim=2)
+    s = torch.einsum("bqhd,bkhd->bhqk", _f(q), kf) * scale
     if causal:
         i = torch.arange(Tq, device=q.device)[:, None]
         j = torch.arange(Tk, device=q.device)[None, :]
@@ -125,7 +130,7 @@ def attention(q, k, v, causal=True, scale=None):
 
 def cross_entropy(logits, target, ignore_index=-100, smoothing=0.0):
     """Per-row CE losses (fp32), F.cross_entropy semantics. gpt-jax.ipynb:503."""
-    return F.cross_entropy(logits.float(), target, ignore_index=ignore_index, reduction="none",
+    return F.cross_entropy(_f(logits), target, ignore_index=ignore_index, reduction="none",
                            label_smoothing=smoothing)
 
 

@@ -309,7 +309,9 @@ def cross_entropy(logits, target, ignore_index=-100, label_smoothing=0.0, reduct
         if reduction == "sum":
             return loss.sum()
         return loss.sum() / (target != ignore_index).sum().clamp_min(1)
-    return torch.nn.functional.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), target.reshape(-1),
+    lg = logits.reshape(-1, logits.shape[-1])
+    lg = lg if lg.dtype == torch.float64 else lg.float()        # fp64 parity tests keep fp64
+    return torch.nn.functional.cross_entropy(lg, target.reshape(-1),
                                              ignore_index=ignore_index, label_smoothing=label_smoothing,
                                              reduction=reduction)
 

@@ -162,6 +162,44 @@ def test_gpt_flax_layout_round_trip():
     assert d["layers_0/attn/qkv/kernel"].shape == (128, 384) and d["lm_head/kernel"].shape == (128, 65)
 
 
+def test_gpt_matches_flax_reference_math_fp64():
+    """Numeric parity with gpt/gpt-jax.ipynb:321-472 (restated in fp64, tests/refimpl.py gpt_forward:
+    fused QKV (in, out) kernel split q|k|v, -1e4 causal fill, tanh GELU, flax LayerNorm eps 1e-6,
+    learned pos_embed, untied bias-free head) and its loss (:499-503), at gpt_ref widths (D256, one
+    256-wide head, V65, T256) with 2 layers: the same Flax pytree loaded into models/gpt.py through
+    from_reference_params gives equal logits and loss (rel <= 1e-10) and equal gradients."""
+    from refimpl import gpt_forward, gpt_loss
+    from solvingpapers_amd.models import gpt
+    c = gpt.config("gpt_ref", num_layers=2)
+    src = gpt.GPT(c, dtype=torch.float64, seed=3)
+    d = src.to_reference_params(dtype=None)
+    m = gpt.GPT(c, dtype=torch.float64, seed=9).from_reference_params(d).eval()
+    ids = torch.randint(0, c.vocab_size, (2, c.block_size + 1), generator=torch.Generator().manual_seed(1))
+    x, y = ids[:, :-1], ids[:, 1:]
+    dr = {k: v.clone().requires_grad_(True) for k, v in d.items()}
+    ref_logits = gpt_forward(dr, x, c.num_heads, c.num_layers)
+    ref_loss = gpt_loss(ref_logits, y)
+    ref_loss.backward()
+    with torch.no_grad():
+        logits = m(x)
+    rel = ((logits - ref_logits.detach()).norm() / ref_logits.detach().norm()).item()
+    assert logits.dtype == torch.float64 and rel <= 1e-10, rel
+    loss = m(x, y)
+    assert abs(loss.item() - ref_loss.item()) <= 1e-10 * abs(ref_loss.item()), (loss.item(), ref_loss.item())
+    loss.backward()
+    saved = {n: p.detach().clone() for n, p in m.named_parameters()}
+    with torch.no_grad():                       # the gradients in the pytree layout
+        for p in m.parameters():
+            p.copy_(p.grad)
+        grads = m.to_reference_params(dtype=None)
+        for n, p in m.named_parameters():
+            p.copy_(saved[n])
+    for k, g in grads.items():
+        want = dr[k].grad
+        r = ((g - want).norm() / want.norm().clamp_min(1e-300)).item()
+        assert r <= 1e-9, (k, r)
+
+
 @pytest.mark.parametrize("kind", ["ae", "vae"])
 def test_autoencoder_training_cpu(kind):
     from solvingpapers_amd.models import autoencoder as A

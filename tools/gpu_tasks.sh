@@ -74,6 +74,24 @@ dkdv5-var)
     run 200 ${O}_st$v.log env SPA_EXT_SO=ab/_C_stamp5.so SPA_ATTN_STAMP=1 SPA_ATTN_DKDV5=$v python -u tools/bench_attn.py --iters 5 --packed
     echo "== SPA_ATTN_DKDV5=$v (stamp build)"; grep -h 'attn B\|role' ${O}_st$v.log | cut -c1-300
   done ;;
+preflight)
+  # multi-GPU pre-flight on one GPU: GPU tests of the forced-collective benches,
+  # the N=8 DP-reduction numerics, full-size benches unforced vs forced through a 1-rank nccl group
+  run 600 ${O}_pytest.log python -u -m pytest tests/test_preflight_gpu.py tests/test_rccl_gpu.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
+  grep -h 'PASS\|FAIL\|passed\|failed' ${O}_pytest.log | cut -c1-200
+  run 400 ${O}_ring.log python -u tools/grad_precision.py --mode ring --layers 2
+  jsonl ${O}_ring.log
+  TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29533"
+  run 400 ${O}_b0.log python -u bench.py --steps 6 --warmup 2
+  run 400 ${O}_b1.log env SPA_FORCE_COLLECTIVES=1 $TR bench.py --steps 6 --warmup 2
+  run 400 ${O}_b2.log env SPA_FORCE_COLLECTIVES=1 SPA_DP_REDUCE=ring $TR bench.py --steps 6 --warmup 2
+  run 400 ${O}_b3.log env SPA_FORCE_COLLECTIVES=1 $TR bench.py --steps 6 --warmup 2 --zero1
+  run 400 ${O}_b4.log python -u bench.py --steps 6 --warmup 2
+  jsonl ${O}_b?.log
+  V3="--preset dsv3_v3 --layers 4 --dense-layers 1 --experts 32 --mb 1 --accum 4 --steps 3 --warmup 1 --fp8"
+  run 400 ${O}_v0.log python -u bench/dsv3_train.py $V3
+  run 400 ${O}_v1.log env SPA_FORCE_COLLECTIVES=1 $TR bench/dsv3_train.py $V3
+  jsonl ${O}_v?.log ;;
 rccl)
   run 300 ${O}_pytest.log python -u -m pytest tests/test_rccl_gpu.py -x -v -s -p no:cacheprovider --timeout 240 --timeout-method thread
   grep -h 'rccl-world1\|passed\|failed' ${O}_pytest.log | cut -c1-200
