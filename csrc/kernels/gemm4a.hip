@@ -1,0 +1,444 @@
+// Grouped / dense bf16 GEMM, third generation: the hipBLASLt tile shape (256 x 256 C tile, 4 waves,
+// one per SIMD, each owning a 128 x 128 quadrant = 64 16x16 MFMA tiles = 256 fp32 accumulators per
+// lane) with the accumulators PINNED in the accumulator register file.
+//
+// Why: written with __builtin_amdgcn_mfma_*, hipcc splits 256 loop-carried accumulators per lane
+// over VGPRs and AGPRs and re-homes them every trip (148-460 v_accvgpr moves per 128 MFMAs,
+// profiles/r5_gemm4w_hipblaslt_shape_probe.txt), so this shape ran 1,108 TF against hipBLASLt's
+// 1,712 at 8192^3. Here every MFMA is an inline-asm v_mfma_f32_16x16x32_bf16 whose C/D operand is an
+// "+a" (AGPR) constraint: the register allocator must keep each accumulator quad in a[...] at every
+// MFMA, so the loop carries them there with no copies; A / B fragments stay in VGPRs (ds_read_b128
+// destinations, waited for by hipcc's own lgkmcnt bookkeeping, which sees the asm operands).
+//
+// Pipeline (per 32-deep K slice, one s_barrier each): a 4-stage LDS ring filled by
+// buffer_load ... lds (16 B per lane, lane-linear images, swizzle in the per-lane SOURCE address)
+// three slices ahead; the wave's 16 fragments of slice t+1 are read (ds_read_b128) into the other
+// register set while the 64 MFMAs of slice t run, interleaved one read per 4 MFMAs with the 8 DMA
+// pieces of slice t+3 spread over the stream. A counted vmcnt before each barrier retires exactly
+// the slice the next one reads; all LDS is one array and every barrier is a bare s_barrier.
+//
+// Modes (grouped_gemm8's contract, csrc/kernels/gemm8.hip):
+//   0 fwd   Y[M, N]  = X[M, K] W_e[N, K]^T        rows grouped by offsets (E = 1: dense X W^T)
+//   1 dX    dX[M, N] = dY[M, K] W_e[K, N]          rows grouped (W_e stored [K=Nw][N=Kw])
+//   2 dW    dW_e[N, K] = dY_e[T, N]^T X_e[T, K]   reduction rows grouped (token segments);
+//           PART: the "experts" are token slices of one dense product, fp32 partials (wgrad4a)
+//
+// LDS images of one operand slice (lane-linear DMA destinations; the swizzle is an involution
+// applied to the per-lane SOURCE address and to the read address):
+//   K-contiguous [256 rows][32 k], 64-B rows: 16-B chunk c of row r at r * 64 + 16 * (c ^ ((r >> 2) & 3))
+//     -- the 16 lanes of a ds_read_b128 quarter (16 consecutive rows, one chunk) hit 16 distinct
+//     16-B bank groups;
+//   K-strided [32 k][256 cols], 512-B rows: chunk c of k-row r at r * 512 + 16 * (c ^ f(r)),
+//     f(r) = ((r & 3) << 2) | ((r >> 2) & 3) -- read with ds_read_b64_tr_b16 (gemm8's recipe).
+#include "gemm_common.h"
+
+#include <type_traits>
+
+SPA_DEBUG_TU("gemm4a.hip")
+
+namespace spa {
+
+namespace g4 {
+
+constexpr int BM = 256, BN = 256, BK = 32, NT = 256, NS = 4;
+constexpr int IMG = 256 * BK * 2;             // one operand slice image (16 KiB)
+constexpr int STAGE = 2 * IMG;                // A + B of one slice (32 KiB)
+constexpr int RING = NS * STAGE;              // 128 KiB
+constexpr int ERS = 256 * 2 + 16;             // epilogue C image row stride (bytes)
+constexpr int SMEM = (RING > 256 * ERS ? RING : 256 * ERS) + 64;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
+  const long nb = bytes < 0 ? 0 : (bytes > 0xFFFFFFFFL ? 0xFFFFFFFFL : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)(unsigned)nb, 0x00020000);
+}
+// byte offset (from the slice origin in global memory) of DMA piece j (0..3) of this thread, 16-B
+// slot q = j * 256 + tid:
+//   K-contiguous: row q >> 2, physical chunk q & 3, logical chunk (q & 3) ^ ((row >> 2) & 3)
+//   K-strided:    k-row q >> 5, physical chunk q & 31, logical chunk (q & 31) ^ f(row)
+__device__ __forceinline__ int ksw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ unsigned dma_off(bool kc, int tid, int j, long ld) {
+  const int q = j * NT + tid;
+  if (kc) {
+    const int r = q >> 2, c = (q & 3) ^ ((r >> 2) & 3);
+    return (unsigned)((r * ld + 8 * c) * 2);
+  }
+  const int r = q >> 5, c = (q & 31) ^ ksw(r);
+  return (unsigned)((r * ld + 8 * c) * 2);
+}
+typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+// 16x16x32 operand of image columns col0 .. col0+15 from a K-strided image (gemm8 rd_ks, 512-B rows)
+__device__ __forceinline__ bf16x8 rd_ks(const char* img, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ch = (col0 >> 3) + (p >> 1);
+  const int ra = 8 * g + q, rb = ra + 4;
+  const s16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + ra * 512 + 16 * (ch ^ ksw(ra)) + 8 * (p & 1)));
+  const s16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + rb * 512 + 16 * (ch ^ ksw(rb)) + 8 * (p & 1)));
+  const bf16x4 av = __builtin_bit_cast(bf16x4, a), bv = __builtin_bit_cast(bf16x4, b);
+  return __builtin_shufflevector(av, bv, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+}  // namespace g4
+
+#define G4_MFMA(ACC, A, B) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(A), "v"(B))
+// first slice: C = inline constant 0, so every definition of an accumulator is an AGPR-constrained
+// asm output (a C++ zero-init is a VGPR def: the loop-carried PHIs then live in VGPRs and are
+// copied into AGPRs around every MFMA)
+#define G4_MFMA0(ACC, A, B) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(ACC) : "v"(A), "v"(B))
+
+template <int MODE, int SCHED = 0, bool PART = false>
+__global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                        bf16* __restrict__ C, const int* __restrict__ offsets, int E,
+                                                        int M, int N, int K, long lda, long ldb, long ldc,
+                                                        long strideB, long strideC, int accumulate, long a_rows,
+                                                        long b_rows, int gm) {
+  using namespace g4;
+  constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  int* scratch = reinterpret_cast<int*>(smem + SMEM - 64);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nnt = (N + BN - 1) / BN;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  int nt = lid % nnt;
+  int mt = lid / nnt;
+  int e = 0;
+  long m0 = 0, mend = M, k0 = 0, kend = K;
+  const bf16* Bp = B;
+  bf16* Cp = C;
+  if (MODE != 2) {
+    if (gm > 1) {   // groups of gm row tiles x all column tiles (L2 reuse of B panels), dense only
+      const int mtiles = gridDim.x / nnt, g = lid / (gm * nnt), r = lid % (gm * nnt);
+      const int gs = min(gm, mtiles - g * gm);
+      mt = g * gm + r % gs;
+      nt = r / gs;
+    }
+    // tile -> (expert, row tile): inclusive scan of the experts' tile counts (one per thread)
+    int* wsum = scratch + 8;
+    const int o0 = tid < E ? offsets[tid] : 0, o1 = tid < E ? offsets[tid + 1] : 0;
+    const int tiles = (o1 - o0 + BM - 1) / BM;
+    int inc = tiles;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    if (tid == 0) scratch[0] = -1;
+    __syncthreads();
+    int pre = inc - tiles;
+    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) {
+      scratch[0] = tid; scratch[1] = mt - pre; scratch[2] = o0; scratch[3] = o1;
+    }
+    __syncthreads();
+    e = __builtin_amdgcn_readfirstlane(scratch[0]);
+    if (e < 0) return;
+    mt = __builtin_amdgcn_readfirstlane(scratch[1]);
+    m0 = __builtin_amdgcn_readfirstlane(scratch[2]) + (long)mt * BM;
+    mend = __builtin_amdgcn_readfirstlane(scratch[3]);
+    Bp = B + e * strideB;
+  } else {
+    const int nmt = (M + BM - 1) / BM;
+    const int per_e = nmt * nnt;
+    if constexpr (!PART) {
+      // heavy experts first, dealt to the XCDs in snake order (gemm8.hip mode 2: every expert owns
+      // the same output tiles but a tile's work is its token count)
+      int* cnt = reinterpret_cast<int*>(smem);
+      const int E4 = (E + 3) & ~3;
+      const int o0 = tid < E ? offsets[tid] : 0, o1 = tid < E ? offsets[tid + 1] : 0;
+      if (tid < E4) cnt[tid] = o1 - o0;
+      __syncthreads();
+      const int4* cnt4 = reinterpret_cast<const int4*>(cnt);
+      long tot = 0;
+      int mx = 0;
+#pragma unroll 4
+      for (int j = 0; j < E4 / 4; ++j) {
+        const int4 v = cnt4[j];
+        tot += (long)v.x + v.y + v.z + v.w;
+        mx = max(max(mx, max(v.x, v.y)), max(v.z, v.w));
+      }
+      const bool snake = E % 8 == 0 && (long)mx * E <= 2 * tot;
+      int pos, r;
+      if (snake) {
+        const int x = blockIdx.x % 8, j = blockIdx.x / 8, u = j / per_e;
+        r = j % per_e;
+        pos = u * 8 + ((u & 1) ? 7 - x : x);
+      } else {
+        pos = blockIdx.x / per_e;
+        r = blockIdx.x % per_e;
+      }
+      if (pos >= E) return;
+      nt = r % nnt;
+      mt = r / nnt;
+      if (tid < E) {
+        const int c = o1 - o0;
+        int rank = 0;
+#pragma unroll 4
+        for (int j = 0; j < E4 / 4; ++j) {
+          const int4 v = cnt4[j];
+          rank += (v.x > c) || (v.x == c && 4 * j < tid);
+          rank += (v.y > c) || (v.y == c && 4 * j + 1 < tid);
+          rank += (v.z > c) || (v.z == c && 4 * j + 2 < tid);
+          rank += (v.w > c) || (v.w == c && 4 * j + 3 < tid);
+        }
+        if (rank == pos) { scratch[0] = tid; scratch[2] = o0; scratch[3] = o1; }
+      }
+      __syncthreads();
+      e = __builtin_amdgcn_readfirstlane(scratch[0]);
+      __syncthreads();   // the count image lives in the ring the prologue DMA fills
+    } else {
+      e = blockIdx.x / per_e;
+      if (e >= E) return;
+      const int r = blockIdx.x % per_e;
+      nt = r % nnt;
+      mt = r / nnt;
+      if (tid == 0) { scratch[2] = offsets[e]; scratch[3] = offsets[e + 1]; }
+      __syncthreads();
+    }
+    m0 = (long)mt * BM;
+    k0 = __builtin_amdgcn_readfirstlane(scratch[2]);
+    kend = __builtin_amdgcn_readfirstlane(scratch[3]);
+    Cp = C + e * strideC;
+  }
+  SPA_DBG_CHECK(e, E);
+  SPA_DBG_ASSERT(MODE == 2 ? kend <= a_rows && kend <= b_rows : mend <= a_rows && m0 < mend,
+                 MODE == 2 ? kend : mend, a_rows);
+  const long n0 = (long)nt * BN;
+  const int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
+  unsigned voA[4], voB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    voA[j] = dma_off(A_KC, tid, j, lda);
+    voB[j] = dma_off(B_KC, tid, j, ldb);
+  }
+  // readable extents (elements): whole operands, or up to the expert's last token (dW)
+  const long limA = MODE == 2 ? kend * lda : a_rows * lda;
+  const long limB = MODE == 2 ? kend * ldb : b_rows * ldb;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+
+  // DMA piece j (0..3 A, 4..7 B) of slice t into its stage
+  auto dma = [&](int t, int j) {
+    char* dst = smem + (t & (NS - 1)) * STAGE + (j >> 2) * IMG + (j & 3) * (NT * 16) + wave_u * 1024;
+    const long kk = k0 + (long)t * BK;
+    const bool ja = j < 4;
+    const bf16* base = ja ? A : Bp;
+    const long origin = ja ? (A_KC ? m0 * lda + kk : kk * lda + m0) : (B_KC ? n0 * ldb + kk : kk * ldb + n0);
+    const long lim = ja ? limA : limB;
+    const __amdgpu_buffer_rsrc_t rs = rsrc(base + origin, (lim - origin) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, ja ? voA[j & 3] : voB[j & 3], 0, 0, 0);
+  };
+  // K-contiguous fragment row r of an image (r = 16 * frag + (lane & 15)), logical chunk lane >> 4
+  const int rl = lane & 15, chunk = (lane >> 4) ^ ((rl >> 2) & 3);
+  const int offA = (wm * 128 + rl) * 64 + 16 * chunk, offB = (wn * 128 + rl) * 64 + 16 * chunk;
+  // K-strided fragment f (image columns 16 f ..): lane (g, q, p) reads k-rows ra = 8 g + q and ra + 4
+  // at chunk ch = (w << 4) | (f << 1) | (p >> 1) -- disjoint bits, so ch ^ sw(r) = c ^ (f << 1) with the
+  // per-lane c = ((w << 4) | (p >> 1)) ^ sw(r); the byte address is then row + 16 (c ^ (f << 1)).
+  const int kg = lane >> 4, kq = (lane & 15) >> 2, kp = lane & 3;
+  const int ra = 8 * kg + kq;
+  int ksA = (((wm << 4) | (kp >> 1)) ^ ksw(ra)) | ((((wm << 4) | (kp >> 1)) ^ ksw(ra + 4)) << 8);
+  int ksB = (((wn << 4) | (kp >> 1)) ^ ksw(ra)) | ((((wn << 4) | (kp >> 1)) ^ ksw(ra + 4)) << 8);
+  const int krow = ra * 512 + 8 * (kp & 1);
+  auto rd = [&](int st, int which, int f) -> bf16x8 {   // stage st (mod NS), which 0: A frag f, 1: B frag f
+    const char* img = smem + (st & (NS - 1)) * STAGE + which * IMG;
+    if ((which ? B_KC : A_KC)) return *reinterpret_cast<const bf16x8*>(img + (which ? offB : offA) + f * 1024);
+    const int cc = which ? ksB : ksA;
+    const int ca = (cc & 255) ^ (f << 1), cb = (cc >> 8) ^ (f << 1);
+    const s16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + krow + 16 * ca));
+    const s16x4_t y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + krow + 2048 + 16 * cb));
+    const bf16x4 xv = __builtin_bit_cast(bf16x4, x), yv = __builtin_bit_cast(bf16x4, y);
+    return __builtin_shufflevector(xv, yv, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  f32x4 acc[8][8];   // [n frag j][m frag i]: C^T tiles (rows n, cols m); defined by slice 0
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+  // prologue: slices 0..2 in flight, slice 0 retired, its fragments read. DMA and fragment reads
+  // run unconditionally past the last slice: a phantom slice's pieces land in a stage nobody reads
+  // again (zero-filled past the operand), so the loop carries no branches and vmcnt stays 8. An
+  // empty reduction (ktiles 0: an expert without tokens in dW) runs slice 0 on zero-filled images.
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(0, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(1, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(2, j);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) { fa0[f] = rd(0, 0, f); fb0[f] = rd(0, 1, f); }
+
+  // one slice: 64 MFMAs on (fa, fb) = slice t, fragments of slice t+1 into (na, nb), DMA of t+3
+  // (t is a multiple of 4 plus the compile-time U, so every LDS offset is an immediate)
+  auto slice = [&](int t, auto U, auto F0, bf16x8 (&fa)[8], bf16x8 (&fb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
+    constexpr int u = decltype(U)::value;
+    constexpr bool first = decltype(F0)::value;
+    if constexpr (!A_KC) asm volatile("" : "+v"(ksA));
+    if constexpr (!B_KC) asm volatile("" : "+v"(ksB));
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {            // 16 groups of 4 MFMAs: n frag j = g >> 1, m frags 4 (g & 1) ..
+      const int j = g >> 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 4 * (g & 1) + q;
+        if constexpr (first) G4_MFMA0(acc[j][i], fb[j], fa[i]);
+        else G4_MFMA(acc[j][i], fb[j], fa[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // one fragment read per group (A frags first)
+      if (g < 8) na[g] = rd(u + 1, 0, g);
+      else nb[g - 8] = rd(u + 1, 1, g - 8);
+      if (SCHED == 0 && (g & 1)) dma(t + 3, g >> 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (SCHED == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dma(t + 3, j);
+    }
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // retire slice t+2; younger: slice t+3
+    __builtin_amdgcn_s_barrier();
+  };
+  using U0 = std::integral_constant<int, 0>;
+  using U1 = std::integral_constant<int, 1>;
+  using U2 = std::integral_constant<int, 2>;
+  using U3 = std::integral_constant<int, 3>;
+  using T1 = std::true_type;
+  using T0 = std::false_type;
+  slice(0, U0{}, T1{}, fa0, fb0, fa1, fb1);
+  for (int t = 1; t < ktiles; t += 4) {
+    slice(t, U1{}, T0{}, fa1, fb1, fa0, fb0);
+    if (t + 1 >= ktiles) break;
+    slice(t + 1, U2{}, T0{}, fa0, fb0, fa1, fb1);
+    if (t + 2 >= ktiles) break;
+    slice(t + 2, U3{}, T0{}, fa1, fb1, fa0, fb0);
+    if (t + 3 >= ktiles) break;
+    slice(t + 3, U0{}, T0{}, fa0, fb0, fa1, fb1);
+  }
+  // drain the phantom DMA before the epilogue reuses the ring; an MFMA's result may not be read
+  // (v_accvgpr_read) within its 8-pass latency by compiler code
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  __syncthreads();
+  const long rowlim = MODE == 2 ? (long)M : mend;
+
+  if constexpr (PART) {
+    // fp32 partials straight from the fragments (16 B per lane along a C row)
+    float* Cf = reinterpret_cast<float*>(C) + (long)e * strideC;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const long gmr = m0 + wm * 128 + 16 * i + (lane & 15);
+        const long gn = n0 + wn * 128 + 16 * j + 4 * (lane >> 4);
+        if (gmr < M && gn < N && SPA_DBG_OK(gn + 3, ldc)) *reinterpret_cast<f32x4*>(Cf + gmr * ldc + gn) = acc[j][i];
+      }
+    return;
+  }
+  // ---- epilogue: C^T fragments -> padded bf16 row image [256][256] in LDS -> 16-B global stores
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 v = acc[j][i];
+      bf16x4 w4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+      const int r = wm * 128 + 16 * i + (lane & 15);
+      const int cn = wn * 128 + 16 * j + 4 * (lane >> 4);
+      *reinterpret_cast<bf16x4*>(smem + r * ERS + cn * 2) = w4;
+    }
+  __syncthreads();
+#pragma unroll 4
+  for (int c = 0; c < 32; ++c) {
+    const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
+    const long gmr = m0 + r;
+    const long gn = n0 + ch * 8;
+    if (gmr < rowlim && gn < N && SPA_DBG_OK(gmr, MODE == 2 ? M : a_rows) & SPA_DBG_OK(gn + 7, ldc)) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * ERS + ch * 16);
+      bf16* cp = Cp + gmr * ldc + gn;
+      if (accumulate) {
+        const bf16x8 o = *reinterpret_cast<const bf16x8*>(cp);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)o[q]);
+      }
+      *reinterpret_cast<bf16x8*>(cp) = v;
+    }
+  }
+}
+#undef G4_MFMA
+
+static int g4_group(int E) {
+  const char* e = getenv("SPA_G4_GM");
+  return E > 1 ? 1 : (e ? std::max(1, atoi(e)) : 4);
+}
+static int g4_sched() {
+  const char* e = getenv("SPA_G4_SCHED");
+  return e ? atoi(e) : 0;
+}
+
+// grouped_gemm8's contract (csrc/kernels/gemm8.hip): modes 0 / 1 need the reduction dim % 32 and
+// N % 8; mode 2 N, K % 8 (any token counts)
+at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t mode,
+                  const c10::optional<at::Tensor>& out_, bool accumulate) {
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "gemm4a: bf16");
+  TORCH_CHECK(a.is_contiguous() && w.is_contiguous() && offsets.scalar_type() == at::kInt && offsets.is_cuda());
+  const int E = offsets.numel() - 1;
+  TORCH_CHECK(E >= 1 && E <= 256, "gemm4a: 1..256 experts");
+  TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)w.data_ptr() % 16 == 0, "gemm4a: 16-B aligned");
+  DeviceGuard g(a.device());
+  auto st = stream();
+  const int sch = g4_sched();
+  if (mode == 0 || mode == 1) {
+    TORCH_CHECK(w.dim() == 3 && w.size(0) == E);
+    const int M = a.size(0), Nw = w.size(1), Kw = w.size(2);
+    const int N = mode == 0 ? Nw : Kw, K = mode == 0 ? Kw : Nw;
+    TORCH_CHECK(a.size(1) == K, "gemm4a: A/W shape mismatch");
+    TORCH_CHECK(K % 32 == 0 && N % 8 == 0, "gemm4a: reduction % 32, output cols % 8");
+    TORCH_CHECK((long)(M + 256) * K * 2 < (1L << 32) && (long)(Nw + 256) * Kw * 2 < (1L << 32),
+                "gemm4a: operands < 4 GiB");
+    auto out = out_ ? *out_ : at::empty({M, N}, a.options());
+    if (M == 0) return out;
+    TORCH_CHECK(out.is_contiguous() && out.size(0) == M && out.size(1) == N);
+    if (K == 0) {
+      if (!accumulate) out.zero_();
+      return out;
+    }
+    const int grid = (cdiv(M, 256) + E) * cdiv(N, 256);
+#define G4_L(MD, S)                                                                                                 \
+  gemm4a_kernel<MD, S><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),                  \
+                                             (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, Kw, N,   \
+                                             (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E))
+    if (mode == 0) { if (sch == 1) G4_L(0, 1); else G4_L(0, 0); }
+    else { if (sch == 1) G4_L(1, 1); else G4_L(1, 0); }
+#undef G4_L
+    SPA_LAUNCH_CHECK();
+    return out;
+  }
+  TORCH_CHECK(mode == 2, "gemm4a: mode 0/1/2");
+  const int N = a.size(1), K = w.size(1), T = a.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == T && N % 8 == 0 && K % 8 == 0);
+  TORCH_CHECK((long)(T + 64) * (N + 256) * 2 < (1L << 32) && (long)(T + 64) * (K + 256) * 2 < (1L << 32),
+              "gemm4a: operands < 4 GiB");
+  auto out = out_ ? *out_ : at::empty({E, N, K}, a.options());
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * N * K);
+  const int grid = E * cdiv(N, 256) * cdiv(K, 256);
+  if (sch == 1)
+    gemm4a_kernel<2, 1><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                              (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
+                                              (long)N * K, accumulate ? 1 : 0, T, T, 1);
+  else
+    gemm4a_kernel<2, 0><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                              (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
+                                              (long)N * K, accumulate ? 1 : 0, T, T, 1);
+  SPA_LAUNCH_CHECK();
+  return out;
+}
+
+}  // namespace spa
+
+TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("gemm4a(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate=False) -> Tensor");
+}
+TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("gemm4a", &spa::gemm4a);
+}
