@@ -32,6 +32,7 @@
 //     f(r) = ((r & 3) << 2) | ((r >> 2) & 3) -- read with ds_read_b64_tr_b16 (gemm8's recipe).
 #include "gemm_common.h"
 
+#include <string>
 #include <type_traits>
 
 SPA_DEBUG_TU("gemm4a.hip")
@@ -87,24 +88,27 @@ __device__ __forceinline__ bf16x8 rd_ks(const char* img, int col0, int lane) {
 // copied into AGPRs around every MFMA)
 #define G4_MFMA0(ACC, A, B) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(ACC) : "v"(A), "v"(B))
 
-template <int MODE, int SCHED = 0, bool PART = false>
-__global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                        bf16* __restrict__ C, const int* __restrict__ offsets, int E,
-                                                        int M, int N, int K, long lda, long ldb, long ldc,
-                                                        long strideB, long strideC, int accumulate, long a_rows,
-                                                        long b_rows, int gm) {
+// block -> output tile: (expert, row tile, column tile) and, in mode 2, the expert's token range.
+// Modes 0 / 1: inclusive scan of the experts' row-tile counts (one expert per thread). Mode 2: heavy
+// experts first, dealt to the XCDs in snake order (gemm8.hip mode 2); PART: plain order. Uses the
+// first E4 ints of smem (before the ring is filled) and scratch[0..15]; false: no tile for this block.
+struct G4Tile {
+  int e;
+  long m0, mend, n0, k0, kend;
+  const bf16* Bp;
+  bf16* Cp;
+};
+template <int MODE, bool PART>
+__device__ __forceinline__ bool g4_map(G4Tile& out, char* smem, int* scratch, const int* __restrict__ offsets, int E,
+                                       int M, int N, long strideB, long strideC, int gm, const bf16* B, bf16* C) {
   using namespace g4;
-  constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-  int* scratch = reinterpret_cast<int*>(smem + SMEM - 64);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
   const int nnt = (N + BN - 1) / BN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   int nt = lid % nnt;
   int mt = lid / nnt;
   int e = 0;
-  long m0 = 0, mend = M, k0 = 0, kend = K;
+  long m0 = 0, mend = M, k0 = 0, kend = 0;
   const bf16* Bp = B;
   bf16* Cp = C;
   if (MODE != 2) {
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
     }
     __syncthreads();
     e = __builtin_amdgcn_readfirstlane(scratch[0]);
-    if (e < 0) return;
+    if (e < 0) return false;
     mt = __builtin_amdgcn_readfirstlane(scratch[1]);
     m0 = __builtin_amdgcn_readfirstlane(scratch[2]) + (long)mt * BM;
     mend = __builtin_amdgcn_readfirstlane(scratch[3]);
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
         pos = blockIdx.x / per_e;
         r = blockIdx.x % per_e;
       }
-      if (pos >= E) return;
+      if (pos >= E) return false;
       nt = r % nnt;
       mt = r / nnt;
       if (tid < E) {
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
       __syncthreads();   // the count image lives in the ring the prologue DMA fills
     } else {
       e = blockIdx.x / per_e;
-      if (e >= E) return;
+      if (e >= E) return false;
       const int r = blockIdx.x % per_e;
       nt = r % nnt;
       mt = r / nnt;
@@ -202,10 +206,99 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
     kend = __builtin_amdgcn_readfirstlane(scratch[3]);
     Cp = C + e * strideC;
   }
+  out.e = e;
+  out.m0 = m0;
+  out.mend = mend;
+  out.n0 = (long)nt * BN;
+  out.k0 = k0;
+  out.kend = kend;
+  out.Bp = Bp;
+  out.Cp = Cp;
+  return true;
+}
+
+// epilogue of both kernels: PART -> fp32 partials straight from the fragments; else C^T fragments ->
+// padded bf16 row image [256][256] in LDS -> 16-B global stores (+ the old value when accumulate)
+template <int MODE, bool PART>
+__device__ __forceinline__ void g4_epilogue(f32x4 (&acc)[8][8], char* smem, bf16* C, bf16* Cp, int e, long m0,
+                                            long n0, long rowlim, int M, int N, long ldc, long strideC,
+                                            int accumulate, long a_rows) {
+  using namespace g4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  if constexpr (PART) {
+    // fp32 partials straight from the fragments (16 B per lane along a C row)
+    float* Cf = reinterpret_cast<float*>(C) + (long)e * strideC;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const long gmr = m0 + wm * 128 + 16 * i + (lane & 15);
+        const long gn = n0 + wn * 128 + 16 * j + 4 * (lane >> 4);
+        if (gmr < M && gn < N && SPA_DBG_OK(gn + 3, ldc)) *reinterpret_cast<f32x4*>(Cf + gmr * ldc + gn) = acc[j][i];
+      }
+    return;
+  }
+  // ---- epilogue: C^T fragments -> padded bf16 row image [256][256] in LDS -> 16-B global stores
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 v = acc[j][i];
+      bf16x4 w4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+      const int r = wm * 128 + 16 * i + (lane & 15);
+      const int cn = wn * 128 + 16 * j + 4 * (lane >> 4);
+      *reinterpret_cast<bf16x4*>(smem + r * ERS + cn * 2) = w4;
+    }
+  __syncthreads();
+#pragma unroll 4
+  for (int c = 0; c < 32; ++c) {
+    const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
+    const long gmr = m0 + r;
+    const long gn = n0 + ch * 8;
+    if (gmr < rowlim && gn < N && SPA_DBG_OK(gmr, MODE == 2 ? M : a_rows) & SPA_DBG_OK(gn + 7, ldc)) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * ERS + ch * 16);
+      bf16* cp = Cp + gmr * ldc + gn;
+      if (accumulate) {
+        const bf16x8 o = *reinterpret_cast<const bf16x8*>(cp);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)o[q]);
+      }
+      *reinterpret_cast<bf16x8*>(cp) = v;
+    }
+  }
+}
+
+template <int MODE, int SCHED = 0, bool PART = false>
+__global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                        bf16* __restrict__ C, const int* __restrict__ offsets, int E,
+                                                        int M, int N, int K, long lda, long ldb, long ldc,
+                                                        long strideB, long strideC, int accumulate, long a_rows,
+                                                        long b_rows, int gm) {
+  using namespace g4;
+  constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
+  // SCHED (profiling ablations, SPA_G4_SCHED; 2-5 compute wrong results by construction):
+  //   0 DMA spread over the MFMA stream, 1 DMA after it, 2 no DMA / vmcnt in the loop,
+  //   3 no fragment reads in the loop, 4 MFMAs only (no DMA, reads, barriers), 5 no DMA, no barrier
+  constexpr bool LOOP_DMA = SCHED <= 1 || SCHED == 3, LOOP_RD = SCHED != 3 && SCHED != 4;
+  constexpr bool LOOP_BAR = SCHED != 4 && SCHED != 5;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  int* scratch = reinterpret_cast<int*>(smem + SMEM - 64);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  G4Tile tl;
+  if (!g4_map<MODE, PART>(tl, smem, scratch, offsets, E, M, N, strideB, strideC, gm, B, C)) return;
+  const int e = tl.e;
+  const long m0 = tl.m0, mend = tl.mend, k0 = tl.k0, kend = MODE == 2 ? tl.kend : K;
+  const bf16* Bp = tl.Bp;
+  bf16* Cp = tl.Cp;
   SPA_DBG_CHECK(e, E);
   SPA_DBG_ASSERT(MODE == 2 ? kend <= a_rows && kend <= b_rows : mend <= a_rows && m0 < mend,
                  MODE == 2 ? kend : mend, a_rows);
-  const long n0 = (long)nt * BN;
+  const long n0 = tl.n0;
   const int ktiles = kend > k0 ? (int)((kend - k0 + BK - 1) / BK) : 0;
   unsigned voA[4], voB[4];
 #pragma unroll
@@ -268,6 +361,10 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int f = 0; f < 8; ++f) { fa0[f] = rd(0, 0, f); fb0[f] = rd(0, 1, f); }
+  if constexpr (!LOOP_RD) {
+#pragma unroll
+    for (int f = 0; f < 8; ++f) { fa1[f] = rd(1, 0, f); fb1[f] = rd(1, 1, f); }
+  }
 
   // one slice: 64 MFMAs on (fa, fb) = slice t, fragments of slice t+1 into (na, nb), DMA of t+3
   // (t is a multiple of 4 plus the compile-time U, so every LDS offset is an immediate)
@@ -287,17 +384,19 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
       }
       __builtin_amdgcn_sched_barrier(0);
       // one fragment read per group (A frags first)
-      if (g < 8) na[g] = rd(u + 1, 0, g);
-      else nb[g - 8] = rd(u + 1, 1, g - 8);
-      if (SCHED == 0 && (g & 1)) dma(t + 3, g >> 1);
+      if constexpr (LOOP_RD) {
+        if (g < 8) na[g] = rd(u + 1, 0, g);
+        else nb[g - 8] = rd(u + 1, 1, g - 8);
+      }
+      if ((SCHED == 0 || SCHED == 3) && (g & 1)) dma(t + 3, g >> 1);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (SCHED == 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) dma(t + 3, j);
     }
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // retire slice t+2; younger: slice t+3
-    __builtin_amdgcn_s_barrier();
+    if constexpr (LOOP_DMA) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // retire slice t+2; younger: slice t+3
+    if constexpr (LOOP_BAR) __builtin_amdgcn_s_barrier();
   };
   using U0 = std::integral_constant<int, 0>;
   using U1 = std::integral_constant<int, 1>;
@@ -319,53 +418,205 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
   // (v_accvgpr_read) within its 8-pass latency by compiler code
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   __syncthreads();
-  const long rowlim = MODE == 2 ? (long)M : mend;
-
-  if constexpr (PART) {
-    // fp32 partials straight from the fragments (16 B per lane along a C row)
-    float* Cf = reinterpret_cast<float*>(C) + (long)e * strideC;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const long gmr = m0 + wm * 128 + 16 * i + (lane & 15);
-        const long gn = n0 + wn * 128 + 16 * j + 4 * (lane >> 4);
-        if (gmr < M && gn < N && SPA_DBG_OK(gn + 3, ldc)) *reinterpret_cast<f32x4*>(Cf + gmr * ldc + gn) = acc[j][i];
-      }
-    return;
-  }
-  // ---- epilogue: C^T fragments -> padded bf16 row image [256][256] in LDS -> 16-B global stores
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const f32x4 v = acc[j][i];
-      bf16x4 w4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
-      const int r = wm * 128 + 16 * i + (lane & 15);
-      const int cn = wn * 128 + 16 * j + 4 * (lane >> 4);
-      *reinterpret_cast<bf16x4*>(smem + r * ERS + cn * 2) = w4;
-    }
-  __syncthreads();
-#pragma unroll 4
-  for (int c = 0; c < 32; ++c) {
-    const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
-    const long gmr = m0 + r;
-    const long gn = n0 + ch * 8;
-    if (gmr < rowlim && gn < N && SPA_DBG_OK(gmr, MODE == 2 ? M : a_rows) & SPA_DBG_OK(gn + 7, ldc)) {
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * ERS + ch * 16);
-      bf16* cp = Cp + gmr * ldc + gn;
-      if (accumulate) {
-        const bf16x8 o = *reinterpret_cast<const bf16x8*>(cp);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)o[q]);
-      }
-      *reinterpret_cast<bf16x8*>(cp) = v;
-    }
-  }
+  g4_epilogue<MODE, PART>(acc, smem, C, Cp, e, m0, n0, MODE == 2 ? (long)M : mend, M, N, ldc, strideC, accumulate,
+                          a_rows);
 }
+
+
+
+// ---------------------------------------------------------------------------------------------
+// gemm4r: the same 4-wave 256 x 256 tile, AGPR-pinned accumulators, with hipBLASLt's staging
+// (read from its gfx950 MT256x256x64 kernels: DTL off, one LDS buffer, prefetch 2): 64-deep K tiles
+// go HBM -> VGPRs (buffer_load_dwordx4, 16 per wave per tile = 64 staging VGPRs) -> LDS
+// (ds_write_b128), two barriers per tile. Why not LDS-DMA: each buffer_load ... lds issue holds the
+// issuing wave for ~60-185 cycles, and at one wave per SIMD that is MFMA time -- gemm4a with its
+// DMA removed runs 1,673 TF at 8192^3, with it 1,180 (profiles/r6_gemm4a_ablations.txt). A register
+// load issues in a few cycles; its ds_write (13) fits an MFMA gap.
+//   phase 1 (K half 0): 64 MFMAs on F0, the 16 K-half-1 fragments of this tile read into F1
+//   lgkmcnt(0) + barrier: every wave is done reading this tile
+//   phase 2 (K half 1): 64 MFMAs on F1; groups 0-7 write the staged next tile to LDS and reload the
+//     staging registers with the tile after it; lgkmcnt(0) + barrier after group 11; groups 12-15
+//     read the next tile's K-half-0 fragments into F0
+// LDS images as gemm8 (64-deep tiles): K-contiguous [256][64] (128-B rows, chunk c of row r at
+// r * 128 + 16 (c ^ ((r >> 1) & 7))), K-strided [64][256] (512-B rows, chunk c ^ f(r)).
+template <int MODE, bool PART = false>
+__global__ __launch_bounds__(256, 1) void gemm4r_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                        bf16* __restrict__ C, const int* __restrict__ offsets, int E,
+                                                        int M, int N, int K, long lda, long ldb, long ldc,
+                                                        long strideB, long strideC, int accumulate, long a_rows,
+                                                        long b_rows, int gm) {
+  using namespace g4;
+  constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
+  constexpr int TK = 64, TIMG = 256 * TK * 2;   // 64-deep tile, one operand image (32 KiB)
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  int* scratch = reinterpret_cast<int*>(smem + SMEM - 64);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  G4Tile tl;
+  if (!g4_map<MODE, PART>(tl, smem, scratch, offsets, E, M, N, strideB, strideC, gm, B, C)) return;
+  const int e = tl.e;
+  const long m0 = tl.m0, mend = tl.mend, n0 = tl.n0, k0 = tl.k0, kend = MODE == 2 ? tl.kend : K;
+  const bf16* Bp = tl.Bp;
+  bf16* Cp = tl.Cp;
+  SPA_DBG_CHECK(e, E);
+  SPA_DBG_ASSERT(MODE == 2 ? kend <= a_rows && kend <= b_rows : mend <= a_rows && m0 < mend,
+                 MODE == 2 ? kend : mend, a_rows);
+  const int ktiles = kend > k0 ? (int)((kend - k0 + TK - 1) / TK) : 0;
+  __syncthreads();   // g4_map's count image (mode 2) is overwritten by the first LDS writes
+
+  // ---- global -> VGPR staging: 8 loads per operand per wave, instruction q = 4 j + wave
+  //   K-contiguous: rows 8q .. 8q+7 (lane: row 8q + l/8, 16-B chunk l%8), soffset 8q*ld*2
+  //   K-strided:    k-rows 2q, 2q+1 (lane: k-row 2q + l/32, chunk l%32), soffset 2q*ld*2
+  // the tile advance moves the descriptor base; the range check zero-fills past the operand (modes
+  // 0/1: its last row; mode 2: the expert's last token)
+  auto lane_voff = [&](bool kc, long ld) -> unsigned {
+    return kc ? (unsigned)(((lane >> 3) * ld + 8 * (lane & 7)) * 2) : (unsigned)(((lane >> 5) * ld + 8 * (lane & 31)) * 2);
+  };
+  const unsigned voA = lane_voff(A_KC, lda), voB = lane_voff(B_KC, ldb);
+  const long limA = MODE == 2 ? kend * lda : a_rows * lda;
+  const long limB = MODE == 2 ? kend * ldb : b_rows * ldb;
+  // tile origins (elements) and per-tile advance
+  const long oA = A_KC ? m0 * lda + k0 : k0 * lda + m0, oB = B_KC ? n0 * ldb + k0 : k0 * ldb + n0;
+  const long stA = A_KC ? TK : TK * lda, stB = B_KC ? TK : TK * ldb;
+  auto load = [&](int t, int j) -> bf16x8 {   // slot j (0..7 A, 8..15 B) of tile t
+    const bool ja = j < 8;
+    const int q = 4 * (j & 7) + wave;
+    const bool kc = ja ? A_KC : B_KC;
+    const long ld = ja ? lda : ldb;
+    const long org = (ja ? oA : oB) + (long)t * (ja ? stA : stB);
+    const long lim = ja ? limA : limB;
+    const __amdgpu_buffer_rsrc_t rs = rsrc((ja ? A : Bp) + org, (lim - org) * 2);
+    const int soff = (int)((kc ? 8 * q : 2 * q) * ld * 2);
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ja ? voA : voB, soff, 0));
+  };
+  // LDS write address of slot j (see the image layouts above)
+  auto waddr = [&](int j) -> int {
+    const bool ja = j < 8;
+    const int q = 4 * (j & 7) + wave;
+    const int img = ja ? 0 : TIMG;
+    if (ja ? A_KC : B_KC) {
+      const int r = 8 * q + (lane >> 3), c = lane & 7;
+      return img + r * 128 + 16 * (c ^ ((r >> 1) & 7));
+    }
+    const int r = 2 * q + (lane >> 5), c = lane & 31;
+    return img + r * 512 + 16 * (c ^ ksw(r));
+  };
+  // fragment reads: K-contiguous operand frag f (rows 16 f + l%16 of the wave's 128), k-slice s
+  const int rl = lane & 15, g4l = lane >> 4, xs = (rl >> 1) & 7;
+  auto kc_addr = [&](int w, int s) -> int {   // + 2048 f
+    return (w * 128 + rl) * 128 + 16 * ((4 * s + g4l) ^ xs);
+  };
+  const int kcA0 = kc_addr(wm, 0), kcA1 = kc_addr(wm, 1), kcB0 = TIMG + kc_addr(wn, 0), kcB1 = TIMG + kc_addr(wn, 1);
+  // K-strided operand frag f (image columns w*128 + 16 f ..), k-slice s: lane (g, q, p) reads k-rows
+  // ra = 32 s + 8 g + q and ra + 4 at chunk ((w << 4) | (f << 1) | (p >> 1)) ^ f(r)
+  const int kq = rl >> 2, kp = lane & 3;
+  auto ks_c = [&](int w, int r) { return (((w << 4) | (kp >> 1)) ^ ksw(r)); };
+  int ksA[2], ksB[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int ra = 32 * s2 + 8 * g4l + kq;
+    ksA[s2] = ks_c(wm, ra) | (ks_c(wm, ra + 4) << 8);
+    ksB[s2] = ks_c(wn, ra) | (ks_c(wn, ra + 4) << 8);
+  }
+  const int krow = (8 * g4l + kq) * 512 + 8 * (kp & 1);
+  auto rd = [&](int which, int s, int f) -> bf16x8 {
+    const bool kc = which ? B_KC : A_KC;
+    if (kc) {
+      const int base = which ? (s ? kcB1 : kcB0) : (s ? kcA1 : kcA0);
+      return *reinterpret_cast<const bf16x8*>(smem + base + 2048 * f);
+    }
+    const char* img = smem + (which ? TIMG : 0) + 32 * 512 * s + krow;
+    const int cc = which ? ksB[s] : ksA[s];
+    const int ca = (cc & 255) ^ (f << 1), cb = (cc >> 8) ^ (f << 1);
+    const s16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + 16 * ca));
+    const s16x4_t y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + 2048 + 16 * cb));
+    return __builtin_shufflevector(__builtin_bit_cast(bf16x4, x), __builtin_bit_cast(bf16x4, y), 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto lds_bar = [&]() {   // this wave's LDS ops done, then the block barrier (no vmcnt: loads stay in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4 acc[8][8];   // [n frag j][m frag i]: C^T tiles; defined by the first tile's MFMAs
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8], stg[16];
+
+  // prologue: tile 0 -> LDS, tile 1 -> staging registers, tile 0's K-half-0 fragments
+#pragma unroll
+  for (int j = 0; j < 16; ++j) stg[j] = load(0, j);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    *reinterpret_cast<bf16x8*>(smem + waddr(j)) = stg[j];
+    stg[j] = load(1, j);
+  }
+  lds_bar();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) { fa0[f] = rd(0, 0, f); fb0[f] = rd(1, 0, f); }
+
+  auto tile = [&](int t, auto F0) {
+    constexpr bool first = decltype(F0)::value;
+    if constexpr (!A_KC) asm volatile("" : "+v"(ksA[0]), "+v"(ksA[1]));
+    if constexpr (!B_KC) asm volatile("" : "+v"(ksB[0]), "+v"(ksB[1]));
+    // ---- phase 1: K half 0 on (fa0, fb0); K half 1 fragments into (fa1, fb1)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int j = g >> 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 4 * (g & 1) + q;
+        if constexpr (first) G4_MFMA0(acc[j][i], fb0[j], fa0[i]);
+        else G4_MFMA(acc[j][i], fb0[j], fa0[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (g < 8) fa1[g] = rd(0, 1, g);
+      else fb1[g - 8] = rd(1, 1, g - 8);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_bar();
+    // ---- phase 2: K half 1 on (fa1, fb1); staged tile t+1 -> LDS, tile t+2 -> staging; then the
+    // next tile's K half 0 fragments
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int j = g >> 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 4 * (g & 1) + q;
+        G4_MFMA(acc[j][i], fb1[j], fa1[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (g < 8) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int sl = 2 * g + h;
+          *reinterpret_cast<bf16x8*>(smem + waddr(sl)) = stg[sl];
+          stg[sl] = load(t + 2, sl);
+        }
+      } else if (g == 11) {
+        lds_bar();
+      } else if (g > 11) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int f = 4 * (g - 12) + h;   // 0..15: A frags 0..7, then B frags
+          if (f < 8) fa0[f] = rd(0, 0, f);
+          else fb0[f - 8] = rd(1, 0, f - 8);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  tile(0, std::true_type{});
+  for (int t = 1; t < ktiles; ++t) tile(t, std::false_type{});
+  // the staging loads of the last tiles (phantom, never read) and the LDS reads drain before the
+  // epilogue reuses LDS; an MFMA's result may not be read within its 8-pass latency
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  __syncthreads();
+  g4_epilogue<MODE, PART>(acc, smem, C, Cp, e, m0, n0, MODE == 2 ? (long)M : mend, M, N, ldc, strideC, accumulate,
+                          a_rows);
+}
+
 #undef G4_MFMA
+#undef G4_MFMA0
 
 static int g4_group(int E) {
   const char* e = getenv("SPA_G4_GM");
@@ -374,6 +625,12 @@ static int g4_group(int E) {
 static int g4_sched() {
   const char* e = getenv("SPA_G4_SCHED");
   return e ? atoi(e) : 0;
+}
+// SPA_G4_IMPL=dma: the LDS-DMA pipeline (gemm4a_kernel, 32-deep slices); default: register staging
+// (gemm4r_kernel, 64-deep tiles; modes 0/1 need the reduction dim % 64)
+static bool g4_dma() {
+  const char* e = getenv("SPA_G4_IMPL");
+  return e && std::string(e) == "dma";
 }
 
 // grouped_gemm8's contract (csrc/kernels/gemm8.hip): modes 0 / 1 need the reduction dim % 32 and
@@ -404,11 +661,33 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
       return out;
     }
     const int grid = (cdiv(M, 256) + E) * cdiv(N, 256);
+    if (!g4_dma()) {
+      TORCH_CHECK(K % 64 == 0, "gemm4a (register-staged): reduction % 64");
+      if (mode == 0)
+        gemm4r_kernel<0><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                               (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, Kw, N,
+                                               (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E));
+      else
+        gemm4r_kernel<1><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                               (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, Kw, N,
+                                               (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E));
+      SPA_LAUNCH_CHECK();
+      return out;
+    }
 #define G4_L(MD, S)                                                                                                 \
   gemm4a_kernel<MD, S><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),                  \
                                              (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, Kw, N,   \
                                              (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E))
-    if (mode == 0) { if (sch == 1) G4_L(0, 1); else G4_L(0, 0); }
+    if (mode == 0) {
+      switch (sch) {
+        case 1: G4_L(0, 1); break;
+        case 2: G4_L(0, 2); break;
+        case 3: G4_L(0, 3); break;
+        case 4: G4_L(0, 4); break;
+        case 5: G4_L(0, 5); break;
+        default: G4_L(0, 0);
+      }
+    }
     else { if (sch == 1) G4_L(1, 1); else G4_L(1, 0); }
 #undef G4_L
     SPA_LAUNCH_CHECK();
@@ -422,7 +701,11 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
   auto out = out_ ? *out_ : at::empty({E, N, K}, a.options());
   TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * N * K);
   const int grid = E * cdiv(N, 256) * cdiv(K, 256);
-  if (sch == 1)
+  if (!g4_dma())
+    gemm4r_kernel<2><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                           (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
+                                           (long)N * K, accumulate ? 1 : 0, T, T, 1);
+  else if (sch == 1)
     gemm4a_kernel<2, 1><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
                                               (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
                                               (long)N * K, accumulate ? 1 : 0, T, T, 1);

@@ -52,20 +52,20 @@ T, E, k, D, F = 8192, 64, 6, 2048, 1408
 idx, _ = M.route(torch.randn(T, E, device=dev), k)
 plan = M.permute(idx, E)
 A = T * k
-x = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
+xg = torch.randn(A, D, device=dev, dtype=torch.bfloat16)
 W13 = torch.randn(E, 2 * F, D, device=dev, dtype=torch.bfloat16) * 0.02
 offs = plan.offsets.to(torch.int32)
 oc = offs.tolist()
-ref = torch.cat([x[oc[e]:oc[e + 1]].float() @ W13[e].float().t() for e in range(E)])
-cases.append(("grouped fwd dsv3_style", x, W13, offs, ref, 2.0 * A * 2 * F * D, None))
+ref = torch.cat([xg[oc[e]:oc[e + 1]].float() @ W13[e].float().t() for e in range(E)])
+cases.append(("grouped fwd dsv3_style", xg, W13, offs, ref, 2.0 * A * 2 * F * D, None))
 # ragged: experts with 0, 1, 255, 257 rows
 cnt = torch.tensor([0, 1, 255, 257, 0, 513, 3, 64], dtype=torch.int32)
 offr = torch.cat([torch.zeros(1, dtype=torch.int32), cnt.cumsum(0).to(torch.int32)]).to(dev)
 xr = torch.randn(int(cnt.sum()), 256, device=dev, dtype=torch.bfloat16)
-wr = torch.randn(8, 136, 256, device=dev, dtype=torch.bfloat16)
+wr = torch.randn(8, 192, 256, device=dev, dtype=torch.bfloat16)
 o = offr.tolist()
 refr = torch.cat([xr[o[e]:o[e + 1]].float() @ wr[e].float().t() for e in range(8)])
-cases.append(("ragged E8 N136 K256", xr, wr, offr, refr, 1.0, None))
+cases.append(("ragged E8 N192 K256", xr, wr, offr, refr, 1.0, None))
 
 for name, x, w, off, ref, fl, blas in cases:
     y4 = ops.gemm4a(x, w, off, 0, None)
@@ -74,6 +74,28 @@ for name, x, w, off, ref, fl, blas in cases:
     print(f"{name}: gemm4a rel {rel(y4, ref):.2e}  gemm8 rel {rel(y8, ref):.2e}  gemm4a==gemm8 {torch.equal(y4, y8)}",
           flush=True)
     assert rel(y4, ref) < 1e-2, name
+
+# modes 1 (dX = dY W_e) and 2 (dW_e = dY_e^T X_e), dsv3_style widths and ragged experts, + accumulate
+dy13 = torch.randn(A, 2 * F, device=dev, dtype=torch.bfloat16)
+mcases = [("grouped dX dsv3_style", dy13, W13, offs, oc, 2.0 * A * 2 * F * D),
+          ("ragged dX", torch.randn(xr.shape[0], 192, device=dev, dtype=torch.bfloat16), wr, offr, o, 1.0)]
+for name, dy, w, off, oo, fl in mcases:
+    y4 = ops.gemm4a(dy, w, off, 1, None)
+    y8 = ops.grouped_gemm8(dy, w, off, 1, None, False)
+    ref = torch.cat([dy[oo[e]:oo[e + 1]].float() @ w[e].float() for e in range(len(oo) - 1)])
+    print(f"{name}: gemm4a rel {rel(y4, ref):.2e}  gemm8 rel {rel(y8, ref):.2e}", flush=True)
+    assert rel(y4, ref) < 1e-2, name
+wcases = [("grouped dW dsv3_style", dy13, xg, offs, oc, 2.0 * A * 2 * F * D),
+          ("ragged dW", torch.randn(xr.shape[0], 192, device=dev, dtype=torch.bfloat16), xr, offr, o, 1.0)]
+for name, dy, xx, off, oo, fl in wcases:
+    y4 = ops.gemm4a(dy, xx, off, 2, None)
+    ref = torch.stack([dy[oo[e]:oo[e + 1]].float().t() @ xx[oo[e]:oo[e + 1]].float() for e in range(len(oo) - 1)])
+    acc0 = torch.randn_like(y4)
+    y4a = ops.gemm4a(dy, xx, off, 2, acc0.clone(), True)
+    print(f"{name}: gemm4a rel {rel(y4, ref):.2e}  accumulate rel {rel(y4a, ref + acc0.float()):.2e}", flush=True)
+    assert rel(y4, ref) < 1e-2 and rel(y4a, ref + acc0.float()) < 1e-2, name
+timed_mw = [("grouped dX dsv3_style", lambda: ops.gemm4a(dy13, W13, offs, 1, None), lambda: ops.grouped_gemm8(dy13, W13, offs, 1, None, False), 2.0 * A * 2 * F * D),
+            ("grouped dW dsv3_style", lambda: ops.gemm4a(dy13, xg, offs, 2, None), lambda: ops.grouped_gemm8(dy13, xg, offs, 2, None, False), 2.0 * A * 2 * F * D)]
 
 arms = [("gemm4a", None)]
 if a.env:
@@ -93,3 +115,6 @@ for r in range(a.rounds):
             res.append(("hipBLASLt", tm(blas)))
         print(f"round {r} {name}: " + "  ".join(f"{lab} {ms:.3f} ms {fl / ms / 1e9:.0f} TF" for lab, ms in res),
               flush=True)
+    for name, f4, f8, fl in timed_mw:
+        t4, t8 = tm(f4), tm(f8)
+        print(f"round {r} {name}: gemm4a {t4:.3f} ms {fl / t4 / 1e9:.0f} TF  gemm8 {t8:.3f} ms {fl / t8 / 1e9:.0f} TF", flush=True)
