@@ -112,13 +112,11 @@ __device__ __forceinline__ bool g4_map(G4Tile& out, char* smem, int* scratch, co
   const bf16* Bp = B;
   bf16* Cp = C;
   if (MODE != 2) {
-    if (gm > 1) {   // groups of gm row tiles x all column tiles (L2 reuse of B panels), dense only
-      const int mtiles = gridDim.x / nnt, g = lid / (gm * nnt), r = lid % (gm * nnt);
-      const int gs = min(gm, mtiles - g * gm);
-      mt = g * gm + r % gs;
-      nt = r / gs;
-    }
-    // tile -> (expert, row tile): inclusive scan of the experts' tile counts (one per thread)
+    // tile -> (expert, row tile): inclusive scan of the experts' row-tile counts (one per thread).
+    // The grid is sized for the worst case (every expert ragged); the REAL tiles R = rows x nnt take
+    // the lowest block ids and the XCD remap runs over R, so no real tile waits behind an empty
+    // block for a second dispatch round (the remap over the whole grid had scattered the empty
+    // blocks: at 4096^3 16 real tiles landed past the 256 CUs and the kernel ran two rounds)
     int* wsum = scratch + 8;
     const int o0 = tid < E ? offsets[tid] : 0, o1 = tid < E ? offsets[tid + 1] : 0;
     const int tiles = (o1 - o0 + BM - 1) / BM;
@@ -131,8 +129,24 @@ __device__ __forceinline__ bool g4_map(G4Tile& out, char* smem, int* scratch, co
     if (lane == 63) wsum[wave] = inc;
     if (tid == 0) scratch[0] = -1;
     __syncthreads();
-    int pre = inc - tiles;
-    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    int pre = inc - tiles, rows = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+      const int v = wsum[w];
+      pre += w < wave ? v : 0;
+      rows += v;
+    }
+    const int R = rows * nnt;
+    if ((int)blockIdx.x >= R) return false;                  // uniform: empty blocks exit together
+    const int lid = xcd_remap(blockIdx.x, R);
+    nt = lid % nnt;
+    mt = lid / nnt;
+    if (gm > 1) {   // groups of gm row tiles x all column tiles (L2 reuse of B panels), dense only
+      const int g = lid / (gm * nnt), r = lid % (gm * nnt);
+      const int gs = min(gm, rows - g * gm);
+      mt = g * gm + r % gs;
+      nt = r / gs;
+    }
     if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) {
       scratch[0] = tid; scratch[1] = mt - pre; scratch[2] = o0; scratch[3] = o1;
     }
@@ -439,7 +453,7 @@ __global__ __launch_bounds__(256, 1) void gemm4a_kernel(const bf16* __restrict__
 //     read the next tile's K-half-0 fragments into F0
 // LDS images as gemm8 (64-deep tiles): K-contiguous [256][64] (128-B rows, chunk c of row r at
 // r * 128 + 16 (c ^ ((r >> 1) & 7))), K-strided [64][256] (512-B rows, chunk c ^ f(r)).
-template <int MODE, bool PART = false>
+template <int MODE, bool PART = false, int POL = 0>
 __global__ __launch_bounds__(256, 1) void gemm4r_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                         bf16* __restrict__ C, const int* __restrict__ offsets, int E,
                                                         int M, int N, int K, long lda, long ldb, long ldc,
@@ -488,7 +502,10 @@ __global__ __launch_bounds__(256, 1) void gemm4r_kernel(const bf16* __restrict__
     const long lim = ja ? limA : limB;
     const __amdgpu_buffer_rsrc_t rs = rsrc((ja ? A : Bp) + org, (lim - org) * 2);
     const int soff = (int)((kc ? 8 * q : 2 * q) * ld * 2);
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ja ? voA : voB, soff, 0));
+    // cache policy (POL, profiling: 1 = A sc0 sc1 / B sc1 as hipBLASLt's NTA3/NTB2 kernels, 2 = swapped)
+    constexpr int PA = POL == 1 ? 17 : POL == 2 ? 16 : 0, PB = POL == 1 ? 16 : POL == 2 ? 17 : 0;
+    if (ja) return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voA, soff, PA));
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voB, soff, PB));
   };
   // LDS write address of slot j (see the image layouts above)
   auto waddr = [&](int j) -> int {
@@ -554,53 +571,45 @@ __global__ __launch_bounds__(256, 1) void gemm4r_kernel(const bf16* __restrict__
 #pragma unroll
   for (int f = 0; f < 8; ++f) { fa0[f] = rd(0, 0, f); fb0[f] = rd(1, 0, f); }
 
+  // one memory instruction per MFMA gap (hipBLASLt's placement: an MFMA of 16x16x32 holds the wave's
+  // vector issue for 8 of its 16 cycles, so one read / write / load beside it is nearly free, a burst
+  // of them is not). MFMA m of a phase: n frag j = m / 8, m frag i = m % 8.
   auto tile = [&](int t, auto F0) {
     constexpr bool first = decltype(F0)::value;
     if constexpr (!A_KC) asm volatile("" : "+v"(ksA[0]), "+v"(ksA[1]));
     if constexpr (!B_KC) asm volatile("" : "+v"(ksB[0]), "+v"(ksB[1]));
-    // ---- phase 1: K half 0 on (fa0, fb0); K half 1 fragments into (fa1, fb1)
+    // ---- phase 1: K half 0 on (fa0, fb0); the 16 K-half-1 fragments into (fa1, fb1), one per MFMA
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int j = g >> 1;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 4 * (g & 1) + q;
-        if constexpr (first) G4_MFMA0(acc[j][i], fb0[j], fa0[i]);
-        else G4_MFMA(acc[j][i], fb0[j], fa0[i]);
+    for (int m = 0; m < 64; ++m) {
+      const int j = m >> 3, i = m & 7;
+      if constexpr (first) G4_MFMA0(acc[j][i], fb0[j], fa0[i]);
+      else G4_MFMA(acc[j][i], fb0[j], fa0[i]);
+      if (m < 16) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (m < 8) fa1[m] = rd(0, 1, m);
+        else fb1[m - 8] = rd(1, 1, m - 8);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      if (g < 8) fa1[g] = rd(0, 1, g);
-      else fb1[g - 8] = rd(1, 1, g - 8);
-      __builtin_amdgcn_sched_barrier(0);
     }
     lds_bar();
-    // ---- phase 2: K half 1 on (fa1, fb1); staged tile t+1 -> LDS, tile t+2 -> staging; then the
-    // next tile's K half 0 fragments
+    // ---- phase 2: K half 1 on (fa1, fb1); staged tile t+1 -> LDS (slot s at MFMA 3 s), tile t+2 ->
+    // staging (at 3 s + 1); barrier after MFMA 47; the next tile's K half 0 fragments at 48..63 in
+    // the order its first MFMAs consume them (fb0[0], fa0[0..7], fb0[1..7])
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int j = g >> 1;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 4 * (g & 1) + q;
-        G4_MFMA(acc[j][i], fb1[j], fa1[i]);
-      }
+    for (int m = 0; m < 64; ++m) {
+      const int j = m >> 3, i = m & 7;
+      G4_MFMA(acc[j][i], fb1[j], fa1[i]);
       __builtin_amdgcn_sched_barrier(0);
-      if (g < 8) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int sl = 2 * g + h;
-          *reinterpret_cast<bf16x8*>(smem + waddr(sl)) = stg[sl];
-          stg[sl] = load(t + 2, sl);
-        }
-      } else if (g == 11) {
-        lds_bar();
-      } else if (g > 11) {
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const int f = 4 * (g - 12) + h;   // 0..15: A frags 0..7, then B frags
-          if (f < 8) fa0[f] = rd(0, 0, f);
-          else fb0[f - 8] = rd(1, 0, f - 8);
-        }
+      if (m < 48) {
+        const int sl = m / 3;
+        if (m % 3 == 0) *reinterpret_cast<bf16x8*>(smem + waddr(sl)) = stg[sl];
+        else if (m % 3 == 1) stg[sl] = load(t + 2, sl);
+        else if (m == 47) lds_bar();
+      } else {
+        const int r = m - 48;
+        if (r == 0) fb0[0] = rd(1, 0, 0);
+        else if (r <= 8) fa0[r - 1] = rd(0, 0, r - 1);
+        else fb0[r - 8] = rd(1, 0, r - 8);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -609,6 +618,184 @@ __global__ __launch_bounds__(256, 1) void gemm4r_kernel(const bf16* __restrict__
   for (int t = 1; t < ktiles; ++t) tile(t, std::false_type{});
   // the staging loads of the last tiles (phantom, never read) and the LDS reads drain before the
   // epilogue reuses LDS; an MFMA's result may not be read within its 8-pass latency
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  __syncthreads();
+  g4_epilogue<MODE, PART>(acc, smem, C, Cp, e, m0, n0, MODE == 2 ? (long)M : mend, M, N, ldc, strideC, accumulate,
+                          a_rows);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// gemm4d: the structure of hipBLASLt's fastest gfx950 bf16 kernel for this tile (its hand-written
+// "Custom_..._MT256x256x64_MI16x16x1" assembly, read from the shipped code object): LDS-DMA into TWO
+// 64-deep tile buffers, two tiles ahead, one DMA piece per ~3 MFMAs of the first K half, three
+// barriers per tile. The DMA pieces of a tile share one descriptor per operand (advanced once per
+// tile), one lane offset VGPR and per-piece scalar offsets, so a piece issues with nothing to wait
+// for -- gemm4a's DMA recomputed a descriptor per piece, and its 32-deep 4-stage ring waited on
+// vmcnt twice as often.
+//   tile t (buffer b = t & 1), MFMAs 0..63 on F0 (K half 0), 64..127 on F1 (K half 1):
+//     m 0..15   read F1 (tile t, buffer b)
+//     m 16      lgkmcnt(0) + barrier: every wave is done reading buffer b
+//     m 18..63  DMA tile t+2 into buffer b (16 pieces, one per 3 MFMAs)
+//     m 96      vmcnt(16) (tile t+1 landed; tile t+2's pieces stay in flight) + barrier
+//     m 97..112 read F0 (tile t+1, buffer b^1)
+template <int MODE, bool PART = false>
+__global__ __launch_bounds__(256, 1) void gemm4d_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                        bf16* __restrict__ C, const int* __restrict__ offsets, int E,
+                                                        int M, int N, int K, long lda, long ldb, long ldc,
+                                                        long strideB, long strideC, int accumulate, long a_rows,
+                                                        long b_rows, int gm) {
+  using namespace g4;
+  constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
+  constexpr int TK = 64, TIMG = 256 * TK * 2, TBUF = 2 * TIMG;   // one operand image 32 KiB, a buffer 64 KiB
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  int* scratch = reinterpret_cast<int*>(smem + SMEM - 64);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  G4Tile tl;
+  if (!g4_map<MODE, PART>(tl, smem, scratch, offsets, E, M, N, strideB, strideC, gm, B, C)) return;
+  const int e = tl.e;
+  const long m0 = tl.m0, mend = tl.mend, n0 = tl.n0, k0 = tl.k0, kend = MODE == 2 ? tl.kend : K;
+  const bf16* Bp = tl.Bp;
+  bf16* Cp = tl.Cp;
+  SPA_DBG_CHECK(e, E);
+  SPA_DBG_ASSERT(MODE == 2 ? kend <= a_rows && kend <= b_rows : mend <= a_rows && m0 < mend,
+                 MODE == 2 ? kend : mend, a_rows);
+  const int ktiles = kend > k0 ? (int)((kend - k0 + TK - 1) / TK) : 0;
+  __syncthreads();   // g4_map's count image (mode 2) lives where the first DMA lands
+
+  // ---- DMA geometry. Piece j (0..7) of an operand for this wave is wave-instruction q = 4 j + wave
+  // of the block: K-contiguous rows 8q .. 8q+7 / K-strided k-rows 2q, 2q+1 -> LDS bytes q*1024 of
+  // the image (lane l at + 16 l). Source: lane offset (one VGPR; two for K-strided: the swizzle of
+  // k-row 8j + 2w + l/32 depends on j's parity) + a per-piece scalar offset.
+  auto lane_src = [&](bool kc, long ld, int par) -> unsigned {
+    if (kc) {
+      const int u = lane >> 3, r = 8 * wave + u;          // rows of q = wave (j = 0); swizzle depends on q & 1 only
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      return (unsigned)((u * ld + 8 * c) * 2);
+    }
+    const int h = lane >> 5, r = 8 * par + 2 * wave + h;  // k-row of piece j with j & 1 = par (j = par)
+    const int c = (lane & 31) ^ ksw(r);
+    return (unsigned)((h * ld + 8 * c) * 2);
+  };
+  const unsigned vA0 = lane_src(A_KC, lda, 0), vA1 = lane_src(A_KC, lda, 1);
+  const unsigned vB0 = lane_src(B_KC, ldb, 0), vB1 = lane_src(B_KC, ldb, 1);
+  const long limA = MODE == 2 ? kend * lda : a_rows * lda;
+  const long limB = MODE == 2 ? kend * ldb : b_rows * ldb;
+  const long oA = A_KC ? m0 * lda + k0 : k0 * lda + m0, oB = B_KC ? n0 * ldb + k0 : k0 * ldb + n0;
+  const long stA = A_KC ? TK : TK * lda, stB = B_KC ? TK : TK * ldb;
+  // per-piece scalar offsets (bytes): K-contiguous q*8 rows, K-strided q*2 k-rows (q = 4 j + wave)
+  auto soff = [&](bool kc, long ld, int j) -> int { return (int)((kc ? 8 : 2) * (4 * j + wave) * ld * 2); };
+  __amdgpu_buffer_rsrc_t rsA, rsB;
+  auto set_rsrc = [&](int t) {   // descriptors of tile t (once per tile per operand)
+    const long a0 = oA + (long)t * stA, b0 = oB + (long)t * stB;
+    rsA = rsrc(A + a0, (limA - a0) * 2);
+    rsB = rsrc(Bp + b0, (limB - b0) * 2);
+  };
+  auto piece = [&](int buf, int j) {   // piece j (0..7 A, 8..15 B) of the tile whose descriptors are set
+    const bool ja = j < 8;
+    const int jj = j & 7;
+    char* dst = smem + buf * TBUF + (ja ? 0 : TIMG) + (4 * jj + wave) * 1024;
+    const bool kc = ja ? A_KC : B_KC;
+    const unsigned vo = ja ? ((jj & 1) && !kc ? vA1 : vA0) : ((jj & 1) && !kc ? vB1 : vB0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ja ? rsA : rsB, (lds_void*)dst, 16, vo, soff(kc, ja ? lda : ldb, jj), 0, 0);
+  };
+
+  // ---- fragment reads (gemm4r's image layouts at a buffer offset)
+  const int rl = lane & 15, g4l = lane >> 4, xs = (rl >> 1) & 7;
+  auto kc_addr = [&](int w, int s) -> int { return (w * 128 + rl) * 128 + 16 * ((4 * s + g4l) ^ xs); };
+  const int kcA0 = kc_addr(wm, 0), kcA1 = kc_addr(wm, 1), kcB0 = TIMG + kc_addr(wn, 0), kcB1 = TIMG + kc_addr(wn, 1);
+  const int kq = rl >> 2, kp = lane & 3;
+  auto ks_c = [&](int w, int r) { return (((w << 4) | (kp >> 1)) ^ ksw(r)); };
+  int ksA[2], ksB[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int ra = 32 * s2 + 8 * g4l + kq;
+    ksA[s2] = ks_c(wm, ra) | (ks_c(wm, ra + 4) << 8);
+    ksB[s2] = ks_c(wn, ra) | (ks_c(wn, ra + 4) << 8);
+  }
+  const int krow = (8 * g4l + kq) * 512 + 8 * (kp & 1);
+  auto rd = [&](int buf, int which, int s, int f) -> bf16x8 {
+    const bool kc = which ? B_KC : A_KC;
+    if (kc) {
+      const int base = which ? (s ? kcB1 : kcB0) : (s ? kcA1 : kcA0);
+      return *reinterpret_cast<const bf16x8*>(smem + buf * TBUF + base + 2048 * f);
+    }
+    const char* img = smem + buf * TBUF + (which ? TIMG : 0) + 32 * 512 * s + krow;
+    const int cc = which ? ksB[s] : ksA[s];
+    const int ca = (cc & 255) ^ (f << 1), cb = (cc >> 8) ^ (f << 1);
+    const s16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + 16 * ca));
+    const s16x4_t y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + 2048 + 16 * cb));
+    return __builtin_shufflevector(__builtin_bit_cast(bf16x4, x), __builtin_bit_cast(bf16x4, y), 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4 acc[8][8];
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+  // prologue: tiles 0 and 1 in flight, tile 0 retired, its K-half-0 fragments
+  set_rsrc(0);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) piece(0, j);
+  set_rsrc(1);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) piece(1, j);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  bar();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) { fb0[f] = rd(0, 1, 0, f); fa0[f] = rd(0, 0, 0, f); }
+
+  auto tile = [&](int t, auto BUF, auto F0) {
+    constexpr int b = decltype(BUF)::value;
+    constexpr bool first = decltype(F0)::value;
+    if constexpr (!A_KC) asm volatile("" : "+v"(ksA[0]), "+v"(ksA[1]));
+    if constexpr (!B_KC) asm volatile("" : "+v"(ksB[0]), "+v"(ksB[1]));
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      const int j = m >> 3, i = m & 7;
+      if constexpr (first) G4_MFMA0(acc[j][i], fb0[j], fa0[i]);
+      else G4_MFMA(acc[j][i], fb0[j], fa0[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (m < 16) {
+        if (m < 8) fb1[m] = rd(b, 1, 1, m);
+        else fa1[m - 8] = rd(b, 0, 1, m - 8);
+      } else if (m == 16) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of buffer b done
+        bar();
+        set_rsrc(t + 2);
+      } else if (m >= 18 && (m - 18) % 3 == 0) {
+        piece(b, (m - 18) / 3);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      const int j = m >> 3, i = m & 7;
+      G4_MFMA(acc[j][i], fb1[j], fa1[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (m == 32) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");    // tile t+1 landed (this wave's pieces)
+        bar();                                               // ... and every wave's
+      } else if (m > 32 && m <= 48) {
+        const int r = m - 33;                                // next tile's K half 0, in consumption order
+        if (r < 8) fb0[r] = rd(b ^ 1, 1, 0, r);
+        else fa0[r - 8] = rd(b ^ 1, 0, 0, r - 8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  tile(0, B0{}, std::true_type{});
+  for (int t = 1; t < ktiles; t += 2) {
+    tile(t, B1{}, std::false_type{});
+    if (t + 1 >= ktiles) break;
+    tile(t + 1, B0{}, std::false_type{});
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   __syncthreads();
   g4_epilogue<MODE, PART>(acc, smem, C, Cp, e, m0, n0, MODE == 2 ? (long)M : mend, M, N, ldc, strideC, accumulate,
@@ -626,12 +813,20 @@ static int g4_sched() {
   const char* e = getenv("SPA_G4_SCHED");
   return e ? atoi(e) : 0;
 }
-// SPA_G4_IMPL=dma: the LDS-DMA pipeline (gemm4a_kernel, 32-deep slices); default: register staging
-// (gemm4r_kernel, 64-deep tiles; modes 0/1 need the reduction dim % 64)
-static bool g4_dma() {
-  const char* e = getenv("SPA_G4_IMPL");
-  return e && std::string(e) == "dma";
+static int g4_pol() {
+  const char* e = getenv("SPA_G4_POL");
+  return e ? atoi(e) : 0;
 }
+// SPA_G4_IMPL: "ring" = the 32-deep 4-stage LDS-DMA ring (gemm4a_kernel), "reg" = register staging
+// (gemm4r_kernel); default: two 64-deep LDS-DMA buffers (gemm4d_kernel). The 64-deep kernels need the
+// reduction dim % 64 in modes 0 / 1.
+static int g4_impl() {
+  const char* e = getenv("SPA_G4_IMPL");
+  if (!e) return 2;
+  const std::string v(e);
+  return v == "ring" ? 0 : v == "reg" ? 1 : 2;
+}
+static bool g4_dma() { return g4_impl() == 0; }
 
 // grouped_gemm8's contract (csrc/kernels/gemm8.hip): modes 0 / 1 need the reduction dim % 32 and
 // N % 8; mode 2 N, K % 8 (any token counts)
@@ -661,9 +856,28 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
       return out;
     }
     const int grid = (cdiv(M, 256) + E) * cdiv(N, 256);
+    if (g4_impl() == 2) {
+      TORCH_CHECK(K % 64 == 0, "gemm4a: reduction % 64");
+#define G4D(MD) gemm4d_kernel<MD><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),         \
+                                                       (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
+                                                       Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E))
+      if (mode == 0) G4D(0); else G4D(1);
+#undef G4D
+      SPA_LAUNCH_CHECK();
+      return out;
+    }
     if (!g4_dma()) {
       TORCH_CHECK(K % 64 == 0, "gemm4a (register-staged): reduction % 64");
-      if (mode == 0)
+      const int pol = g4_pol();
+      if (mode == 0 && pol == 1)
+        gemm4r_kernel<0, false, 1><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                               (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, Kw, N,
+                                               (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E));
+      else if (mode == 0 && pol == 2)
+        gemm4r_kernel<0, false, 2><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                               (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, Kw, N,
+                                               (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E));
+      else if (mode == 0)
         gemm4r_kernel<0><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
                                                (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, Kw, N,
                                                (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g4_group(E));
@@ -701,7 +915,11 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
   auto out = out_ ? *out_ : at::empty({E, N, K}, a.options());
   TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * N * K);
   const int grid = E * cdiv(N, 256) * cdiv(K, 256);
-  if (!g4_dma())
+  if (g4_impl() == 2)
+    gemm4d_kernel<2><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
+                                           (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
+                                           (long)N * K, accumulate ? 1 : 0, T, T, 1);
+  else if (!g4_dma())
     gemm4r_kernel<2><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
                                            (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
                                            (long)N * K, accumulate ? 1 : 0, T, T, 1);

@@ -159,14 +159,11 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int nnt = (N + BN - 1) / BN;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  int nt = lid % nnt;
-  int mt = lid / nnt;
-  if (MODE != 2 && gm > 1) {   // groups of gm row tiles x all column tiles (L2 / MALL reuse of B panels)
-    const int mtiles = gridDim.x / nnt, g = lid / (gm * nnt), r = lid % (gm * nnt);
-    const int gs = min(gm, mtiles - g * gm);
-    mt = g * gm + r % gs;
-    nt = r / gs;
+  int nt = 0, mt = 0;
+  if (MODE == 2) {
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    nt = lid % nnt;
+    mt = lid / nnt;
   }
   int e = 0;
   long m0 = 0, mend = M, k0 = 0, kend = K;
@@ -174,7 +171,10 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   bf16* Cp = C;
   if (MODE != 2) {
     int* wsum = scratch + 8;
-    // the expert's row range travels through LDS with its id (no second global round trip)
+    // the expert's row range travels through LDS with its id (no second global round trip). The
+    // grid is sized for the worst case (every expert ragged): the REAL tiles R = rows x nnt take the
+    // lowest block ids and the XCD remap runs over R (a remap over the whole grid scattered the
+    // empty blocks, and real tiles landed behind them in an extra dispatch round)
     const int o0 = tid < E ? offsets[tid] : 0, o1 = tid < E ? offsets[tid + 1] : 0;
     const int cnt = o1 - o0;
     const int tiles = (cnt + BM - 1) / BM;
@@ -187,8 +187,24 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     if (lane == 63) wsum[wave] = inc;
     if (tid == 0) scratch[0] = -1;
     __syncthreads();
-    int pre = inc - tiles;
-    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    int pre = inc - tiles, rows = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+      const int v = wsum[w];
+      pre += w < wave ? v : 0;
+      rows += v;
+    }
+    const int R = rows * nnt;
+    if ((int)blockIdx.x >= R) return;
+    const int lid = xcd_remap(blockIdx.x, R);
+    nt = lid % nnt;
+    mt = lid / nnt;
+    if (gm > 1) {   // groups of gm row tiles x all column tiles (L2 / MALL reuse of B panels)
+      const int g = lid / (gm * nnt), r = lid % (gm * nnt);
+      const int gs = min(gm, rows - g * gm);
+      mt = g * gm + r % gs;
+      nt = r / gs;
+    }
     if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) {
       scratch[0] = tid; scratch[1] = mt - pre; scratch[2] = o0; scratch[3] = o1;
     }

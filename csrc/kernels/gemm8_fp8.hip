@@ -93,8 +93,8 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int nnt = (N + BN - 1) / BN;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = lid % nnt;
+  int lid = xcd_remap(blockIdx.x, gridDim.x);
+  int nt = lid % nnt;
   int mt = lid / nnt;
   int e = 0;
   long m0 = 0, mend = M, k0 = 0, kend = K;
@@ -111,8 +111,20 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
     if (lane == 63) wsum[wave] = inc;
     if (tid == 0) scratch[0] = -1;
     __syncthreads();
-    int pre = inc - tiles;
-    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    int pre = inc - tiles, rows = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const int v = wsum[w];
+      pre += w < wave ? v : 0;
+      rows += v;
+    }
+    // real tiles on the lowest block ids, XCD remap over them only (gemm8.hip: the empty blocks of
+    // the worst-case grid must not push real tiles into another dispatch round)
+    const int R = rows * nnt;
+    if ((int)blockIdx.x >= R) return;
+    lid = xcd_remap(blockIdx.x, R);
+    nt = lid % nnt;
+    mt = lid / nnt;
     if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) { scratch[0] = tid; scratch[1] = mt - pre; }
     __syncthreads();
     e = __builtin_amdgcn_readfirstlane(scratch[0]);

@@ -310,8 +310,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int nnt = (N + BN - 1) / BN;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = lid % nnt;
+  int lid = xcd_remap(blockIdx.x, gridDim.x);
+  int nt = lid % nnt;
   int mt = lid / nnt;
   if (WG) {
     const int mtn = (Mw + BM - 1) / BM;
@@ -329,8 +329,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void grouped_gemm_fp8_kernel(
     if (lane == 63) wsum[wave] = inc;
     if (tid == 0) s_e = -1;
     __syncthreads();
-    int pre = inc - tiles;
-    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    int pre = inc - tiles, rows = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+      const int v = wsum[w];
+      pre += w < wave ? v : 0;
+      rows += v;
+    }
+    // real tiles on the lowest block ids, XCD remap over them only (see gemm8.hip)
+    const int R = rows * nnt;
+    if ((int)blockIdx.x >= R) return;
+    lid = xcd_remap(blockIdx.x, R);
+    nt = lid % nnt;
+    mt = lid / nnt;
     if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) { s_e = tid; s_mt = mt - pre; }
     __syncthreads();
   }

@@ -15,7 +15,7 @@ from solvingpapers_amd.ops import _ext
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--rounds", type=int, default=2)
-ap.add_argument("--env", default=None, help="NAME=V1,V2,...: extra gemm4a arms with NAME set to each value")
+ap.add_argument("--env", action="append", default=[], help="NAME=V1,V2,...: extra gemm4a arms with NAME set to each value (repeatable)")
 a = ap.parse_args()
 ops = _ext.ops()
 dev = "cuda"
@@ -98,9 +98,9 @@ timed_mw = [("grouped dX dsv3_style", lambda: ops.gemm4a(dy13, W13, offs, 1, Non
             ("grouped dW dsv3_style", lambda: ops.gemm4a(dy13, xg, offs, 2, None), lambda: ops.grouped_gemm8(dy13, xg, offs, 2, None, False), 2.0 * A * 2 * F * D)]
 
 arms = [("gemm4a", None)]
-if a.env:
-    k_, vs = a.env.split("=")
-    arms += [(f"gemm4a {k_}={v}", (k_, v)) for v in vs.split(",")]
+for ev_ in a.env:
+    k_, vs = ev_.split("=")
+    arms += [(f"{k_}={v}", (k_, v)) for v in vs.split(",")]
 for r in range(a.rounds):
     for name, x, w, off, ref, fl, blas in cases[:3]:
         res = []

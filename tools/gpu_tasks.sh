@@ -310,6 +310,15 @@ defer-prof)
     python tools/rocpd_summary.py /tmp/${task}_$arm/run_results.db --last-step adamw --top 30 > ${O}_$arm.txt 2>&1
     head -24 ${O}_$arm.txt | cut -c1-150
   done ;;
+g4pmc)
+  # gemm4a (register-staged) vs gemm8 vs hipBLASLt, dense 8192^3: two counter passes
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+    -d ${O}_a -o run --output-format csv -- python3 tools/gemm4a_pmc_prog.py > ${O}_a.log 2>&1 || { tail -5 ${O}_a.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_INSTS_LDS TCC_HIT_sum TCC_MISS_sum \
+    -d ${O}_b -o run --output-format csv -- python3 tools/gemm4a_pmc_prog.py > ${O}_b.log 2>&1 || { tail -5 ${O}_b.log; exit 1; }
+  for d in ${O}_a ${O}_b; do python tools/pmc_summary.py "$(find $d -name '*counter_collection.csv' | head -1)"; done > ${O}.txt 2>&1
+  rm -rf ${O}_a ${O}_b
+  cat ${O}.txt | cut -c1-600 ;;
 gemm-pmc)
   run 120 ${O}_bench.log python -u tools/bench_gemm8_dense.py 8192 --iters 20
   cat ${O}_bench.log | grep -v amdgpu.ids
