@@ -667,8 +667,8 @@ __global__ __launch_bounds__(256, 1) void gemm4d_kernel(const bf16* __restrict__
 
   // ---- DMA geometry. Piece j (0..7) of an operand for this wave is wave-instruction q = 4 j + wave
   // of the block: K-contiguous rows 8q .. 8q+7 / K-strided k-rows 2q, 2q+1 -> LDS bytes q*1024 of
-  // the image (lane l at + 16 l). Source: lane offset (one VGPR; two for K-strided: the swizzle of
-  // k-row 8j + 2w + l/32 depends on j's parity) + a per-piece scalar offset.
+  // the image (lane l at + 16 l). Source: the lane's offset within the piece (the swizzle of a
+  // K-strided k-row 8j + 2w + l/32 depends on j's parity) + the piece's offset.
   auto lane_src = [&](bool kc, long ld, int par) -> unsigned {
     if (kc) {
       const int u = lane >> 3, r = 8 * wave + u;          // rows of q = wave (j = 0); swizzle depends on q & 1 only
@@ -679,27 +679,38 @@ __global__ __launch_bounds__(256, 1) void gemm4d_kernel(const bf16* __restrict__
     const int c = (lane & 31) ^ ksw(r);
     return (unsigned)((h * ld + 8 * c) * 2);
   };
-  const unsigned vA0 = lane_src(A_KC, lda, 0), vA1 = lane_src(A_KC, lda, 1);
-  const unsigned vB0 = lane_src(B_KC, ldb, 0), vB1 = lane_src(B_KC, ldb, 1);
+  // per-piece lane offsets (the piece's scalar offset folded in: a non-constant soffset operand of
+  // __builtin_amdgcn_raw_ptr_buffer_load_lds makes hipcc's host pass drop the kernel instantiation)
+  auto soff = [&](bool kc, long ld, int j) -> unsigned { return (unsigned)((kc ? 8 : 2) * (4 * j + wave) * ld * 2); };
+  unsigned voA[8], voB[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    voA[j] = lane_src(A_KC, lda, j & 1) + soff(A_KC, lda, j);
+    voB[j] = lane_src(B_KC, ldb, j & 1) + soff(B_KC, ldb, j);
+  }
   const long limA = MODE == 2 ? kend * lda : a_rows * lda;
   const long limB = MODE == 2 ? kend * ldb : b_rows * ldb;
   const long oA = A_KC ? m0 * lda + k0 : k0 * lda + m0, oB = B_KC ? n0 * ldb + k0 : k0 * ldb + n0;
   const long stA = A_KC ? TK : TK * lda, stB = B_KC ? TK : TK * ldb;
-  // per-piece scalar offsets (bytes): K-contiguous q*8 rows, K-strided q*2 k-rows (q = 4 j + wave)
-  auto soff = [&](bool kc, long ld, int j) -> int { return (int)((kc ? 8 : 2) * (4 * j + wave) * ld * 2); };
-  __amdgpu_buffer_rsrc_t rsA, rsB;
-  auto set_rsrc = [&](int t) {   // descriptors of tile t (once per tile per operand)
+  // descriptor inputs of the current tile (base, bytes) per operand; the descriptors themselves are
+  // built at each piece from these (a pure op: hipcc keeps one per tile). A descriptor-typed local
+  // captured by the lambdas made the host pass drop the kernel's instantiation (undefined launch stub).
+  const bf16* pA = A;
+  const bf16* pB = Bp;
+  long nA = 0, nB = 0;
+  auto set_rsrc = [&](int t) {   // tile t's descriptor inputs (once per tile per operand)
     const long a0 = oA + (long)t * stA, b0 = oB + (long)t * stB;
-    rsA = rsrc(A + a0, (limA - a0) * 2);
-    rsB = rsrc(Bp + b0, (limB - b0) * 2);
+    pA = A + a0;
+    pB = Bp + b0;
+    nA = (limA - a0) * 2;
+    nB = (limB - b0) * 2;
   };
   auto piece = [&](int buf, int j) {   // piece j (0..7 A, 8..15 B) of the tile whose descriptors are set
     const bool ja = j < 8;
     const int jj = j & 7;
     char* dst = smem + buf * TBUF + (ja ? 0 : TIMG) + (4 * jj + wave) * 1024;
-    const bool kc = ja ? A_KC : B_KC;
-    const unsigned vo = ja ? ((jj & 1) && !kc ? vA1 : vA0) : ((jj & 1) && !kc ? vB1 : vB0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ja ? rsA : rsB, (lds_void*)dst, 16, vo, soff(kc, ja ? lda : ldb, jj), 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ja ? rsrc(pA, nA) : rsrc(pB, nB), (lds_void*)dst, 16,
+                                             ja ? voA[jj] : voB[jj], 0, 0, 0);
   };
 
   // ---- fragment reads (gemm4r's image layouts at a buffer offset)

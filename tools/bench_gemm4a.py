@@ -116,5 +116,12 @@ for r in range(a.rounds):
         print(f"round {r} {name}: " + "  ".join(f"{lab} {ms:.3f} ms {fl / ms / 1e9:.0f} TF" for lab, ms in res),
               flush=True)
     for name, f4, f8, fl in timed_mw:
-        t4, t8 = tm(f4), tm(f8)
-        print(f"round {r} {name}: gemm4a {t4:.3f} ms {fl / t4 / 1e9:.0f} TF  gemm8 {t8:.3f} ms {fl / t8 / 1e9:.0f} TF", flush=True)
+        res = []
+        for lab, ev in arms:
+            if ev:
+                os.environ[ev[0]] = ev[1]
+            res.append((lab, tm(f4)))
+            if ev:
+                os.environ.pop(ev[0])
+        res.append(("gemm8", tm(f8)))
+        print(f"round {r} {name}: " + "  ".join(f"{lab} {ms:.3f} ms {fl / ms / 1e9:.0f} TF" for lab, ms in res), flush=True)
