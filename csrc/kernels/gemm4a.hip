@@ -837,12 +837,14 @@ static int g4_impl() {
   const std::string v(e);
   return v == "ring" ? 0 : v == "reg" ? 1 : 2;
 }
-static bool g4_dma() { return g4_impl() == 0; }
+
 
 // grouped_gemm8's contract (csrc/kernels/gemm8.hip): modes 0 / 1 need the reduction dim % 32 and
 // N % 8; mode 2 N, K % 8 (any token counts)
 at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets, int64_t mode,
-                  const c10::optional<at::Tensor>& out_, bool accumulate) {
+                  const c10::optional<at::Tensor>& out_, bool accumulate, int64_t impl_) {
+  // impl: -1 = SPA_G4_IMPL / default (two-buffer LDS-DMA), 0 ring, 1 register staging, 2 two-buffer DMA
+  const int impl = impl_ >= 0 ? (int)impl_ : g4_impl();
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "gemm4a: bf16");
   TORCH_CHECK(a.is_contiguous() && w.is_contiguous() && offsets.scalar_type() == at::kInt && offsets.is_cuda());
   const int E = offsets.numel() - 1;
@@ -867,7 +869,7 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
       return out;
     }
     const int grid = (cdiv(M, 256) + E) * cdiv(N, 256);
-    if (g4_impl() == 2) {
+    if (impl == 2) {
       TORCH_CHECK(K % 64 == 0, "gemm4a: reduction % 64");
 #define G4D(MD) gemm4d_kernel<MD><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),         \
                                                        (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
@@ -877,7 +879,7 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
       SPA_LAUNCH_CHECK();
       return out;
     }
-    if (!g4_dma()) {
+    if (impl == 1) {
       TORCH_CHECK(K % 64 == 0, "gemm4a (register-staged): reduction % 64");
       const int pol = g4_pol();
       if (mode == 0 && pol == 1)
@@ -926,11 +928,11 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
   auto out = out_ ? *out_ : at::empty({E, N, K}, a.options());
   TORCH_CHECK(out.is_contiguous() && out.numel() == (long)E * N * K);
   const int grid = E * cdiv(N, 256) * cdiv(K, 256);
-  if (g4_impl() == 2)
+  if (impl == 2)
     gemm4d_kernel<2><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
                                            (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
                                            (long)N * K, accumulate ? 1 : 0, T, T, 1);
-  else if (!g4_dma())
+  else if (impl == 1)
     gemm4r_kernel<2><<<grid, 256, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),
                                            (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, N, K, 0, N, K, K, 0,
                                            (long)N * K, accumulate ? 1 : 0, T, T, 1);
@@ -946,10 +948,19 @@ at::Tensor gemm4a(const at::Tensor& a, const at::Tensor& w, const at::Tensor& of
   return out;
 }
 
+// fp32 partials of a dense weight gradient split over S token slices (wgrad8's contract, gemm8.hip):
+// part[s] = dy[slice s]^T x[slice s], [S, N, K] fp32, on the register-staged kernel's mode 2
+void launch_gemm4r_wgrad_part(const bf16* dy, const bf16* x, float* part, const int* offsets, int S, int N, int K,
+                              long lda, long ldb, long T, hipStream_t st) {
+  const int grid = S * cdiv(N, 256) * cdiv(K, 256);
+  gemm4r_kernel<2, true><<<grid, 256, 0, st>>>(dy, x, reinterpret_cast<bf16*>(part), offsets, S, N, K, 0, lda, ldb,
+                                               K, 0, (long)N * K, 0, T, T, 1);
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
-  m.def("gemm4a(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate=False) -> Tensor");
+  m.def("gemm4a(Tensor a, Tensor w, Tensor offsets, int mode, Tensor(a!)? out, bool accumulate=False, int impl=-1) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("gemm4a", &spa::gemm4a);

@@ -660,6 +660,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+void launch_gemm4r_wgrad_part(const bf16* dy, const bf16* x, float* part, const int* offsets, int S, int N, int K,
+                              long lda, long ldb, long T, hipStream_t st);
+// SPA_WGRAD_G4=0: the partial products on this file's 8-phase kernel instead of gemm4a.hip's gemm4r
+static bool wgrad_g4() {
+  const char* e = getenv("SPA_WGRAD_G4");
+  return !(e && e[0] == '0');
+}
+
 // Dense weight gradient out[N, K] (+)= dy[T, N]^T x[T, K] on the 8-phase kernel's token-major
 // (mode 2) path, split over tokens into S slices so that S x tiles fills the chip; fp32
 // partials, deterministic reduce. For the T >> N, K products (ViT-B/16: T = 50432, N, K
@@ -711,9 +719,13 @@ at::Tensor wgrad8(const at::Tensor& dy, const at::Tensor& x, const c10::optional
     offsets = it->second;
   }
   auto part = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
-  grouped_gemm8_kernel<2, 0, false, true><<<S * tiles, 512, 0, st>>>(
-      (const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(), reinterpret_cast<bf16*>(part.data_ptr<float>()),
-      offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T);
+  if (wgrad_g4())   // the register-staged 4-wave kernel (gemm4a.hip): grouped dW +11 % over this one
+    launch_gemm4r_wgrad_part((const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(), part.data_ptr<float>(),
+                             offsets.data_ptr<int>(), S, N, K, lda, ldb, T, st);
+  else
+    grouped_gemm8_kernel<2, 0, false, true><<<S * tiles, 512, 0, st>>>(
+        (const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(), reinterpret_cast<bf16*>(part.data_ptr<float>()),
+        offsets.data_ptr<int>(), S, N, K, 0, lda, ldb, K, 0, (long)N * K, 0, T, T);
   SPA_LAUNCH_CHECK();
   const long n = (long)N * K;
   const int rb = (int)std::min<long>((n / 4 + 255) / 256, 4096);

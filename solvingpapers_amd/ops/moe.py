@@ -218,10 +218,19 @@ def _gg8_ok(a, w, mode):
     return GG8_DW and a.shape[1] % 8 == 0 and w.shape[1] % 8 == 0
 
 
+# the expert weight gradients (mode 2) on gemm4a.hip's register-staged 4-wave kernel (AGPR-resident
+# accumulators): 817-820 vs 732-734 TF for gemm8 at dsv3_style widths, same process
+# (profiles/r6_gemm4a.txt); fwd / dX stay on gemm8 (987 / 929 vs 939 / 924 TF). SPA_GG_DW=g8 reverts.
+GG_DW_G4 = os.environ.get("SPA_GG_DW", "g4r") == "g4r"
+
+
 def grouped_gemm(a, w, offsets, mode, out=None, accumulate=False):
     """mode 0: a_e @ w_e^T ; mode 1: a_e @ w_e ; mode 2: per-expert a_e^T @ w_e (w = X rows)."""
     if _gpu(a):
         a, w = a.contiguous(), w.contiguous()
+        if mode == 2 and GG_DW_G4 and _gg8_ok(a, w, mode) and a.shape[1] % 8 == 0 and w.shape[1] % 8 == 0 \
+                and offsets.numel() - 1 <= 256:
+            return ops().gemm4a(a, w, offsets, 2, out, accumulate, 1)
         if GG8 and _gg8_ok(a, w, mode):
             return ops().grouped_gemm8(a, w, offsets, mode, out, accumulate)
         return ops().grouped_gemm(a, w, offsets, mode, out, accumulate)

@@ -310,6 +310,19 @@ defer-prof)
     python tools/rocpd_summary.py /tmp/${task}_$arm/run_results.db --last-step adamw --top 30 > ${O}_$arm.txt 2>&1
     head -24 ${O}_$arm.txt | cut -c1-150
   done ;;
+mapab)
+  # grouped-GEMM tile mapping (real tiles on the lowest block ids) vs the previous build
+  # (B = SPA_EXT_SO=ab/_C_premap.so), dsv3_style accum 1 and dsv3_v3 fp8 accum 4, B N N B
+  base=${BASE_SO:-ab/_C_premap.so}
+  V3="--preset dsv3_v3 --layers 4 --dense-layers 1 --experts 32 --mb 1 --accum 4 --steps 6 --warmup 2 --fp8"
+  for arm in B N N B; do
+    if [ $arm = B ]; then export SPA_EXT_SO=$base; else unset SPA_EXT_SO; fi
+    run 400 ${O}_s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 10 --warmup 3
+    echo "$arm dsv3_style $(grep -ho '"value": [0-9.]*' ${O}_s.log)"
+    run 400 ${O}_v.log python -u bench/dsv3_train.py $V3
+    echo "$arm dsv3_v3_fp8 $(grep -ho '"value": [0-9.]*' ${O}_v.log)"
+  done
+  unset SPA_EXT_SO ;;
 g4pmc)
   # gemm4a (register-staged) vs gemm8 vs hipBLASLt, dense 8192^3: two counter passes
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE \
