@@ -310,6 +310,19 @@ defer-prof)
     python tools/rocpd_summary.py /tmp/${task}_$arm/run_results.db --last-step adamw --top 30 > ${O}_$arm.txt 2>&1
     head -24 ${O}_$arm.txt | cut -c1-150
   done ;;
+g4wire)
+  # gemm4a / gemm4r wiring: GPU tests, then ViT-B/16 (wgrad8 partials: gemm4r vs gemm8) and dsv3_style
+  # (expert dW: gemm4r vs gemm8), each default (N) vs the gemm8 path (B), B N N B
+  run 600 ${O}_pytest.log python -u -m pytest tests/test_gemm4a_gpu.py tests/test_moe_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  tail -2 ${O}_pytest.log
+  for arm in B N N B; do
+    if [ $arm = B ]; then export SPA_WGRAD_G4=0 SPA_GG_DW=g8; else unset SPA_WGRAD_G4 SPA_GG_DW; fi
+    run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
+    echo "$arm vit $(grep -ho '"value": [0-9.]*' ${O}_vit.log)"
+    run 400 ${O}_s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 10 --warmup 3
+    echo "$arm dsv3_style $(grep -ho '"value": [0-9.]*' ${O}_s.log)"
+  done
+  unset SPA_WGRAD_G4 SPA_GG_DW ;;
 mapab)
   # grouped-GEMM tile mapping (real tiles on the lowest block ids) vs the previous build
   # (B = SPA_EXT_SO=ab/_C_premap.so), dsv3_style accum 1 and dsv3_v3 fp8 accum 4, B N N B
