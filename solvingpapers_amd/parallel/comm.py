@@ -277,7 +277,8 @@ class _A2AStart(torch.autograd.Function):
     def backward(ctx, g):
         box = ctx.box
         box.bwork.wait()
-        dx, box.dx, box.gkeep = box.dx, None, None
+        # drop the Work too: it holds the exchange's input and output until it is destroyed
+        dx, box.dx, box.gkeep, box.bwork = box.dx, None, None, None
         return dx, None
 
 
@@ -288,6 +289,7 @@ class _A2AFinish(torch.autograd.Function):
     @staticmethod
     def forward(ctx, buf, box):
         box.work.wait()
+        box.work = None
         ctx.box = box
         return buf.view_as(buf)
 
@@ -343,6 +345,7 @@ class _ARFinish(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, box):
         box.work.wait()
+        box.work = None
         return y.view_as(y)
 
     @staticmethod
@@ -376,7 +379,7 @@ class _GradARStart(torch.autograd.Function):
     def backward(ctx, g):
         box = ctx.box
         box.bwork.wait()
-        dx, box.dx = box.dx, None
+        dx, box.dx, box.bwork = box.dx, None, None
         return dx, None
 
 

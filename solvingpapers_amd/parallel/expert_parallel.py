@@ -130,7 +130,7 @@ class _Fp8DispatchStart(torch.autograd.Function):
     def backward(ctx, g):
         box = ctx.box
         box.bwork.wait()
-        dx, box.dx, box.gkeep = box.dx, None, None
+        dx, box.dx, box.gkeep, box.bwork = box.dx, None, None, None
         if box.cap is not None:                 # [P*C] block slots -> expert-sorted rows
             dx = _map_rows(dx, box.cap.send_back)
         return dx, None
@@ -146,6 +146,7 @@ class _Fp8DispatchFinish(torch.autograd.Function):
     @staticmethod
     def forward(ctx, token, W13, rc, offsets, box):
         box.work.wait()
+        box.work = None
         D = box.D
         KB = D // 128
         pl = regroup_rows(box.recv, rc, True) if box.cap is None else _map_rows(box.recv, box.cap.recv_to)

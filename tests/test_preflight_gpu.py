@@ -34,7 +34,13 @@ def _launch(script, args, extra_env=None, timeout=240):
     print(r.stdout[-3000:])
     print(r.stderr[-3000:], file=sys.stderr)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    lines = []
+    for l in r.stdout.splitlines():
+        if l.startswith("{"):
+            try:
+                lines.append(json.loads(l))
+            except ValueError:            # a diagnostic dict print, not the result line
+                pass
     assert lines, r.stdout[-2000:]
     return lines[-1]
 
@@ -53,6 +59,16 @@ def test_dsv3_v3_fp8_ep_dispatch_through_rccl_world1():
                                           "--steps", "2", "--warmup", "1", "--gemm-table", "none"])
     assert "forced-collectives" in out["config"]["parallelism"]
     assert out["value"] > 0 and out["loss"] == out["loss"]
+
+
+def test_ep_rccl_live_memory_flat_across_microbatches():
+    """Regression (profiles/r6_ep_memory.txt): through a real RCCL group the EP exchanges' Work objects
+    used to stay referenced after wait() and pinned ~3 GB per MoE layer and micro-batch."""
+    out = _launch("tools/ep_mem_probe.py", ["--check", "--seq", "2048"])
+    for a in out["arms"]:
+        assert a["arm"] == "ep-forced"
+        assert abs(a["growth_gb"]) < 0.05, out
+        assert a["live_boxes"] == 0, out
 
 
 @pytest.mark.parametrize("N,n", [(1, 4096), (8, 1 << 20), (8, 1000 + 3), (4, 8 * 7919)])
