@@ -35,6 +35,7 @@
 #   epcap [CF]     capacity-mode EP dispatch: MoE GPU tests + EP=8 proxy one-by-one exact vs capacity
 #   dbgbounds      debug-bounds build (device guards) over the ragged-shape GPU cases
 #   gradprec [N]   bf16-vs-fp32 gradient accumulation: 8B-width error test + N-step loss-curve A/B
+#   v3mem          dsv3_v3 fp8 (4 layers, accum 4) unforced vs through a 1-rank RCCL group: peak memory after the Work fix
 #   rccl           world-1 RCCL test (every collective path) + headline ABBA with TENSILE_STREAMK_DATA_PARALLEL=1
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -91,6 +92,14 @@ preflight)
   V3="--preset dsv3_v3 --layers 4 --dense-layers 1 --experts 32 --mb 1 --accum 4 --steps 3 --warmup 1 --fp8"
   run 400 ${O}_v0.log python -u bench/dsv3_train.py $V3
   run 400 ${O}_v1.log env SPA_FORCE_COLLECTIVES=1 $TR bench/dsv3_train.py $V3
+  jsonl ${O}_v?.log ;;
+v3mem)
+  TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29533"
+  V3="--preset dsv3_v3 --layers 4 --dense-layers 1 --experts 32 --mb 1 --accum 4 --steps 3 --warmup 1 --fp8"
+  run 400 ${O}_v0.log python -u bench/dsv3_train.py $V3
+  run 400 ${O}_v1.log env SPA_FORCE_COLLECTIVES=1 $TR bench/dsv3_train.py $V3
+  run 400 ${O}_v2.log python -u bench/dsv3_train.py $V3
+  run 400 ${O}_v3.log env SPA_FORCE_COLLECTIVES=1 $TR bench/dsv3_train.py $V3
   jsonl ${O}_v?.log ;;
 rccl)
   run 300 ${O}_pytest.log python -u -m pytest tests/test_rccl_gpu.py -x -v -s -p no:cacheprovider --timeout 240 --timeout-method thread
