@@ -145,7 +145,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
                                                                bf16* __restrict__ C, const int* __restrict__ offsets,
                                                                int E, int M, int N, int K, long lda, long ldb, long ldc,
                                                                long strideB, long strideC, int accumulate, long a_rows,
-                                                               long b_rows, int gm = 1) {
+                                                               long b_rows, int gm = 1, int tailr = 0) {
   using namespace g8;
   constexpr bool A_KC = MODE != 2, B_KC = MODE == 0;
   // ONE LDS array (a second __shared__ object can make hipcc drain the DMA queue before ds_reads);
@@ -166,6 +166,7 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     mt = lid / nnt;
   }
   int e = 0;
+  bool tail = false;
   long m0 = 0, mend = M, k0 = 0, kend = K;
   const bf16* Bp = B;
   bf16* Cp = C;
@@ -176,9 +177,14 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     // lowest block ids and the XCD remap runs over R (a remap over the whole grid scattered the
     // empty blocks, and real tiles landed behind them in an extra dispatch round)
     const int o0 = tid < E ? offsets[tid] : 0, o1 = tid < E ? offsets[tid + 1] : 0;
-    const int cnt = o1 - o0;
-    const int tiles = (cnt + BM - 1) / BM;
-    int inc = tiles;
+    const int cnt = o1 - o0, rem = cnt & (BM - 1);
+    // tail tiles: an expert's last <= tailr (<= TR) rows past a multiple of 256 go to a 64-row tile
+    // (below) instead of a 256-row one paid in full -- at dsv3_style routing half the experts end
+    // 1-55 rows past a multiple of 256, 15 % of the grid (tools/bench_gg_counts.py)
+    const bool tl = rem > 0 && rem <= tailr;
+    const int tiles = (cnt >> 8) + (rem > 0 && !tl ? 1 : 0);
+    const int pk = tiles + (tl ? 1 << 20 : 0);   // row tiles | tail tiles << 20, scanned together
+    int inc = pk;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int v = __shfl_up(inc, o, 64);
@@ -187,26 +193,38 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
     if (lane == 63) wsum[wave] = inc;
     if (tid == 0) scratch[0] = -1;
     __syncthreads();
-    int pre = inc - tiles, rows = 0;
+    int pre = inc - pk, rows = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) {
       const int v = wsum[w];
       pre += w < wave ? v : 0;
       rows += v;
     }
+    const int pre_t = pre >> 20, tails = rows >> 20;
+    pre &= (1 << 20) - 1;
+    rows &= (1 << 20) - 1;
     const int R = rows * nnt;
-    if ((int)blockIdx.x >= R) return;
-    const int lid = xcd_remap(blockIdx.x, R);
-    nt = lid % nnt;
-    mt = lid / nnt;
-    if (gm > 1) {   // groups of gm row tiles x all column tiles (L2 / MALL reuse of B panels)
-      const int g = lid / (gm * nnt), r = lid % (gm * nnt);
-      const int gs = min(gm, rows - g * gm);
-      mt = g * gm + r % gs;
-      nt = r / gs;
-    }
-    if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) {
-      scratch[0] = tid; scratch[1] = mt - pre; scratch[2] = o0; scratch[3] = o1;
+    if ((int)blockIdx.x >= R + tails * nnt) return;
+    tail = (int)blockIdx.x >= R;
+    if (!tail) {
+      const int lid = xcd_remap(blockIdx.x, R);
+      nt = lid % nnt;
+      mt = lid / nnt;
+      if (gm > 1) {   // groups of gm row tiles x all column tiles (L2 / MALL reuse of B panels)
+        const int g = lid / (gm * nnt), r = lid % (gm * nnt);
+        const int gs = min(gm, rows - g * gm);
+        mt = g * gm + r % gs;
+        nt = r / gs;
+      }
+      if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) {
+        scratch[0] = tid; scratch[1] = mt - pre; scratch[2] = o0; scratch[3] = o1;
+      }
+    } else {          // tail tile j of the tail experts (in expert order), column tile nt
+      const int t = blockIdx.x - R, j = t / nnt;
+      nt = t % nnt;
+      if (tid < E && tl && pre_t == j) {
+        scratch[0] = tid; scratch[1] = cnt >> 8; scratch[2] = o0; scratch[3] = o1;
+      }
     }
     __syncthreads();
     e = __builtin_amdgcn_readfirstlane(scratch[0]);
@@ -399,6 +417,90 @@ __global__ __launch_bounds__(512, 1) void grouped_gemm8_kernel(const bf16* __res
   //   P1 stages B1(t+1)   P2 A1(t+1)   P3 A0(t+2)   P4 B0(t+2)
   // => 4 halves (8 DMA per thread) stay in flight across every wait; each half has 5-6 phases
   // between issue and first read. Waits (end of P1, P2, P4) retire exactly the next reader's half.
+  if constexpr (MODE != 2 && ABL == 0 && !ILV) {
+    if (__builtin_amdgcn_readfirstlane((int)tail)) {
+      // Tail tile: rows [m0, mend) (<= TR = 64) x 256 columns, 3-stage ring of 40 KiB K-tiles (A: 64
+      // rows, one DMA piece per thread; B0 / B1: the usual 128-column halves), two K-tiles in flight:
+      // 16 MFMAs per wave per K-tile are too few to cover a one-deep prefetch's latency. Wave (tm, wn)
+      // owns rows tm * 32 + [0, 32), cols 64 wn + [0, 64); the tail blocks run last, in the grid's
+      // final partial dispatch round.
+      constexpr int TS = 8192 + 2 * HALF;
+      const int tm = wave >> 2;
+      f32x4 tacc[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto tstage = [&](int t) {
+        char* dst = smem + (t % 3) * TS + wave_u * 1024;
+        const long kk = k0 + (long)t * BK;
+        {
+          const long origin = m0 * lda + kk;       // A is K-contiguous in modes 0 and 1
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(A + origin, (limA - origin) * 2), (lds_void*)dst, 16, voA[0], 0, 0, 0);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const long c = n0 + 128 * h;
+          const long origin = B_KC ? c * ldb + kk : kk * ldb + c;
+          const __amdgpu_buffer_rsrc_t rs = rsrc(Bp + origin, (limB - origin) * 2);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 8192 + h * HALF + j * (NT * 16)), 16, voB[j], 0, 0, 0);
+        }
+      };
+      if (ktiles > 0) tstage(0);
+      if (ktiles > 1) tstage(1);
+      for (int t = 0; t < ktiles; ++t) {
+        const char* ts = smem + (t % 3) * TS;
+        if (t + 2 < ktiles) { tstage(t + 2); G8_WAIT_VM(10); } else if (t + 1 < ktiles) { G8_WAIT_VM(5); } else { G8_WAIT_VM(0); }
+        __builtin_amdgcn_s_barrier();
+        bf16x8 ta[2][2], tb[4][2];
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) ta[i][ss] = rd_kc(ts, tm * 32 + 16 * i, ss, lane);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c = 64 * wn + 16 * j;
+            const char* hb = ts + 8192 + (c >> 7) * HALF;
+            tb[j][ss] = B_KC ? rd_kc(hb, c & 127, ss, lane) : rd_ks(hb, c & 127, ss, lane);
+          }
+        }
+        G8_WAIT_LGKM0();
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              tacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tb[j][ss], ta[i][ss], tacc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_barrier();
+      }
+      // C^T fragments: lane holds C[row0 + (lane & 15)][col0 + 4 (lane >> 4) + q], 8 B per lane
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long gm = m0 + tm * 32 + 16 * i + (lane & 15);
+          const int gn = n0 + 64 * wn + 16 * j + 4 * (lane >> 4);
+          if (gm < mend && gn < N && SPA_DBG_OK(gm, M) & SPA_DBG_OK(gn + 3, ldc)) {
+            bf16* cp = Cp + gm * ldc + gn;
+            const f32x4 v = tacc[i][j];
+            bf16x4 w4;
+            if (accumulate) {
+              const bf16x4 o = *reinterpret_cast<const bf16x4*>(cp);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w4[q] = (bf16)(v[q] + (float)o[q]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+            }
+            *reinterpret_cast<bf16x4*>(cp) = w4;
+          }
+        }
+      return;
+    }
+  }
   const bool late = __builtin_amdgcn_readfirstlane(wave) >= 4;   // scalar branch, not an EXEC mask
   if (ILV) {
     // (measured slower; kept for the A/B) DMA issue inside the MFMA clusters (after the phase's first barrier): with the stagger a
@@ -743,6 +845,12 @@ static int ablation() {
   const char* e = getenv("SPA_GG8_ABLATE");
   return e ? atoi(e) : 0;
 }
+// SPA_GG8_TAIL (read per call): an expert's last rows past a multiple of 256 go to a 64-row tail
+// tile when there are at most this many (default 64, the tail tile's capacity; 0: always a full tile)
+static int g8_tail() {
+  const char* e = getenv("SPA_GG8_TAIL");
+  return e ? std::max(0, std::min(64, atoi(e))) : 64;
+}
 // SPA_G8_GM (read per call): row tiles per tile group of a dense (E = 1) forward / dX grid
 // (default 4: 4 x 8 tiles per XCD wave instead of 1 x 32 -- dense 8192^3 +5 % fwd, +14 % dX);
 // grouped GEMMs keep the row-major order (the grouping measured -3 % on their forward)
@@ -779,7 +887,8 @@ at::Tensor grouped_gemm8(const at::Tensor& a, const at::Tensor& w, const at::Ten
       N, K, K, Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g8_group(E));                      \
   else grouped_gemm8_kernel<MD, AB><<<grid, 512, 0, st>>>((const bf16*)a.data_ptr(), (const bf16*)w.data_ptr(),     \
                                                      (bf16*)out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, \
-                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g8_group(E))
+                                                     Kw, N, (long)Nw * Kw, 0, accumulate ? 1 : 0, M, Nw, g8_group(E), \
+                                                     abl == 0 ? g8_tail() : 0)
     const int abl = ablation();
     if (mode == 0) {
       if (abl == 1) { G8_L(0, 1); } else if (abl == 2) { G8_L(0, 2); } else if (abl == 3) { G8_L(0, 3); } else if (abl == 8) { G8_L(0, 8); } else { G8_L(0, 0); }

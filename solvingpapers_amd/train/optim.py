@@ -17,6 +17,9 @@ import torch
 from ..ops import optim_kernels as K
 from ..utils.flat import FlatParams
 
+# priority of the overlapped optimizer's side stream (torch: 0 default, -1 high). SPA_OPT_PRIO
+OPT_STREAM_PRIORITY = int(__import__("os").environ.get("SPA_OPT_PRIO", "0"))
+
 
 class FlatOptimizer:
     def __init__(self, flat: FlatParams, lr: float, weight_decay: float = 0.0, max_grad_norm: Optional[float] = None,
@@ -107,7 +110,7 @@ class FlatOptimizer:
         if overlap and self.flat.device.type == "cuda":
             main = torch.cuda.current_stream(self.flat.device)
             if not hasattr(self, "_side"):
-                self._side = torch.cuda.Stream(self.flat.device, priority=0)
+                self._side = torch.cuda.Stream(self.flat.device, priority=OPT_STREAM_PRIORITY)
             side = self._side
             side.wait_stream(main)
             if coef is not None:

@@ -278,6 +278,47 @@ def test_grouped_gemm8_elementwise(counts, N, K, gm, monkeypatch):
     check(dw2.reshape(E * N, K), 2 * ref.reshape(E * N, K))
 
 
+@pytest.mark.parametrize("counts,N,K", [
+    ([769, 812, 768, 1, 64, 65, 0, 320, 63, 2], 2816, 256),   # tails of 1 / 44 / 63 / 64 rows, one of 65 (full tile)
+    ([5, 0, 17], 200, 128),                                   # only tails, N % 256 != 0
+    ([256 * 3 + 7] * 8 + [256 * 2 + 64] * 8, 512, 192),
+])
+def test_grouped_gemm8_tail_tiles_bitwise(counts, N, K, monkeypatch):
+    """gemm8 modes 0/1: an expert's last <= 64 rows past a multiple of 256 run on a 64-row tail tile
+    (SPA_GG8_TAIL, default 64). Every output element sums the same K-slices in the same order on
+    either tile, so the result is bitwise the full-tile one (SPA_GG8_TAIL=0); accumulate adds onto C
+    (rounded once on the tail tile)."""
+    g = torch.Generator().manual_seed(7)
+    E, M_ = len(counts), sum(counts)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    x = torch.randn(M_, K, generator=g).to(dev, torch.bfloat16)
+    W = (torch.randn(E, N, K, generator=g) / K ** 0.5).to(dev, torch.bfloat16)
+    dy = torch.randn(M_, N, generator=g).to(dev, torch.bfloat16)
+    c0 = torch.randn(M_, N, generator=g).to(dev, torch.bfloat16)
+    ops = M.ops()
+    res = {}
+    for tail in ("0", "64", "40"):
+        monkeypatch.setenv("SPA_GG8_TAIL", tail)
+        y = ops.grouped_gemm8(x, W, off, 0, None, False)
+        # mode 1: dX[M, K] = dY[M, N] W_e[N, K] (reduction over N: % 64)
+        dx = ops.grouped_gemm8(dy, W, off, 1, None, False) if N % 64 == 0 else None
+        ya = c0.clone()
+        ops.grouped_gemm8(x, W, off, 0, ya, True)
+        res[tail] = (y, dx, ya)
+    ref = _oracle(x, W, off, 0)
+    err = (res["64"][0].float().cpu() - ref).abs().max() / ref.abs().max()
+    assert err < 2e-2, float(err)
+    assert ((res["64"][2].float() - (res["64"][0].float() + c0.float())).abs().max() < 0.1)
+    for t in ("64", "40"):
+        assert torch.equal(res[t][0], res["0"][0]), t
+        # accumulate: the tail tile rounds acc + C once, the full tile's LDS epilogue rounds acc to bf16
+        # first (one bf16 step apart at most)
+        d = (res[t][2].float() - res["0"][2].float()).abs()
+        assert (d <= (res["0"][0].float().abs() + c0.float().abs()) * 2 ** -7 + 1e-6).all(), t
+        if res[t][1] is not None:
+            assert torch.equal(res[t][1], res["0"][1]), t
+
+
 def test_fp8_block_quant_matches_reference():
     """quant_act_fp8_blk / quant_weight_fp8_blk (E8M0 block scales) == the torch reference bit for
     bit; W^T bytes are the transpose of W's; scales are powers of two with amax / 2^e <= 448."""

@@ -146,6 +146,15 @@ headline-prof)
   jsonl ${O}.log
   python tools/rocpd_summary.py /tmp/$task/run_results.db --last-step adamw --top 40 > ${O}_summary.txt 2>&1
   head -50 ${O}_summary.txt | cut -c1-160 ;;
+opt-overlap)
+  # does the side-stream AdamW co-run with the next step's forward? kernel traces at the default and
+  # at high side-stream priority (SPA_OPT_PRIO=-1): busy-union vs summed kernel time per arm
+  for pr in 0 -1; do
+    run 400 ${O}_$pr.log env SPA_OPT_PRIO=$pr rocprofv3 --kernel-trace -d /tmp/${task}_$pr -o run -- python3 bench.py --steps 3 --warmup 1
+    jsonl ${O}_$pr.log
+    python tools/rocpd_summary.py /tmp/${task}_$pr/run_results.db --top 4 > ${O}_${pr}_summary.txt 2>&1
+    echo "== SPA_OPT_PRIO=$pr"; head -8 ${O}_${pr}_summary.txt | cut -c1-160
+  done ;;
 headline-pmc)
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
     -d ${O}_a -o run --output-format csv -- python3 bench.py --layers 4 --steps 1 --warmup 1 > ${O}_a.log 2>&1 || exit 1
