@@ -85,7 +85,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
                                                            const int* __restrict__ offsets, int E, int M, int N,
                                                            int K, long lda, long ldb, long strideB, long a_rows,
                                                            long b_rows, int KB, long ldsa, long ldsb, long sa_bytes,
-                                                           long sb_bytes, int accumulate, int out_f32) {
+                                                           long sb_bytes, int accumulate, int out_f32, int tailr = 0) {
   using namespace g8f;
   // ONE LDS array: a second __shared__ object can make hipcc drain the DMA queue before ds_reads
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 64];
@@ -97,12 +97,16 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
   int nt = lid % nnt;
   int mt = lid / nnt;
   int e = 0;
+  bool tail = false;
   long m0 = 0, mend = M, k0 = 0, kend = K;
   if (!WG) {
     int* wsum = scratch + 8;
-    const int cnt = tid < E ? offsets[tid + 1] - offsets[tid] : 0;
-    const int tiles = (cnt + BM - 1) / BM;
-    int inc = tiles;
+    const int cnt = tid < E ? offsets[tid + 1] - offsets[tid] : 0, rem = cnt & (BM - 1);
+    // tail tiles (gemm8.hip): an expert's last <= tailr rows past a multiple of 256 run on a 64-row tile
+    const bool tl = rem > 0 && rem <= tailr;
+    const int tiles = (cnt >> 8) + (rem > 0 && !tl ? 1 : 0);
+    const int pk = tiles + (tl ? 1 << 20 : 0);   // row tiles | tail tiles << 20
+    int inc = pk;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int v = __shfl_up(inc, o, 64);
@@ -111,21 +115,31 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
     if (lane == 63) wsum[wave] = inc;
     if (tid == 0) scratch[0] = -1;
     __syncthreads();
-    int pre = inc - tiles, rows = 0;
+    int pre = inc - pk, rows = 0;
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
       const int v = wsum[w];
       pre += w < wave ? v : 0;
       rows += v;
     }
+    const int pre_t = pre >> 20, tails = rows >> 20;
+    pre &= (1 << 20) - 1;
+    rows &= (1 << 20) - 1;
     // real tiles on the lowest block ids, XCD remap over them only (gemm8.hip: the empty blocks of
-    // the worst-case grid must not push real tiles into another dispatch round)
+    // the worst-case grid must not push real tiles into another dispatch round); tail tiles last
     const int R = rows * nnt;
-    if ((int)blockIdx.x >= R) return;
-    lid = xcd_remap(blockIdx.x, R);
-    nt = lid % nnt;
-    mt = lid / nnt;
-    if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) { scratch[0] = tid; scratch[1] = mt - pre; }
+    if ((int)blockIdx.x >= R + tails * nnt) return;
+    tail = (int)blockIdx.x >= R;
+    if (!tail) {
+      lid = xcd_remap(blockIdx.x, R);
+      nt = lid % nnt;
+      mt = lid / nnt;
+      if (tid < E && tiles > 0 && mt >= pre && mt < pre + tiles) { scratch[0] = tid; scratch[1] = mt - pre; }
+    } else {
+      const int t = blockIdx.x - R, j = t / nnt;
+      nt = t % nnt;
+      if (tid < E && tl && pre_t == j) { scratch[0] = tid; scratch[1] = cnt >> 8; }
+    }
     __syncthreads();
     e = __builtin_amdgcn_readfirstlane(scratch[0]);
     if (e < 0) return;
@@ -237,6 +251,108 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
   // A1(t+1), P3 A0(t+2), P4 B0(t+2), waits 8 / 8 / 8. Waits (end of P1, P2, P4) retire exactly the
   // next reader's half (waves 0 / 1 count one scale piece more per A0 half, so their waits are one
   // piece stricter); waves 4-7 run one barrier behind waves 0-3.
+  if constexpr (!WG) {
+    if (__builtin_amdgcn_readfirstlane((int)tail)) {
+      // Tail tile (gemm8.hip): rows [m0, mend) (<= 64) x 256 columns, 3-stage ring of 42 KiB K-tiles
+      // (A: 64 rows, one DMA piece per thread; B0 / B1 halves; the tile's scale slots, waves 0 / 1);
+      // wave (tm, wn) owns rows tm * 32 + [0, 32), cols 64 wn + [0, 64): 8 scaled MFMAs per K-tile
+      constexpr int TS = 8192 + 2 * HALF + SCL;
+      const int tm = wave >> 2;
+      f32x4 tacc[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto tstage = [&](int t) {
+        char* dst = smem + (t % 3) * TS;
+        const long kk = k0 + (long)t * BK;
+        const int kb = (int)(kk / BK);
+        if (wave_u < 2) {   // wave 0: A scales, wave 1: B scales of tile t
+          const uint8_t* sb = wave_u == 0 ? sAt + (long)kb * ldsa + (m0 & ~15L) : sBt + ((long)e * KB + kb) * ldsb + (nb0 & ~15L);
+          const long lim = wave_u == 0 ? sa_bytes - (long)(sb - sAt) : sb_bytes - (long)(sb - sBt);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(sb, lim), (lds_void*)(dst + 8192 + 2 * HALF + wave_u * 1024), 16,
+                                                   (unsigned)(lane * 16), 0, 0, 0);
+        }
+        {
+          const long origin = m0 * lda + kk;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(A + origin, limA - origin), (lds_void*)(dst + wave_u * 1024), 16, voA[0], 0, 0, 0);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const long origin = (n0 + 128 * h) * ldb + kk;
+          const __amdgpu_buffer_rsrc_t rs = rsrc(Bp + origin, limB - origin);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 8192 + h * HALF + wave_u * 1024 + j * (NT * 16)), 16,
+                                                     voB[j], 0, 0, 0);
+        }
+      };
+      const bool sw = wave_u < 2;             // waves 0 / 1 issue one scale piece more per stage
+      if (ktiles > 0) tstage(0);
+      if (ktiles > 1) tstage(1);
+      for (int t = 0; t < ktiles; ++t) {
+        const char* ts = smem + (t % 3) * TS;
+        if (t + 2 < ktiles) {
+          tstage(t + 2);
+          if (sw) { G8F_WAIT_VM(12); } else { G8F_WAIT_VM(10); }
+        } else if (t + 1 < ktiles) {
+          if (sw) { G8F_WAIT_VM(6); } else { G8F_WAIT_VM(5); }
+        } else {
+          G8F_WAIT_VM(0);
+        }
+        __builtin_amdgcn_s_barrier();
+        i32x8 ta[2], tb[4];
+        int tsa[2], tsb[4];
+        const uint8_t* sa = reinterpret_cast<const uint8_t*>(ts + 8192 + 2 * HALF) + dA;
+        const uint8_t* sbp = reinterpret_cast<const uint8_t*>(ts + 8192 + 2 * HALF + 1024) + dB;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          ta[i] = rd_op(ts, tm * 32 + 16 * i, lane);
+          tsa[i] = sa[tm * 32 + 16 * i + (lane & 15)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = 64 * wn + 16 * j;
+          tb[j] = rd_op(ts + 8192 + (c >> 7) * HALF, c & 127, lane);
+          tsb[j] = sbp[c >> 7];
+        }
+        G8F_WAIT_LGKM0();
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            tacc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(tb[j], ta[i], tacc[i][j], 0, 0, 0, tsb[j], 0, tsa[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(tacc[i][j]));
+        __builtin_amdgcn_s_barrier();
+      }
+      bf16* Cb = reinterpret_cast<bf16*>(C);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long gm = m0 + tm * 32 + 16 * i + (lane & 15);
+          const int gn = n0 + 64 * wn + 16 * j + 4 * (lane >> 4);
+          if (gm < mend && gn < N && SPA_DBG_OK(gn + 3, N)) {
+            bf16* cp = Cb + gm * N + gn;
+            const f32x4 v = tacc[i][j];
+            bf16x4 w4;
+            if (accumulate) {
+              const bf16x4 o = *reinterpret_cast<const bf16x4*>(cp);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w4[q] = (bf16)(v[q] + (float)o[q]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w4[q] = (bf16)v[q];
+            }
+            *reinterpret_cast<bf16x4*>(cp) = w4;
+          }
+        }
+      return;
+    }
+  }
   constexpr bool S2 = !WG;
   const bool late = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (ktiles > 0) {
@@ -412,10 +528,12 @@ at::Tensor gemm8_fp8_blk(const at::Tensor& xq, const at::Tensor& sx, const at::T
   auto sbt = scale_t(sw, NB, KB, E);           // [E][KB][ldsb]
   const long ldsa = (M + 15) / 16 * 16, ldsb = (NB + 15) / 16 * 16;
   const int grid = (cdiv(M, 256) + E) * cdiv(N, 256);
+  const char* te = getenv("SPA_GG8_TAIL");      // as gemm8.hip: tail tiles for <= 64 trailing rows
+  const int tailr = te ? std::max(0, std::min(64, atoi(te))) : 64;
   gemm8_fp8_kernel<false><<<grid, 512, 0, stream()>>>(
       (const uint8_t*)xq.data_ptr(), (const uint8_t*)wq.data_ptr(), sat.data_ptr<uint8_t>(), sbt.data_ptr<uint8_t>(),
       out.data_ptr(), offsets.data_ptr<int>(), E, M, N, K, K, K, (long)N * K, M, N, KB, ldsa, ldsb,
-      sat.numel(), sbt.numel(), 0, 0);
+      sat.numel(), sbt.numel(), 0, 0, tailr);
   SPA_LAUNCH_CHECK();
   return out;
 }

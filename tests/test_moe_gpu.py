@@ -421,6 +421,27 @@ def test_gemm8_fp8_matches_dequantized_and_register_kernel(K, N, counts):
     assert _rel(y.cpu(), y_old.cpu()) < 5e-3
 
 
+@pytest.mark.parametrize("K,N,counts", [(128, 264, [769, 1, 64, 65, 0, 320]), (1024, 512, [1024 + 37, 1024 + 3, 1024, 5])])
+def test_gemm8_fp8_tail_tiles_bitwise(K, N, counts, monkeypatch):
+    """gemm8_fp8 forward: the 64-row tail tiles (SPA_GG8_TAIL, default 64) give bitwise the full-tile
+    result (same scaled MFMAs in the same K order per element); 1 and 8 K-tiles, N % 256 != 0."""
+    g = torch.Generator().manual_seed(11)
+    E, M_ = len(counts), sum(counts)
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=dev)
+    x = (torch.randn(M_, K, generator=g) * torch.logspace(-2, 1, K)).to(dev, torch.bfloat16)
+    W = (torch.randn(E, (N + 127) // 128 * 128, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    xq, sx = M.quant_act_fp8_blk(x)
+    wq, _, sw, _ = M.quant_weight_fp8_blk(W)
+    wq = wq[:, :N].contiguous()
+    ys = {}
+    for tail in ("0", "64", "20"):
+        monkeypatch.setenv("SPA_GG8_TAIL", tail)
+        ys[tail] = M.ops().gemm8_fp8_blk(xq, sx, wq, sw, off)
+    y_old = M.ops().grouped_gemm_fp8_blk(xq, sx, wq, sw, off)
+    assert _rel(ys["64"].cpu(), y_old.cpu()) < 5e-3
+    assert torch.equal(ys["64"], ys["0"]) and torch.equal(ys["20"], ys["0"])
+
+
 @pytest.mark.parametrize("counts", [[300, 0, 129, 1, 64, 700, 0, 33], [1100, 5]])
 def test_wgrad8_fp8_matches_register_kernel(counts):
     """8-phase fp8 Wgrad (token segments of 1..9 K-tiles) == the register-staged kernel, bf16 and

@@ -36,6 +36,8 @@
 #   dbgbounds      debug-bounds build (device guards) over the ragged-shape GPU cases
 #   gradprec [N]   bf16-vs-fp32 gradient accumulation: 8B-width error test + N-step loss-curve A/B
 #   v3mem          dsv3_v3 fp8 (4 layers, accum 4) unforced vs through a 1-rank RCCL group: peak memory after the Work fix
+#   env-ab ENV CMD B N N B of one env switch on any bench command (separate processes)
+#   opt-overlap    kernel traces of the headline at side-stream priority 0 / -1 (optimizer overlap)
 #   rccl           world-1 RCCL test (every collective path) + headline ABBA with TENSILE_STREAMK_DATA_PARALLEL=1
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -146,6 +148,14 @@ headline-prof)
   jsonl ${O}.log
   python tools/rocpd_summary.py /tmp/$task/run_results.db --last-step adamw --top 40 > ${O}_summary.txt 2>&1
   head -50 ${O}_summary.txt | cut -c1-160 ;;
+env-ab)
+  # env-ab SPA_X=v "bench/dsv3_train.py --preset dsv3_style --steps 10 --warmup 2": B N N B, separate processes
+  ab=${1:?SPA_X=v}; cmd=${2:?bench command}
+  for arm in base var var base; do
+    if [ $arm = var ]; then run 400 ${O}_$arm.log env $ab python -u $cmd
+    else run 400 ${O}_$arm.log python -u $cmd; fi
+    echo "$arm $ab $(grep -ho '"value": [0-9.]*' ${O}_$arm.log)"
+  done ;;
 opt-overlap)
   # does the side-stream AdamW co-run with the next step's forward? kernel traces at the default and
   # at high side-stream priority (SPA_OPT_PRIO=-1): busy-union vs summed kernel time per arm
