@@ -138,11 +138,15 @@ validate)
   tail -2 ${O}_pytest.log
   run 180 ${O}_smoke.log python -c "import __graft_entry__ as g; g.smoke()"
   tail -1 ${O}_smoke.log
-  run 600 ${O}_bench.log python -u bench.py --steps 6 --warmup 2
+  # the driver's headline window (20 timed steps), secondary benches over >= 10 steps
+  run 600 ${O}_bench.log python -u bench.py --steps 20 --warmup 3
   run 300 ${O}_vit.log python -u bench/vit_train.py --steps 20 --warmup 5
-  run 300 ${O}_dsv3s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 4 --warmup 2
-  run 400 ${O}_gemma.log python -u bench/gemma_tp.py --layers 28 --steps 3 --warmup 1
-  jsonl ${O}_bench.log ${O}_vit.log ${O}_dsv3s.log ${O}_gemma.log ;;
+  run 300 ${O}_dsv3s.log python -u bench/dsv3_train.py --preset dsv3_style --steps 10 --warmup 2
+  V3="--preset dsv3_v3 --layers 4 --dense-layers 1 --experts 32 --mb 1 --accum 4 --steps 10 --warmup 1"
+  run 300 ${O}_v3.log python -u bench/dsv3_train.py $V3
+  run 300 ${O}_v3fp8.log python -u bench/dsv3_train.py $V3 --fp8
+  run 400 ${O}_gemma.log python -u bench/gemma_tp.py --layers 28 --steps 10 --warmup 1
+  jsonl ${O}_bench.log ${O}_vit.log ${O}_dsv3s.log ${O}_v3.log ${O}_v3fp8.log ${O}_gemma.log ;;
 headline-prof)
   run 400 ${O}.log rocprofv3 --kernel-trace --stats -d /tmp/$task -o run -- python3 bench.py --steps 2 --warmup 1
   jsonl ${O}.log
