@@ -72,6 +72,11 @@ def cases():
     gr = torch.full((n,), 1e-3, device=DEV, dtype=BF)
     out["adamw_268M"] = (lambda: optim_kernels.adamw_(p, mst, gr, m, v, 3e-4, 0.9, 0.95, 1e-8, 0.1, 1),
                          n * (2 + 2 + 3 * 4 * 2 + 2))
+    mb, vb = (torch.zeros(n, device=DEV, dtype=BF) for _ in range(2))   # bf16 moments (DeepSeek benches)
+    out["adamw_268M_bf16mom"] = (lambda: optim_kernels.adamw_(p, mst, gr, mb, vb, 3e-4, 0.9, 0.95, 1e-8, 0.1, 1),
+                                 n * (2 + 2 + 4 * 2 + 2 * 2 * 2))
+    out["sqsum_268M_bf16"] = (lambda: optim_kernels.sqsum(gr),
+                              n * 2)
     s, t = rn(16384, 1000, dtype=torch.float32), rn(16384, 1000, dtype=torch.float32)
     y = torch.randint(0, 1000, (16384,), device=DEV, generator=g)
     out["kd_loss_16384x1000"] = (lambda: misc.distillation_loss(s, t, y, 7.0, 0.3), 2 * 16384 * 1000 * 4)
