@@ -135,14 +135,16 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 }
 
 static int opt_grid(long n) { return (int)std::max<long>(1, std::min<long>((n / 8 + 255) / 256 + 1, 4096)); }
-// Grid of the streaming optimizer kernels (the env var named overrides the block count for A/Bs).
-// In isolation one 4-wave block per CU runs AdamW with bf16 moments 20 % faster (5.40 vs 4.48 TB/s,
-// profiles/r6_adamw_grid.txt), but in a training step the overlapped optimizer then holds every CU
-// for the whole bucket and the next forward's kernels queue behind it: dsv3_style 57.1K vs 65.0K
-// tok/s. The many-block grid lets the forward's blocks in as AdamW blocks retire, so it stays.
+// Grid of AdamW (SPA_ADAMW_GRID overrides the block count for A/Bs): one 8-element vector per thread,
+// no grid stride. The overlapped optimizer shares the GPU with the next step's forward, and short
+// blocks let the forward's kernels in as they retire: dsv3_style +0.6 % (65.3K vs 64.9K tok/s B N N B),
+// headline and Gemma-7B even. In isolation one 4-wave block per CU runs bf16-moment AdamW 20 % faster
+// (5.40 vs 4.48 TB/s), but in the step it holds every CU for a whole bucket: dsv3_style 57.1K vs 65.0K
+// (profiles/r6_adamw_grid.txt).
 static int stream_grid(long n, const char* env) {
   const char* e = getenv(env);
-  return e ? std::min(std::max(1, atoi(e)), opt_grid(n)) : opt_grid(n);
+  const long full = std::min<long>((n / 8 + 255) / 256 + 1, 1L << 30);   // one 8-element vector per thread
+  return (int)(e ? std::min<long>(std::max(1, atoi(e)), full) : full);
 }
 
 void adamw_(const at::Tensor& p, const c10::optional<at::Tensor>& master, const at::Tensor& g, const at::Tensor& m,
