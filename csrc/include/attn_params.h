@@ -81,15 +81,17 @@ __device__ __forceinline__ int ds_slot(int s, int h, int k) { return (k >> 2) * 
 
 // dK^T / dV^T accumulator (rows d = 32dt + (r&3) + 8(r>>2) + 4hh, column = key) -> global:
 // bf16 (dk scaled) when the block owns all q-heads of its kv-head, else fp32 partials.
-template <int HD>
-__device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 (&acc)[HD / 32], bool is_k,
-                                              int b, int hk, int key, int split, int hh) {
+// NDT < HD / 32: the accumulator holds the 32-dim tiles dt0 .. dt0 + NDT - 1 only (a role's share).
+template <int HD, int NDT = HD / 32>
+__device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 (&acc)[NDT], bool is_k,
+                                              int b, int hk, int key, int split, int hh, int dt0 = 0) {
   if (key >= p.Tk) return;
   if (!(SPA_DBG_BRH(b, key, p.Tk, hk, p.Hkv) & SPA_DBG_OK(split, p.hsplit))) return;
-  constexpr int DT = HD / 32;
+  static_assert(NDT <= HD / 32, "store_kv_grad: more tiles than the head dim");
+  constexpr int DT = NDT;
   if (p.hsplit == 1) {
-    bf16* dst = is_k ? p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh
-                     : p.dv + b * p.sdvb + (long)key * p.sdvt + hk * p.sdvh;
+    bf16* dst = (is_k ? p.dk + b * p.sdkb + (long)key * p.sdkt + hk * p.sdkh
+                      : p.dv + b * p.sdvb + (long)key * p.sdvt + hk * p.sdvh) + 32 * dt0;
     const float sc = is_k ? p.scale : 1.f;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -102,7 +104,7 @@ __device__ __forceinline__ void store_kv_grad(const AttnParams& p, const f32x16 
       }
   } else {
     float* dst = (is_k ? p.dkacc : p.dvacc) +
-                 ((((long)split * p.B + b) * p.Tk + key) * p.Hkv + hk) * HD;
+                 ((((long)split * p.B + b) * p.Tk + key) * p.Hkv + hk) * HD + 32 * dt0;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll

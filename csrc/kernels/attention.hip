@@ -1108,11 +1108,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 // HDK != HDV (MLA's q/k 192, v 128): role A's fragments / accumulator span HDK / HDV and role B's
 // HDV / HDK; the Q and dO images keep their own widths; 32-query intervals (MT = 1) past head dim
 // 128, where a 3-deep ring of 64-query tiles would not fit the LDS.
-template <int HDK, int HDV, bool CAUSAL, bool DSOUT = false>
+// DVS (head dim 256, Gemma MQA; with DSOUT): no dK here -- dK = dS^T Q is its own streaming pass over
+// the stored dS (attn_bwd_dk_ds256_kernel) -- and the dV^T accumulator is split between the roles:
+// role A: K fragments + dV^T dims 0..127 (S 16 MFMAs + dV 8 per interval), role B: V fragments +
+// dV^T dims 128..255 (dP 16 + dV 8). 64 fragment + 64 accumulator registers per role, where one
+// role of the full kernel (fragments + a 256-dim accumulator) spilled 103-130 dwords at 2 waves/SIMD.
+template <int HDK, int HDV, bool CAUSAL, bool DSOUT = false, bool DVS = false>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
+  static_assert(!DVS || (DSOUT && HDK == HDV), "dkdv3 DVS: the dS-materialising square-head form only");
   constexpr int MT = (HDK > 128 || HDV > 128) ? 1 : 2, BMQ = 32 * MT, BNK = 128, NT = 512;
   constexpr int KSK = HDK / 16, KSV = HDV / 16, DTK = HDK / 32, DTV = HDV / 32;
-  constexpr int KSX = KSK > KSV ? KSK : KSV, DTX = DTK > DTV ? DTK : DTV;
+  constexpr int KSX = KSK > KSV ? KSK : KSV, DTX = DVS ? DTV / 2 : (DTK > DTV ? DTK : DTV);
   constexpr int IWK = img_w<HDK>(), IWV = img_w<HDV>();
   constexpr int TQ = BMQ * IWK, TB = TQ + BMQ * IWV, PSLOT = 4 * MT * 2 * 64 * 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[3 * TB];     // [ring][Q | dO]
@@ -1149,7 +1155,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
 #pragma unroll
     for (int s = 0; s < KSX; ++s) xf[s] = kvalid && s < nks ? *reinterpret_cast<const bf16x8*>(xp + 16 * s) : zero8();
   }
-  f32x16 acc[DTX];  // A: dV^T (DTV), B: dK^T (DTK)
+  f32x16 acc[DTX];  // A: dV^T (DTV), B: dK^T (DTK); DVS: A / B dV^T dims 0.. / HDV/2.. (DTV/2 each)
 #pragma unroll
   for (int i = 0; i < DTX; ++i) acc[i] = splat16(0.f);
 
@@ -1233,11 +1239,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 0) * 512);
           const bf16x8 pb = *reinterpret_cast<const bf16x8*>(pr + (t * 2 + 1) * 512);
 #pragma unroll
-          for (int dt = 0; dt < DTV; ++dt) {
+          for (int dt = 0; dt < (DVS ? DTX : DTV); ++dt) {
             acc[dt] = mfma32(ld_tr(Dp + 32 * t * IWV, offv.tra[dt], offv.trb[dt]), pa, acc[dt]);
             acc[dt] = mfma32(ld_tr(Dp + (32 * t + 16) * IWV, offv.tra[dt], offv.trb[dt]), pb, acc[dt]);
           }
-          if (DKDV3_SCHED) chain_sched<2 * DTV, 2, 2, 2>();
+          if (DKDV3_SCHED || DVS) chain_sched<2 * (DVS ? DTX : DTV), 2, 2, 2>();
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -1323,12 +1329,21 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
         DK3_TICK(1);
+        if constexpr (DVS) {   // dV^T dims HDV/2.. += dO(k-1)^T P(k-1) (role A holds dims 0..)
 #pragma unroll
-        for (int dt = 0; dt < DTK; ++dt) {
-          acc[dt] = mfma32(ld_tr(Qp + 32 * t * IWK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
-          acc[dt] = mfma32(ld_tr(Qp + (32 * t + 16) * IWK, offk.tra[dt], offk.trb[dt]), sb, acc[dt]);
+          for (int dt = 0; dt < DTX; ++dt) {
+            acc[dt] = mfma32(ld_tr(Dpr + 32 * t * IWV, offv.tra[DTX + dt], offv.trb[DTX + dt]), pa, acc[dt]);
+            acc[dt] = mfma32(ld_tr(Dpr + (32 * t + 16) * IWV, offv.tra[DTX + dt], offv.trb[DTX + dt]), pb, acc[dt]);
+          }
+          chain_sched<2 * DTX, 2, 2>();
+        } else {
+#pragma unroll
+          for (int dt = 0; dt < DTK; ++dt) {
+            acc[dt] = mfma32(ld_tr(Qp + 32 * t * IWK, offk.tra[dt], offk.trb[dt]), sa, acc[dt]);
+            acc[dt] = mfma32(ld_tr(Qp + (32 * t + 16) * IWK, offk.tra[dt], offk.trb[dt]), sb, acc[dt]);
+          }
+          if (DKDV3_SCHED) chain_sched<2 * DTK, 2, 2, 2>();  // + the P(k-1) reads
         }
-        if (DKDV3_SCHED) chain_sched<2 * DTK, 2, 2, 2>();  // + the P(k-1) reads
         __builtin_amdgcn_sched_barrier(0);
         DK3_TICK(2);
       }
@@ -1355,7 +1370,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
       if (k + 2 <= total) interval(k + 2, IC<2>{}, IC<1>{});
     }
   }
-  if constexpr (HDK == HDV) {
+  if constexpr (DVS) {
+    store_kv_grad<HDV>(p, acc, false, b, hk, key, split, hh, role * DTX);
+  } else if constexpr (HDK == HDV) {
     store_kv_grad<HDK>(p, acc, role == 1, b, hk, key, split, hh);
   } else {
     if (role == 1) {
@@ -1653,6 +1670,109 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds256_kernel(AttnParams p)
       for (int i = 0; i < 4; ++i) wv[i] = (bf16)(acc[dt][4 * gq + i] * p.scale);
       *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * gq + 4 * hh) = wv;
     }
+}
+
+// Backward dK from the materialised dS at head dim 256 (after attn_bwd_dkdv3_kernel<256, 256, .., DSOUT,
+// DVS>, whose two roles keep only dV^T):  dK^T[d][key] = sum_q Q^T[d][q] dS[q][key].
+// Key-parallel like the dK/dV kernels: block = 4 waves x 32 keys (128 keys), the same (q-head, 32-query
+// tile) iteration space and q-head split (hsplit shares, fp32 partials summed by attn_kv_reduce_kernel),
+// so dK sums its products in the single-wave kernel's order. Per step the block DMAs the step's 32 x 256
+// Q tile (16 KiB, a quarter per wave: four 1 KiB pieces) and each wave its own 2 KiB dS block straight
+// into LDS -- 6 DMAs per wave per step, the vmcnt(6) discipline of the dQ pass, 3
+// slots of 24 KiB, two blocks per CU. dS comes out of the ds_slot image as the MFMA's B operand with a
+// plain 16-B read (the slot of (half s, lane half hh, key) IS the dK/dV kernel's packed accumulator),
+// Q^T with the transposed reads of the swizzled Q image.
+template <bool CAUSAL, bool NT>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dk_ds256_kernel(AttnParams p) {
+  constexpr int HD = 256, DT = HD / 32, BNK = 128, QIMG = 32 * HD, WSLOT = 1024, SLOT = QIMG + 4 * WSLOT, NSLOT = 3;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSLOT * SLOT];   // [slot][Q | 4 waves x 1 dS block]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, lk = lane & 31;
+  const int nbh = p.Hkv * p.B;
+  const int bh = blockIdx.x % nbh;
+  const int rest = blockIdx.x / nbh;   // causal: low key blocks are heaviest, launched first
+  const int split = rest % p.hsplit, kb = rest / p.hsplit;
+  const int hk = bh % p.Hkv, b = bh / p.Hkv;
+  SPA_DBG_CHECK(b, p.B);
+  SPA_DBG_CHECK(split, p.hsplit);
+  const int G = p.H / p.Hkv;
+  const int h0 = hk * G;
+  const int kt = kb * (BNK / 32) + wave;   // this wave's 32-key tile
+  const int key = kt * 32 + lk;
+  const int qstart = CAUSAL ? max(0, kb * BNK - p.causal_off) : 0;
+  const int t0 = qstart / 32;
+  const int ntq = p.Tq > 0 ? cdiv(p.Tq, 32) : 0;
+  const int nper = ntq - t0 > 0 ? ntq - t0 : 0;
+  const int tot_all = nper * G;
+  const int iper = cdiv(tot_all, p.hsplit);
+  const int ib = min(tot_all, split * iper);
+  const int nsteps = min(tot_all, ib + iper) - ib;
+
+  // Q tile DMA: wave `wave` fills rows 8*wave .. +7 (four 1 KiB pieces of 2 rows); lane -> row
+  // r = 8*wave + 2j + lane/32, image chunk lane%32 holding source chunk (lane%32) ^ swz(r)
+  unsigned qvo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 8 * wave + 2 * j + (lane >> 5);
+    qvo[j] = (unsigned)(((long)r * p.sqt + 8 * ((lane & 31) ^ swz<HD>(r))) * 2);
+  }
+  const bf16* dskv = p.dsbuf + ((long)b * p.Hkv + hk) * p.ds_kvstride;
+  auto live = [&](int tq) { return kt < p.ds_nkt && tq < p.ds_nqt && (!CAUSAL || kt <= tq); };
+  auto issue = [&](int j, int slot) {
+    bf16* sl = smem + slot * SLOT;
+    const int it = ib + j, g = it / nper, tq = t0 + it % nper;
+    const int q0 = 32 * tq;
+    const long qbytes = q0 < p.Tq ? ((long)(p.Tq - q0 - 1) * p.sqt + HD) * 2 : 0;
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.q + b * p.sqb + (h0 + g) * p.sqh + (long)q0 * p.sqt), 0, (int)min(qbytes, 0x7fffffffL), 0x00020000);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) dma16_asm(rq, qvo[jj], lds_addr(sl + (8 * wave + 2 * jj) * HD));
+    const bool lv = live(tq);
+    if (lv) SPA_DBG_CHECK(ds_index(tq, kt, g, G, p.ds_nkt, CAUSAL), p.ds_kvstride / 1024);
+    const bf16* src = lv ? dskv + ds_index(tq, kt, g, G, p.ds_nkt, CAUSAL) * 1024 : p.dsbuf;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, lv ? 2048 : 0, 0x00020000);
+    bf16* dst = sl + QIMG + wave * WSLOT;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) dma16_asm<NT>(rd, (unsigned)(lane * 16 + jj * 1024), lds_addr(dst + jj * 512));
+  };
+  LdsOff<HD> off;
+  off.init(lane);
+  const int dso0 = 8 * ds_slot(0, hh, lk);   // elements; half s = 1 is 8 slots on (+64 elements)
+  f32x16 acc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) acc[i] = splat16(0.f);
+
+  auto compute = [&](int j, const bf16* sl) {
+    const int it = ib + j;
+    if (!live(t0 + it % nper)) return;
+    const bf16* Qs = sl;
+    const bf16* Dw = sl + QIMG + wave * WSLOT;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 d0 = ld_row(Dw, dso0 + 64 * s);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma32(ld_tr(Qs + 16 * s * HD, off.tra[dt], off.trb[dt]), d0, acc[dt]);
+      chain_sched<DT, 2, 2, 1>();
+    }
+  };
+  if (nsteps > 0) issue(0, 0);
+  if (nsteps > 1) issue(1, 1);
+  for (int j = 0; j < nsteps; j += 3) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int jj = j + r;
+      if (jj < nsteps) {
+        if (jj + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // step jj landed, jj+1 in flight
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step jj-1's LDS reads done before its slot is restaged
+        __builtin_amdgcn_s_barrier();
+        if (jj + 2 < nsteps) issue(jj + 2, (r + 2) % 3);
+        compute(jj, smem + r * SLOT);
+      }
+    }
+  }
+  store_kv_grad<HD>(p, acc, true, b, hk, key, split, hh);
 }
 
 // sum the q-head-split fp32 partials of ONE tensor (dK with HD = HDK, or dV with HD = HDV)
@@ -1970,7 +2090,37 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
       // MLA without a head split: the paired, pipelined dK/dV kernel (role A: K fragments + dV^T,
       // role B: V fragments + dK^T, 2 waves per SIMD); SPA_ATTN_DKDV_MLA=1 (per call) keeps the
       // single-wave kernel (both accumulator sets in one wave, 1 wave per SIMD)
-      bool paired_mla = false;
+      bool paired_mla = false, dvs = false;
+      AttnParams pk = p;   // dvs: the dK pass with its own q-head split
+      at::Tensor dkpart;
+      if constexpr (HDK == 256 && HDV == 256) {
+        // Gemma: the paired dK/dV kernel with the dV^T accumulator split over its roles (2 waves per
+        // SIMD), then dK = dS^T Q streamed from the stored dS beside the dQ pass; needs whole q-heads
+        // per split. SPA_ATTN_DKDV256=0 (per call) keeps the single-wave kernel (dK + dV, 1 wave/SIMD)
+        const char* ve = getenv("SPA_ATTN_DKDV256");
+        dvs = !(ve && atoi(ve) == 0) && G % p.hsplit == 0;
+        if (dvs) {
+          if (causal) attn_bwd_dkdv3_kernel<HDK, HDV, true, true, true><<<g2, 512, 0, st>>>(p);
+          else attn_bwd_dkdv3_kernel<HDK, HDV, false, true, true><<<g2, 512, 0, st>>>(p);
+          // the dK pass runs two blocks per CU, all of one round at Gemma's 512 blocks: the causal
+          // key blocks' unequal work (key block 0 sees every query tile, the last one 4) then set its
+          // time (0.427 ms, 645 TF). Finer q-head shares (>= 1024 blocks, heaviest launched first)
+          // let the light blocks fill in behind the heavy ones
+          int hs2 = p.hsplit;
+          while (nkv * hs2 < 1024 && hs2 < G) {
+            int d = hs2 + 1;
+            while (G % d) ++d;
+            hs2 = d;
+          }
+          pk.hsplit = hs2;
+          if (hs2 > 1) {
+            dkpart = at::empty({(long)hs2 * p.B * p.Tk * p.Hkv * HDK}, bf16_opts.dtype(at::kFloat));
+            pk.dkacc = dkpart.data_ptr<float>();
+          }
+          if (causal) attn_bwd_dk_ds256_kernel<true, true><<<nkv * hs2, 256, 0, st>>>(pk);
+          else attn_bwd_dk_ds256_kernel<false, true><<<nkv * hs2, 256, 0, st>>>(pk);
+        }
+      }
       if constexpr (HDK == 192 && HDV == 128) {
         const char* me = getenv("SPA_ATTN_DKDV_MLA");
         paired_mla = p.hsplit == 1 && !(me && atoi(me) == 1);
@@ -1979,7 +2129,7 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
           else attn_bwd_dkdv3_kernel<HDK, HDV, false, true><<<g2, 512, 0, st>>>(p);
         }
       }
-      if (!paired_mla) {
+      if (!paired_mla && !dvs) {
         if (causal) attn_bwd_dkdv_kernel<HDK, HDV, true, 1, false, false, true><<<g2, 256, 0, st>>>(p);
         else attn_bwd_dkdv_kernel<HDK, HDV, false, 1, false, false, true><<<g2, 256, 0, st>>>(p);
       }
@@ -1992,11 +2142,11 @@ static void launch_bwd(AttnParams& p, bool causal, bool fused, int dkdv_mode, in
         if (causal) attn_bwd_dq_ds256_kernel<HDK, true, false><<<wg, 256, 0, st>>>(p);
         else attn_bwd_dq_ds256_kernel<HDK, false, false><<<wg, 256, 0, st>>>(p);
       }
-      if (p.hsplit > 1) {
-        const long kr = (long)p.B * p.Tk * p.Hkv;
-        attn_kv_reduce_kernel<HDK><<<(int)std::min<long>((kr * (HDK / 8) + 255) / 256, 65536), 256, 0, st>>>(p, 1);
+      const long kr = (long)p.B * p.Tk * p.Hkv;
+      if ((dvs ? pk : p).hsplit > 1)
+        attn_kv_reduce_kernel<HDK><<<(int)std::min<long>((kr * (HDK / 8) + 255) / 256, 65536), 256, 0, st>>>(dvs ? pk : p, 1);
+      if (p.hsplit > 1)
         attn_kv_reduce_kernel<HDV><<<(int)std::min<long>((kr * (HDV / 8) + 255) / 256, 65536), 256, 0, st>>>(p, 0);
-      }
       return;
     }
   }

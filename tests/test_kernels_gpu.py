@@ -428,6 +428,7 @@ def test_flash_attention(B, Tq, Tk, H, Hkv, hd, causal):
     (1, 1024, 2, 1, True, 256),     # its TP=8 rank (dK/dV iteration split)
     (2, 200, 4, 2, True, 256),      # ragged tail
     (1, 300, 3, 1, False, 256),     # non-causal, G = 3 (units span two query tiles per block)
+    (4, 2048, 8, 8, True, 256),     # hd 256 with >= 512 key blocks: no q-head split (bf16 dK / dV stores)
     (1, 1024, 8, 8, True, (192, 128)),   # MLA (q/k 128 nope + 64 rope, v 128)
     (2, 200, 4, 4, True, (192, 128)),    # MLA, ragged tail
     (1, 300, 2, 2, False, (192, 128)),   # MLA, non-causal
@@ -448,13 +449,15 @@ def test_attn_bwd_ds_path(B, T, H, Hkv, causal, hd, monkeypatch):
     out, lse = _ext.ops().attn_fwd(q, k, v, sc, causal)
     do = torch.randn_like(out)
     grads = {}
-    extra = ("mla1",) if hdv != hd else ("v3",) if hd == 128 else ()
+    extra = ("mla1",) if hdv != hd else ("v3",) if hd == 128 else ("s1",)
     for mode in ("2", "0") + extra:   # 2: the dS path whatever the grid size
         if mode == "mla1":     # MLA dS path with the single-wave dK/dV kernel instead of the paired one
             monkeypatch.setenv("SPA_ATTN_DKDV_MLA", "1")
         if mode == "v3":       # hd 128: dkdv3 (register-staged) instead of the default dkdv5 (LDS-DMA staged)
             monkeypatch.setenv("SPA_ATTN_DKDV5", "0")
-        monkeypatch.setenv("SPA_ATTN_DQ_DS", "2" if mode in ("mla1", "v3") else mode)
+        if mode == "s1":       # hd 256: the single-wave dK/dV kernel instead of the paired dV-split one + dK pass
+            monkeypatch.setenv("SPA_ATTN_DKDV256", "0")
+        monkeypatch.setenv("SPA_ATTN_DQ_DS", "2" if mode in ("mla1", "v3", "s1") else mode)
         dq, dk, dv = torch.full_like(q, float("nan")), torch.empty_like(k), torch.empty_like(v)
         _ext.ops().attn_bwd(do, q, k, v, out, lse, dq, dk, dv, sc, causal)
         torch.cuda.synchronize()
