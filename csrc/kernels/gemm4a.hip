@@ -255,6 +255,24 @@ __device__ __forceinline__ void g4_epilogue(f32x4 (&acc)[8][8], char* smem, bf16
     return;
   }
   // ---- epilogue: C^T fragments -> padded bf16 row image [256][256] in LDS -> 16-B global stores
+  // accumulate: this thread's 32 old C chunks are requested first (128 VGPRs, free once the main
+  // loop is done), so their latency hides under the image build and its barrier; read inside the
+  // store loop they cost one memory round trip per unrolled group of 4 (8 per tile), which at the
+  // expert dW's ~768-deep reductions was as long as a third of the tile's MFMA work
+  bf16x8 old[32];
+  if (accumulate) {
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
+      const long gmr = m0 + r;
+      const long gn = n0 + ch * 8;
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = (bf16)0.f;
+      if (gmr < rowlim && gn < N) o = *reinterpret_cast<const bf16x8*>(Cp + gmr * ldc + gn);
+      old[c] = o;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -268,21 +286,29 @@ __device__ __forceinline__ void g4_epilogue(f32x4 (&acc)[8][8], char* smem, bf16
       *reinterpret_cast<bf16x4*>(smem + r * ERS + cn * 2) = w4;
     }
   __syncthreads();
+  if (accumulate) {
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
+      const long gmr = m0 + r;
+      const long gn = n0 + ch * 8;
+      if (gmr < rowlim && gn < N && SPA_DBG_OK(gmr, MODE == 2 ? M : a_rows) & SPA_DBG_OK(gn + 7, ldc)) {
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * ERS + ch * 16);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)old[c][q]);
+        *reinterpret_cast<bf16x8*>(Cp + gmr * ldc + gn) = v;
+      }
+    }
+    return;
+  }
+  // write only: the round-5 loop (a fully unrolled one measured 5 % slower here)
 #pragma unroll 4
   for (int c = 0; c < 32; ++c) {
     const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
     const long gmr = m0 + r;
     const long gn = n0 + ch * 8;
-    if (gmr < rowlim && gn < N && SPA_DBG_OK(gmr, MODE == 2 ? M : a_rows) & SPA_DBG_OK(gn + 7, ldc)) {
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * ERS + ch * 16);
-      bf16* cp = Cp + gmr * ldc + gn;
-      if (accumulate) {
-        const bf16x8 o = *reinterpret_cast<const bf16x8*>(cp);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)o[q]);
-      }
-      *reinterpret_cast<bf16x8*>(cp) = v;
-    }
+    if (gmr < rowlim && gn < N && SPA_DBG_OK(gmr, MODE == 2 ? M : a_rows) & SPA_DBG_OK(gn + 7, ldc))
+      *reinterpret_cast<bf16x8*>(Cp + gmr * ldc + gn) = *reinterpret_cast<const bf16x8*>(smem + r * ERS + ch * 16);
   }
 }
 
