@@ -437,6 +437,23 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
   __syncthreads();
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
+    // accumulate: the half's 8 old chunks of this thread are requested before its image is built
+    // (the store loop's loads could not move above the stores before them -- the row stride is not a
+    // constant -- so each chunk paid a memory round trip; gemm4a.hip g4_epilogue, r6_gemm4_acc_epilogue)
+    bf16x8 old[8];
+    if (accumulate) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int idx = tid + c * NT, r = idx >> 5, ch = idx & 31;
+        const long gm = m0 + mh * 128 + r;
+        const int gn = n0 + ch * 8;
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = (bf16)0.f;
+        if (gm < mlim && gn < N) o = *reinterpret_cast<const bf16x8*>(Cb + gm * N + gn);
+        old[c] = o;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -461,9 +478,8 @@ __global__ __launch_bounds__(512, 1) void gemm8_fp8_kernel(const uint8_t* __rest
         bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * RS + ch * 16);
         bf16* cp = Cb + gm * N + gn;
         if (accumulate) {
-          const bf16x8 old = *reinterpret_cast<const bf16x8*>(cp);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)old[q]);
+          for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)old[c][q]);
         }
         *reinterpret_cast<bf16x8*>(cp) = v;
       }
