@@ -1083,6 +1083,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 #ifndef DKDV3_SCHED
 #define DKDV3_SCHED 0   // 1: chain_sched hints (no effect at 256 VGPRs: one operand register quad; kept for experiments)
 #endif
+#ifndef DKDV3_DVS_SCHED
+#define DKDV3_DVS_SCHED 1   // DVS (hd 256): chain_sched on both roles' dV^T chains
+#endif
 // SPA_DKDV3_STAMP=1 (a profiling build, never the shipped one: each s_memtime read drains the
 // LDS counter): per-wave s_memtime segment sums of the interval loop into p.stamp when the host
 // sets it (SPA_ATTN_STAMP=1), [blocks * 8 waves, 8] int64: staging, compute 1 (A: dV^T; B: dP,
@@ -1243,7 +1246,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
             acc[dt] = mfma32(ld_tr(Dp + 32 * t * IWV, offv.tra[dt], offv.trb[dt]), pa, acc[dt]);
             acc[dt] = mfma32(ld_tr(Dp + (32 * t + 16) * IWV, offv.tra[dt], offv.trb[dt]), pb, acc[dt]);
           }
-          if (DKDV3_SCHED || DVS) chain_sched<2 * (DVS ? DTX : DTV), 2, 2, 2>();
+          if (DKDV3_SCHED || (DVS && DKDV3_DVS_SCHED)) chain_sched<2 * (DVS ? DTX : DTV), 2, 2, 2>();
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -1335,7 +1338,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv3_kernel(AttnParams p) {
             acc[dt] = mfma32(ld_tr(Dpr + 32 * t * IWV, offv.tra[DTX + dt], offv.trb[DTX + dt]), pa, acc[dt]);
             acc[dt] = mfma32(ld_tr(Dpr + (32 * t + 16) * IWV, offv.tra[DTX + dt], offv.trb[DTX + dt]), pb, acc[dt]);
           }
-          chain_sched<2 * DTX, 2, 2>();
+          if (DKDV3_DVS_SCHED) chain_sched<2 * DTX, 2, 2>();
         } else {
 #pragma unroll
           for (int dt = 0; dt < DTK; ++dt) {
@@ -2260,8 +2263,11 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   const int G = H / Hkv;
   const int nkv = cdiv(Tk, 128) * Hkv * B;
   int hsplit = 1;
+  // SPA_ATTN_KVBLOCKS (read per call, default 512): the dK/dV grid the q-head split aims for
+  const char* kbe = getenv("SPA_ATTN_KVBLOCKS");
+  const int kvblocks = kbe ? std::max(1, atoi(kbe)) : 512;
   if (!fused)
-    while (nkv * hsplit < 512 && hsplit < G) {
+    while (nkv * hsplit < kvblocks && hsplit < G) {
       int d = hsplit + 1;
       while (G % d) ++d;
       hsplit = d;
@@ -2270,7 +2276,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   // number of shares: past the q-heads (TP-sharded MQA: G = 2), split the q-tiles too
   const bool pairedk = HDK == HDV && HDK <= 128 && !drop && (dkdv_mode == 3 || (dkdv_mode == 0 && HDV == 128));
   if (!fused && !pairedk)
-    while (nkv * hsplit < 512 && hsplit < 16 && cdiv(Tq, 32) / (2 * hsplit) >= 4) hsplit *= 2;
+    while (nkv * hsplit < kvblocks && hsplit < 16 && cdiv(Tq, 32) / (2 * hsplit) >= 4) hsplit *= 2;
   p.hsplit = hsplit;
   // SPA_ATTN_STAMP=1: per-wave s_memtime segment sums of the pipelined dK/dV loop (in a build
   // with -DSPA_DKDV3_STAMP=1, tools/build_variant.sh), kept in a process-global buffer the
