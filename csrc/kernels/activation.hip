@@ -81,6 +81,83 @@ __global__ __launch_bounds__(256) void glu_bwd_kernel(const T* __restrict__ dy, 
   }
 }
 
+// glu_bwd that also writes the transposed gradient dgu^T [2F, M] (bf16): the weight gradient of the
+// [gate | up] projection is dW = dgu^T X, which hipBLASLt runs fastest with both operands
+// token-contiguous ("both" form, profiles/r6_wgrad_glu_t.txt); producing dgu^T here saves the
+// separate transpose's read of dgu. Block = 64 tokens x 64 features of F (gate and up halves):
+// 16-byte loads of gu / dy, dgu in fp32 -> bf16, stored row-major AND staged in two padded LDS
+// tiles whose columns leave as 16-byte runs of 8 tokens of dgu^T rows (f and F + f).
+template <int KIND>
+__global__ __launch_bounds__(256) void glu_bwd_t_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ gu,
+                                                        bf16* __restrict__ dgu, bf16* __restrict__ dgut, int M, int F) {
+  // block = 64 tokens x 128 features (256-B row segments per half on the read side, 128-B runs of
+  // dgu^T rows on the write side). LDS tiles [gate / up][token][feature], 272-B rows, the 16-B chunk
+  // index XOR-swizzled by the token row's 8-row group so the transposed phase's 8-byte reads (4
+  // features of one token) spread over the banks
+  constexpr int TT = 64, TF = 128, LD = TF + 8;
+  __shared__ __attribute__((aligned(16))) bf16 tile[2][TT * LD];
+  const int r0 = blockIdx.y * TT, f0 = blockIdx.x * TF;
+  auto soff = [](int r, int c16) { return r * LD + 8 * (c16 ^ ((r >> 3) & 7)); };
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {              // 64 tokens x 16 chunks of 8 features
+    const int idx = threadIdx.x + 256 * c, r = idx >> 4, ch = idx & 15;
+    const int m = r0 + r, f = f0 + ch * 8;
+    float g[8], u[8], d[8], dg[8], du[8];
+    const bool ok = m < M && f < F;
+    if (ok) {
+      load8(gu + (long)m * 2 * F + f, g);
+      load8(gu + (long)m * 2 * F + F + f, u);
+      load8(dy + (long)m * F + f, d);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      du[k] = ok ? d[k] * act_f(KIND, g[k], 0.f) : 0.f;
+      dg[k] = ok ? d[k] * u[k] * act_df(KIND, g[k], 0.f) : 0.f;
+    }
+    if (ok) {
+      store8(dgu + (long)m * 2 * F + f, dg);
+      store8(dgu + (long)m * 2 * F + F + f, du);
+    }
+    bf16x8 a8, b8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { a8[k] = (bf16)dg[k]; b8[k] = (bf16)du[k]; }
+    *reinterpret_cast<bf16x8*>(&tile[0][soff(r, ch)]) = a8;
+    *reinterpret_cast<bf16x8*>(&tile[1][soff(r, ch)]) = b8;
+  }
+  __syncthreads();
+  // jobs: half h, features 4 jq .. 4 jq + 3 (32 groups), tokens 8 ch .. 8 ch + 7 -> four 16-B runs of
+  // dgu^T rows each (8 x ds_read_b64 + 16 v_perm)
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int idx = threadIdx.x + 256 * c, h = idx >> 8, jq = (idx >> 3) & 31, ch = idx & 7;
+    uint2 rw[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int r = ch * 8 + e;
+      rw[e] = *reinterpret_cast<const uint2*>(&tile[h][soff(r, jq >> 1) + 4 * (jq & 1)]);
+    }
+    const int m = r0 + ch * 8;
+    if (m < M) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {         // feature 4 jq + q: 16-bit half (q & 1) of word (q >> 1)
+        const int f = f0 + 4 * jq + q;
+        if (f < F) {
+          const unsigned sel = (q & 1) ? 0x07060302u : 0x05040100u;   // high / low halves of (b, a)
+          unsigned w[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] = (q >> 1) ? rw[e].y : rw[e].x;
+          uint4 o;
+          o.x = __builtin_amdgcn_perm(w[1], w[0], sel);
+          o.y = __builtin_amdgcn_perm(w[3], w[2], sel);
+          o.z = __builtin_amdgcn_perm(w[5], w[4], sel);
+          o.w = __builtin_amdgcn_perm(w[7], w[6], sel);
+          *reinterpret_cast<uint4*>(dgut + (long)(h * F + f) * M + m) = o;
+        }
+      }
+    }
+  }
+}
+
 // Backward of act(u) fused with the bias gradient of the Linear that produced u: dU = dY * act'(u)
 // is written AND summed over rows (the bias gradient is colsum(dU)), so dU is not read a second
 // time. Layout of rowsum_part_kernel (norm.hip): block (bx, by) covers 256 columns x rows
@@ -251,9 +328,31 @@ at::Tensor glu_bwd(const at::Tensor& dy_, const at::Tensor& gu_, int64_t kind) {
   return dgu;
 }
 
+// (dgu [.., 2F], dgu^T [2F, M]) -- see glu_bwd_t_kernel; bf16, M % 8 == 0 and F % 8 == 0
+std::vector<at::Tensor> glu_bwd_t(const at::Tensor& dy_, const at::Tensor& gu_, int64_t kind) {
+  auto gu = gu_.contiguous();
+  auto dy = dy_.contiguous();
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "glu_bwd_t: bf16");
+  const int F2 = gu.size(-1), F = F2 / 2;
+  const long M = gu.numel() / F2;
+  TORCH_CHECK(dy.numel() == M * F, "glu_bwd_t: dy must be [.., F]");
+  TORCH_CHECK(M % 8 == 0 && F % 8 == 0 && M < (1L << 31) && (long)F2 * M < (1L << 40), "glu_bwd_t: M, F % 8");
+  auto dgu = at::empty_like(gu);
+  auto dgut = at::empty({F2, M}, gu.options());
+  if (M == 0) return {dgu, dgut};
+  DeviceGuard g(gu.device());
+  const dim3 grid(cdiv(F, 128), (int)cdiv(M, 64L));
+  ACT_SWITCH(kind, glu_bwd_t_kernel<K_><<<grid, 256, 0, stream()>>>(
+                       (const bf16*)dy.data_ptr(), (const bf16*)gu.data_ptr(), (bf16*)dgu.data_ptr(),
+                       (bf16*)dgut.data_ptr(), (int)M, F));
+  SPA_LAUNCH_CHECK();
+  return {dgu, dgut};
+}
+
 }  // namespace spa
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
+  m.def("glu_bwd_t(Tensor dy, Tensor gu, int kind) -> Tensor[]");
   m.def("act_fwd(Tensor x, int kind, float alpha) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int kind, float alpha) -> Tensor");
   m.def("act_bwd_colsum(Tensor dy, Tensor u, int kind, float alpha) -> Tensor[]");
@@ -261,6 +360,7 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("glu_bwd(Tensor dy, Tensor gu, int kind) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
+  m.impl("glu_bwd_t", &spa::glu_bwd_t);
   m.impl("act_fwd", &spa::act_fwd);
   m.impl("act_bwd", &spa::act_bwd);
   m.impl("act_bwd_colsum", &spa::act_bwd_colsum);

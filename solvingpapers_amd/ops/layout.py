@@ -58,21 +58,24 @@ def wgrad8_ok(dy2: torch.Tensor, x2: torch.Tensor, out=None) -> bool:
             and (out is None or (out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32))))
 
 
-def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False, x2t=None):
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, accumulate=False, x2t=None, dyt=None):
     """dW = dy2^T @ x2 ([N, K] from [T, N] and [T, K]) into a fresh tensor, or written into /
     added to ``out`` (any float dtype, e.g. an fp32 main_grad). Many tokens with a narrow
     operand: wgrad8; else the narrower operand is transposed to token-contiguous rows first
-    when both are wide and T is large (x2t: x2 already transposed)."""
-    if wgrad8_ok(dy2, x2, out):
+    when both are wide and T is large (x2t: x2 already transposed). ``dyt``: dy2 already
+    transposed by its producer (linear.py linear_glu) -> the both-token-contiguous form."""
+    if dyt is None and wgrad8_ok(dy2, x2, out):
         return _ext.ops().wgrad8(dy2, x2, out, accumulate, 0)
     f32out = (out is not None and out.dtype == torch.float32 and dy2.dtype == torch.bfloat16 and dy2.is_cuda
               and out.is_contiguous() and _MM_F32[0] is not False)
     if out is not None and out.dtype != dy2.dtype and not f32out:
-        g = wgrad(dy2, x2, x2t=x2t)
+        g = wgrad(dy2, x2, x2t=x2t, dyt=dyt)
         out.add_(g) if accumulate else out.copy_(g)
         return out
     N, K = dy2.shape[1], x2.shape[1]
-    if wgrad_nt_ok(dy2, x2) and min(N, K) >= WGRAD_NT_MIN_WIDTH:
+    if dyt is not None:
+        a, b = dyt, (x2t if x2t is not None else transpose2d(x2)).t()
+    elif wgrad_nt_ok(dy2, x2) and min(N, K) >= WGRAD_NT_MIN_WIDTH:
         if K <= N:
             a, b = dy2.t(), (x2t if x2t is not None else transpose2d(x2)).t()
         else:

@@ -167,6 +167,48 @@ class _LinearActFn(torch.autograd.Function):
         return dx, gw, gb, None, None
 
 
+class _LinearGluFn(torch.autograd.Function):
+    """glu(x W^T) for a row-stacked [gate ; up] weight (LLaMA's w13, llama3/LLaMA-jax.ipynb:854-855).
+    Forward: one GEMM + the GLU kernel, as glu(linear(x, W)). Backward: the GLU backward also writes
+    the transposed gradient (activation.hip glu_bwd_t), so dW = dH^T X runs in hipBLASLt's fastest
+    form -- both operands token-contiguous -- without the separate transpose pass the plain path
+    spends on X (or dH); dX = dH W as in :class:`_LinearFn`."""
+
+    @staticmethod
+    def forward(ctx, x, w, kind):
+        x2 = x.reshape(-1, x.shape[-1])
+        h = torch.mm(x2, w.t())
+        f = _ext.ops().glu_fwd(h, kind)
+        ctx.save_for_backward(x, h)
+        ctx.w, ctx.kind = w, kind
+        return torch.ops.aten._unsafe_view(f, (*x.shape[:-1], w.shape[0] // 2))
+
+    @staticmethod
+    def backward(ctx, df):
+        x, h = ctx.saved_tensors
+        w = ctx.w
+        x2 = x.reshape(-1, x.shape[-1])
+        dh, dht = _ext.ops().glu_bwd_t(df.reshape(-1, df.shape[-1]), h, ctx.kind)
+        dx = dgrad(dh, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gw = commit(w, lambda out, acc: wgrad(dh, x2, out, acc, dyt=dht))
+        return dx, gw, None
+
+
+def linear_glu(x, w, kind="silu"):
+    """glu(linear(x, w), kind) -- on the GPU (bf16, many tokens, widths % 8; SPA_GLU_T=0, read per
+    call, keeps the plain composition) through :class:`_LinearGluFn`."""
+    from .activation import glu
+    from .reference import ACT_KINDS
+    T = x.numel() // x.shape[-1] if x.shape[-1] else 0
+    if (os.environ.get("SPA_GLU_T", "1") != "0" and x.is_cuda and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.dim() == 2 and w.shape[0] % 16 == 0 and x.shape[-1] % 8 == 0
+            and T >= 2048 and T % 8 == 0 and not torch.cuda.is_current_stream_capturing()):
+        return _LinearGluFn.apply(x, w, ACT_KINDS[kind])
+    return glu(linear(x, w), kind)
+
+
 def linear_act(x, w, b, kind="gelu", alpha=None):
     """act(linear(x, w, b)) with the activation backward and the bias gradient fused into one
     pass on the GPU (bf16, bias present, widths % 8); elsewhere the two ops in sequence."""

@@ -121,6 +121,52 @@ def test_mlp_matches_fp32(kind, R, D, F):
         assert rel(p_.grad, f_.grad) < 2e-2, p_.shape
 
 
+@pytest.mark.parametrize("M,F", [(1000, 200), (4096, 1024), (8, 8)])
+def test_glu_bwd_t_matches_glu_bwd(M, F):
+    """glu_bwd_t (the GLU backward that also writes dgu^T for the both-token-contiguous dW) == glu_bwd
+    bitwise, and its second output is exactly the transpose; ragged token / feature tiles."""
+    from solvingpapers_amd.ops import _ext
+    torch.manual_seed(8)
+    gu = torch.randn(M, 2 * F, device=DEV).bfloat16()
+    dy = torch.randn(M, F, device=DEV).bfloat16()
+    ref = _ext.ops().glu_bwd(dy, gu, 6)
+    dgu, dgut = _ext.ops().glu_bwd_t(dy, gu, 6)
+    torch.cuda.synchronize()
+    assert torch.equal(dgu, ref)
+    assert dgut.shape == (2 * F, M) and torch.equal(dgut, ref.t())
+
+
+@pytest.mark.parametrize("acc", [False, True])
+def test_linear_glu_matches_composition(acc, monkeypatch):
+    """ops.linear.linear_glu (glu_bwd_t + the both-transposed dW form) == glu(linear(x, w13)) on every
+    gradient (SPA_GLU_T=0 arm), into a flat bf16 main_grad with and without accumulation."""
+    import importlib
+    L = importlib.import_module("solvingpapers_amd.ops.linear")
+    T, D, F = 2048, 256, 512
+    torch.manual_seed(9)
+    x0 = (torch.randn(T, D, device=DEV) * 0.5).bfloat16()
+    w0 = (torch.randn(2 * F, D, device=DEV) * D ** -0.5).bfloat16()
+    g = torch.randn(T, F, device=DEV).bfloat16()
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SPA_GLU_T", mode)
+        x = x0.clone().requires_grad_()
+        w = w0.clone().requires_grad_()
+        w.main_grad = torch.full_like(w0, 0.25) if acc else torch.zeros_like(w0)
+        from solvingpapers_amd.utils.grad import _Gen
+        w._spa_gen = _Gen.value if acc else -1
+        y = L.linear_glu(x, w, "silu")
+        y.backward(g)
+        res[mode] = (y.detach(), x.grad, w.main_grad.clone())
+    assert torch.equal(res["1"][0], res["0"][0])
+    assert torch.equal(res["1"][1], res["0"][1])
+    assert rel(res["1"][2], res["0"][2]) < 1e-2, rel(res["1"][2], res["0"][2])
+    xf, wf = x0.float().requires_grad_(), w0.float().requires_grad_()
+    gate, up = (xf @ wf.t()).chunk(2, -1)
+    (torch.nn.functional.silu(gate) * up).backward(g.float())
+    assert rel(res["1"][2] - (0.25 if acc else 0.0), wf.grad) < 2e-2
+
+
 def R_act(x, kind):
     return R.act(x, kind, 0.0)
 

@@ -58,12 +58,19 @@ def main():
             "x": (lambda: torch.mm(dy.t(), xT.t(), out=out), lambda: transpose2d(x)),
             "direct": (lambda: torch.mm(dy.t(), x, out=out), None),
             "wgrad8": (lambda: _ext.ops().wgrad8(dy, x, out, False, 0), None),
+            # accumulating into the gradient (micro-batches 2.. of a step): out += ...
+            "both+a": (lambda: out.addmm_(dyT, xT.t()), lambda: (transpose2d(dy), transpose2d(x))),
+            "dy+a": (lambda: out.addmm_(dyT, x), lambda: transpose2d(dy)),
+            "x+a": (lambda: out.addmm_(dy.t(), xT.t()), lambda: transpose2d(x)),
+            "direct+a": (lambda: out.addmm_(dy.t(), x), None),
         }
 
         ref = torch.mm(dy.t(), x)
         for f, (g, tr) in forms.items():
             if tune:
                 print(f"  tuning {name}/{f} ...", flush=True)
+            if f.endswith("+a"):
+                out.zero_()
             g()
             assert torch.allclose(out.float(), ref.float(), atol=1e-1, rtol=2e-2), (name, f)
             tg = tm(g)
