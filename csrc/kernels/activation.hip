@@ -158,6 +158,60 @@ __global__ __launch_bounds__(256) void glu_bwd_t_kernel(const bf16* __restrict__
   }
 }
 
+// glu_fwd that also writes y^T [F, M] (bf16): the down projection's weight gradient dW2 = dY^T y then
+// runs in the both-token-contiguous form too (ops/linear.py swiglu_mlp keeps y^T instead of y for the
+// backward). Same tiling as glu_bwd_t: 64 tokens x 128 features, swizzled LDS tile, 8-byte reads + v_perm.
+template <int KIND>
+__global__ __launch_bounds__(256) void glu_fwd_t_kernel(const bf16* __restrict__ gu, bf16* __restrict__ y,
+                                                        bf16* __restrict__ yt, int M, int F) {
+  constexpr int TT = 64, TF = 128, LD = TF + 8;
+  __shared__ __attribute__((aligned(16))) bf16 tile[TT * LD];
+  const int r0 = blockIdx.y * TT, f0 = blockIdx.x * TF;
+  auto soff = [](int r, int c16) { return r * LD + 8 * (c16 ^ ((r >> 3) & 7)); };
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int idx = threadIdx.x + 256 * c, r = idx >> 4, ch = idx & 15;
+    const int m = r0 + r, f = f0 + ch * 8;
+    float g[8], u[8];
+    const bool ok = m < M && f < F;
+    if (ok) {
+      load8(gu + (long)m * 2 * F + f, g);
+      load8(gu + (long)m * 2 * F + F + f, u);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = ok ? act_f(KIND, g[k], 0.f) * u[k] : 0.f;
+    if (ok) store8(y + (long)m * F + f, g);
+    bf16x8 a8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a8[k] = (bf16)g[k];
+    *reinterpret_cast<bf16x8*>(&tile[soff(r, ch)]) = a8;
+  }
+  __syncthreads();
+  const int jq = threadIdx.x >> 3, ch = threadIdx.x & 7;   // features 4 jq .., tokens 8 ch ..
+  uint2 rw[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) rw[e] = *reinterpret_cast<const uint2*>(&tile[soff(ch * 8 + e, jq >> 1) + 4 * (jq & 1)]);
+  const int m = r0 + ch * 8;
+  if (m < M) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = f0 + 4 * jq + q;
+      if (f < F) {
+        const unsigned sel = (q & 1) ? 0x07060302u : 0x05040100u;
+        unsigned w[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = (q >> 1) ? rw[e].y : rw[e].x;
+        uint4 o;
+        o.x = __builtin_amdgcn_perm(w[1], w[0], sel);
+        o.y = __builtin_amdgcn_perm(w[3], w[2], sel);
+        o.z = __builtin_amdgcn_perm(w[5], w[4], sel);
+        o.w = __builtin_amdgcn_perm(w[7], w[6], sel);
+        *reinterpret_cast<uint4*>(yt + (long)f * M + m) = o;
+      }
+    }
+  }
+}
+
 // Backward of act(u) fused with the bias gradient of the Linear that produced u: dU = dY * act'(u)
 // is written AND summed over rows (the bias gradient is colsum(dU)), so dU is not read a second
 // time. Layout of rowsum_part_kernel (norm.hip): block (bx, by) covers 256 columns x rows
@@ -328,6 +382,26 @@ at::Tensor glu_bwd(const at::Tensor& dy_, const at::Tensor& gu_, int64_t kind) {
   return dgu;
 }
 
+// (y [.., F], y^T [F, M]) -- see glu_fwd_t_kernel; bf16, M % 8 == 0 and F % 8 == 0
+std::vector<at::Tensor> glu_fwd_t(const at::Tensor& gu_, int64_t kind) {
+  auto gu = gu_.contiguous();
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16, "glu_fwd_t: bf16");
+  const int F2 = gu.size(-1), F = F2 / 2;
+  const long M = gu.numel() / F2;
+  TORCH_CHECK(F2 % 16 == 0 && M % 8 == 0 && M < (1L << 31), "glu_fwd_t: M % 8, F % 8");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto y = at::empty(sizes, gu.options());
+  auto yt = at::empty({F, M}, gu.options());
+  if (M == 0) return {y, yt};
+  DeviceGuard g(gu.device());
+  const dim3 grid(cdiv(F, 128), (int)cdiv(M, 64L));
+  ACT_SWITCH(kind, glu_fwd_t_kernel<K_><<<grid, 256, 0, stream()>>>((const bf16*)gu.data_ptr(), (bf16*)y.data_ptr(),
+                                                                      (bf16*)yt.data_ptr(), (int)M, F));
+  SPA_LAUNCH_CHECK();
+  return {y, yt};
+}
+
 // (dgu [.., 2F], dgu^T [2F, M]) -- see glu_bwd_t_kernel; bf16, M % 8 == 0 and F % 8 == 0
 std::vector<at::Tensor> glu_bwd_t(const at::Tensor& dy_, const at::Tensor& gu_, int64_t kind) {
   auto gu = gu_.contiguous();
@@ -353,6 +427,7 @@ std::vector<at::Tensor> glu_bwd_t(const at::Tensor& dy_, const at::Tensor& gu_, 
 
 TORCH_LIBRARY_FRAGMENT(spa, m) {
   m.def("glu_bwd_t(Tensor dy, Tensor gu, int kind) -> Tensor[]");
+  m.def("glu_fwd_t(Tensor gu, int kind) -> Tensor[]");
   m.def("act_fwd(Tensor x, int kind, float alpha) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int kind, float alpha) -> Tensor");
   m.def("act_bwd_colsum(Tensor dy, Tensor u, int kind, float alpha) -> Tensor[]");
@@ -361,6 +436,7 @@ TORCH_LIBRARY_FRAGMENT(spa, m) {
 }
 TORCH_LIBRARY_IMPL(spa, CUDA, m) {
   m.impl("glu_bwd_t", &spa::glu_bwd_t);
+  m.impl("glu_fwd_t", &spa::glu_fwd_t);
   m.impl("act_fwd", &spa::act_fwd);
   m.impl("act_bwd", &spa::act_bwd);
   m.impl("act_bwd_colsum", &spa::act_bwd_colsum);

@@ -29,7 +29,7 @@ from ..infer.cache import KVCache
 from ..infer.graph import DecodeState
 from ..infer.sampling import sample  # noqa: F401  (re-exported: reference-style sampling)
 from ..ops import _ext, attention_packed, embedding, linear, linear_cross_entropy, rms_norm, rope_packed_
-from ..ops.linear import linear_glu
+from ..ops.linear import swiglu_mlp
 from ..ops.attention import decode_attention
 from ..ops.rope import RopeCache, apply_rope
 from ..utils.grad import mark_ready
@@ -152,8 +152,7 @@ class LlamaBlock(nn.Module):
             n1, h = rms_norm(delta, self.attention_norm, c.norm_eps, residual=res)
         a = self.attn(n1, kv_cache, pos)
         n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
-        f = linear_glu(n2, self.w13, "silu")
-        return h2, linear(f, self.w2)
+        return h2, swiglu_mlp(n2, self.w13, self.w2, "silu")
 
 
 class Llama3(nn.Module):

@@ -201,12 +201,66 @@ def linear_glu(x, w, kind="silu"):
     call, keeps the plain composition) through :class:`_LinearGluFn`."""
     from .activation import glu
     from .reference import ACT_KINDS
-    T = x.numel() // x.shape[-1] if x.shape[-1] else 0
-    if (os.environ.get("SPA_GLU_T", "1") != "0" and x.is_cuda and x.dtype == torch.bfloat16
-            and w.dtype == torch.bfloat16 and w.dim() == 2 and w.shape[0] % 16 == 0 and x.shape[-1] % 8 == 0
-            and T >= 2048 and T % 8 == 0 and not torch.cuda.is_current_stream_capturing()):
+    if _glu_t_mode() >= 1 and _glu_t_ok(x, w):
         return _LinearGluFn.apply(x, w, ACT_KINDS[kind])
     return glu(linear(x, w), kind)
+
+
+class _SwiGluMLPFn(torch.autograd.Function):
+    """w2(glu(x W13^T)) -- LLaMA's feed-forward (llama3/LLaMA-jax.ipynb:854-855) with both weight
+    gradients in hipBLASLt's both-token-contiguous form: the GLU forward also writes y^T (kept for
+    the backward instead of y) and the GLU backward writes dH^T (activation.hip glu_fwd_t /
+    glu_bwd_t); only dY of the down projection is transposed by a separate pass."""
+
+    @staticmethod
+    def forward(ctx, x, w13, w2, kind):
+        x2 = x.reshape(-1, x.shape[-1])
+        h = torch.mm(x2, w13.t())
+        f, ft = _ext.ops().glu_fwd_t(h, kind)
+        y = torch.mm(f, w2.t())
+        ctx.save_for_backward(x, h, ft)
+        ctx.w13, ctx.w2, ctx.kind = w13, w2, kind
+        return torch.ops.aten._unsafe_view(y, (*x.shape[:-1], w2.shape[0]))
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .layout import transpose2d
+        x, h, ft = ctx.saved_tensors
+        w13, w2 = ctx.w13, ctx.w2
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        need = ctx.needs_input_grad
+        dx = gw13 = gw2 = None
+        if need[2]:
+            dyt = transpose2d(dy2)
+            gw2 = commit(w2, lambda out, acc: wgrad(dy2, ft.t(), out, acc, x2t=ft, dyt=dyt))
+        dh, dht = _ext.ops().glu_bwd_t(dgrad(dy2, w2), h, ctx.kind)
+        if need[0]:
+            dx = dgrad(dh, w13).view(x.shape)
+        if need[1]:
+            gw13 = commit(w13, lambda out, acc: wgrad(dh, x2, out, acc, dyt=dht))
+        return dx, gw13, gw2, None
+
+
+def _glu_t_mode() -> int:
+    """SPA_GLU_T (read per call): 0 plain glu(linear(..)), 1 linear_glu only, 2 (default) swiglu_mlp."""
+    return int(os.environ.get("SPA_GLU_T", "2"))
+
+
+def _glu_t_ok(x, w) -> bool:
+    T = x.numel() // x.shape[-1] if x.shape[-1] else 0
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2
+            and w.shape[0] % 16 == 0 and x.shape[-1] % 8 == 0 and T >= 2048 and T % 8 == 0
+            and not torch.cuda.is_current_stream_capturing())
+
+
+def swiglu_mlp(x, w13, w2, kind="silu"):
+    """linear(glu(linear(x, w13), kind), w2) with the transposed-operand weight gradients of
+    :class:`_SwiGluMLPFn` where it applies (else linear_glu / the plain composition)."""
+    if _glu_t_mode() >= 2 and _glu_t_ok(x, w13) and w2.dtype == torch.bfloat16 and w2.dim() == 2:
+        from .reference import ACT_KINDS
+        return _SwiGluMLPFn.apply(x, w13, w2, ACT_KINDS[kind])
+    return linear(linear_glu(x, w13, kind), w2)
 
 
 def linear_act(x, w, b, kind="gelu", alpha=None):

@@ -167,6 +167,49 @@ def test_linear_glu_matches_composition(acc, monkeypatch):
     assert rel(res["1"][2] - (0.25 if acc else 0.0), wf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("M,F", [(1000, 200), (4096, 1024), (8, 8)])
+def test_glu_fwd_t_matches_glu_fwd(M, F):
+    """glu_fwd_t == glu_fwd bitwise, its second output exactly the transpose (ragged tiles)."""
+    from solvingpapers_amd.ops import _ext
+    torch.manual_seed(10)
+    gu = torch.randn(M, 2 * F, device=DEV).bfloat16()
+    ref = _ext.ops().glu_fwd(gu, 6)
+    y, yt = _ext.ops().glu_fwd_t(gu, 6)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref) and yt.shape == (F, M) and torch.equal(yt, ref.t())
+
+
+@pytest.mark.parametrize("acc", [False, True])
+def test_swiglu_mlp_matches_composition(acc, monkeypatch):
+    """ops.linear.swiglu_mlp (y^T kept from the forward, dH^T from the backward: both weight gradients
+    in the both-transposed form) == linear(glu(linear(x, w13)), w2) (SPA_GLU_T=0) on every output and
+    gradient, into flat bf16 main_grads with and without accumulation."""
+    import importlib
+    from solvingpapers_amd.utils.grad import _Gen
+    L = importlib.import_module("solvingpapers_amd.ops.linear")
+    T, D, F = 2048, 256, 512
+    torch.manual_seed(11)
+    x0 = (torch.randn(T, D, device=DEV) * 0.5).bfloat16()
+    w13_0 = (torch.randn(2 * F, D, device=DEV) * D ** -0.5).bfloat16()
+    w2_0 = (torch.randn(D, F, device=DEV) * F ** -0.5).bfloat16()
+    g = torch.randn(T, D, device=DEV).bfloat16()
+    res = {}
+    for mode in ("2", "0"):
+        monkeypatch.setenv("SPA_GLU_T", mode)
+        x = x0.clone().requires_grad_()
+        w13, w2 = w13_0.clone().requires_grad_(), w2_0.clone().requires_grad_()
+        for w in (w13, w2):
+            w.main_grad = torch.full_like(w, 0.25) if acc else torch.zeros_like(w)
+            w._spa_gen = _Gen.value if acc else -1
+        y = L.swiglu_mlp(x, w13, w2, "silu")
+        y.backward(g)
+        res[mode] = (y.detach(), x.grad, w13.main_grad.clone(), w2.main_grad.clone())
+    assert torch.equal(res["2"][0], res["0"][0])
+    assert rel(res["2"][1], res["0"][1]) < 1e-2
+    for i in (2, 3):
+        assert rel(res["2"][i], res["0"][i]) < 1e-2, (i, rel(res["2"][i], res["0"][i]))
+
+
 def R_act(x, kind):
     return R.act(x, kind, 0.0)
 
