@@ -28,6 +28,7 @@ import torch.nn as tnn
 from .. import nn as snn
 from ..infer.graph import DecodeState
 from ..ops import _ext, attention_packed, embedding, glu, linear, linear_cross_entropy, rms_norm, rope_packed_
+from ..ops.linear import swiglu_mlp
 from ..ops.attention import decode_attention, flash_attention
 from ..ops.linear import linear_rows
 from ..ops.misc import dropout
@@ -284,8 +285,7 @@ class GemmaBlock(tnn.Module):
             o = o.reshape(B, T, self.hl * hd)
         a = reduce_from_tp(linear(o, self.wo), tp_group)
         n2, h2 = rms_norm(a, self.ffn_norm, c.norm_eps, residual=h)
-        f = glu(linear(copy_to_tp(n2, tp_group), self.w13), "gelu_tanh")
-        return h2, reduce_from_tp(linear(f, self.w2), tp_group)
+        return h2, reduce_from_tp(swiglu_mlp(copy_to_tp(n2, tp_group), self.w13, self.w2, "gelu_tanh"), tp_group)
 
     # ---- sequence-parallel pieces. Between the TP regions the residual stream is a [B, T/tp, D]
     # sequence shard h; each region starts from the all-gathered full sequence hf (its norm runs on
@@ -320,7 +320,7 @@ class GemmaBlock(tnn.Module):
         (TP-partial [B, T, D])."""
         from ..parallel.tensor_parallel import add_owner_rows
         n2f = rms_norm(hf, self.ffn_norm, self.c.norm_eps)
-        return add_owner_rows(linear(glu(linear(n2f, self.w13), "gelu_tanh"), self.w2), h, g)
+        return add_owner_rows(swiglu_mlp(n2f, self.w13, self.w2, "gelu_tanh"), h, g)
 
 
 class Gemma(tnn.Module):
