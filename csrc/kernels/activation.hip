@@ -81,6 +81,14 @@ __global__ __launch_bounds__(256) void glu_bwd_kernel(const T* __restrict__ dy, 
   }
 }
 
+// token rows per block of the GLU transpose kernels below (64 or 128; tools/bench_glu_t.py, one box:
+// glu_bwd_t 0.340 ms at 64 vs 0.320 at 128, glu_fwd_t 0.200 at 64 vs 0.213 at 128)
+#ifndef GLU_T_TT_BWD
+#define GLU_T_TT_BWD 128
+#endif
+#ifndef GLU_T_TT_FWD
+#define GLU_T_TT_FWD 64
+#endif
 // glu_bwd that also writes the transposed gradient dgu^T [2F, M] (bf16): the weight gradient of the
 // [gate | up] projection is dW = dgu^T X, which hipBLASLt runs fastest with both operands
 // token-contiguous ("both" form, profiles/r6_wgrad_glu_t.txt); producing dgu^T here saves the
@@ -94,12 +102,12 @@ __global__ __launch_bounds__(256) void glu_bwd_t_kernel(const bf16* __restrict__
   // dgu^T rows on the write side). LDS tiles [gate / up][token][feature], 272-B rows, the 16-B chunk
   // index XOR-swizzled by the token row's 8-row group so the transposed phase's 8-byte reads (4
   // features of one token) spread over the banks
-  constexpr int TT = 64, TF = 128, LD = TF + 8;
+  constexpr int TT = GLU_T_TT_BWD, TF = 128, LD = TF + 8, CT = TT / 8;
   __shared__ __attribute__((aligned(16))) bf16 tile[2][TT * LD];
   const int r0 = blockIdx.y * TT, f0 = blockIdx.x * TF;
   auto soff = [](int r, int c16) { return r * LD + 8 * (c16 ^ ((r >> 3) & 7)); };
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {              // 64 tokens x 16 chunks of 8 features
+  for (int c = 0; c < TT / 16; ++c) {        // TT tokens x 16 chunks of 8 features
     const int idx = threadIdx.x + 256 * c, r = idx >> 4, ch = idx & 15;
     const int m = r0 + r, f = f0 + ch * 8;
     float g[8], u[8], d[8], dg[8], du[8];
@@ -128,8 +136,8 @@ __global__ __launch_bounds__(256) void glu_bwd_t_kernel(const bf16* __restrict__
   // jobs: half h, features 4 jq .. 4 jq + 3 (32 groups), tokens 8 ch .. 8 ch + 7 -> four 16-B runs of
   // dgu^T rows each (8 x ds_read_b64 + 16 v_perm)
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int idx = threadIdx.x + 256 * c, h = idx >> 8, jq = (idx >> 3) & 31, ch = idx & 7;
+  for (int c = 0; c < CT / 4; ++c) {
+    const int idx = threadIdx.x + 256 * c, h = idx / (32 * CT), jq = (idx / CT) & 31, ch = idx % CT;
     uint2 rw[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -164,12 +172,12 @@ __global__ __launch_bounds__(256) void glu_bwd_t_kernel(const bf16* __restrict__
 template <int KIND>
 __global__ __launch_bounds__(256) void glu_fwd_t_kernel(const bf16* __restrict__ gu, bf16* __restrict__ y,
                                                         bf16* __restrict__ yt, int M, int F) {
-  constexpr int TT = 64, TF = 128, LD = TF + 8;
+  constexpr int TT = GLU_T_TT_FWD, TF = 128, LD = TF + 8, CT = TT / 8;
   __shared__ __attribute__((aligned(16))) bf16 tile[TT * LD];
   const int r0 = blockIdx.y * TT, f0 = blockIdx.x * TF;
   auto soff = [](int r, int c16) { return r * LD + 8 * (c16 ^ ((r >> 3) & 7)); };
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < TT / 16; ++c) {
     const int idx = threadIdx.x + 256 * c, r = idx >> 4, ch = idx & 15;
     const int m = r0 + r, f = f0 + ch * 8;
     float g[8], u[8];
@@ -187,7 +195,9 @@ __global__ __launch_bounds__(256) void glu_fwd_t_kernel(const bf16* __restrict__
     *reinterpret_cast<bf16x8*>(&tile[soff(r, ch)]) = a8;
   }
   __syncthreads();
-  const int jq = threadIdx.x >> 3, ch = threadIdx.x & 7;   // features 4 jq .., tokens 8 ch ..
+#pragma unroll
+  for (int c = 0; c < CT / 8; ++c) {        // features 4 jq .., tokens 8 ch ..
+  const int idx = threadIdx.x + 256 * c, jq = idx / CT, ch = idx % CT;
   uint2 rw[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) rw[e] = *reinterpret_cast<const uint2*>(&tile[soff(ch * 8 + e, jq >> 1) + 4 * (jq & 1)]);
@@ -209,6 +219,7 @@ __global__ __launch_bounds__(256) void glu_fwd_t_kernel(const bf16* __restrict__
         *reinterpret_cast<uint4*>(yt + (long)f * M + m) = o;
       }
     }
+  }
   }
 }
 
@@ -395,7 +406,7 @@ std::vector<at::Tensor> glu_fwd_t(const at::Tensor& gu_, int64_t kind) {
   auto yt = at::empty({F, M}, gu.options());
   if (M == 0) return {y, yt};
   DeviceGuard g(gu.device());
-  const dim3 grid(cdiv(F, 128), (int)cdiv(M, 64L));
+  const dim3 grid(cdiv(F, 128), (int)cdiv(M, (long)GLU_T_TT_FWD));
   ACT_SWITCH(kind, glu_fwd_t_kernel<K_><<<grid, 256, 0, stream()>>>((const bf16*)gu.data_ptr(), (bf16*)y.data_ptr(),
                                                                       (bf16*)yt.data_ptr(), (int)M, F));
   SPA_LAUNCH_CHECK();
@@ -415,7 +426,7 @@ std::vector<at::Tensor> glu_bwd_t(const at::Tensor& dy_, const at::Tensor& gu_, 
   auto dgut = at::empty({F2, M}, gu.options());
   if (M == 0) return {dgu, dgut};
   DeviceGuard g(gu.device());
-  const dim3 grid(cdiv(F, 128), (int)cdiv(M, 64L));
+  const dim3 grid(cdiv(F, 128), (int)cdiv(M, (long)GLU_T_TT_BWD));
   ACT_SWITCH(kind, glu_bwd_t_kernel<K_><<<grid, 256, 0, stream()>>>(
                        (const bf16*)dy.data_ptr(), (const bf16*)gu.data_ptr(), (bf16*)dgu.data_ptr(),
                        (bf16*)dgut.data_ptr(), (int)M, F));

@@ -52,6 +52,9 @@ for r in range(2):
     t_dgt = tm(lambda: torch.mm(dht.t(), w13t.t()))
     t_dgt2 = tm(lambda: torch.mm(dht.t(), w13))
     print(f"round {r}: dX from dH {t_dg:.3f} ms | from dH^T (on W^T) {t_dgt:.3f} ms | from dH^T (on W) {t_dgt2:.3f} ms", flush=True)
+    t_f = tm(lambda: ops.glu_fwd(h, 6))
+    t_ft = tm(lambda: ops.glu_fwd_t(h, 6))
+    print(f"round {r}: glu_fwd {t_f:.3f} ms | glu_fwd_t {t_ft:.3f} ms", flush=True)
     print(f"round {r}: glu_bwd {t_b:.3f} ms | glu_bwd_t {t_bt:.3f} ms | transpose dH {t_tr:.3f} ms | "
           f"dW x-form {t_x:.3f} ms | dW both-form {t_both:.3f} ms | plain {t_b + t_x:.3f} vs glu_t {t_bt + t_both:.3f}",
           flush=True)
