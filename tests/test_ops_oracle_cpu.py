@@ -207,3 +207,25 @@ def test_attention_dropout_cpu_mask_is_seeded_and_calibrated():
     pr = torch.softmax(s, -1) * m1 / 0.75
     want = torch.einsum("bhqk,bkhd->bqhd", pr, v)
     assert torch.allclose(o, want, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["silu", "gelu_tanh"])
+def test_swiglu_mlp_cpu_is_the_composition(kind):
+    """ops.linear.swiglu_mlp off the GPU (and for tensors its kernels do not take) is exactly
+    linear(glu(linear(x, w13), kind), w2) -- the fp64 reference composition, gradients included."""
+    from solvingpapers_amd.ops.linear import swiglu_mlp
+    torch.manual_seed(0)
+    x = torch.randn(6, 16, dtype=torch.float64, requires_grad=True)
+    w13 = torch.randn(2 * 24, 16, dtype=torch.float64, requires_grad=True)
+    w2 = torch.randn(16, 24, dtype=torch.float64, requires_grad=True)
+    y = swiglu_mlp(x, w13, w2, kind)
+    h = x @ w13.t()
+    g, u = h[:, :24], h[:, 24:]
+    act = F.silu(g) if kind == "silu" else F.gelu(g, approximate="tanh")
+    ref = (act * u) @ w2.t()
+    assert torch.allclose(y, ref, rtol=1e-12, atol=1e-12)
+    gy = torch.randn_like(y)
+    ga = torch.autograd.grad(y, (x, w13, w2), gy)
+    gb = torch.autograd.grad(ref, (x, w13, w2), gy)
+    for a, b in zip(ga, gb):
+        assert torch.allclose(a, b, rtol=1e-10, atol=1e-10)
