@@ -121,19 +121,21 @@ def test_mlp_matches_fp32(kind, R, D, F):
         assert rel(p_.grad, f_.grad) < 2e-2, p_.shape
 
 
+@pytest.mark.parametrize("kind", [6, 4])   # silu (LLaMA SwiGLU), gelu_tanh (Gemma GeGLU)
 @pytest.mark.parametrize("M,F", [(1000, 200), (4096, 1024), (8, 8)])
-def test_glu_bwd_t_matches_glu_bwd(M, F):
+def test_glu_bwd_t_matches_glu_bwd(M, F, kind):
     """glu_bwd_t (the GLU backward that also writes dgu^T for the both-token-contiguous dW) == glu_bwd
-    bitwise, and its second output is exactly the transpose; ragged token / feature tiles."""
+    (bitwise for silu), and its second output is exactly the transpose; ragged token / feature tiles."""
     from solvingpapers_amd.ops import _ext
     torch.manual_seed(8)
     gu = torch.randn(M, 2 * F, device=DEV).bfloat16()
     dy = torch.randn(M, F, device=DEV).bfloat16()
-    ref = _ext.ops().glu_bwd(dy, gu, 6)
-    dgu, dgut = _ext.ops().glu_bwd_t(dy, gu, 6)
+    ref = _ext.ops().glu_bwd(dy, gu, kind)
+    dgu, dgut = _ext.ops().glu_bwd_t(dy, gu, kind)
     torch.cuda.synchronize()
-    assert torch.equal(dgu, ref)
-    assert dgut.shape == (2 * F, M) and torch.equal(dgut, ref.t())
+    # silu: bitwise; gelu_tanh: hipcc contracts tanh's polynomial differently per kernel (fp32 last bits)
+    assert torch.equal(dgu, ref) if kind == 6 else rel(dgu, ref) < 1e-2
+    assert dgut.shape == (2 * F, M) and torch.equal(dgut, dgu.t())
 
 
 @pytest.mark.parametrize("acc", [False, True])
@@ -167,20 +169,23 @@ def test_linear_glu_matches_composition(acc, monkeypatch):
     assert rel(res["1"][2] - (0.25 if acc else 0.0), wf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("kind", [6, 4])
 @pytest.mark.parametrize("M,F", [(1000, 200), (4096, 1024), (8, 8)])
-def test_glu_fwd_t_matches_glu_fwd(M, F):
-    """glu_fwd_t == glu_fwd bitwise, its second output exactly the transpose (ragged tiles)."""
+def test_glu_fwd_t_matches_glu_fwd(M, F, kind):
+    """glu_fwd_t == glu_fwd (bitwise for silu), its second output exactly the transpose (ragged tiles)."""
     from solvingpapers_amd.ops import _ext
     torch.manual_seed(10)
     gu = torch.randn(M, 2 * F, device=DEV).bfloat16()
-    ref = _ext.ops().glu_fwd(gu, 6)
-    y, yt = _ext.ops().glu_fwd_t(gu, 6)
+    ref = _ext.ops().glu_fwd(gu, kind)
+    y, yt = _ext.ops().glu_fwd_t(gu, kind)
     torch.cuda.synchronize()
-    assert torch.equal(y, ref) and yt.shape == (F, M) and torch.equal(yt, ref.t())
+    assert torch.equal(y, ref) if kind == 6 else rel(y, ref) < 1e-2
+    assert yt.shape == (F, M) and torch.equal(yt, y.t())
 
 
+@pytest.mark.parametrize("kind", ["silu", "gelu_tanh"])
 @pytest.mark.parametrize("acc", [False, True])
-def test_swiglu_mlp_matches_composition(acc, monkeypatch):
+def test_swiglu_mlp_matches_composition(acc, kind, monkeypatch):
     """ops.linear.swiglu_mlp (y^T kept from the forward, dH^T from the backward: both weight gradients
     in the both-transposed form) == linear(glu(linear(x, w13)), w2) (SPA_GLU_T=0) on every output and
     gradient, into flat bf16 main_grads with and without accumulation."""
@@ -201,7 +206,7 @@ def test_swiglu_mlp_matches_composition(acc, monkeypatch):
         for w in (w13, w2):
             w.main_grad = torch.full_like(w, 0.25) if acc else torch.zeros_like(w)
             w._spa_gen = _Gen.value if acc else -1
-        y = L.swiglu_mlp(x, w13, w2, "silu")
+        y = L.swiglu_mlp(x, w13, w2, kind)
         y.backward(g)
         res[mode] = (y.detach(), x.grad, w13.main_grad.clone(), w2.main_grad.clone())
     assert torch.equal(res["2"][0], res["0"][0])
