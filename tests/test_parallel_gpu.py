@@ -25,15 +25,15 @@ def _port():
     return p
 
 
-def _model():
+def _model(seq=256):
     from solvingpapers_amd.models import llama3
-    c = llama3.config("llama3_tiny", max_seq_len=256)
+    c = llama3.config("llama3_tiny", max_seq_len=seq)
     return llama3.Llama3(c, device="cuda:0", dtype=torch.bfloat16, seed=3)
 
 
-def _ids():
+def _ids(seq=256):
     g = torch.Generator().manual_seed(7)
-    return torch.randint(0, 1024, (4, 257), generator=g)
+    return torch.randint(0, 1024, (4, seq + 1), generator=g)
 
 
 def _setup(m):
@@ -44,17 +44,17 @@ def _setup(m):
     return flat, opt
 
 
-def _worker(rank, world, port, q, accum):
+def _worker(rank, world, port, q, accum, seq):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), SPA_DIST_BACKEND="gloo")
     from solvingpapers_amd.parallel import dist as sdist
     from solvingpapers_amd.parallel.data_parallel import DataParallel
     info = sdist.init_distributed()
     assert info.backend == "gloo" and info.device == torch.device("cuda", 0)
-    m = _model()
+    m = _model(seq)
     flat, opt = _setup(m)
     dp = DataParallel(m, flat)
-    ids = _ids().cuda()[rank * 2:(rank + 1) * 2]
+    ids = _ids(seq).cuda()[rank * 2:(rank + 1) * 2]
     opt.zero_grad()
     for i in range(accum):
         x = ids[i * 2 // accum:(i + 1) * 2 // accum]
@@ -68,13 +68,15 @@ def _worker(rank, world, port, q, accum):
     sdist.cleanup()
 
 
-@pytest.mark.parametrize("accum", [1, 2])
-def test_dp2_gloo_on_one_gpu_matches_single_process(accum):
+# seq 1024, accum 1: 2048 tokens per rank's micro-batch, so the feed-forward takes swiglu_mlp's
+# transposed-operand weight gradients (ops/linear.py, T >= 2048) under the DP bucket hooks
+@pytest.mark.parametrize("accum,seq", [(1, 256), (2, 256), (1, 1024)])
+def test_dp2_gloo_on_one_gpu_matches_single_process(accum, seq):
     from solvingpapers_amd.ops import _ext
     assert _ext.load(), "HIP extension must load on the GPU box"
-    m = _model()
+    m = _model(seq)
     flat, opt = _setup(m)
-    ids = _ids().cuda()
+    ids = _ids(seq).cuda()
     opt.zero_grad()
     loss = 0.5 * (m(ids[:2, :-1], ids[:2, 1:]) + m(ids[2:, :-1], ids[2:, 1:]))
     loss.backward()
@@ -87,7 +89,7 @@ def test_dp2_gloo_on_one_gpu_matches_single_process(accum):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, accum)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, accum, seq)) for r in range(2)]
     for p in ps:
         p.start()
     out = [q.get(timeout=100) for _ in ps]
